@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""Benchmark: gossip messages delivered per second in the broadcast phase.
+
+Workload (BASELINE.json metric "gossip messages delivered/sec at N=1e9"): one
+push-flooding broadcast over a GPU-built overlay of N = 1e9 nodes, fanout 5,
+fanin 6, delays 10-20 ms, droprate 0.1, crashrate 0.01 (config C5's loss and
+crash settings, reference model; the push-pull and failure-mask extensions are
+not in this line).  A "step" is one whole broadcast: gs_broadcast_begin, ticks
+until a 10-tick poll sees float32(received)/float32(N) >= 0.99
+(simulator.go:239-253), then gs_reset.  Inputs (peer table, state) are resident
+in HBM before the timed region; the overlay build is timed separately.
+
+Multi-GPU: one process per GPU; each rank runs an independent trial (its own
+overlay, trial = rank) -- batched Monte Carlo trials with no data-path
+collective, so "scaling" is weak and value = all ranks' delivered sends / the
+slowest rank's time.
+
+Roofline: HBM-bound; 12 algorithmic bytes per delivered send (4-B friend id +
+4-B read and 4-B write of the target's state word), divided by
+the device time of the tick kernels measured with HIP events on the engine's
+own stream (an extra, instrumented broadcast after the timed steps).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+BYTES_PER_SEND = 12
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=1_000_000_000)
+    ap.add_argument("--fanout", type=int, default=5)
+    ap.add_argument("--fanin", type=int, default=6)
+    ap.add_argument("--delaylow", type=int, default=10)
+    ap.add_argument("--delayhigh", type=int, default=20)
+    ap.add_argument("--droprate", type=float, default=0.1)
+    ap.add_argument("--crashrate", type=float, default=0.01)
+    ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--cpu-n", type=int, default=10_000_000,
+                    help="nodes in the bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--no-roofline", action="store_true")
+    return ap.parse_args()
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import gossip_simulator_amd as gs
+
+    cfg = gs.Config(n=a.n, fanout=a.fanout, fanin=a.fanin, delaylow=a.delaylow,
+                    delayhigh=a.delayhigh, droprate=a.droprate, crashrate=a.crashrate,
+                    seed=a.seed, trial=rank, device=local)
+    sim = gs.Simulator(cfg)
+    t0 = time.perf_counter()
+    wins, stab = sim.build_overlay()
+    overlay_s = time.perf_counter() - t0
+    log(f"rank {rank}: overlay n={a.n} stabilised at {stab} ms simulated, {overlay_s:.2f} s wall")
+
+    def one_step():
+        sim.reset()
+        sim.broadcast_begin(-1)
+        polls, status = sim.run(poll=10)
+        tot = sim.totals()
+        return tot, status
+
+    for _ in range(a.warmup):
+        tot, status = one_step()
+        log(f"rank {rank}: warmup ticks={tot['tick']} sent={tot['sent']} status={status}")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t1 = time.perf_counter()
+    sent = 0
+    ticks = []
+    for _ in range(a.steps):
+        tot, status = one_step()
+        sent += tot["sent"]
+        ticks.append(tot["tick"])
+    barrier()
+    elapsed = time.perf_counter() - t1
+    msgs = tot["messages"]
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        st = torch.tensor([sent], dtype=torch.float64, device="cuda")
+        dist.all_reduce(st, op=dist.ReduceOp.SUM)
+        sent_all = int(st.item())
+    else:
+        sent_all = sent
+    value = sent_all / elapsed
+
+    roof = None
+    if not a.no_roofline:
+        sim.set_flags(True)
+        sim.reset()
+        sim.broadcast_begin(-1)
+        sim.run(poll=10)
+        tm = sim.timing()
+        tot_r = sim.totals()
+        kern_ms = tm["deliver_ms"] + tm["resolve_ms"]
+        launches = int(tm["deliver_launches"])
+        achieved = BYTES_PER_SEND * tot_r["sent"] / (kern_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                "kernel": "k_tick (COUNT+RESOLVE per tick)" if a.crashrate >= 0.01 else
+                          "k_tick (FLOOD per tick)",
+                "avg_launch_us": round(kern_ms * 1e3 / max(launches, 1), 2),
+                "launches": launches, "bytes_per_launch": int(BYTES_PER_SEND * tot_r["sent"] /
+                                                              max(launches, 1))}
+        sim.set_flags(False)
+
+    cpu = None
+    if rank == 0 and world == 1 and a.cpu_n > 0:
+        cpu = cpu_baseline(a, gs)
+
+    sim.close()
+    if rank == 0:
+        line = {
+            "metric": "gossip messages delivered/sec (node) at N=1e9; rounds-to-coverage parity",
+            "value": round(value, 1),
+            "unit": "msgs/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed * 1e3 / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (GPU-built overlay, keyed Philox)",
+            "config": {"workload": "C5-reference-model: single push-flood broadcast per GPU",
+                       "n": a.n, "fanout": a.fanout, "fanin": a.fanin,
+                       "delaylow": a.delaylow, "delayhigh": a.delayhigh,
+                       "droprate": a.droprate, "crashrate": a.crashrate,
+                       "ticks_to_99": ticks[-1], "delivered_per_step": sent // a.steps,
+                       "messages_per_step": msgs, "overlay_s": round(overlay_s, 3),
+                       "overlay_stabilised_ms": stab, "parallelism": f"trials{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(a, gs):
+    """The oracle (C restatement, 1 thread) on a bounded sample: one whole
+    broadcast at n = cpu_n, same parameters, over a table the GPU overlay
+    built (copied to the host); times only the oracle's tick loop."""
+    from oracle import pyoracle as O
+    O.build()
+    n = a.cpu_n
+    cfg = gs.Config(n=n, fanout=a.fanout, fanin=a.fanin, delaylow=a.delaylow,
+                    delayhigh=a.delayhigh, droprate=a.droprate, crashrate=a.crashrate,
+                    seed=a.seed, trial=0, device=0)
+    with gs.Simulator(cfg) as s:
+        s.build_overlay()
+        deg, ids = s.read_peers()
+    p = O.make_params(n=n, fanout=a.fanout, fanin=a.fanin, delay_low=a.delaylow,
+                      delay_high=a.delayhigh, drop_rate=a.droprate, crash_rate=a.crashrate,
+                      seed=a.seed, trial=0)
+    e = O.Engine(p, deg, ids)
+    e.begin(-1)
+    sent = 0
+    t0 = time.perf_counter()
+    while True:
+        st = e.step(10)
+        sent += int(st[:, 2].sum())
+        if O.covered(int(st[-1, 4]), n) or int(st[-1, 6]) == 0 or time.perf_counter() - t0 > 30:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(sent / dt, 1), "unit": "msgs/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/gsoracle.c tick engine, one broadcast at n={n} to 99% coverage "
+                      f"({sent} delivered sends, {dt:.2f} s), same params, GPU-built overlay"}
+
+
+if __name__ == "__main__":
+    main()

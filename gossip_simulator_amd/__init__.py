@@ -1,0 +1,17 @@
+"""gossip_simulator_amd -- MI355X-native engine for the broadcast round loop of
+go-distributed/gossip_simulator (simulator.go).
+
+Layers:
+  include/gossip.h          C ABI (the drop-in seam; cgo binding in INTEGRATION.md)
+  csrc/gs_broadcast.hip     tick kernels: delivery, infection, crash, stats
+  csrc/gs_overlay.hip       overlay construction (makeup/breakup) on the GPU
+  csrc/gs_api.cpp           C ABI implementation (device state, stream, polling)
+  csrc/gossip_sim.cpp       CLI with the reference's flags and stdout
+  engine.py                 Python host API (ctypes)
+  peers.py                  injected peer-table file format
+  dist.py                   multi-GPU sharding (trials; node ranges)
+"""
+from ._lib import GossipError, load  # noqa: F401
+from .engine import Config, Simulator, covered  # noqa: F401
+
+__all__ = ["Config", "Simulator", "GossipError", "covered", "load"]

@@ -1,0 +1,143 @@
+"""ctypes binding of libgossip_hip.so (include/gossip.h).
+
+The product path: there is no CPU fallback.  If the in-tree library is missing
+or a GPU is absent, calls fail loudly (GossipError / OSError).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libgossip_hip.so")
+CLI_PATH = os.path.join(PKG_DIR, "bin", "gossip_sim")
+
+GS_OK, GS_EINVAL, GS_ELIVELOCK, GS_EREJECT, GS_ENOMEM, GS_EDEVICE, GS_EOVERFLOW = (
+    0, -1, -2, -3, -4, -5, -6)
+GS_FLAG_TIMING = 1
+GS_RUN_COVERED, GS_RUN_QUIESCENT, GS_RUN_MAX_TICKS = 0, 1, 2
+
+# Every symbol include/gossip.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "gs_version", "gs_strerror", "gs_create", "gs_destroy", "gs_last_error",
+    "gs_load_peers", "gs_load_peers_device", "gs_read_peers", "gs_build_overlay",
+    "gs_set_failed", "gs_broadcast_begin", "gs_step", "gs_run", "gs_totals",
+    "gs_read_received", "gs_read_crashed", "gs_timing_get", "gs_format_float32",
+    "gs_format_float64", "gs_format_duration", "gs_threshold", "gs_philox",
+    "gs_set_flags", "gs_reset",
+)
+
+
+class GossipError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{msg} [code {code}]")
+        self.code = code
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint64),
+        ("fanout", C.c_int32),
+        ("fanin", C.c_int32),
+        ("delay_low", C.c_int32),
+        ("delay_high", C.c_int32),
+        ("drop_rate", C.c_double),
+        ("crash_rate", C.c_double),
+        ("seed", C.c_uint64),
+        ("trial", C.c_uint32),
+        ("device", C.c_int32),
+        ("flags", C.c_uint32),
+        ("reserved_", C.c_uint32 * 7),
+    ]
+
+
+class TickStats(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in
+                ("tick", "fired", "sent", "messages", "received", "crashed", "pending")]
+
+
+class Window(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in ("tick", "makeups", "breakups")]
+
+
+class Timing(C.Structure):
+    _fields_ = [("deliver_ms", C.c_double), ("resolve_ms", C.c_double),
+                ("deliver_launches", C.c_uint64), ("resolve_launches", C.c_uint64),
+                ("overlay_ms", C.c_double)]
+
+
+_lib = None
+
+
+def load():
+    """Load the in-tree library (raises OSError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(LIB_PATH)
+    P, vp, sz = C.POINTER, C.c_void_p, C.c_size_t
+    ctx = vp
+    sig = {
+        "gs_version": ([], C.c_int),
+        "gs_strerror": ([C.c_int], C.c_char_p),
+        "gs_create": ([P(Params), P(vp)], C.c_int),
+        "gs_destroy": ([ctx], None),
+        "gs_last_error": ([ctx], C.c_char_p),
+        "gs_load_peers": ([ctx, vp, vp, C.c_uint32], C.c_int),
+        "gs_load_peers_device": ([ctx, vp, vp, C.c_uint32], C.c_int),
+        "gs_read_peers": ([ctx, vp, vp, P(C.c_uint32)], C.c_int),
+        "gs_build_overlay": ([ctx, C.c_uint64, P(Window), sz, P(sz), P(C.c_uint64)], C.c_int),
+        "gs_set_failed": ([ctx, vp, sz], C.c_int),
+        "gs_broadcast_begin": ([ctx, C.c_int64], C.c_int),
+        "gs_step": ([ctx, C.c_uint32, P(TickStats)], C.c_int),
+        "gs_run": ([ctx, C.c_uint32, C.c_uint64, P(TickStats), sz, P(sz), P(C.c_int32)], C.c_int),
+        "gs_totals": ([ctx, P(TickStats)], C.c_int),
+        "gs_read_received": ([ctx, vp, sz], C.c_int),
+        "gs_read_crashed": ([ctx, vp, sz], C.c_int),
+        "gs_timing_get": ([ctx, P(Timing)], C.c_int),
+        "gs_format_float32": ([C.c_float, C.c_char_p, sz], sz),
+        "gs_format_float64": ([C.c_double, C.c_char_p, sz], sz),
+        "gs_format_duration": ([C.c_int64, C.c_char_p, sz], sz),
+        "gs_threshold": ([C.c_double], C.c_int32),
+        "gs_philox": ([P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)], None),
+        "gs_set_flags": ([ctx, C.c_uint32], C.c_int),
+        "gs_reset": ([ctx], C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def format_float32(x: float) -> str:
+    b = C.create_string_buffer(64)
+    load().gs_format_float32(x, b, 64)
+    return b.value.decode()
+
+
+def format_float64(x: float) -> str:
+    b = C.create_string_buffer(64)
+    load().gs_format_float64(x, b, 64)
+    return b.value.decode()
+
+
+def format_duration(ns: int) -> str:
+    b = C.create_string_buffer(64)
+    load().gs_format_duration(ns, b, 64)
+    return b.value.decode("utf-8")
+
+
+def threshold(rate: float) -> int:
+    return int(load().gs_threshold(rate))
+
+
+def philox(ctr, key):
+    c = (C.c_uint32 * 4)(*[int(x) & 0xFFFFFFFF for x in ctr])
+    k = (C.c_uint32 * 2)(*[int(x) & 0xFFFFFFFF for x in key])
+    o = (C.c_uint32 * 4)()
+    load().gs_philox(c, k, o)
+    return [int(x) for x in o]

@@ -1,0 +1,91 @@
+// gs_internal.h -- device-state layout shared by the broadcast and overlay
+// translation units and the C-ABI implementation.
+//
+// HBM layout for one broadcast (N nodes, W = ceil(N/64) words, R ring slots):
+//   deg     u8 [N]              friends-list length   (simulator.go:45)
+//   ids     u32[N * stride]     friends rows          (simulator.go:45)
+//   recv    u64[W]              received bitset       (simulator.go:38)
+//   crash   u64[W]              crashed bitset        (simulator.go:39)
+//   ring    u64[R][W]           fire ring: slot s holds every Broadcast whose
+//                               time.After(delay) expires at a tick = s mod R
+//                               (simulator.go:141-142)
+//   cflag   u32[R][C]           1 if chunk c (4096 nodes = 64 words) of slot s
+//                               has a pending fire bit
+//   clist   u32[R][32][CS]      active chunks of slot s, 32 shards (c mod 32)
+//   ccount  u32[R][32 * 16]     shard fill counters, one 64-B line each
+//   cnt     u32[N]              per-tick arrival counts (only if crash% > 0)
+//   stats   u64[4096][8]        per-tick counters, ring-indexed by tick
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+
+#include "gs_rng.h"
+
+namespace gs {
+
+constexpr uint32_t kWave = 64;
+constexpr uint32_t kChunkNodesLog = 12;  // 4096 nodes = 64 words per chunk
+constexpr uint32_t kChunkWords = 64;
+constexpr uint32_t kShards = 32;
+constexpr uint32_t kCounterStride = 16;  // u32s between shard counters (64 B)
+constexpr uint32_t kStatFields = 8;
+constexpr uint32_t kStatSlots = 4096;
+constexpr uint32_t kListCap = 1024;      // per-wave LDS list of firing nodes
+constexpr uint32_t kTickBlock = 256;
+constexpr uint32_t kTickGridMax = 2048;
+
+enum Stat : uint32_t {
+  ST_FIRED = 0, ST_SENT = 1, ST_MSGS = 2, ST_RECV = 3, ST_CRASH = 4, ST_SCHED = 5,
+  ST_ERR = 6, ST_RSVD = 7
+};
+
+// Tick kernel modes.
+enum Mode : int {
+  MODE_FLOOD = 0,    // crash% == 0: deliver + infect fused, one atomicOr per send
+  MODE_COUNT = 1,    // crash% > 0, pass 1: count arrivals per node
+  MODE_RESOLVE = 2   // crash% > 0, pass 2: one owner per node runs the ordinals
+};
+
+struct DevState {
+  const uint8_t* deg;
+  const uint32_t* ids;
+  unsigned long long* recv;
+  unsigned long long* crash;
+  uint32_t* cnt;
+  unsigned long long* ring;
+  uint32_t* cflag;
+  uint32_t* clist;
+  uint32_t* ccount;
+  unsigned long long* stats;
+  uint64_t n, W;
+  uint32_t C, CS, R, stride;
+  uint32_t stride_magic;   // floor(2^32 / stride) + 1: exact q/stride for q < 2^18
+  int32_t delay_low;
+  uint32_t delay_span;
+  int32_t kd, kc;
+  int32_t check_crashed;   // FLOOD mode: a pre-failed mask is present
+  Key key;
+};
+
+// Launchers (gs_broadcast.hip).
+hipError_t launch_tick(const DevState& st, uint32_t tick, int mode, hipStream_t s);
+hipError_t launch_slot_reset(const DevState& st, uint32_t slot, hipStream_t s);
+hipError_t launch_schedule_one(const DevState& st, uint32_t node, uint32_t tick, hipStream_t s);
+uint32_t tick_grid(const DevState& st);
+
+// Overlay builder (gs_overlay.hip).
+struct OverlayResult {
+  uint64_t final_tick;
+  int rc;  // GS_* code
+  char msg[160];
+};
+struct OverlayWindowSink {
+  void (*push)(void* self, uint64_t tick, uint64_t makeups, uint64_t breakups);
+  void* self;
+};
+int overlay_build(uint64_t n, int32_t fanout, int32_t fanin, int32_t delay_low,
+                  int32_t delay_high, Key key, uint8_t* d_deg, uint32_t* d_ids,
+                  uint32_t stride, uint64_t max_ticks, hipStream_t stream,
+                  OverlayWindowSink sink, OverlayResult* res);
+
+}  // namespace gs

@@ -1,0 +1,78 @@
+// gs_rng.h -- keyed Philox4x32-10 streams shared by host and device code.
+//
+// Every rand.Intn call site of simulator.go becomes a pure function of
+// (seed; kind, trial, tick, node, slot), so a decision does not depend on
+// which lane, block, XCD or GPU makes it:
+//   kind SENDER  simulator.go:240   ctr {0, 0, 0, .}            out[0] -> U_n
+//   kind DELAY   simulator.go:167   ctr {v, t, 0, .}            out[0] -> U_(high-low)
+//   kind DROP    simulator.go:172   ctr {v, t, j/4, .}          out[j%4] -> U_100
+//   kind CRASH   simulator.go:180   ctr {u, t, i/4, .}          out[i%4] -> U_100
+//   kind PICK    simulator.go:97    ctr {v, 0, j, .}            out[0] -> U_n
+//   kind OVDELAY simulator.go:153,160 ctr {u, t, k, .}          out[0] -> U_(high-low)
+//   kind VICTIM  simulator.go:71    ctr {u, t, k, .}            out[0] -> U_deg
+//   kind REPLACE simulator.go:86-88 ctr {u, t, k*64+a/4, .}     out[a%4] -> U_n
+// with counter word 3 = kind << 24 | trial.  U_m(r) = floor(r*m / 2^32).
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+
+namespace gs {
+
+enum Kind : uint32_t {
+  K_SENDER = 1, K_DELAY = 2, K_DROP = 3, K_CRASH = 4,
+  K_PICK = 5, K_OVDELAY = 6, K_VICTIM = 7, K_REPLACE = 8
+};
+
+struct u32x4 { uint32_t x, y, z, w; };
+
+__host__ __device__ __forceinline__ uint32_t mulhi32(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umulhi(a, b);
+#else
+  return (uint32_t)(((uint64_t)a * b) >> 32);
+#endif
+}
+
+// Philox4x32-10 (Random123 round and key schedule).
+__host__ __device__ __forceinline__ u32x4 philox(uint32_t c0, uint32_t c1, uint32_t c2,
+                                                 uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t h0 = mulhi32(0xD2511F53u, c0), l0 = 0xD2511F53u * c0;
+    const uint32_t h1 = mulhi32(0xCD9E8D57u, c2), l1 = 0xCD9E8D57u * c2;
+    const uint32_t n0 = h1 ^ c1 ^ k0, n2 = h0 ^ c3 ^ k1;
+    c0 = n0; c1 = l1; c2 = n2; c3 = l0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  return u32x4{c0, c1, c2, c3};
+}
+
+__host__ __device__ __forceinline__ uint32_t lane_of(const u32x4& v, uint32_t i) {
+  return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+}
+
+__host__ __device__ __forceinline__ uint32_t uniform(uint32_t r, uint32_t m) {
+  return mulhi32(r, m);
+}
+
+__host__ __device__ __forceinline__ uint32_t ctr3(uint32_t kind, uint32_t trial) {
+  return (kind << 24) | (trial & 0xFFFFFFu);
+}
+
+struct Key {
+  uint32_t k0, k1, trial;
+};
+
+__host__ __device__ __forceinline__ uint32_t draw0(const Key& k, uint32_t kind, uint32_t a,
+                                                   uint32_t b, uint32_t c) {
+  return philox(a, b, c, ctr3(kind, k.trial), k.k0, k.k1).x;
+}
+
+// Delay of a Broadcast/Makeup/Breakup in ticks (simulator.go:166-168); a
+// delay below one tick runs as one tick.
+__host__ __device__ __forceinline__ uint32_t fire_offset(int32_t low, uint32_t span, uint32_t r) {
+  const int64_t d = (int64_t)low + (int64_t)uniform(r, span);
+  return d < 1 ? 1u : (uint32_t)d;
+}
+
+}  // namespace gs

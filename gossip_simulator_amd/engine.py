@@ -1,0 +1,169 @@
+"""Python host API over the C ABI: the operator-level mirror of simulator.go.
+
+`Simulator` keeps the reference's parameter names (simulator.go:11-20,
+186-193) and phases: `build_overlay()` = main :214-235, `broadcast_begin()` =
+:239-241, `step()` / `run()` = the receive/broadcast actors plus the poll loop
+:243-251.  All compute runs in libgossip_hip.so on a gfx950 device.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import GossipError, Params, TickStats, Timing, Window
+
+STAT_FIELDS = ("tick", "fired", "sent", "messages", "received", "crashed", "pending")
+
+
+@dataclass
+class Config:
+    """The reference's flags (simulator.go:187-193) plus additive knobs."""
+    n: int = 50000
+    fanout: int = 5
+    fanin: int = 6          # Fanout+1 evaluated before Parse -> always 6 (:189)
+    delaylow: int = 10
+    delayhigh: int = 20
+    droprate: float = 0.1
+    crashrate: float = 0.001
+    seed: int = 1
+    trial: int = 0
+    device: int = 0
+    timing: bool = False
+
+    def to_params(self) -> Params:
+        p = Params()
+        p.n, p.fanout, p.fanin = self.n, self.fanout, self.fanin
+        p.delay_low, p.delay_high = self.delaylow, self.delayhigh
+        p.drop_rate, p.crash_rate = self.droprate, self.crashrate
+        p.seed, p.trial, p.device = self.seed, self.trial, self.device
+        p.flags = _lib.GS_FLAG_TIMING if self.timing else 0
+        return p
+
+
+def _stats_array(buf, k: int) -> np.ndarray:
+    return np.array([[getattr(buf[i], f) for f in STAT_FIELDS] for i in range(k)],
+                    dtype=np.uint64).reshape(k, len(STAT_FIELDS))
+
+
+class Simulator:
+    """One broadcast on one GPU (a gs_ctx)."""
+
+    def __init__(self, cfg: Config):
+        self.cfg = cfg
+        self.L = _lib.load()
+        self._p = cfg.to_params()
+        h = C.c_void_p()
+        rc = self.L.gs_create(C.byref(self._p), C.byref(h))
+        if rc != 0:
+            raise GossipError(rc, f"gs_create failed: {self.L.gs_strerror(rc).decode()}")
+        self.h = h
+        self.n = cfg.n
+        self.words = (cfg.n + 63) // 64
+
+    # -- plumbing --------------------------------------------------------
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            msg = self.L.gs_last_error(self.h).decode(errors="replace")
+            raise GossipError(rc, f"{what}: {msg}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.gs_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- overlay (simulator.go:62-106, 127-164, 214-235) -------------------
+    def load_peers(self, deg: np.ndarray, ids: np.ndarray):
+        deg = np.ascontiguousarray(deg, dtype=np.uint8)
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        if deg.shape != (self.n,) or ids.ndim != 2 or ids.shape[0] != self.n:
+            raise ValueError("deg must be [n], ids [n, stride]")
+        self._check(self.L.gs_load_peers(self.h, deg.ctypes.data, ids.ctypes.data, ids.shape[1]),
+                    "gs_load_peers")
+
+    def load_peers_device(self, deg_ptr: int, ids_ptr: int, stride: int):
+        self._check(self.L.gs_load_peers_device(self.h, deg_ptr, ids_ptr, stride),
+                    "gs_load_peers_device")
+
+    def build_overlay(self, max_ticks: int = 10_000_000, wcap: int = 1 << 16):
+        win = (Window * wcap)()
+        nwin = C.c_size_t(0)
+        ft = C.c_uint64(0)
+        self._check(self.L.gs_build_overlay(self.h, max_ticks, win, wcap, C.byref(nwin),
+                                            C.byref(ft)), "gs_build_overlay")
+        ws = [(win[i].tick, win[i].makeups, win[i].breakups)
+              for i in range(min(nwin.value, wcap))]
+        return ws, int(ft.value)
+
+    def read_peers(self):
+        stride = C.c_uint32(0)
+        self._check(self.L.gs_read_peers(self.h, None, None, C.byref(stride)), "gs_read_peers")
+        deg = np.zeros(self.n, dtype=np.uint8)
+        ids = np.zeros((self.n, stride.value), dtype=np.uint32)
+        self._check(self.L.gs_read_peers(self.h, deg.ctypes.data, ids.ctypes.data, C.byref(stride)),
+                    "gs_read_peers")
+        return deg, ids
+
+    def set_failed(self, words: np.ndarray):
+        words = np.ascontiguousarray(words, dtype=np.uint64)
+        self._check(self.L.gs_set_failed(self.h, words.ctypes.data, words.size), "gs_set_failed")
+
+    # -- broadcast (simulator.go:107-123, 140-149, 237-253) ----------------
+    def broadcast_begin(self, sender: int = -1):
+        self._check(self.L.gs_broadcast_begin(self.h, sender), "gs_broadcast_begin")
+
+    def step(self, ticks: int = 1) -> np.ndarray:
+        buf = (TickStats * ticks)()
+        self._check(self.L.gs_step(self.h, ticks, buf), "gs_step")
+        return _stats_array(buf, ticks)
+
+    def run(self, poll: int = 10, max_ticks: int = 10_000_000, cap: int = 1 << 16):
+        buf = (TickStats * cap)()
+        nout = C.c_size_t(0)
+        status = C.c_int32(0)
+        self._check(self.L.gs_run(self.h, poll, max_ticks, buf, cap, C.byref(nout),
+                                  C.byref(status)), "gs_run")
+        return _stats_array(buf, min(nout.value, cap)), int(status.value)
+
+    def totals(self) -> dict:
+        t = TickStats()
+        self._check(self.L.gs_totals(self.h, C.byref(t)), "gs_totals")
+        return {f: int(getattr(t, f)) for f in STAT_FIELDS}
+
+    def received(self) -> np.ndarray:
+        w = np.zeros(self.words, dtype=np.uint64)
+        self._check(self.L.gs_read_received(self.h, w.ctypes.data, w.size), "gs_read_received")
+        return w
+
+    def crashed(self) -> np.ndarray:
+        w = np.zeros(self.words, dtype=np.uint64)
+        self._check(self.L.gs_read_crashed(self.h, w.ctypes.data, w.size), "gs_read_crashed")
+        return w
+
+    def set_flags(self, timing: bool):
+        self._check(self.L.gs_set_flags(self.h, _lib.GS_FLAG_TIMING if timing else 0),
+                    "gs_set_flags")
+
+    def reset(self):
+        self._check(self.L.gs_reset(self.h), "gs_reset")
+
+    def timing(self) -> dict:
+        t = Timing()
+        self._check(self.L.gs_timing_get(self.h, C.byref(t)), "gs_timing_get")
+        return {f: getattr(t, f) for f, _ in Timing._fields_}
+
+
+def covered(recv: int, n: int) -> bool:
+    """simulator.go:246-248 in float32."""
+    return bool(np.float32(recv) / np.float32(n) >= np.float32(0.99))

@@ -1,0 +1,166 @@
+/*
+ * gossip.h -- C ABI of libgossip_hip.so, the MI355X (gfx950) engine for the
+ * broadcast round loop of go-distributed/gossip_simulator (simulator.go).
+ *
+ * The reference has no FFI/plugin seam: it is one Go `package main`.  This ABI
+ * is the seam a maintainer adds behind its `main` (simulator.go:207-253); each
+ * entry point names the reference code it replaces.  A cgo binding is shown in
+ * INTEGRATION.md.
+ *
+ * Conventions
+ *  - return 0 on success, <0 on error (GS_E*); message via gs_last_error().
+ *  - all caller buffers are caller-owned and copied during the call; nothing
+ *    is retained across calls (cgo pointer rules).
+ *  - one gs_ctx is single-threaded; it owns one HIP device, one stream.
+ *  - node ids are uint32 (n <= 2^31-1); friend rows are uint32[stride] with a
+ *    uint8 length per node (a friends list is at most 255 long).
+ *  - every random decision is drawn from Philox4x32-10 keyed by
+ *    (seed; kind, trial, tick, node, slot) -- see DESIGN.md "Tick model".
+ */
+#ifndef GOSSIP_H
+#define GOSSIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_ABI_VERSION 1
+
+enum {
+  GS_OK = 0,
+  GS_EINVAL = -1,     /* bad parameter or call order                          */
+  GS_ELIVELOCK = -2,  /* overlay never stabilised (fanin <= fanout livelock)  */
+  GS_EREJECT = -3,    /* replacement-friend rejection exhausted (n <= 2)      */
+  GS_ENOMEM = -4,     /* host or device allocation failed                     */
+  GS_EDEVICE = -5,    /* HIP runtime error / no gfx950 device                 */
+  GS_EOVERFLOW = -6   /* a counter exceeded its range                         */
+};
+
+/* Flags (gs_params.flags). */
+#define GS_FLAG_TIMING 1u /* time every tick kernel with HIP events (gs_timing) */
+
+/* simulator.go:11-20 (Parameters) + the additive -seed/-trial knobs. */
+typedef struct gs_params {
+  uint64_t n;          /* -n          simulator.go:187                       */
+  int32_t fanout;      /* -fanout     simulator.go:188                       */
+  int32_t fanin;       /* -fanin      simulator.go:189 (default 6, see :189) */
+  int32_t delay_low;   /* -delaylow   simulator.go:190 (ms = ticks)          */
+  int32_t delay_high;  /* -delayhigh  simulator.go:191                       */
+  double drop_rate;    /* -droprate   simulator.go:192 -> int(rate*100) %    */
+  double crash_rate;   /* -crashrate  simulator.go:193 -> int(rate*100) %    */
+  uint64_t seed;       /* Philox key                                          */
+  uint32_t trial;      /* Philox counter word 3, low 24 bits                  */
+  int32_t device;      /* HIP device ordinal                                  */
+  uint32_t flags;      /* GS_FLAG_*                                           */
+  uint32_t reserved_[7];
+} gs_params;
+
+/* One tick (1 ms) of the broadcast phase; the reference exposes these as the
+ * int32 atomics of simulator.go:26-31, read by main's poll loop (:243-253). */
+typedef struct gs_tick_stats {
+  uint64_t tick;      /* simulated ms since Broadcast() (:239-241)            */
+  uint64_t fired;     /* Broadcast goroutines whose delay expired (:142)     */
+  uint64_t sent;      /* friend slots not dropped = delivered sends (:144-145)*/
+  uint64_t messages;  /* TotalMessage increments (:111)                      */
+  uint64_t received;  /* TotalReceived, cumulative (:121)                    */
+  uint64_t crashed;   /* TotalCrashed, cumulative (:114)                     */
+  uint64_t pending;   /* broadcasts scheduled, not yet fired                  */
+} gs_tick_stats;
+
+/* One 10-ms poll window of overlay construction (simulator.go:222-234). */
+typedef struct gs_window {
+  uint64_t tick;      /* end of the window (ms)                               */
+  uint64_t makeups;   /* MakeUps  in the window (:67)                         */
+  uint64_t breakups;  /* BreakUps in the window (:77)                         */
+} gs_window;
+
+/* Device time spent in the broadcast tick kernels (GS_FLAG_TIMING). */
+typedef struct gs_timing {
+  double deliver_ms;       /* sum over launches of the delivery kernel       */
+  double resolve_ms;       /* sum over launches of the resolve kernel (kc>0) */
+  uint64_t deliver_launches;
+  uint64_t resolve_launches;
+  double overlay_ms;       /* wall time of the last gs_build_overlay          */
+} gs_timing;
+
+/* gs_run status */
+enum { GS_RUN_COVERED = 0, GS_RUN_QUIESCENT = 1, GS_RUN_MAX_TICKS = 2 };
+
+typedef struct gs_ctx gs_ctx;
+
+int gs_version(void);
+const char* gs_strerror(int code);
+
+/* Replaces simulator.go:186-212 (flag globals, GlobalView/NewNode allocation).
+ * Validates params exactly as the reference would fail: n == 0 (:240 panics),
+ * delay_high <= delay_low (:167 panics). */
+int gs_create(const gs_params* params, gs_ctx** out);
+void gs_destroy(gs_ctx* ctx);
+const char* gs_last_error(const gs_ctx* ctx);
+
+/* Injects a peer table in place of the overlay (the `friends` slices,
+ * simulator.go:45,58).  deg[n] uint8, ids[n*stride] uint32 row-major.
+ * Host buffers; copied. */
+int gs_load_peers(gs_ctx* ctx, const uint8_t* deg, const uint32_t* ids, uint32_t stride);
+/* Same, from device-resident buffers (copied device-to-device). */
+int gs_load_peers_device(gs_ctx* ctx, const void* d_deg, const void* d_ids, uint32_t stride);
+/* Copies the current table out (stride = max(fanout, fanin) after an overlay). */
+int gs_read_peers(gs_ctx* ctx, uint8_t* deg, uint32_t* ids, uint32_t* stride_out);
+
+/* Replaces simulator.go:62-106,127-164 (makeup/breakup handlers, Makeup,
+ * Breakup, removeFriend) and the stabilisation loop :214-235, on the GPU.
+ * Writes one gs_window per non-final poll (up to cap; *nwin gets the total)
+ * and the stabilising poll's tick.  GS_ELIVELOCK after max_ticks. */
+int gs_build_overlay(gs_ctx* ctx, uint64_t max_ticks, gs_window* win, size_t cap,
+                     size_t* nwin, uint64_t* final_tick);
+
+/* Pre-failed node mask (extension, config C5): words[ceil(n/64)], set bits
+ * are crash-stopped before the broadcast (they never count nor forward). */
+int gs_set_failed(gs_ctx* ctx, const uint64_t* words, size_t nwords);
+
+/* Replaces simulator.go:239-241.  sender < 0 draws it from the keyed stream
+ * like rand.Intn(len(GlobalView)).  The sender is NOT marked received. */
+int gs_broadcast_begin(gs_ctx* ctx, int64_t sender);
+/* Advances `ticks` ticks of the receive/broadcast actors (simulator.go:107-123,
+ * 140-149, 166-184); out[i] (may be NULL) gets each tick's stats. */
+int gs_step(gs_ctx* ctx, uint32_t ticks, gs_tick_stats* out);
+/* Replaces the poll loop simulator.go:243-251: steps `poll` ticks at a time
+ * until float32(received)/float32(n) >= 0.99 at a poll (GS_RUN_COVERED), no
+ * broadcast is pending (GS_RUN_QUIESCENT; the reference would spin forever),
+ * or max_ticks.  out (may be NULL) receives one gs_tick_stats per poll. */
+int gs_run(gs_ctx* ctx, uint32_t poll, uint64_t max_ticks, gs_tick_stats* out,
+           size_t cap, size_t* nout, int32_t* status);
+/* Cumulative totals so far (tick, fired/sent/messages summed). */
+int gs_totals(gs_ctx* ctx, gs_tick_stats* out);
+
+/* Bitset dumps for per-round parity: words[ceil(n/64)], bit v of word v/64. */
+int gs_read_received(gs_ctx* ctx, uint64_t* words, size_t nwords);
+int gs_read_crashed(gs_ctx* ctx, uint64_t* words, size_t nwords);
+
+int gs_timing_get(gs_ctx* ctx, gs_timing* out);
+/* Replace gs_params.flags (e.g. toggle GS_FLAG_TIMING between runs). */
+int gs_set_flags(gs_ctx* ctx, uint32_t flags);
+/* Return to the state before gs_broadcast_begin: clears received/crashed,
+ * the fire ring and the counters; keeps the peer table and failure mask
+ * (a fresh process in the reference, simulator.go:207). */
+int gs_reset(gs_ctx* ctx);
+
+/* ---- host-only helpers for the reference's stdout contract ------------- */
+/* Go fmt %v of a float32 (strconv 'g', -1, 32), e.g. 99.61 or 9.9999994e-08
+ * (simulator.go:247).  Returns the length written (NUL-terminated). */
+size_t gs_format_float32(float x, char* buf, size_t cap);
+/* Go fmt %v of a float64 (flag echo, simulator.go:199). */
+size_t gs_format_float64(double x, char* buf, size_t cap);
+/* Go time.Duration.String() of `ns` nanoseconds, e.g. 1.5s, 120ms, 1m0s. */
+size_t gs_format_duration(int64_t ns, char* buf, size_t cap);
+/* Go int(rate*100) (simulator.go:172,180), clamped to [0,100]. */
+int32_t gs_threshold(double rate);
+/* Philox4x32-10 (for replay tooling and tests). */
+void gs_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

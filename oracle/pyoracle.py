@@ -1,0 +1,231 @@
+"""ctypes binding of the CPU restatement (oracle/gsoracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, always as the checker -- never by the product
+package.  Parity with the reference is unpinned by reference artefacts (see
+gsoracle.h); the pins are the hand-derived known answers under tests/.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libgsoracle.so")
+
+
+def build() -> str:
+    """Compile the restatement (gcc) into oracle/_build/."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint64),
+        ("fanout", C.c_int32),
+        ("fanin", C.c_int32),
+        ("delay_low", C.c_int32),
+        ("delay_high", C.c_int32),
+        ("drop_rate", C.c_double),
+        ("crash_rate", C.c_double),
+        ("seed", C.c_uint64),
+        ("trial", C.c_uint32),
+        ("pad_", C.c_uint32),
+    ]
+
+
+class TickStats(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in
+                ("tick", "fired", "sent", "messages", "received", "crashed", "pending")]
+
+
+class Window(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in ("tick", "makeups", "breakups")]
+
+
+class RefsimResult(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in
+                ("tick_99", "poll_99", "messages", "crashed", "received", "sent",
+                 "overlay_ticks")] + [
+        ("deg_hist", C.c_uint64 * 256),
+        ("reached", C.c_int32),
+        ("pad_", C.c_int32),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        P = C.POINTER
+        L.or_threshold.argtypes = [C.c_double]
+        L.or_threshold.restype = C.c_int32
+        L.or_philox.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
+        L.or_uniform.argtypes = [C.c_uint32, C.c_uint32]
+        L.or_uniform.restype = C.c_uint32
+        L.or_pick_sender.argtypes = [P(Params)]
+        L.or_pick_sender.restype = C.c_uint64
+        L.or_overlay.argtypes = [P(Params), C.c_void_p, C.c_void_p, P(Window), C.c_size_t,
+                                 P(C.c_size_t), C.c_uint64, P(C.c_uint64)]
+        L.or_engine_new.argtypes = [P(Params), C.c_void_p, C.c_void_p, C.c_uint32]
+        L.or_engine_new.restype = C.c_void_p
+        L.or_engine_free.argtypes = [C.c_void_p]
+        L.or_engine_begin.argtypes = [C.c_void_p, C.c_int64]
+        L.or_engine_step.argtypes = [C.c_void_p, C.c_uint32, P(TickStats)]
+        L.or_engine_read_received.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.or_engine_read_crashed.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.or_engine_set_failed.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.or_engine_tick.argtypes = [C.c_void_p]
+        L.or_engine_tick.restype = C.c_uint64
+        L.or_refsim.argtypes = [P(Params), C.c_uint64, C.c_uint64, P(RefsimResult)]
+        L.or_refsim_broadcast.argtypes = [P(Params), C.c_void_p, C.c_void_p, C.c_uint32,
+                                          C.c_uint64, C.c_uint64, P(RefsimResult)]
+        _lib = L
+    return _lib
+
+
+def make_params(n=50000, fanout=5, fanin=6, delay_low=10, delay_high=20,
+                drop_rate=0.1, crash_rate=0.001, seed=0x5EED, trial=0) -> Params:
+    return Params(n, fanout, fanin, delay_low, delay_high, drop_rate, crash_rate,
+                  seed, trial, 0)
+
+
+def threshold(rate: float) -> int:
+    return lib().or_threshold(rate)
+
+
+def philox(ctr, key):
+    c = (C.c_uint32 * 4)(*[int(x) & 0xFFFFFFFF for x in ctr])
+    k = (C.c_uint32 * 2)(*[int(x) & 0xFFFFFFFF for x in key])
+    o = (C.c_uint32 * 4)()
+    lib().or_philox(c, k, o)
+    return [int(x) for x in o]
+
+
+def pick_sender(p: Params) -> int:
+    return int(lib().or_pick_sender(C.byref(p)))
+
+
+class OverlayError(RuntimeError):
+    pass
+
+
+def overlay(p: Params, max_ticks: int = 1_000_000, wcap: int = 100000):
+    """Tick-model overlay.  Returns (deg u8[n], ids u32[n, stride], windows, final_tick)."""
+    stride = max(p.fanout, p.fanin, 1)
+    deg = np.zeros(p.n, dtype=np.uint8)
+    ids = np.zeros((p.n, stride), dtype=np.uint32)
+    win = (Window * wcap)()
+    nwin = C.c_size_t(0)
+    ft = C.c_uint64(0)
+    rc = lib().or_overlay(C.byref(p), deg.ctypes.data, ids.ctypes.data, win, wcap,
+                          C.byref(nwin), max_ticks, C.byref(ft))
+    if rc != 0:
+        raise OverlayError(f"or_overlay failed: {rc}")
+    ws = [(win[i].tick, win[i].makeups, win[i].breakups) for i in range(min(nwin.value, wcap))]
+    return deg, ids, ws, int(ft.value)
+
+
+class Engine:
+    """Tick-model broadcast engine (bit-exact spec of the HIP engine)."""
+
+    def __init__(self, p: Params, deg: np.ndarray, ids: np.ndarray):
+        self.p = p
+        self.n = int(p.n)
+        self.W = (self.n + 63) // 64
+        deg = np.ascontiguousarray(deg, dtype=np.uint8)
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        self.stride = ids.shape[1]
+        self._keep = (deg, ids)
+        self.h = lib().or_engine_new(C.byref(p), deg.ctypes.data, ids.ctypes.data, self.stride)
+        if not self.h:
+            raise ValueError("or_engine_new rejected the parameters/table")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_engine_free(self.h)
+            self.h = None
+
+    def begin(self, sender: int = -1):
+        if lib().or_engine_begin(self.h, sender) != 0:
+            raise ValueError("or_engine_begin failed")
+
+    def set_failed(self, words: np.ndarray):
+        words = np.ascontiguousarray(words, dtype=np.uint64)
+        if lib().or_engine_set_failed(self.h, words.ctypes.data, words.size) != 0:
+            raise ValueError("or_engine_set_failed failed")
+
+    def step(self, ticks: int = 1) -> np.ndarray:
+        out = (TickStats * ticks)()
+        if lib().or_engine_step(self.h, ticks, out) != 0:
+            raise RuntimeError("or_engine_step failed")
+        return np.array([[out[i].tick, out[i].fired, out[i].sent, out[i].messages,
+                          out[i].received, out[i].crashed, out[i].pending]
+                         for i in range(ticks)], dtype=np.uint64).reshape(ticks, 7)
+
+    def received(self) -> np.ndarray:
+        w = np.zeros(self.W, dtype=np.uint64)
+        lib().or_engine_read_received(self.h, w.ctypes.data, self.W)
+        return w
+
+    def crashed(self) -> np.ndarray:
+        w = np.zeros(self.W, dtype=np.uint64)
+        lib().or_engine_read_crashed(self.h, w.ctypes.data, self.W)
+        return w
+
+    @property
+    def tick(self) -> int:
+        return int(lib().or_engine_tick(self.h))
+
+
+STAT_FIELDS = ("tick", "fired", "sent", "messages", "received", "crashed", "pending")
+
+
+def covered(recv: int, n: int) -> bool:
+    """simulator.go:246-248 in float32."""
+    return bool(np.float32(recv) / np.float32(n) >= np.float32(0.99))
+
+
+def run_to_coverage(p: Params, deg, ids, sender=-1, poll=10, max_ticks=100000,
+                    failed=None):
+    """Poll every `poll` ticks like simulator.go:243-251; returns (stats rows, engine)."""
+    e = Engine(p, deg, ids)
+    if failed is not None:
+        e.set_failed(failed)
+    e.begin(sender)
+    rows = []
+    while True:
+        s = e.step(poll)
+        rows.append(s)
+        last = s[-1]
+        if covered(int(last[4]), p.n) or int(last[6]) == 0 or int(last[0]) >= max_ticks:
+            break
+    return np.concatenate(rows), e
+
+
+def refsim(p: Params, rng_seed: int, max_ms: int = 10_000_000) -> RefsimResult:
+    r = RefsimResult()
+    rc = lib().or_refsim(C.byref(p), rng_seed, max_ms, C.byref(r))
+    if rc != 0:
+        raise RuntimeError(f"or_refsim failed: {rc}")
+    return r
+
+
+def refsim_broadcast(p: Params, deg, ids, rng_seed: int, max_ms: int = 10_000_000):
+    deg = np.ascontiguousarray(deg, dtype=np.uint8)
+    ids = np.ascontiguousarray(ids, dtype=np.uint32)
+    r = RefsimResult()
+    rc = lib().or_refsim_broadcast(C.byref(p), deg.ctypes.data, ids.ctypes.data,
+                                   ids.shape[1], rng_seed, max_ms, C.byref(r))
+    if rc != 0:
+        raise RuntimeError(f"or_refsim_broadcast failed: {rc}")
+    return r

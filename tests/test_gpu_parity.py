@@ -1,0 +1,216 @@
+"""Parity of the HIP engine (through the C ABI) against the CPU restatement.
+
+Bar: bit-exact -- per-tick counters and the per-tick received bitset (and the
+crashed bitset) must equal the oracle's on the same injected peer table and
+keyed Philox decisions; the GPU overlay must produce the oracle's table.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CASES = ["a_n100_tick", "b_n1000_default", "c_n4133_hop", "d_n10000_crash"]
+
+
+@pytest.fixture(scope="module")
+def gs():
+    import gossip_simulator_amd as gs
+    gs.load()  # fails loudly if the in-tree library is missing
+    return gs
+
+
+def cfg_from(gs, kw):
+    return gs.Config(n=kw["n"], fanout=kw["fanout"], fanin=kw["fanin"], delaylow=kw["delay_low"],
+                     delayhigh=kw["delay_high"], droprate=kw["drop_rate"],
+                     crashrate=kw["crash_rate"], seed=kw["seed"], trial=kw["trial"])
+
+
+def sha(words):
+    return hashlib.sha256(np.ascontiguousarray(words, dtype="<u8").tobytes()).hexdigest()
+
+
+def masked(deg, ids):
+    m = np.arange(ids.shape[1])[None, :] < deg[:, None]
+    return np.where(m, ids, 0).astype(np.uint32)
+
+
+def load_case(name):
+    with open(os.path.join(GOLDEN, f"{name}.json")) as f:
+        doc = json.load(f)
+    z = np.load(os.path.join(GOLDEN, f"{name}_peers.npz"))
+    return doc, z["deg"], z["ids"]
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_golden_broadcast_per_tick(gs, name):
+    doc, deg, ids = load_case(name)
+    with gs.Simulator(cfg_from(gs, doc["params"])) as sim:
+        sim.load_peers(deg, ids)
+        sim.broadcast_begin(-1)
+        for i, tk in enumerate(doc["ticks"]):
+            s = sim.step(1)[0]
+            assert [int(x) for x in s] == tk["stats"], f"tick {i + 1} stats differ"
+            assert sha(sim.received()) == tk["received_sha256"], f"tick {i + 1} received set differs"
+        assert sha(sim.crashed()) == doc["crashed_sha256_final"]
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_golden_overlay(gs, name):
+    doc, deg, ids = load_case(name)
+    with gs.Simulator(cfg_from(gs, doc["params"])) as sim:
+        wins, final = sim.build_overlay()
+        assert final == doc["overlay_final_tick"]
+        assert [list(w) for w in wins] == doc["overlay_windows"]
+        gdeg, gids = sim.read_peers()
+        assert np.array_equal(gdeg, deg)
+        assert np.array_equal(masked(gdeg, gids)[:, :ids.shape[1]], ids)
+
+
+def random_table(n, stride, deg_lo, deg_hi, seed):
+    rng = np.random.default_rng(seed)
+    deg = rng.integers(deg_lo, deg_hi + 1, size=n).astype(np.uint8)
+    ids = rng.integers(0, n, size=(n, stride)).astype(np.uint32)
+    return deg, ids
+
+
+def run_both(gs, oracle, kw, deg, ids, sender=-1, ticks=400, failed=None, chunk=1):
+    p = oracle.make_params(**kw)
+    e = oracle.Engine(p, deg, ids)
+    if failed is not None:
+        e.set_failed(failed)
+    e.begin(sender)
+    with gs.Simulator(cfg_from(gs, kw)) as sim:
+        sim.load_peers(deg, ids)
+        if failed is not None:
+            sim.set_failed(failed)
+        sim.broadcast_begin(sender)
+        done = 0
+        while done < ticks:
+            a = e.step(chunk)
+            b = sim.step(chunk)
+            assert np.array_equal(a, b), f"stats differ after tick {done + chunk}:\n{a}\n{b}"
+            assert np.array_equal(e.received(), sim.received()), f"received differs at {done + chunk}"
+            done += chunk
+            if int(a[-1][6]) == 0:
+                break
+        assert np.array_equal(e.crashed(), sim.crashed())
+        return a[-1]
+
+
+BASE = dict(fanout=5, fanin=6, delay_low=10, delay_high=20, drop_rate=0.1, crash_rate=0.001,
+            seed=11, trial=0)
+
+
+@pytest.mark.parametrize("kw,stride,dlo,dhi", [
+    (dict(BASE, n=1), 2, 1, 2),                                   # self-friend
+    (dict(BASE, n=2, crash_rate=0.3), 3, 0, 3),                   # tiny, zero-degree nodes
+    (dict(BASE, n=777, delay_low=1, delay_high=2), 6, 0, 6),      # hop mode, ragged words
+    (dict(BASE, n=5000, fanout=18, fanin=19), 19, 18, 19),        # C4-like wide rows
+    (dict(BASE, n=9000, drop_rate=0.0, crash_rate=0.0), 6, 5, 6), # flood, no loss
+    (dict(BASE, n=9000, drop_rate=0.29, crash_rate=0.57), 6, 5, 6),  # heavy crash (kc=56)
+    (dict(BASE, n=4097, delay_low=0, delay_high=3), 4, 1, 4),     # 0-ms delays clamp to 1 tick
+    (dict(BASE, n=20000, drop_rate=1.0), 6, 5, 6),                # every send dropped
+    (dict(BASE, n=12345, delay_low=3, delay_high=40, trial=9), 8, 2, 8),  # long ring
+])
+def test_random_tables_bit_exact(gs, oracle, kw, stride, dlo, dhi):
+    deg, ids = random_table(kw["n"], stride, dlo, dhi, seed=kw["n"])
+    run_both(gs, oracle, kw, deg, ids)
+
+
+def test_sender_argument_and_multi_tick_steps(gs, oracle):
+    kw = dict(BASE, n=3000, crash_rate=0.02)
+    deg, ids = random_table(3000, 6, 5, 6, seed=5)
+    run_both(gs, oracle, kw, deg, ids, sender=1234, chunk=7)
+
+
+def test_failed_mask_flood_and_crash(gs, oracle):
+    n = 6000
+    rng = np.random.default_rng(2)
+    bits = rng.random(n) < 0.05
+    words = np.zeros((n + 63) // 64, dtype=np.uint64)
+    for v in np.nonzero(bits)[0]:
+        words[v >> 6] |= np.uint64(1) << np.uint64(v & 63)
+    deg, ids = random_table(n, 6, 5, 6, seed=3)
+    run_both(gs, oracle, dict(BASE, n=n, crash_rate=0.0), deg, ids, failed=words)
+    run_both(gs, oracle, dict(BASE, n=n, crash_rate=0.03), deg, ids, failed=words)
+
+
+def test_ring_graph_bfs_layers(gs):
+    """drop 0, crash 0, constant delay d: hop h reaches exactly ring distance h."""
+    n, d = 1001, 3
+    deg = np.full(n, 2, np.uint8)
+    ids = np.stack([(np.arange(n) - 1) % n, (np.arange(n) + 1) % n], 1).astype(np.uint32)
+    kw = dict(BASE, n=n, delay_low=d, delay_high=d + 1, drop_rate=0.0, crash_rate=0.0)
+    with gs.Simulator(cfg_from(gs, kw)) as sim:
+        sim.load_peers(deg, ids)
+        s0 = 17
+        sim.broadcast_begin(s0)
+        for h in range(1, 30):
+            sim.step(d)
+            recv = np.unpackbits(sim.received().view(np.uint8), bitorder="little")[:n]
+            dist = np.minimum((np.arange(n) - s0) % n, (s0 - np.arange(n)) % n)
+            # the sender itself is received only via the echo at hop 2
+            want = (dist <= h) & (dist >= 1) | ((dist == 0) & (h >= 2))
+            assert np.array_equal(recv.astype(bool), want), f"hop {h}"
+
+
+def test_overlay_c2_size_matches_oracle(gs, oracle):
+    """Config C2 shape (fanout 3, fanin 6) at n=2e5: GPU overlay == oracle overlay."""
+    kw = dict(n=200000, fanout=3, fanin=6, delay_low=10, delay_high=20, drop_rate=0.1,
+              crash_rate=0.001, seed=1, trial=0)
+    deg, ids, wins, final = oracle.overlay(oracle.make_params(**kw))
+    with gs.Simulator(cfg_from(gs, kw)) as sim:
+        gw, gf = sim.build_overlay()
+        assert gf == final
+        assert [tuple(w) for w in gw] == [tuple(w) for w in wins]
+        gdeg, gids = sim.read_peers()
+        assert np.array_equal(gdeg, deg)
+        assert np.array_equal(masked(gdeg, gids), masked(deg, ids))
+        # invariant simulator.go:68,80,96: fanout <= len(friends) <= fanin
+        assert gdeg.min() >= 3 and gdeg.max() <= 6
+
+
+@pytest.mark.parametrize("mode", ["tick", "hop"])
+def test_c2_full_size_bit_exact(gs, oracle, mode):
+    """Config C2: N=1e6, fanout 3 (fanin 6); GPU overlay + broadcast vs oracle, per poll."""
+    kw = dict(n=1_000_000, fanout=3, fanin=6, delay_low=10, delay_high=20 if mode == "tick" else 11,
+              drop_rate=0.1, crash_rate=0.001, seed=1, trial=0)
+    p = oracle.make_params(**kw)
+    deg, ids, _, _ = oracle.overlay(p)
+    e = oracle.Engine(p, deg, ids)
+    e.begin(-1)
+    with gs.Simulator(cfg_from(gs, kw)) as sim:
+        sim.build_overlay()
+        gdeg, gids = sim.read_peers()
+        assert np.array_equal(gdeg, deg) and np.array_equal(masked(gdeg, gids), masked(deg, ids))
+        sim.broadcast_begin(-1)
+        while True:
+            a = e.step(10)
+            b = sim.step(10)
+            assert np.array_equal(a, b)
+            if gs.covered(int(a[-1][4]), p.n) or int(a[-1][6]) == 0:
+                break
+        assert np.array_equal(e.received(), sim.received())
+        assert np.array_equal(e.crashed(), sim.crashed())
+
+
+def test_run_polls_like_reference(gs, oracle):
+    kw = dict(BASE, n=50000, seed=1)
+    p = oracle.make_params(**kw)
+    deg, ids, _, _ = oracle.overlay(p)
+    rows, _ = oracle.run_to_coverage(p, deg, ids)
+    with gs.Simulator(cfg_from(gs, kw)) as sim:
+        sim.load_peers(deg, ids)
+        sim.broadcast_begin(-1)
+        polls, status = sim.run(poll=10)
+        assert status == 0  # GS_RUN_COVERED
+        assert int(polls[-1][0]) == int(rows[-1][0])
+        assert int(polls[-1][4]) == int(rows[-1][4])
+        assert int(polls[:, 3].sum()) == int(rows[:, 3].sum())
