@@ -24,7 +24,7 @@ EXPORTS = (
     "gs_set_failed", "gs_broadcast_begin", "gs_step", "gs_run", "gs_totals",
     "gs_read_received", "gs_read_crashed", "gs_timing_get", "gs_format_float32",
     "gs_format_float64", "gs_format_duration", "gs_threshold", "gs_philox",
-    "gs_set_flags", "gs_reset",
+    "gs_set_flags", "gs_reset", "gs_set_stream", "gs_frontier_export", "gs_frontier_import",
 )
 
 
@@ -47,7 +47,10 @@ class Params(C.Structure):
         ("trial", C.c_uint32),
         ("device", C.c_int32),
         ("flags", C.c_uint32),
-        ("reserved_", C.c_uint32 * 7),
+        ("reserved0_", C.c_uint32),
+        ("node_lo", C.c_uint64),
+        ("node_hi", C.c_uint64),
+        ("reserved_", C.c_uint64 * 4),
     ]
 
 
@@ -104,6 +107,9 @@ def load():
         "gs_philox": ([P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)], None),
         "gs_set_flags": ([ctx, C.c_uint32], C.c_int),
         "gs_reset": ([ctx], C.c_int),
+        "gs_set_stream": ([ctx, vp], C.c_int),
+        "gs_frontier_export": ([ctx, C.c_uint64, vp, C.c_uint64, C.c_uint64], C.c_int),
+        "gs_frontier_import": ([ctx, C.c_uint64, vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -20,7 +20,8 @@ using namespace gs;
 struct gs_ctx {
   gs_params p{};
   int dev = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // where device work is issued (own, or gs_set_stream's)
+  hipStream_t own = nullptr;     // the context's own stream
   std::string err;
   DevState st{};
   uint8_t* d_deg = nullptr;
@@ -179,11 +180,28 @@ int gs_create(const gs_params* params, gs_ctx** out) {
     delete c;
     return GS_EDEVICE;
   }
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return GS_EDEVICE;
   }
+  c->stream = c->own;
   DevState& s = c->st;
+  {
+    uint64_t lo = c->p.node_lo, hi = c->p.node_hi;
+    if (lo == 0 && hi == 0) hi = c->p.n;
+    if (lo > hi || hi > c->p.n || ((lo & 4095) && lo != c->p.n) ||
+        ((hi & 4095) && hi != c->p.n)) {
+      fprintf(stderr, "gs_create: node range [%llu, %llu) must be 4096-aligned within [0, n]\n",
+              (unsigned long long)lo, (unsigned long long)hi);
+      gs_destroy(c);
+      return GS_EINVAL;
+    }
+    s.lo = (uint32_t)lo;
+    s.hi = (uint32_t)hi;
+    s.chunk_lo = (uint32_t)(lo >> kChunkNodesLog);
+    s.chunk_hi = (uint32_t)((hi + (1ull << kChunkNodesLog) - 1) >> kChunkNodesLog);
+    s.sharded = !(lo == 0 && hi == c->p.n);
+  }
   s.n = c->p.n;
   s.W = (s.n + 63) / 64;
   s.C = (uint32_t)((s.n + (1ull << kChunkNodesLog) - 1) >> kChunkNodesLog);
@@ -245,7 +263,7 @@ void gs_destroy(gs_ctx* c) {
   if (c->d_cnt) (void)hipFree(c->d_cnt);
   if (c->d_failed) (void)hipFree(c->d_failed);
   if (c->h_stats) (void)hipHostFree(c->h_stats);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
 }
 
@@ -362,11 +380,36 @@ int gs_broadcast_begin(gs_ctx* c, int64_t sender) {
                           : (uint64_t)sender;
   if (s >= c->p.n) return fail(c, GS_EINVAL, "sender out of range");
   CK(c, hipSetDevice(c->dev));
-  CK(c, launch_schedule_one(c->st, (uint32_t)s, 0, c->stream));
+  const bool mine = s >= c->st.lo && s < c->st.hi;  // only the sender's owner schedules it
+  if (mine) CK(c, launch_schedule_one(c->st, (uint32_t)s, 0, c->stream));
   CK(c, hipStreamSynchronize(c->stream));
   c->t = 0;
-  c->pending = 1;
+  c->pending = mine ? 1 : 0;
   c->begun = true;
+  return GS_OK;
+}
+
+int gs_set_stream(gs_ctx* c, void* hip_stream) {
+  if (!c) return GS_EINVAL;
+  CK(c, hipStreamSynchronize(c->stream));
+  c->stream = hip_stream ? (hipStream_t)hip_stream : c->own;
+  return GS_OK;
+}
+
+int gs_frontier_export(gs_ctx* c, uint64_t tick, void* dst, uint64_t word_lo, uint64_t nwords) {
+  if (!c || !dst || word_lo + nwords > c->st.W) return fail(c, GS_EINVAL, "bad frontier range");
+  if (!nwords) return GS_OK;
+  const size_t slot = (size_t)(tick % c->st.R);
+  CK(c, hipMemcpyAsync(dst, c->st.ring + slot * c->st.W + word_lo, nwords * 8,
+                       hipMemcpyDeviceToDevice, c->stream));
+  return GS_OK;
+}
+
+int gs_frontier_import(gs_ctx* c, uint64_t tick, const void* src) {
+  if (!c || !src) return fail(c, GS_EINVAL, "bad frontier source");
+  const size_t slot = (size_t)(tick % c->st.R);
+  CK(c, hipMemcpyAsync(c->st.ring + slot * c->st.W, src, c->st.W * 8, hipMemcpyDeviceToDevice,
+                       c->stream));
   return GS_OK;
 }
 

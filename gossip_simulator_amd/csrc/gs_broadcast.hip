@@ -91,7 +91,7 @@ __device__ __forceinline__ void process_chunk(const DevState& st, uint32_t t, ui
   if (MODE != MODE_COUNT) {
     if (bits) *wp = 0ull;                                 // slot reused at t + R
     if (lane == 0) st.cflag[(size_t)slot * st.C + chunk] = 0u;
-    c.v[ST_FIRED] += __popcll(bits);
+    if (chunk >= st.chunk_lo && chunk < st.chunk_hi) c.v[ST_FIRED] += __popcll(bits);
   }
   const uint32_t S = st.stride;
   const uint32_t node0 = (chunk << kChunkNodesLog) + (lane << 6);
@@ -123,6 +123,7 @@ __device__ __forceinline__ void process_chunk(const DevState& st, uint32_t t, ui
       const u32x4 r = philox(v, t, j >> 2, c3drop, st.key.k0, st.key.k1);
       if ((int32_t)uniform(lane_of(r, j & 3), 100u) < st.kd) continue;
       const uint32_t u = st.ids[(size_t)v * S + j];        // GlobalView[id] (:145)
+      if (u < st.lo || u >= st.hi) continue;               // another shard's target
       if (MODE == MODE_FLOOD) {
         c.v[ST_SENT]++;
         const unsigned long long bit = 1ull << (u & 63);
@@ -161,13 +162,18 @@ __global__ __launch_bounds__(kTickBlock) void k_tick(const DevState st, uint32_t
     for (uint32_t i = 0; i < kShards; ++i) s_pref[i + 1] += s_pref[i];
   }
   __syncthreads();
-  const uint32_t total = s_pref[kShards];
+  // Sharded runs visit every chunk: the slot was overwritten by the frontier
+  // all-gather, so this rank's active-chunk list does not cover it.
+  const uint32_t total = st.sharded ? st.C : s_pref[kShards];
   Counters c{};
   const uint32_t wpb = kTickBlock / kWave;
   for (uint32_t g = blockIdx.x * wpb + wid; g < total; g += gridDim.x * wpb) {
-    uint32_t sh = 0;
-    while (s_pref[sh + 1] <= g) ++sh;
-    const uint32_t chunk = st.clist[((size_t)slot * kShards + sh) * st.CS + (g - s_pref[sh])];
+    uint32_t chunk = g;
+    if (!st.sharded) {
+      uint32_t sh = 0;
+      while (s_pref[sh + 1] <= g) ++sh;
+      chunk = st.clist[((size_t)slot * kShards + sh) * st.CS + (g - s_pref[sh])];
+    }
     process_chunk<MODE, CHECK_CRASHED>(st, t, slot, chunk, s_list[wid], lane, c);
   }
   // wave -> LDS -> one atomic per block and field

@@ -64,6 +64,9 @@ struct DevState {
   uint32_t delay_span;
   int32_t kd, kc;
   int32_t check_crashed;   // FLOOD mode: a pre-failed mask is present
+  int32_t sharded;         // node-range sharding: visit every chunk (the slot was all-gathered)
+  uint32_t lo, hi;         // owned node range
+  uint32_t chunk_lo, chunk_hi;  // owned chunks [lo/4096, ceil(hi/4096))
   Key key;
 };
 

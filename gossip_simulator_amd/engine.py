@@ -51,10 +51,12 @@ def _stats_array(buf, k: int) -> np.ndarray:
 class Simulator:
     """One broadcast on one GPU (a gs_ctx)."""
 
-    def __init__(self, cfg: Config):
+    def __init__(self, cfg: Config, node_range=None):
         self.cfg = cfg
         self.L = _lib.load()
         self._p = cfg.to_params()
+        if node_range is not None:
+            self._p.node_lo, self._p.node_hi = int(node_range[0]), int(node_range[1])
         h = C.c_void_p()
         rc = self.L.gs_create(C.byref(self._p), C.byref(h))
         if rc != 0:
@@ -157,6 +159,17 @@ class Simulator:
 
     def reset(self):
         self._check(self.L.gs_reset(self.h), "gs_reset")
+
+    # -- node-range sharding hooks ---------------------------------------
+    def set_stream(self, hip_stream: int | None):
+        self._check(self.L.gs_set_stream(self.h, hip_stream), "gs_set_stream")
+
+    def frontier_export(self, tick: int, dst_ptr: int, word_lo: int, nwords: int):
+        self._check(self.L.gs_frontier_export(self.h, tick, dst_ptr, word_lo, nwords),
+                    "gs_frontier_export")
+
+    def frontier_import(self, tick: int, src_ptr: int):
+        self._check(self.L.gs_frontier_import(self.h, tick, src_ptr), "gs_frontier_import")
 
     def timing(self) -> dict:
         t = Timing()

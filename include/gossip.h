@@ -54,7 +54,11 @@ typedef struct gs_params {
   uint32_t trial;      /* Philox counter word 3, low 24 bits                  */
   int32_t device;      /* HIP device ordinal                                  */
   uint32_t flags;      /* GS_FLAG_*                                           */
-  uint32_t reserved_[7];
+  uint32_t reserved0_;
+  /* Node-range sharding (config C4): this context owns nodes [node_lo,
+   * node_hi); both multiples of 4096 except node_hi == n.  0,0 = all nodes. */
+  uint64_t node_lo, node_hi;
+  uint64_t reserved_[4];
 } gs_params;
 
 /* One tick (1 ms) of the broadcast phase; the reference exposes these as the
@@ -146,6 +150,19 @@ int gs_set_flags(gs_ctx* ctx, uint32_t flags);
  * the fire ring and the counters; keeps the peer table and failure mask
  * (a fresh process in the reference, simulator.go:207). */
 int gs_reset(gs_ctx* ctx);
+
+/* ---- node-range sharding hooks (no reference counterpart: the reference
+ * runs every node as a goroutine of one process, simulator.go:214-217) ---- */
+/* Run all later device work on `hip_stream` (a hipStream_t, e.g. the stream
+ * RCCL collectives are issued on); NULL restores the context's own stream. */
+int gs_set_stream(gs_ctx* ctx, void* hip_stream);
+/* Enqueue a copy of words [word_lo, word_lo+nwords) of the fire slot that
+ * tick `tick` will process into the device buffer dst (no host sync). */
+int gs_frontier_export(gs_ctx* ctx, uint64_t tick, void* dst, uint64_t word_lo,
+                       uint64_t nwords);
+/* Enqueue an overwrite of that fire slot with ceil(n/64) words from the
+ * device buffer src (the all-gathered global firing set; no host sync). */
+int gs_frontier_import(gs_ctx* ctx, uint64_t tick, const void* src);
 
 /* ---- host-only helpers for the reference's stdout contract ------------- */
 /* Go fmt %v of a float32 (strconv 'g', -1, 32), e.g. 99.61 or 9.9999994e-08

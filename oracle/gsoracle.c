@@ -270,6 +270,7 @@ struct or_engine {
   uint32_t* cnt;
   uint32_t* touched;
   uint64_t t, recv, crashed_cnt, pending;
+  uint64_t lo, hi; /* owned node range (node-range sharding) */
   int begun;
 };
 
@@ -286,6 +287,8 @@ or_engine* or_engine_new(const or_params* p, const uint8_t* deg,
   e->R = ring_size(p);
   e->kd = or_threshold(p->drop_rate);
   e->kc = or_threshold(p->crash_rate);
+  e->lo = 0;
+  e->hi = p->n;
   keyof(p, e->key);
   e->deg = (uint8_t*)malloc(e->n);
   e->ids = (uint32_t*)malloc(e->n * stride * sizeof(uint32_t));
@@ -332,7 +335,8 @@ int or_engine_begin(or_engine* e, int64_t sender) {
   uint64_t s = sender < 0 ? or_pick_sender(&e->p) : (uint64_t)sender;
   if (s >= e->n) return -1;
   e->t = 0;
-  schedule(e, (uint32_t)s, 0);   /* simulator.go:241; sender NOT marked received */
+  if (s >= e->lo && s < e->hi)   /* only the owner of the sender schedules it */
+    schedule(e, (uint32_t)s, 0); /* simulator.go:241; sender NOT marked received */
   e->begun = 1;
   return 0;
 }
@@ -359,7 +363,7 @@ int or_engine_step(or_engine* e, uint32_t ticks, or_tick_stats* out) {
       while (bits) {
         uint32_t v = (uint32_t)(w * 64 + (uint64_t)__builtin_ctzll(bits));
         bits &= bits - 1;
-        ++fired;
+        if (v >= e->lo && v < e->hi) ++fired;
         uint32_t d = e->deg[v];
         const uint32_t* row = e->ids + (uint64_t)v * e->stride;
         uint32_t rnd[4] = {0, 0, 0, 0};
@@ -369,8 +373,9 @@ int or_engine_step(or_engine* e, uint32_t ticks, or_tick_stats* out) {
             or_philox(ctr, e->key, rnd);
           }
           if ((int32_t)or_uniform(rnd[j & 3], 100) < e->kd) continue; /* :144,:172 */
-          ++sent;
           uint32_t u = row[j];                                         /* :145 */
+          if (u < e->lo || u >= e->hi) continue;  /* another rank's target */
+          ++sent;
           if (e->cnt[u]++ == 0) e->touched[nt++] = u;
         }
       }
@@ -425,6 +430,25 @@ int or_engine_read_crashed(const or_engine* e, uint64_t* words, size_t nwords) {
 }
 
 uint64_t or_engine_tick(const or_engine* e) { return e ? e->t : 0; }
+
+int or_engine_set_range(or_engine* e, uint64_t lo, uint64_t hi) {
+  if (!e || e->begun || lo > hi || hi > e->n) return -1;
+  e->lo = lo;
+  e->hi = hi;
+  return 0;
+}
+
+int or_engine_get_slot(const or_engine* e, uint64_t tick, uint64_t* words, size_t nwords) {
+  if (!e || nwords < e->W) return -1;
+  memcpy(words, e->ring + (tick % e->R) * e->W, e->W * 8);
+  return 0;
+}
+
+int or_engine_set_slot(or_engine* e, uint64_t tick, const uint64_t* words, size_t nwords) {
+  if (!e || nwords < e->W) return -1;
+  memcpy(e->ring + (tick % e->R) * e->W, words, e->W * 8);
+  return 0;
+}
 
 /* ======================================================================== */
 /* or_refsim: event-driven, sequential-RNG restatement (Go-like).            */

@@ -108,6 +108,14 @@ int or_engine_read_crashed(const or_engine* e, uint64_t* words, size_t nwords);
 /* Pre-failed node mask (C5 extension): words of ceil(n/64); set bits crash-stop. */
 int or_engine_set_failed(or_engine* e, const uint64_t* words, size_t nwords);
 uint64_t or_engine_tick(const or_engine* e);
+/* Node-range sharding (config C4): this engine owns nodes [lo, hi).  Every
+ * rank evaluates every firing node of the (all-gathered) fire slot with the
+ * same keyed draws, but only counts fired nodes it owns and only delivers to
+ * targets it owns, so the union over ranks equals the unsharded run. */
+int or_engine_set_range(or_engine* e, uint64_t lo, uint64_t hi);
+/* Fire-ring slot that tick `tick` will process: copy out / overwrite. */
+int or_engine_get_slot(const or_engine* e, uint64_t tick, uint64_t* words, size_t nwords);
+int or_engine_set_slot(or_engine* e, uint64_t tick, const uint64_t* words, size_t nwords);
 
 /* ---- event-driven Go-like model with a sequential RNG -------------------- */
 typedef struct or_refsim_result {

@@ -86,6 +86,9 @@ def lib():
         L.or_engine_set_failed.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.or_engine_tick.argtypes = [C.c_void_p]
         L.or_engine_tick.restype = C.c_uint64
+        L.or_engine_set_range.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64]
+        L.or_engine_get_slot.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_size_t]
+        L.or_engine_set_slot.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_size_t]
         L.or_refsim.argtypes = [P(Params), C.c_uint64, C.c_uint64, P(RefsimResult)]
         L.or_refsim_broadcast.argtypes = [P(Params), C.c_void_p, C.c_void_p, C.c_uint32,
                                           C.c_uint64, C.c_uint64, P(RefsimResult)]
@@ -185,6 +188,20 @@ class Engine:
     @property
     def tick(self) -> int:
         return int(lib().or_engine_tick(self.h))
+
+    def set_range(self, lo: int, hi: int):
+        if lib().or_engine_set_range(self.h, lo, hi) != 0:
+            raise ValueError("or_engine_set_range failed")
+
+    def get_slot(self, tick: int) -> np.ndarray:
+        w = np.zeros(self.W, dtype=np.uint64)
+        lib().or_engine_get_slot(self.h, tick, w.ctypes.data, self.W)
+        return w
+
+    def set_slot(self, tick: int, words: np.ndarray):
+        words = np.ascontiguousarray(words, dtype=np.uint64)
+        if lib().or_engine_set_slot(self.h, tick, words.ctypes.data, words.size) != 0:
+            raise ValueError("or_engine_set_slot failed")
 
 
 STAT_FIELDS = ("tick", "fired", "sent", "messages", "received", "crashed", "pending")

@@ -36,7 +36,7 @@ def test_exports_every_declared_symbol(L):
 
 def test_struct_sizes_match_header(L):
     import ctypes as C
-    assert C.sizeof(L.Params) == 8 + 4 * 4 + 8 + 8 + 8 + 4 + 4 + 4 + 7 * 4
+    assert C.sizeof(L.Params) == 8 + 4 * 4 + 8 + 8 + 8 + 4 + 4 + 4 + 4 + 8 + 8 + 4 * 8
     assert C.sizeof(L.TickStats) == 7 * 8
     assert C.sizeof(L.Window) == 3 * 8
 
