@@ -15,6 +15,7 @@ CLI_PATH = os.path.join(PKG_DIR, "bin", "gossip_sim")
 GS_OK, GS_EINVAL, GS_ELIVELOCK, GS_EREJECT, GS_ENOMEM, GS_EDEVICE, GS_EOVERFLOW = (
     0, -1, -2, -3, -4, -5, -6)
 GS_FLAG_TIMING = 1
+GS_FLAG_TICK_ENGINE = 2
 GS_RUN_COVERED, GS_RUN_QUIESCENT, GS_RUN_MAX_TICKS = 0, 1, 2
 
 # Every symbol include/gossip.h declares (checked by tests/test_abi.py).

@@ -36,6 +36,13 @@ struct gs_ctx {
   uint64_t t = 0, fired = 0, sent = 0, msgs = 0, recv = 0, crashed = 0, pending = 0;
   std::vector<hipEvent_t> ev;
   gs_timing timing{};
+  // window engine (gs_window.hip)
+  bool win = false;
+  WinState ws{};
+  void* d_win = nullptr;      // fcount + small per-window buffers
+  void* d_flist = nullptr;    // [R][nfine][16384] u16
+  size_t fcount_bytes = 0;
+  struct Buf { void* p = nullptr; size_t bytes = 0; } amsg, cmsg, fmsg, tmp;
 };
 
 namespace {
@@ -43,6 +50,75 @@ namespace {
 int fail(gs_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
   return code;
+}
+
+bool grow(gs_ctx::Buf& b, size_t bytes) {
+  if (b.bytes >= bytes) return true;
+  const size_t nb = std::max(bytes, b.bytes + b.bytes / 4);
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+  if (hipMalloc(&b.p, nb) != hipSuccess) return false;
+  b.bytes = nb;
+  return true;
+}
+
+// Window-engine buffers.  Sizes at n = 1e9, R = 20: flist 40 GB (two bytes
+// per node per ring slot), fcount 4.9 MB; message buffers grow on demand.
+int alloc_window(gs_ctx* c) {
+  const DevState& s = c->st;
+  WinState& w = c->ws;
+  w.n = s.n;
+  w.W = s.W;
+  w.nfine = (uint32_t)((s.n + kFineNodes - 1) >> kFineLog);
+  w.ncoarse = (w.nfine + 255) / 256;
+  w.R = s.R;
+  w.delay_low = s.delay_low;
+  w.delay_span = s.delay_span;
+  w.kd = s.kd;
+  w.kc = s.kc;
+  w.key = s.key;
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t units = (size_t)kMaxWindow * w.nfine + 1;
+  const size_t b_fc = al((size_t)w.R * w.nfine * 4), b_units = al(units * 8),
+               b_small = al(256 * 8) * 3 + al(257 * 4) + al(257 * 8),
+               b_fhist = al(((size_t)w.ncoarse * 256 + 1) * 8), b_fbase = al(((size_t)w.nfine + 1) * 8),
+               b_ffill = al((size_t)w.nfine * 8);
+  const size_t total = b_fc + 2 * b_units + b_small + b_fhist + b_fbase + b_ffill;
+  if (hipMalloc(&c->d_win, total) != hipSuccess)
+    return fail(c, GS_ENOMEM, "cannot allocate window-engine buffers");
+  const size_t flist = (size_t)w.R * w.nfine * kFineNodes * 2;
+  if (hipMalloc(&c->d_flist, flist) != hipSuccess)
+    return fail(c, GS_ENOMEM, "cannot allocate " + std::to_string(flist >> 20) + " MiB of fire lists");
+  char* q = (char*)c->d_win;
+  w.fcount = (uint32_t*)q; q += b_fc;
+  w.usize = (unsigned long long*)q; q += b_units;
+  w.unit_off = (unsigned long long*)q; q += b_units;
+  w.chist = (unsigned long long*)q; q += al(256 * 8);
+  w.cfill = (unsigned long long*)q; q += al(256 * 8);
+  w.cbase = (unsigned long long*)q; q += al(257 * 8);
+  w.tprefix = (uint32_t*)q;
+  q = (char*)c->d_win + b_fc + 2 * b_units + b_small;
+  w.fhist = (unsigned long long*)q; q += b_fhist;
+  w.fbase = (unsigned long long*)q; q += b_fbase;
+  w.ffill = (unsigned long long*)q; q += b_ffill;
+  w.flist = (uint16_t*)c->d_flist;
+  c->fcount_bytes = (size_t)w.R * w.nfine * 4;
+  if (hipMemsetAsync(c->d_win, 0, total, c->stream) != hipSuccess)
+    return fail(c, GS_EDEVICE, "memset of window buffers failed");
+  return GS_OK;
+}
+
+void refresh_window(gs_ctx* c) {
+  WinState& w = c->ws;
+  w.deg = c->st.deg;
+  w.ids = c->st.ids;
+  w.recv = c->st.recv;
+  w.crash = c->st.crash;
+  w.stats = c->st.stats;
+  w.err = c->d_err;
+  w.stride = c->st.stride;
+  w.stride_magic = c->st.stride_magic;
 }
 
 #define CK(c, expr)                                                                   \
@@ -74,12 +150,14 @@ void refresh_state(gs_ctx* c) {
   DevState& s = c->st;
   s.deg = c->d_deg;
   s.ids = c->d_ids;
+  if (c->win) refresh_window(c);
 }
 
 int set_stride(gs_ctx* c, uint32_t stride) {
   if (stride < 2 || stride > 255) return fail(c, GS_EINVAL, "row stride must be in [2, 255]");
   c->st.stride = stride;
   c->st.stride_magic = (uint32_t)((1ull << 32) / stride + 1);
+  if (c->win) refresh_window(c);
   return GS_OK;
 }
 
@@ -212,11 +290,17 @@ int gs_create(const gs_params* params, gs_ctx** out) {
   s.kd = gs_threshold(c->p.drop_rate);
   s.kc = gs_threshold(c->p.crash_rate);
   s.key = Key{(uint32_t)c->p.seed, (uint32_t)(c->p.seed >> 32), c->p.trial};
-  // One state allocation, 256-B aligned sub-buffers.
+  // Engine: the window engine (gs_window.hip) unless the run is node-range
+  // sharded (per-tick frontier exchange) or its ring is too long for LDS.
+  c->win = !s.sharded && s.R <= kWinMaxRing && !(c->p.flags & GS_FLAG_TICK_ENGINE);
+  // One state allocation, 256-B aligned sub-buffers; everything before
+  // `stats` is per-broadcast state that gs_reset clears.
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  const size_t b_bits = al(s.W * 8), b_ring = al((size_t)s.R * s.W * 8),
-               b_cflag = al((size_t)s.R * s.C * 4), b_clist = al((size_t)s.R * kShards * s.CS * 4),
-               b_ccount = al((size_t)s.R * kShards * kCounterStride * 4),
+  const bool tick = !c->win;
+  const size_t b_bits = al(s.W * 8), b_ring = tick ? al((size_t)s.R * s.W * 8) : 0,
+               b_cflag = tick ? al((size_t)s.R * s.C * 4) : 0,
+               b_clist = tick ? al((size_t)s.R * kShards * s.CS * 4) : 0,
+               b_ccount = tick ? al((size_t)s.R * kShards * kCounterStride * 4) : 0,
                b_stats = al((size_t)kStatSlots * kStatFields * 8);
   const size_t total = 2 * b_bits + b_ring + b_cflag + b_clist + b_ccount + b_stats + 256;
   c->state_bytes = total;
@@ -234,7 +318,7 @@ int gs_create(const gs_params* params, gs_ctx** out) {
   s.ccount = (uint32_t*)q; q += b_ccount;
   s.stats = (unsigned long long*)q; q += b_stats;
   c->d_err = (uint32_t*)q;
-  if (s.kc > 0) {
+  if (tick && s.kc > 0) {
     if (hipMalloc(&c->d_cnt, s.n * 4) != hipSuccess) {
       fprintf(stderr, "gs_create: cannot allocate arrival counters\n");
       gs_destroy(c);
@@ -242,6 +326,14 @@ int gs_create(const gs_params* params, gs_ctx** out) {
     }
   }
   s.cnt = c->d_cnt;
+  if (c->win) {
+    rc = alloc_window(c);
+    if (rc) {
+      fprintf(stderr, "gs_create: %s\n", c->err.c_str());
+      gs_destroy(c);
+      return rc;
+    }
+  }
   if (hipMemsetAsync(c->d_state, 0, total, c->stream) != hipSuccess ||
       (c->d_cnt && hipMemsetAsync(c->d_cnt, 0, s.n * 4, c->stream) != hipSuccess) ||
       hipHostMalloc((void**)&c->h_stats, (size_t)kStatSlots * kStatFields * 8) != hipSuccess ||
@@ -262,6 +354,10 @@ void gs_destroy(gs_ctx* c) {
   if (c->d_state) (void)hipFree(c->d_state);
   if (c->d_cnt) (void)hipFree(c->d_cnt);
   if (c->d_failed) (void)hipFree(c->d_failed);
+  if (c->d_win) (void)hipFree(c->d_win);
+  if (c->d_flist) (void)hipFree(c->d_flist);
+  for (gs_ctx::Buf* b : {&c->amsg, &c->cmsg, &c->fmsg, &c->tmp})
+    if (b->p) (void)hipFree(b->p);
   if (c->h_stats) (void)hipHostFree(c->h_stats);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
@@ -381,7 +477,8 @@ int gs_broadcast_begin(gs_ctx* c, int64_t sender) {
   if (s >= c->p.n) return fail(c, GS_EINVAL, "sender out of range");
   CK(c, hipSetDevice(c->dev));
   const bool mine = s >= c->st.lo && s < c->st.hi;  // only the sender's owner schedules it
-  if (mine) CK(c, launch_schedule_one(c->st, (uint32_t)s, 0, c->stream));
+  if (mine && c->win) CK(c, win_schedule_one(c->ws, (uint32_t)s, 0, c->stream));
+  else if (mine) CK(c, launch_schedule_one(c->st, (uint32_t)s, 0, c->stream));
   CK(c, hipStreamSynchronize(c->stream));
   c->t = 0;
   c->pending = mine ? 1 : 0;
@@ -413,6 +510,85 @@ int gs_frontier_import(gs_ctx* c, uint64_t tick, const void* src) {
   return GS_OK;
 }
 
+// Window engine: ticks [t0, t0 + n) as windows of <= min(max(delaylow,1),16)
+// ticks (gs_window.hip).  One host sync per window reads its task count.
+static int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing) {
+  WinState& w = c->ws;
+  const uint32_t Lmax = std::min<uint32_t>(std::max<int32_t>(c->p.delay_low, 1), kMaxWindow);
+  uint32_t done = 0, widx = 0;
+  std::vector<std::pair<uint32_t, uint32_t>> evs;
+  while (done < n) {
+    const uint32_t L = std::min(Lmax, n - done);
+    const uint32_t t = (uint32_t)(t0 + done);
+    CK(c, win_units(w, t, L, c->stream));
+    size_t need = 0;
+    CK(c, win_scan_units(w, L, nullptr, need, c->stream));
+    if (!grow(c->tmp, need)) return fail(c, GS_ENOMEM, "cannot allocate scan scratch");
+    need = c->tmp.bytes;
+    CK(c, win_scan_units(w, L, c->tmp.p, need, c->stream));
+    unsigned long long T = 0;
+    CK(c, hipMemcpyAsync(&T, w.unit_off + (size_t)L * w.nfine, 8, hipMemcpyDeviceToHost, c->stream));
+    CK(c, hipStreamSynchronize(c->stream));
+    if (!grow(c->amsg, T * 4 + 16) || !grow(c->cmsg, T * 4 + 16) || !grow(c->fmsg, T * 4 + 16))
+      return fail(c, GS_ENOMEM, "cannot allocate " + std::to_string(T) + " window messages");
+    w.amsg = (uint32_t*)c->amsg.p;
+    w.cmsg = (uint32_t*)c->cmsg.p;
+    w.fmsg = (uint32_t*)c->fmsg.p;
+    hipEvent_t* e = timing ? &c->ev[(size_t)widx * 3] : nullptr;
+    if (e) CK(c, hipEventRecord(e[0], c->stream));
+    if (T) {
+      CK(c, hipMemsetAsync(w.chist, 0, 256 * 8, c->stream));
+      CK(c, win_expand(w, t, L, c->stream, T));
+    }
+    // the window's fire lists are consumed: later ticks t + R may reuse the slots
+    const uint32_t s0 = t % w.R;
+    const uint32_t first = std::min(L, w.R - s0);
+    CK(c, hipMemsetAsync(w.fcount + (size_t)s0 * w.nfine, 0, (size_t)first * w.nfine * 4, c->stream));
+    if (first < L) CK(c, hipMemsetAsync(w.fcount, 0, (size_t)(L - first) * w.nfine * 4, c->stream));
+    if (T) {
+      CK(c, win_coarse_scan(w, c->stream));
+      CK(c, win_part1(w, T, L, c->stream));
+      CK(c, hipMemsetAsync(w.fhist, 0, ((size_t)w.ncoarse * 256 + 1) * 8, c->stream));
+      CK(c, hipMemsetAsync(w.ffill, 0, (size_t)w.nfine * 8, c->stream));
+      CK(c, win_part2(w, T, false, c->stream));
+      need = 0;
+      CK(c, win_scan_fine(w, nullptr, need, c->stream));
+      if (!grow(c->tmp, need)) return fail(c, GS_ENOMEM, "cannot allocate scan scratch");
+      need = c->tmp.bytes;
+      CK(c, win_scan_fine(w, c->tmp.p, need, c->stream));
+      CK(c, win_part2(w, T, true, c->stream));
+      if (e) CK(c, hipEventRecord(e[1], c->stream));
+      CK(c, win_resolve(w, t, L, c->stream));
+    } else if (e) {
+      CK(c, hipEventRecord(e[1], c->stream));
+    }
+    if (e) {
+      CK(c, hipEventRecord(e[2], c->stream));
+      evs.emplace_back(widx * 3, T ? 1u : 0u);
+    }
+    ++widx;
+    done += L;
+  }
+  if (timing) {
+    CK(c, hipStreamSynchronize(c->stream));
+    for (auto& pr : evs) {
+      hipEvent_t* e = &c->ev[pr.first];
+      float ms = 0;
+      CK(c, hipEventElapsedTime(&ms, e[0], e[1]));
+      c->timing.deliver_ms += ms;
+      CK(c, hipEventElapsedTime(&ms, e[1], e[2]));
+      c->timing.resolve_ms += ms;
+      c->timing.deliver_launches += pr.second;
+      c->timing.resolve_launches += pr.second;
+    }
+  }
+  uint32_t err = 0;
+  CK(c, hipMemcpyAsync(&err, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+  CK(c, hipStreamSynchronize(c->stream));
+  if (err & 4) return fail(c, GS_EOVERFLOW, "more than 65535 arrivals at one node in one tick");
+  return GS_OK;
+}
+
 int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
   if (!c) return GS_EINVAL;
   if (!c->begun) return fail(c, GS_EINVAL, "gs_broadcast_begin first");
@@ -430,13 +606,17 @@ int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
                          c->stream));
     if (first < batch)
       CK(c, hipMemsetAsync(c->st.stats, 0, (size_t)(batch - first) * kStatFields * 8, c->stream));
-    const uint32_t nev = timing ? batch * (flood ? 2 : 4) : 0;
+    const uint32_t nev = timing ? batch * (c->win ? 3 : flood ? 2 : 4) : 0;
     while (c->ev.size() < nev) {
       hipEvent_t e;
       CK(c, hipEventCreate(&e));
       c->ev.push_back(e);
     }
-    for (uint32_t i = 0; i < batch; ++i) {
+    if (c->win) {
+      int rc = run_windows(c, t0, batch, timing);
+      if (rc) return rc;
+    }
+    for (uint32_t i = 0; i < batch && !c->win; ++i) {
       const uint32_t tt = (uint32_t)(t0 + i);
       hipEvent_t* e = timing ? &c->ev[(size_t)i * (flood ? 2 : 4)] : nullptr;
       if (e) CK(c, hipEventRecord(e[0], c->stream));
@@ -455,7 +635,7 @@ int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
       CK(c, hipMemcpyAsync(c->h_stats, c->st.stats, (size_t)(batch - first) * kStatFields * 8,
                            hipMemcpyDeviceToHost, c->stream));
     CK(c, hipStreamSynchronize(c->stream));
-    if (timing) {
+    if (timing && !c->win) {
       for (uint32_t i = 0; i < batch; ++i) {
         hipEvent_t* e = &c->ev[(size_t)i * (flood ? 2 : 4)];
         float ms = 0;
@@ -556,6 +736,7 @@ int gs_reset(gs_ctx* c) {
   // everything in the state block except the stats ring and error word
   CK(c, hipMemsetAsync(c->d_state, 0, (char*)c->st.stats - (char*)c->d_state, c->stream));
   if (c->d_cnt) CK(c, hipMemsetAsync(c->d_cnt, 0, c->p.n * 4, c->stream));
+  if (c->win) CK(c, hipMemsetAsync(c->ws.fcount, 0, c->fcount_bytes, c->stream));
   if (c->failed)
     CK(c, hipMemcpyAsync(c->st.crash, c->d_failed, c->st.W * 8, hipMemcpyDeviceToDevice, c->stream));
   CK(c, hipStreamSynchronize(c->stream));

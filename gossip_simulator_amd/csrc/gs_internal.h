@@ -70,6 +70,58 @@ struct DevState {
   Key key;
 };
 
+// ---- window engine (gs_window.hip) --------------------------------------
+// Fires scheduled at tick t land at t + off with off >= max(delaylow, 1), so
+// the firing sets of the next L = min(max(delaylow,1), 16) ticks are known
+// before any of them is processed: a WINDOW of L ticks is expanded,
+// partitioned by target bucket and resolved in one pass.
+constexpr uint32_t kFineLog = 14;               // 16384 nodes per fine bucket
+constexpr uint32_t kFineNodes = 1u << kFineLog;
+constexpr uint32_t kCoarseShift = kFineLog + 8; // 256 fine buckets per coarse bucket
+constexpr uint32_t kMaxWindow = 16;             // tick offset in 4 bits
+constexpr uint32_t kWinMaxRing = 256;
+constexpr uint32_t kEmptyMsg = 0xFFFFFFFFu;
+constexpr uint32_t kPartTile = 4096;            // messages per partition tile
+
+struct WinState {
+  const uint8_t* deg;
+  const uint32_t* ids;
+  unsigned long long* recv;
+  unsigned long long* crash;
+  unsigned long long* stats;
+  uint32_t* err;
+  uint32_t* fcount;              // [R][nfine] fire-list lengths
+  uint16_t* flist;               // [R][nfine][16384] local ids of firing nodes
+  unsigned long long* usize;     // [L*nfine + 1] tasks per (tick, bucket) unit
+  unsigned long long* unit_off;  // [L*nfine + 1] exclusive scan of usize
+  uint32_t* amsg;                // expand output, one slot per task (kEmptyMsg = none)
+  uint32_t* cmsg;                // coarse-partitioned: u_in_coarse | k << 22
+  uint32_t* fmsg;                // fine-partitioned:   u_in_fine   | k << 14
+  unsigned long long* chist;     // [256] coarse counts
+  unsigned long long* cbase;     // [257] coarse offsets
+  unsigned long long* cfill;     // [256]
+  uint32_t* tprefix;             // [257] partition tiles per coarse bucket (prefix)
+  unsigned long long* fhist;     // [ncoarse*256 + 1] fine counts
+  unsigned long long* fbase;     // [nfine + 1] fine offsets
+  unsigned long long* ffill;     // [nfine]
+  uint64_t n, W;
+  uint32_t nfine, ncoarse, R, stride, stride_magic;
+  int32_t delay_low;
+  uint32_t delay_span;
+  int32_t kd, kc;
+  Key key;
+};
+
+hipError_t win_units(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
+hipError_t win_scan_units(const WinState& w, uint32_t L, void* tmp, size_t& tmp_bytes, hipStream_t s);
+hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s, uint64_t T);
+hipError_t win_coarse_scan(const WinState& w, hipStream_t s);
+hipError_t win_scan_fine(const WinState& w, void* tmp, size_t& tmp_bytes, hipStream_t s);
+hipError_t win_part1(const WinState& w, uint64_t T, uint32_t L, hipStream_t s);
+hipError_t win_part2(const WinState& w, uint64_t T, bool scatter, hipStream_t s);
+hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
+hipError_t win_schedule_one(const WinState& w, uint32_t node, uint32_t tick, hipStream_t s);
+
 // Launchers (gs_broadcast.hip).
 hipError_t launch_tick(const DevState& st, uint32_t tick, int mode, hipStream_t s);
 hipError_t launch_slot_reset(const DevState& st, uint32_t slot, hipStream_t s);

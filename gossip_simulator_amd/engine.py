@@ -32,6 +32,7 @@ class Config:
     trial: int = 0
     device: int = 0
     timing: bool = False
+    engine: str = "window"  # "window" (default) or "tick" (per-tick atomic engine)
 
     def to_params(self) -> Params:
         p = Params()
@@ -39,7 +40,8 @@ class Config:
         p.delay_low, p.delay_high = self.delaylow, self.delayhigh
         p.drop_rate, p.crash_rate = self.droprate, self.crashrate
         p.seed, p.trial, p.device = self.seed, self.trial, self.device
-        p.flags = _lib.GS_FLAG_TIMING if self.timing else 0
+        p.flags = (_lib.GS_FLAG_TIMING if self.timing else 0) | \
+            (_lib.GS_FLAG_TICK_ENGINE if self.engine == "tick" else 0)
         return p
 
 
@@ -154,8 +156,9 @@ class Simulator:
         return w
 
     def set_flags(self, timing: bool):
-        self._check(self.L.gs_set_flags(self.h, _lib.GS_FLAG_TIMING if timing else 0),
-                    "gs_set_flags")
+        flags = (_lib.GS_FLAG_TIMING if timing else 0) | \
+            (_lib.GS_FLAG_TICK_ENGINE if self.cfg.engine == "tick" else 0)
+        self._check(self.L.gs_set_flags(self.h, flags), "gs_set_flags")
 
     def reset(self):
         self._check(self.L.gs_reset(self.h), "gs_reset")

@@ -40,6 +40,7 @@ enum {
 
 /* Flags (gs_params.flags). */
 #define GS_FLAG_TIMING 1u /* time every tick kernel with HIP events (gs_timing) */
+#define GS_FLAG_TICK_ENGINE 2u /* force the per-tick atomic engine (default: window engine) */
 
 /* simulator.go:11-20 (Parameters) + the additive -seed/-trial knobs. */
 typedef struct gs_params {

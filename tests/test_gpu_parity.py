@@ -19,17 +19,28 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASES = ["a_n100_tick", "b_n1000_default", "c_n4133_hop", "d_n10000_crash"]
 
 
-@pytest.fixture(scope="module")
-def gs():
-    import gossip_simulator_amd as gs
-    gs.load()  # fails loudly if the in-tree library is missing
-    return gs
+class _Engine:
+    """The package, plus which broadcast engine the Configs should select."""
+
+    def __init__(self, mod, engine):
+        self.mod, self.engine = mod, engine
+
+    def __getattr__(self, k):
+        return getattr(self.mod, k)
+
+
+@pytest.fixture(scope="module", params=["window", "tick"])
+def gs(request):
+    import gossip_simulator_amd as mod
+    mod.load()  # fails loudly if the in-tree library is missing
+    return _Engine(mod, request.param)
 
 
 def cfg_from(gs, kw):
     return gs.Config(n=kw["n"], fanout=kw["fanout"], fanin=kw["fanin"], delaylow=kw["delay_low"],
                      delayhigh=kw["delay_high"], droprate=kw["drop_rate"],
-                     crashrate=kw["crash_rate"], seed=kw["seed"], trial=kw["trial"])
+                     crashrate=kw["crash_rate"], seed=kw["seed"], trial=kw["trial"],
+                     engine=getattr(gs, "engine", "window"))
 
 
 def sha(words):
