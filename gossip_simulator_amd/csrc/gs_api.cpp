@@ -526,9 +526,10 @@ static int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing) {
     if (!grow(c->tmp, need)) return fail(c, GS_ENOMEM, "cannot allocate scan scratch");
     need = c->tmp.bytes;
     CK(c, win_scan_units(w, L, c->tmp.p, need, c->stream));
-    unsigned long long T = 0;
-    CK(c, hipMemcpyAsync(&T, w.unit_off + (size_t)L * w.nfine, 8, hipMemcpyDeviceToHost, c->stream));
+    unsigned long long Tn = 0;  // broadcasts firing in the window
+    CK(c, hipMemcpyAsync(&Tn, w.unit_off + (size_t)L * w.nfine, 8, hipMemcpyDeviceToHost, c->stream));
     CK(c, hipStreamSynchronize(c->stream));
+    const unsigned long long T = Tn * w.stride;  // friend slots = expand outputs
     if (!grow(c->amsg, T * 4 + 16) || !grow(c->cmsg, T * 4 + 16) || !grow(c->fmsg, T * 4 + 16))
       return fail(c, GS_ENOMEM, "cannot allocate " + std::to_string(T) + " window messages");
     w.amsg = (uint32_t*)c->amsg.p;
@@ -536,10 +537,7 @@ static int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing) {
     w.fmsg = (uint32_t*)c->fmsg.p;
     hipEvent_t* e = timing ? &c->ev[(size_t)widx * 3] : nullptr;
     if (e) CK(c, hipEventRecord(e[0], c->stream));
-    if (T) {
-      CK(c, hipMemsetAsync(w.chist, 0, 256 * 8, c->stream));
-      CK(c, win_expand(w, t, L, c->stream, T));
-    }
+    if (T) CK(c, win_expand(w, t, L, c->stream, Tn));
     // the window's fire lists are consumed: later ticks t + R may reuse the slots
     const uint32_t s0 = t % w.R;
     const uint32_t first = std::min(L, w.R - s0);
@@ -548,8 +546,6 @@ static int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing) {
     if (T) {
       CK(c, win_coarse_scan(w, c->stream));
       CK(c, win_part1(w, T, L, c->stream));
-      CK(c, hipMemsetAsync(w.fhist, 0, ((size_t)w.ncoarse * 256 + 1) * 8, c->stream));
-      CK(c, hipMemsetAsync(w.ffill, 0, (size_t)w.nfine * 8, c->stream));
       CK(c, win_part2(w, T, false, c->stream));
       need = 0;
       CK(c, win_scan_fine(w, nullptr, need, c->stream));

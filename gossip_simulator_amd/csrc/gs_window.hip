@@ -32,24 +32,32 @@ namespace gs {
 namespace {
 
 constexpr uint32_t kExpandBlock = 256;
-constexpr uint32_t kTasksPerWave = 1024;
 constexpr uint32_t kResolveBlock = 512;
-constexpr uint32_t kResolveMsgCap = 4096;
+constexpr uint32_t kResolveMsgCap = 8192;
 
-__global__ void k_units(const WinState w, uint32_t t0, uint32_t L, unsigned long long* usize) {
+// Units = (tick k, fine bucket f); usize = fires.  Also zeroes the window's
+// histograms (one launch instead of several memsets).
+__global__ void k_units(const WinState w, uint32_t t0, uint32_t L) {
   const uint32_t units = L * w.nfine;
-  for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u <= units; u += gridDim.x * blockDim.x) {
-    if (u == units) { usize[u] = 0; continue; }
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+  for (uint32_t u = tid; u <= units; u += nth) {
+    if (u == units) { w.usize[u] = 0; continue; }
     const uint32_t k = u / w.nfine, f = u - k * w.nfine;
     const uint32_t s = (t0 + k) % w.R;
-    usize[u] = (unsigned long long)w.fcount[(size_t)s * w.nfine + f] * w.stride;
+    w.usize[u] = w.fcount[(size_t)s * w.nfine + f];
   }
+  for (uint32_t i = tid; i < 256; i += nth) w.chist[i] = 0;
+  for (uint32_t i = tid; i <= w.ncoarse * 256; i += nth) w.fhist[i] = 0;
+  for (uint32_t i = tid; i < w.nfine; i += nth) w.ffill[i] = 0;
 }
 
-// Wave-level work: a contiguous range of kTasksPerWave tasks of the window's
-// task space; lane l walks tasks x = start + l, start + l + 64, ...
+// One lane per firing node (Node.Broadcast, simulator.go:141-147): its row is
+// read once, one Philox block gives the drop rolls of 4 friend slots, and the
+// node's `stride` output slots start at (firing index) * stride.  A wave
+// walks kNodesPerWave consecutive firing nodes of the window.
+constexpr uint32_t kNodesPerWave = 256;
 __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint32_t t0, uint32_t L,
-                                                         unsigned long long T) {
+                                                         unsigned long long Tn) {
   __shared__ uint32_t s_hist[256];
   __shared__ unsigned long long s_acc[kMaxWindow][2];
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) s_hist[i] = 0;
@@ -61,11 +69,11 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
   const uint32_t c3drop = ctr3(K_DROP, w.key.trial);
   const unsigned long long* uo = w.unit_off;
   uint32_t one_bin = 0;  // messages when there is a single coarse bucket
-  const unsigned long long nwaves = (T + kTasksPerWave - 1) / kTasksPerWave;
-  for (unsigned long long g = (unsigned long long)blockIdx.x * (kExpandBlock / 64) + wid; g < nwaves;
-       g += (unsigned long long)gridDim.x * (kExpandBlock / 64)) {
-    const unsigned long long start = g * kTasksPerWave;
-    // unit containing `start`: last u with uo[u] <= start (wave-uniform search)
+  const unsigned long long nwaves = (Tn + kNodesPerWave - 1) / kNodesPerWave;
+  for (unsigned long long gw = (unsigned long long)blockIdx.x * (kExpandBlock / 64) + wid; gw < nwaves;
+       gw += (unsigned long long)gridDim.x * (kExpandBlock / 64)) {
+    const unsigned long long start = gw * kNodesPerWave;
+    // unit holding `start`: last u with uo[u] <= start (wave-uniform search)
     uint32_t lo = 0, hi = units;
     while (lo < hi) {
       const uint32_t mid = (lo + hi + 1) >> 1;
@@ -73,10 +81,10 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
     }
     uint32_t u = lo;
     uint32_t cur_k = 0xFFFFFFFFu, sent = 0, fired = 0;
-    for (uint32_t it = 0; it < kTasksPerWave / 64; ++it) {
-      const unsigned long long x = start + it * 64 + lane;
-      if (x >= T) break;
-      while (uo[u + 1] <= x) ++u;  // skip to the unit holding x (empty units skipped)
+    for (uint32_t it = 0; it < kNodesPerWave / 64; ++it) {
+      const unsigned long long g = start + it * 64 + lane;
+      if (g >= Tn) break;
+      while (uo[u + 1] <= g) ++u;  // empty units are skipped
       const uint32_t k = u / w.nfine, f = u - k * w.nfine;
       if (k != cur_k) {
         if (cur_k != 0xFFFFFFFFu) {
@@ -85,24 +93,31 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
         }
         cur_k = k; sent = 0; fired = 0;
       }
-      const uint32_t q = (uint32_t)(x - uo[u]);
-      const uint32_t i = __umulhi(q, w.stride_magic);
-      const uint32_t j = q - i * S;
       const uint32_t t = t0 + k;
       const uint32_t s = t % w.R;
+      const uint32_t i = (uint32_t)(g - uo[u]);
       const uint32_t v = (f << kFineLog) + w.flist[((size_t)s * w.nfine + f) * kFineNodes + i];
-      uint32_t msg = kEmptyMsg;
-      if (j == 0) ++fired;
-      if (j < w.deg[v]) {
-        const u32x4 r = philox(v, t, j >> 2, c3drop, w.key.k0, w.key.k1);   // :144, :172
-        if ((int32_t)uniform(lane_of(r, j & 3), 100u) >= w.kd) {
-          msg = w.ids[(size_t)v * S + j];                                    // :145
-          ++sent;
-          if (w.ncoarse == 1) ++one_bin;
-          else atomicAdd(&s_hist[msg >> kCoarseShift], 1u);
+      const uint32_t d = w.deg[v];
+      const uint32_t* row = w.ids + (size_t)v * S;
+      uint32_t* out = w.amsg + g * S;
+      ++fired;
+      for (uint32_t jg = 0; jg * 4 < S; ++jg) {
+        u32x4 r{0, 0, 0, 0};
+        if (jg * 4 < d) r = philox(v, t, jg, c3drop, w.key.k0, w.key.k1);   // :144, :172
+#pragma unroll
+        for (uint32_t jj = 0; jj < 4; ++jj) {
+          const uint32_t j = jg * 4 + jj;
+          if (j >= S) break;
+          uint32_t msg = kEmptyMsg;
+          if (j < d && (int32_t)uniform(lane_of(r, jj), 100u) >= w.kd) {
+            msg = row[j];                                                    // :145
+            ++sent;
+            if (w.ncoarse == 1) ++one_bin;
+            else atomicAdd(&s_hist[msg >> kCoarseShift], 1u);
+          }
+          out[j] = msg;
         }
       }
-      w.amsg[x] = msg;
     }
     if (cur_k != 0xFFFFFFFFu) {
       if (sent) atomicAdd(&s_acc[cur_k][1], (unsigned long long)sent);
@@ -173,7 +188,7 @@ __global__ __launch_bounds__(256) void k_part1(const WinState w, unsigned long l
   __shared__ TileSort ts;
   __shared__ unsigned long long s_kb[kMaxWindow + 1];
   const uint32_t tid = threadIdx.x;
-  if (tid <= L) s_kb[tid] = w.unit_off[(size_t)tid * w.nfine];
+  if (tid <= L) s_kb[tid] = w.unit_off[(size_t)tid * w.nfine] * w.stride;  // tick bounds in slots
   ts.cnt[tid] = 0;
   __syncthreads();
   const unsigned long long base = (unsigned long long)blockIdx.x * kPartTile;
@@ -283,10 +298,76 @@ struct ResolveLds {
   uint32_t crash[kFineNodes / 32];
   uint32_t cnt[kFineNodes / 2];  // two u16 arrival counters per word
   uint32_t fc[kWinMaxRing];      // fire-list lengths of this bucket, per ring slot
-  uint32_t msg[kResolveMsgCap];
+  uint32_t tcnt[kMaxWindow];     // messages per tick of the window
+  uint32_t toff[kMaxWindow + 1];
   uint32_t st[kMaxWindow][4];    // msgs, recv, crash, sched per tick
   uint32_t err;
+  uint32_t msg[kResolveMsgCap];  // the bucket's messages, sorted by tick
 };
+
+// The receive case of Node.Start (simulator.go:107-123) for node `loc` of the
+// bucket with kk arrivals at tick t: ordinals 0..kk-1, keyed crash rolls.
+__device__ __forceinline__ void resolve_node(const WinState& w, ResolveLds& sm, uint32_t f,
+                                             uint32_t loc, uint32_t kk, uint32_t t, uint32_t c3crash,
+                                             uint32_t& cm, uint32_t& cr, uint32_t& cc, uint32_t& cs) {
+  const uint32_t u = (f << kFineLog) + loc, bit = 1u << (loc & 31), wi = loc >> 5;
+  bool crashed = (sm.crash[wi] & bit) != 0;
+  bool received = (sm.recv[wi] & bit) != 0;
+  u32x4 r{0, 0, 0, 0};
+  for (uint32_t i = 0; i < kk; ++i) {
+    if (crashed) break;                                          // :108
+    ++cm;                                                        // :111
+    if (w.kc > 0) {
+      if ((i & 3) == 0) r = philox(u, t, i >> 2, c3crash, w.key.k0, w.key.k1);
+      if ((int32_t)uniform(lane_of(r, i & 3), 100u) < w.kc) {   // :112-115
+        atomicOr(&sm.crash[wi], bit);
+        ++cc;
+        crashed = true;
+        break;
+      }
+    }
+    if (received) continue;                                      // :117
+    atomicOr(&sm.recv[wi], bit);                                 // :120
+    received = true;
+    ++cr;                                                        // :121
+    // Broadcast() (:122, :141-142): fire at t + off
+    const uint32_t off = fire_offset(w.delay_low, w.delay_span, draw0(w.key, K_DELAY, u, t, 0));
+    const uint32_t s = (t + off) % w.R;
+    const uint32_t pos = atomicAdd(&sm.fc[s], 1u);
+    w.flist[((size_t)s * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
+    ++cs;
+  }
+}
+
+// One tick's receipts over messages m[lo, hi): count arrivals per node, then
+// the lane whose atomicAnd takes a node's nonzero count resolves that node.
+template <class Src>
+__device__ __forceinline__ void resolve_tick(const WinState& w, ResolveLds& sm, uint32_t f,
+                                             const Src& src, uint32_t lo, uint32_t hi, uint32_t k,
+                                             bool filter, uint32_t t, uint32_t c3crash) {
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t p = lo + tid; p < hi; p += kResolveBlock) {
+    const uint32_t m = src[p];
+    if (filter && (m >> kFineLog) != k) continue;
+    const uint32_t loc = m & (kFineNodes - 1), sh = (loc & 1) * 16;
+    const uint32_t old = atomicAdd(&sm.cnt[loc >> 1], 1u << sh);
+    if (((old >> sh) & 0xFFFFu) == 0xFFFFu) sm.err = 1;
+  }
+  __syncthreads();
+  uint32_t cm = 0, cr = 0, cc = 0, cs = 0;
+  for (uint32_t p = lo + tid; p < hi; p += kResolveBlock) {
+    const uint32_t m = src[p];
+    if (filter && (m >> kFineLog) != k) continue;
+    const uint32_t loc = m & (kFineNodes - 1), sh = (loc & 1) * 16;
+    const uint32_t kk = (atomicAnd(&sm.cnt[loc >> 1], ~(0xFFFFu << sh)) >> sh) & 0xFFFFu;
+    if (kk) resolve_node(w, sm, f, loc, kk, t, c3crash, cm, cr, cc, cs);
+  }
+  if (cm) atomicAdd(&sm.st[k][0], cm);
+  if (cr) atomicAdd(&sm.st[k][1], cr);
+  if (cc) atomicAdd(&sm.st[k][2], cc);
+  if (cs) atomicAdd(&sm.st[k][3], cs);
+  __syncthreads();
+}
 
 __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
   __shared__ ResolveLds sm;
@@ -304,67 +385,33 @@ __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uin
   for (uint32_t i = tid; i < kFineNodes / 2; i += kResolveBlock) sm.cnt[i] = 0;
   for (uint32_t s = tid; s < w.R; s += kResolveBlock) sm.fc[s] = w.fcount[(size_t)s * w.nfine + f];
   if (tid < kMaxWindow * 4) (&sm.st[0][0])[tid] = 0;
+  if (tid < kMaxWindow) sm.tcnt[tid] = 0;
   if (tid == 0) sm.err = 0;
   const unsigned long long mb = w.fbase[f];
   const uint32_t M = (uint32_t)(w.fbase[f + 1] - mb);
-  const bool in_lds = M <= kResolveMsgCap;
-  if (in_lds)
-    for (uint32_t p = tid; p < M; p += kResolveBlock) sm.msg[p] = w.fmsg[mb + p];
-  __syncthreads();
-  const uint32_t* msgs = in_lds ? sm.msg : w.fmsg + mb;
+  const uint32_t* gm = w.fmsg + mb;
   const uint32_t c3crash = ctr3(K_CRASH, w.key.trial);
-  for (uint32_t k = 0; k < L; ++k) {
-    const uint32_t t = t0 + k;
-    // arrivals of tick t per node (the ordinal of each receipt is irrelevant)
-    for (uint32_t p = tid; p < M; p += kResolveBlock) {
-      const uint32_t m = msgs[p];
-      if ((m >> kFineLog) != k) continue;
-      const uint32_t loc = m & (kFineNodes - 1), sh = (loc & 1) * 16;
-      const uint32_t old = atomicAdd(&sm.cnt[loc >> 1], 1u << sh);
-      if (((old >> sh) & 0xFFFFu) == 0xFFFFu) sm.err = 1;
+  __syncthreads();
+  if (M <= kResolveMsgCap) {
+    // counting sort of the bucket's messages by tick, into LDS
+    for (uint32_t p = tid; p < M; p += kResolveBlock) atomicAdd(&sm.tcnt[gm[p] >> kFineLog], 1u);
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t a = 0;
+      for (uint32_t k = 0; k < L; ++k) { sm.toff[k] = a; a += sm.tcnt[k]; sm.tcnt[k] = 0; }
+      sm.toff[L] = a;
     }
     __syncthreads();
-    uint32_t cm = 0, cr = 0, cc = 0, cs = 0;
     for (uint32_t p = tid; p < M; p += kResolveBlock) {
-      const uint32_t m = msgs[p];
-      if ((m >> kFineLog) != k) continue;
-      const uint32_t loc = m & (kFineNodes - 1), sh = (loc & 1) * 16;
-      const uint32_t kk = (atomicAnd(&sm.cnt[loc >> 1], ~(0xFFFFu << sh)) >> sh) & 0xFFFFu;
-      if (!kk) continue;  // another lane owns this node for this tick
-      // receive case of Node.Start (simulator.go:107-123), ordinals 0..kk-1
-      const uint32_t u = node0 + loc, bit = 1u << (loc & 31), wi = loc >> 5;
-      bool crashed = (sm.crash[wi] & bit) != 0;
-      bool received = (sm.recv[wi] & bit) != 0;
-      u32x4 r{0, 0, 0, 0};
-      for (uint32_t i = 0; i < kk; ++i) {
-        if (crashed) break;                                          // :108
-        ++cm;                                                        // :111
-        if (w.kc > 0) {
-          if ((i & 3) == 0) r = philox(u, t, i >> 2, c3crash, w.key.k0, w.key.k1);
-          if ((int32_t)uniform(lane_of(r, i & 3), 100u) < w.kc) {   // :112-115
-            atomicOr(&sm.crash[wi], bit);
-            ++cc;
-            crashed = true;
-            break;
-          }
-        }
-        if (received) continue;                                      // :117
-        atomicOr(&sm.recv[wi], bit);                                 // :120
-        received = true;
-        ++cr;                                                        // :121
-        // Broadcast() (:122, :141-142): fire at t + off
-        const uint32_t off = fire_offset(w.delay_low, w.delay_span, draw0(w.key, K_DELAY, u, t, 0));
-        const uint32_t s = (t + off) % w.R;
-        const uint32_t pos = atomicAdd(&sm.fc[s], 1u);
-        w.flist[((size_t)s * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
-        ++cs;
-      }
+      const uint32_t m = gm[p], k = m >> kFineLog;
+      sm.msg[sm.toff[k] + atomicAdd(&sm.tcnt[k], 1u)] = m;
     }
-    if (cm) atomicAdd(&sm.st[k][0], cm);
-    if (cr) atomicAdd(&sm.st[k][1], cr);
-    if (cc) atomicAdd(&sm.st[k][2], cc);
-    if (cs) atomicAdd(&sm.st[k][3], cs);
     __syncthreads();
+    for (uint32_t k = 0; k < L; ++k)
+      resolve_tick(w, sm, f, sm.msg, sm.toff[k], sm.toff[k + 1], k, false, t0 + k, c3crash);
+  } else {
+    // large bucket: stream the messages from global memory once per pass
+    for (uint32_t k = 0; k < L; ++k) resolve_tick(w, sm, f, gm, 0, M, k, true, t0 + k, c3crash);
   }
   uint32_t* rw = (uint32_t*)w.recv;
   uint32_t* cw = (uint32_t*)w.crash;
@@ -392,18 +439,17 @@ __global__ void k_schedule_one_win(const WinState w, uint32_t node, uint32_t t) 
 }  // namespace
 
 hipError_t win_units(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s) {
-  const uint32_t units = L * w.nfine + 1;
+  const uint32_t units = std::max<uint32_t>(L * w.nfine + 1, w.ncoarse * 256 + 1);
   const uint32_t blocks = std::min<uint32_t>((units + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_units, dim3(blocks), dim3(256), 0, s, w, t0, L,
-                     (unsigned long long*)w.usize);
+  hipLaunchKernelGGL(k_units, dim3(blocks), dim3(256), 0, s, w, t0, L);
   return hipGetLastError();
 }
 
-hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s, uint64_t T) {
-  const uint64_t waves = (T + kTasksPerWave - 1) / kTasksPerWave;
+hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s, uint64_t Tn) {
+  const uint64_t waves = (Tn + kNodesPerWave - 1) / kNodesPerWave;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((waves + 3) / 4, 16384);
   hipLaunchKernelGGL(k_expand, dim3(blocks ? blocks : 1), dim3(kExpandBlock), 0, s, w, t0, L,
-                     (unsigned long long)T);
+                     (unsigned long long)Tn);
   return hipGetLastError();
 }
 
