@@ -42,7 +42,10 @@ struct gs_ctx {
   void* d_win = nullptr;      // fcount + small per-window buffers
   void* d_flist = nullptr;    // [R][nfine][16384] u16
   size_t fcount_bytes = 0;
-  struct Buf { void* p = nullptr; size_t bytes = 0; } amsg, cmsg, fmsg, tmp;
+  struct Buf { void* p = nullptr; size_t bytes = 0; } gmap, cmsg, fmsg, tmp;
+  unsigned long long* h_cap = nullptr;  // pinned [257] coarse region plan
+  unsigned long long* h_misc = nullptr; // pinned scratch (counts, flags)
+  uint64_t exact_redos = 0;             // windows whose partition was redone exactly
 };
 
 namespace {
@@ -96,17 +99,36 @@ int alloc_window(gs_ctx* c) {
   w.unit_off = (unsigned long long*)q; q += b_units;
   w.chist = (unsigned long long*)q; q += al(256 * 8);
   w.cfill = (unsigned long long*)q; q += al(256 * 8);
-  w.cbase = (unsigned long long*)q; q += al(257 * 8);
+  w.ccap = (unsigned long long*)q; q += al(257 * 8);
   w.tprefix = (uint32_t*)q;
   q = (char*)c->d_win + b_fc + 2 * b_units + b_small;
   w.fhist = (unsigned long long*)q; q += b_fhist;
-  w.fbase = (unsigned long long*)q; q += b_fbase;
+  w.fstart = (unsigned long long*)q; q += b_fbase;
   w.ffill = (unsigned long long*)q; q += b_ffill;
   w.flist = (uint16_t*)c->d_flist;
   c->fcount_bytes = (size_t)w.R * w.nfine * 4;
   if (hipMemsetAsync(c->d_win, 0, total, c->stream) != hipSuccess)
     return fail(c, GS_EDEVICE, "memset of window buffers failed");
+  if (hipHostMalloc((void**)&c->h_cap, 257 * 8) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_misc, 512 * 8) != hipSuccess)
+    return fail(c, GS_ENOMEM, "cannot allocate pinned window buffers");
   return GS_OK;
+}
+
+// Coarse region plan: bucket c gets its node share of the window's T friend
+// slots (a kept send is at most one slot) plus 4096, or exactly `exact[c]`.
+void plan_coarse(gs_ctx* c, uint64_t T, const unsigned long long* exact) {
+  const WinState& w = c->ws;
+  unsigned long long a = 0;
+  for (uint32_t b = 0; b < 256; ++b) {
+    c->h_cap[b] = a;
+    if (b >= w.ncoarse) continue;
+    if (exact) { a += exact[b]; continue; }
+    const uint64_t lo = (uint64_t)b << kCoarseShift;
+    const uint64_t hi = std::min<uint64_t>(w.n, lo + (1ull << kCoarseShift));
+    a += (unsigned long long)((long double)T * (long double)(hi - lo) / (long double)w.n) + 4096;
+  }
+  c->h_cap[256] = a;
 }
 
 void refresh_window(gs_ctx* c) {
@@ -155,6 +177,8 @@ void refresh_state(gs_ctx* c) {
 
 int set_stride(gs_ctx* c, uint32_t stride) {
   if (stride < 2 || stride > 255) return fail(c, GS_EINVAL, "row stride must be in [2, 255]");
+  if (c->win && stride > kWinMaxStride)
+    return fail(c, GS_EINVAL, "rows longer than 32 need GS_FLAG_TICK_ENGINE (or fanin > 32 at create)");
   c->st.stride = stride;
   c->st.stride_magic = (uint32_t)((1ull << 32) / stride + 1);
   if (c->win) refresh_window(c);
@@ -292,7 +316,8 @@ int gs_create(const gs_params* params, gs_ctx** out) {
   s.key = Key{(uint32_t)c->p.seed, (uint32_t)(c->p.seed >> 32), c->p.trial};
   // Engine: the window engine (gs_window.hip) unless the run is node-range
   // sharded (per-tick frontier exchange) or its ring is too long for LDS.
-  c->win = !s.sharded && s.R <= kWinMaxRing && !(c->p.flags & GS_FLAG_TICK_ENGINE);
+  c->win = !s.sharded && s.R <= kWinMaxRing && !(c->p.flags & GS_FLAG_TICK_ENGINE) &&
+           (uint32_t)std::max(c->p.fanout, c->p.fanin) <= kWinMaxStride;
   // One state allocation, 256-B aligned sub-buffers; everything before
   // `stats` is per-broadcast state that gs_reset clears.
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -356,8 +381,10 @@ void gs_destroy(gs_ctx* c) {
   if (c->d_failed) (void)hipFree(c->d_failed);
   if (c->d_win) (void)hipFree(c->d_win);
   if (c->d_flist) (void)hipFree(c->d_flist);
-  for (gs_ctx::Buf* b : {&c->amsg, &c->cmsg, &c->fmsg, &c->tmp})
+  for (gs_ctx::Buf* b : {&c->gmap, &c->cmsg, &c->fmsg, &c->tmp})
     if (b->p) (void)hipFree(b->p);
+  if (c->h_cap) (void)hipHostFree(c->h_cap);
+  if (c->h_misc) (void)hipHostFree(c->h_misc);
   if (c->h_stats) (void)hipHostFree(c->h_stats);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
@@ -517,47 +544,79 @@ static int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing) {
   const uint32_t Lmax = std::min<uint32_t>(std::max<int32_t>(c->p.delay_low, 1), kMaxWindow);
   uint32_t done = 0, widx = 0;
   std::vector<std::pair<uint32_t, uint32_t>> evs;
+  // Receipts per fine bucket are ~density * 16384 whatever N is; a window whose
+  // slots would overflow k_resolve's LDS message buffer on average is cut short.
+  const uint64_t slot_budget = (uint64_t)w.nfine * kWinSlotsPerBucket;
   while (done < n) {
-    const uint32_t L = std::min(Lmax, n - done);
+    const uint32_t Lw = std::min(Lmax, n - done);
     const uint32_t t = (uint32_t)(t0 + done);
-    CK(c, win_units(w, t, L, c->stream));
+    CK(c, win_units(w, t, Lw, c->stream));
     size_t need = 0;
-    CK(c, win_scan_units(w, L, nullptr, need, c->stream));
+    CK(c, win_scan_units(w, Lw, nullptr, need, c->stream));
     if (!grow(c->tmp, need)) return fail(c, GS_ENOMEM, "cannot allocate scan scratch");
     need = c->tmp.bytes;
-    CK(c, win_scan_units(w, L, c->tmp.p, need, c->stream));
-    unsigned long long Tn = 0;  // broadcasts firing in the window
-    CK(c, hipMemcpyAsync(&Tn, w.unit_off + (size_t)L * w.nfine, 8, hipMemcpyDeviceToHost, c->stream));
+    CK(c, win_scan_units(w, Lw, c->tmp.p, need, c->stream));
+    // firing index at the start of every tick of the window (units are tick-major)
+    CK(c, hipMemcpy2DAsync(c->h_misc, 8, w.unit_off, (size_t)w.nfine * 8, 8, Lw + 1,
+                           hipMemcpyDeviceToHost, c->stream));
     CK(c, hipStreamSynchronize(c->stream));
-    const unsigned long long T = Tn * w.stride;  // friend slots = expand outputs
-    if (!grow(c->amsg, T * 4 + 16) || !grow(c->cmsg, T * 4 + 16) || !grow(c->fmsg, T * 4 + 16))
+    uint32_t L = 1;
+    while (L < Lw && c->h_misc[L + 1] * w.stride <= slot_budget) ++L;
+    const unsigned long long Tn = c->h_misc[L];  // broadcasts firing in the window
+    const unsigned long long T = Tn * w.stride;  // friend slots of the firing nodes
+    plan_coarse(c, T, nullptr);
+    const uint64_t fcap = T + T / 8 + (uint64_t)w.ncoarse * 256 * 513 + 16;
+    if (!grow(c->gmap, ((Tn + 63) / 64 + 1) * 4) || !grow(c->cmsg, (c->h_cap[256] + 16) * 4) ||
+        !grow(c->fmsg, fcap * 4))
       return fail(c, GS_ENOMEM, "cannot allocate " + std::to_string(T) + " window messages");
-    w.amsg = (uint32_t*)c->amsg.p;
+    w.gmap = (uint32_t*)c->gmap.p;
     w.cmsg = (uint32_t*)c->cmsg.p;
     w.fmsg = (uint32_t*)c->fmsg.p;
     hipEvent_t* e = timing ? &c->ev[(size_t)widx * 3] : nullptr;
     if (e) CK(c, hipEventRecord(e[0], c->stream));
-    if (T) CK(c, win_expand(w, t, L, c->stream, Tn));
+    if (T) {
+      CK(c, hipMemcpyAsync(w.ccap, c->h_cap, 257 * 8, hipMemcpyHostToDevice, c->stream));
+      CK(c, win_groupmap(w, L, c->stream));
+      CK(c, win_expand(w, t, L, Tn, 1, c->stream));
+      CK(c, win_plan(w, false, c->stream));
+      CK(c, win_part2(w, T, true, c->stream));
+      // regions sized from estimates: check, and redo exactly on overflow
+      CK(c, hipMemcpyAsync(c->h_misc, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+      CK(c, hipStreamSynchronize(c->stream));
+      uint32_t err = (uint32_t)c->h_misc[0];
+      if (err & kErrCoarse) {
+        CK(c, hipMemsetAsync(w.chist, 0, 256 * 8, c->stream));
+        CK(c, win_expand(w, t, L, Tn, 0, c->stream));
+        CK(c, hipMemcpyAsync(c->h_misc, w.chist, 256 * 8, hipMemcpyDeviceToHost, c->stream));
+        CK(c, hipStreamSynchronize(c->stream));
+        plan_coarse(c, T, c->h_misc);
+        CK(c, hipMemcpyAsync(w.ccap, c->h_cap, 257 * 8, hipMemcpyHostToDevice, c->stream));
+        CK(c, hipMemsetAsync(w.cfill, 0, 256 * 8, c->stream));
+        CK(c, win_expand(w, t, L, Tn, 2, c->stream));
+        CK(c, win_plan(w, false, c->stream));
+        err = kErrFine;  // the fine regions must be redone as well
+      }
+      if (err & kErrFine) {
+        CK(c, hipMemsetAsync(w.fhist, 0, ((size_t)w.ncoarse * 256 + 1) * 8, c->stream));
+        CK(c, win_plan(w, true, c->stream));
+        CK(c, win_part2(w, T, false, c->stream));
+        size_t need2 = 0;
+        CK(c, win_scan_fine(w, nullptr, need2, c->stream));
+        if (!grow(c->tmp, need2)) return fail(c, GS_ENOMEM, "cannot allocate scan scratch");
+        need2 = c->tmp.bytes;
+        CK(c, win_scan_fine(w, c->tmp.p, need2, c->stream));
+        CK(c, hipMemsetAsync(w.ffill, 0, (size_t)w.nfine * 8, c->stream));
+        CK(c, win_part2(w, T, true, c->stream));
+        ++c->exact_redos;
+      }
+    }
     // the window's fire lists are consumed: later ticks t + R may reuse the slots
     const uint32_t s0 = t % w.R;
     const uint32_t first = std::min(L, w.R - s0);
     CK(c, hipMemsetAsync(w.fcount + (size_t)s0 * w.nfine, 0, (size_t)first * w.nfine * 4, c->stream));
     if (first < L) CK(c, hipMemsetAsync(w.fcount, 0, (size_t)(L - first) * w.nfine * 4, c->stream));
-    if (T) {
-      CK(c, win_coarse_scan(w, c->stream));
-      CK(c, win_part1(w, T, L, c->stream));
-      CK(c, win_part2(w, T, false, c->stream));
-      need = 0;
-      CK(c, win_scan_fine(w, nullptr, need, c->stream));
-      if (!grow(c->tmp, need)) return fail(c, GS_ENOMEM, "cannot allocate scan scratch");
-      need = c->tmp.bytes;
-      CK(c, win_scan_fine(w, c->tmp.p, need, c->stream));
-      CK(c, win_part2(w, T, true, c->stream));
-      if (e) CK(c, hipEventRecord(e[1], c->stream));
-      CK(c, win_resolve(w, t, L, c->stream));
-    } else if (e) {
-      CK(c, hipEventRecord(e[1], c->stream));
-    }
+    if (e) CK(c, hipEventRecord(e[1], c->stream));
+    if (T) CK(c, win_resolve(w, t, L, c->stream));
     if (e) {
       CK(c, hipEventRecord(e[2], c->stream));
       evs.emplace_back(widx * 3, T ? 1u : 0u);

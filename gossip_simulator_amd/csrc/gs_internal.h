@@ -80,8 +80,11 @@ constexpr uint32_t kFineNodes = 1u << kFineLog;
 constexpr uint32_t kCoarseShift = kFineLog + 8; // 256 fine buckets per coarse bucket
 constexpr uint32_t kMaxWindow = 16;             // tick offset in 4 bits
 constexpr uint32_t kWinMaxRing = 256;
+constexpr uint32_t kWinMaxStride = 32;          // friends-row length the window engine takes
 constexpr uint32_t kEmptyMsg = 0xFFFFFFFFu;
 constexpr uint32_t kPartTile = 4096;            // messages per partition tile
+constexpr uint32_t kWinSlotsPerBucket = 7168;   // window cut: friend slots per fine bucket
+                                                // (k_resolve keeps <= 8192 receipts in LDS)
 
 struct WinState {
   const uint8_t* deg;
@@ -92,18 +95,19 @@ struct WinState {
   uint32_t* err;
   uint32_t* fcount;              // [R][nfine] fire-list lengths
   uint16_t* flist;               // [R][nfine][16384] local ids of firing nodes
-  unsigned long long* usize;     // [L*nfine + 1] tasks per (tick, bucket) unit
+  unsigned long long* usize;     // [L*nfine + 1] fires per (tick, bucket) unit
   unsigned long long* unit_off;  // [L*nfine + 1] exclusive scan of usize
-  uint32_t* amsg;                // expand output, one slot per task (kEmptyMsg = none)
-  uint32_t* cmsg;                // coarse-partitioned: u_in_coarse | k << 22
-  uint32_t* fmsg;                // fine-partitioned:   u_in_fine   | k << 14
-  unsigned long long* chist;     // [256] coarse counts
-  unsigned long long* cbase;     // [257] coarse offsets
-  unsigned long long* cfill;     // [256]
-  uint32_t* tprefix;             // [257] partition tiles per coarse bucket (prefix)
-  unsigned long long* fhist;     // [ncoarse*256 + 1] fine counts
-  unsigned long long* fbase;     // [nfine + 1] fine offsets
-  unsigned long long* ffill;     // [nfine]
+  uint32_t* gmap;                // [ceil(fires/64)] unit of every 64th firing index
+  uint32_t* cmsg;                // coarse regions: u_in_coarse | k << 22
+  uint32_t* fmsg;                // fine regions:   u_in_fine   | k << 14
+  unsigned long long* chist;     // [256] exact coarse counts (fallback)
+  unsigned long long* ccap;      // [257] coarse region starts (host-planned)
+  unsigned long long* cfill;     // [256] coarse region fill
+  uint32_t* tprefix;             // [257] part2 tiles per coarse bucket (prefix)
+  unsigned long long* fhist;     // [ncoarse*256 + 1] exact fine counts (fallback)
+  unsigned long long* fstart;    // [nfine + 1] fine region starts
+  unsigned long long* ffill;     // [nfine] fine region fill
+  unsigned long long* dbg;       // diagnostic phase stamps (GS_STAMPS=1), else null
   uint64_t n, W;
   uint32_t nfine, ncoarse, R, stride, stride_magic;
   int32_t delay_low;
@@ -111,13 +115,19 @@ struct WinState {
   int32_t kd, kc;
   Key key;
 };
+constexpr uint32_t kStampPhases = 8;
+
+constexpr uint32_t kErrArrivals = 4;  // > 65535 arrivals at one node in one tick
+constexpr uint32_t kErrCoarse = 8;    // a coarse region overflowed its estimate
+constexpr uint32_t kErrFine = 16;     // a fine region overflowed its estimate
 
 hipError_t win_units(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
 hipError_t win_scan_units(const WinState& w, uint32_t L, void* tmp, size_t& tmp_bytes, hipStream_t s);
-hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s, uint64_t T);
-hipError_t win_coarse_scan(const WinState& w, hipStream_t s);
+hipError_t win_groupmap(const WinState& w, uint32_t L, hipStream_t s);
+hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, int mode,
+                      hipStream_t s);
+hipError_t win_plan(const WinState& w, bool exact, hipStream_t s);
 hipError_t win_scan_fine(const WinState& w, void* tmp, size_t& tmp_bytes, hipStream_t s);
-hipError_t win_part1(const WinState& w, uint64_t T, uint32_t L, hipStream_t s);
 hipError_t win_part2(const WinState& w, uint64_t T, bool scatter, hipStream_t s);
 hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
 hipError_t win_schedule_one(const WinState& w, uint32_t node, uint32_t tick, hipStream_t s);

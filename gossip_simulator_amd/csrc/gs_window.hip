@@ -7,22 +7,25 @@
 // scheduled when tick t0 starts.  The L ticks are processed together; the
 // receipts of each tick are still resolved in tick order per node.
 //
-// Pipeline of one window (one launch each):
-//   units   tasks per (tick k, fine bucket f) = fired(k,f) * stride
-//   (scan)  hipcub exclusive sum -> a fixed output slot for every task
-//   expand  for every firing node v and friend slot j: keyed RandomDrop
-//           (:143-147); kept -> target id u into its task slot (no atomics,
-//           coalesced), per-tick fired/sent counts, coarse histogram
-//   part1   tiles of the expand output -> 256 coarse buckets (u >> 22),
-//           LDS counting sort + one global reservation per (tile, bucket)
-//   part2   per coarse bucket: count, scan, scatter into fine buckets
-//           (16384 nodes each); message = u_in_fine | k << 14
-//   resolve one workgroup per fine bucket: the bucket's received/crashed
-//           bits and per-node arrival counters live in LDS; for each tick k
-//           the arrivals are counted, then one owner lane per node replays
-//           ordinals 0..count-1 of the receive case (:107-123) with keyed
-//           crash rolls; infections append to the fire list of
-//           (slot (t+off) mod R, f) -- a list only this workgroup writes.
+// Pipeline of one window:
+//   units     fires per (tick k, fine bucket f); hipcub scan -> firing index
+//   groupmap  first unit of every 64-node group of firing indices
+//   expand    one thread per firing node (Node.Broadcast, :141-147): row read
+//             once, keyed RandomDrop per slot (one Philox per 4 slots), kept
+//             targets counting-sorted in LDS by coarse bucket (target >> 22)
+//             and written as coalesced runs into coarse regions sized from
+//             the node share (+ margin); message = u_in_coarse | k << 22
+//   plan      fine-bucket regions (16384 nodes) inside each coarse region,
+//             sized from the coarse count (+ margin)
+//   part2     one pass per coarse tile: LDS counting sort by fine digit,
+//             coalesced runs into fine regions; message = u_in_fine | k << 14
+//   resolve   one workgroup per fine bucket: received/crashed bits and u16
+//             arrival counters in LDS; per tick, count then let one owner lane
+//             per node replay ordinals 0..count-1 of the receive case
+//             (:107-123); infections append to the fire list (slot, f) that
+//             only this workgroup writes
+// A region that overflows its estimated size is detected and the window's
+// partition is redone with exact counts (expand and part2 are idempotent).
 // Fire lists: fcount[R][nfine] + flist[R][nfine][16384] (u16 local ids).
 #include <hipcub/hipcub.hpp>
 
@@ -32,11 +35,12 @@ namespace gs {
 namespace {
 
 constexpr uint32_t kExpandBlock = 256;
+constexpr uint32_t kExpandSlots = 4096;   // LDS message slots per expand round
 constexpr uint32_t kResolveBlock = 512;
 constexpr uint32_t kResolveMsgCap = 8192;
 
 // Units = (tick k, fine bucket f); usize = fires.  Also zeroes the window's
-// histograms (one launch instead of several memsets).
+// counters (one launch instead of several memsets).
 __global__ void k_units(const WinState w, uint32_t t0, uint32_t L) {
   const uint32_t units = L * w.nfine;
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
@@ -46,120 +50,40 @@ __global__ void k_units(const WinState w, uint32_t t0, uint32_t L) {
     const uint32_t s = (t0 + k) % w.R;
     w.usize[u] = w.fcount[(size_t)s * w.nfine + f];
   }
-  for (uint32_t i = tid; i < 256; i += nth) w.chist[i] = 0;
-  for (uint32_t i = tid; i <= w.ncoarse * 256; i += nth) w.fhist[i] = 0;
+  for (uint32_t i = tid; i < 256; i += nth) { w.chist[i] = 0; w.cfill[i] = 0; }
   for (uint32_t i = tid; i < w.nfine; i += nth) w.ffill[i] = 0;
+  if (tid == 0) *w.err &= ~(kErrCoarse | kErrFine);
 }
 
-// One lane per firing node (Node.Broadcast, simulator.go:141-147): its row is
-// read once, one Philox block gives the drop rolls of 4 friend slots, and the
-// node's `stride` output slots start at (firing index) * stride.  A wave
-// walks kNodesPerWave consecutive firing nodes of the window.
-constexpr uint32_t kNodesPerWave = 256;
-__global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint32_t t0, uint32_t L,
-                                                         unsigned long long Tn) {
-  __shared__ uint32_t s_hist[256];
-  __shared__ unsigned long long s_acc[kMaxWindow][2];
-  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) s_hist[i] = 0;
-  if (threadIdx.x < kMaxWindow * 2) (&s_acc[0][0])[threadIdx.x] = 0;
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+// gmap[q] = unit holding firing index 64*q.
+__global__ void k_groupmap(const WinState w, uint32_t L) {
   const uint32_t units = L * w.nfine;
-  const uint32_t S = w.stride;
-  const uint32_t c3drop = ctr3(K_DROP, w.key.trial);
-  const unsigned long long* uo = w.unit_off;
-  uint32_t one_bin = 0;  // messages when there is a single coarse bucket
-  const unsigned long long nwaves = (Tn + kNodesPerWave - 1) / kNodesPerWave;
-  for (unsigned long long gw = (unsigned long long)blockIdx.x * (kExpandBlock / 64) + wid; gw < nwaves;
-       gw += (unsigned long long)gridDim.x * (kExpandBlock / 64)) {
-    const unsigned long long start = gw * kNodesPerWave;
-    // unit holding `start`: last u with uo[u] <= start (wave-uniform search)
-    uint32_t lo = 0, hi = units;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi + 1) >> 1;
-      if (uo[mid] <= start) lo = mid; else hi = mid - 1;
-    }
-    uint32_t u = lo;
-    uint32_t cur_k = 0xFFFFFFFFu, sent = 0, fired = 0;
-    for (uint32_t it = 0; it < kNodesPerWave / 64; ++it) {
-      const unsigned long long g = start + it * 64 + lane;
-      if (g >= Tn) break;
-      while (uo[u + 1] <= g) ++u;  // empty units are skipped
-      const uint32_t k = u / w.nfine, f = u - k * w.nfine;
-      if (k != cur_k) {
-        if (cur_k != 0xFFFFFFFFu) {
-          if (sent) atomicAdd(&s_acc[cur_k][1], (unsigned long long)sent);
-          if (fired) atomicAdd(&s_acc[cur_k][0], (unsigned long long)fired);
-        }
-        cur_k = k; sent = 0; fired = 0;
-      }
-      const uint32_t t = t0 + k;
-      const uint32_t s = t % w.R;
-      const uint32_t i = (uint32_t)(g - uo[u]);
-      const uint32_t v = (f << kFineLog) + w.flist[((size_t)s * w.nfine + f) * kFineNodes + i];
-      const uint32_t d = w.deg[v];
-      const uint32_t* row = w.ids + (size_t)v * S;
-      uint32_t* out = w.amsg + g * S;
-      ++fired;
-      for (uint32_t jg = 0; jg * 4 < S; ++jg) {
-        u32x4 r{0, 0, 0, 0};
-        if (jg * 4 < d) r = philox(v, t, jg, c3drop, w.key.k0, w.key.k1);   // :144, :172
-#pragma unroll
-        for (uint32_t jj = 0; jj < 4; ++jj) {
-          const uint32_t j = jg * 4 + jj;
-          if (j >= S) break;
-          uint32_t msg = kEmptyMsg;
-          if (j < d && (int32_t)uniform(lane_of(r, jj), 100u) >= w.kd) {
-            msg = row[j];                                                    // :145
-            ++sent;
-            if (w.ncoarse == 1) ++one_bin;
-            else atomicAdd(&s_hist[msg >> kCoarseShift], 1u);
-          }
-          out[j] = msg;
-        }
-      }
-    }
-    if (cur_k != 0xFFFFFFFFu) {
-      if (sent) atomicAdd(&s_acc[cur_k][1], (unsigned long long)sent);
-      if (fired) atomicAdd(&s_acc[cur_k][0], (unsigned long long)fired);
-    }
-  }
-  if (one_bin) atomicAdd(&s_hist[0], one_bin);
-  __syncthreads();
-  for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x)
-    if (s_hist[b]) atomicAdd(&w.chist[b], (unsigned long long)s_hist[b]);
-  if (threadIdx.x < L * 2) {
-    const uint32_t k = threadIdx.x >> 1, fld = threadIdx.x & 1;
-    const unsigned long long v = s_acc[k][fld];
-    if (v) atomicAdd(&w.stats[(size_t)((t0 + k) % kStatSlots) * kStatFields + (fld ? ST_SENT : ST_FIRED)], v);
+  for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
+    const unsigned long long a = w.unit_off[u], b = w.unit_off[u + 1];
+    for (unsigned long long q = (a + 63) >> 6; (q << 6) < b; ++q) w.gmap[q] = u;
   }
 }
 
-__global__ void k_coarse_scan(const WinState w) {
-  __shared__ unsigned long long s[257];
-  __shared__ uint32_t st[257];
-  const uint32_t b = threadIdx.x;  // 256 threads
-  s[b + 1] = w.chist[b];
-  st[b + 1] = (uint32_t)((w.chist[b] + kPartTile - 1) / kPartTile);
-  if (b == 0) { s[0] = 0; st[0] = 0; }
-  __syncthreads();
-  if (b == 0) {
-    for (int i = 1; i <= 256; ++i) { s[i] += s[i - 1]; st[i] += st[i - 1]; }
+// Unit of firing index g: search [gmap[g/64], gmap[g/64 + 1]].
+__device__ __forceinline__ uint32_t unit_of(const WinState& w, unsigned long long g,
+                                            unsigned long long Tn, uint32_t units) {
+  const unsigned long long q = g >> 6;
+  uint32_t lo = w.gmap[q];
+  uint32_t hi = ((q + 1) << 6) < Tn ? w.gmap[q + 1] : units - 1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (w.unit_off[mid] <= g) lo = mid; else hi = mid - 1;
   }
-  __syncthreads();
-  w.cbase[b] = s[b];
-  w.tprefix[b] = st[b];
-  w.cfill[b] = 0;
-  if (b == 0) { w.cbase[256] = s[256]; w.tprefix[256] = st[256]; }
+  return lo;
 }
 
-// LDS counting sort of one tile by an 8-bit digit, then coalesced runs out.
-struct TileSort {
-  uint32_t buf[kPartTile];
-  uint8_t bin[kPartTile];
+struct ExpandLds {
+  uint32_t sorted[kExpandSlots];
+  uint8_t sbin[kExpandSlots];
   uint32_t cnt[256];
   uint32_t off[257];
   unsigned long long gbase[256];
+  unsigned long long acc[kMaxWindow][2];  // fired, sent per tick
 };
 
 __device__ __forceinline__ void block_scan256(uint32_t* cnt, uint32_t* off) {
@@ -183,53 +107,134 @@ __device__ __forceinline__ void block_scan256(uint32_t* cnt, uint32_t* off) {
   }
 }
 
-// part1: expand output -> coarse buckets; message = u_in_coarse | k << 22
-__global__ __launch_bounds__(256) void k_part1(const WinState w, unsigned long long T, uint32_t L) {
-  __shared__ TileSort ts;
-  __shared__ unsigned long long s_kb[kMaxWindow + 1];
+// Expand + coarse partition.  WRITE=false only counts (exact fallback).
+// Expand + coarse partition; a thread's messages stay in registers (MAXS >=
+// stride) so the LDS footprint is the 4096-entry sort buffer only.
+template <bool WRITE, uint32_t MAXS>
+__global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint32_t t0, uint32_t L,
+                                                         unsigned long long Tn, int add_stats) {
+  __shared__ ExpandLds sm;
   const uint32_t tid = threadIdx.x;
-  if (tid <= L) s_kb[tid] = w.unit_off[(size_t)tid * w.nfine] * w.stride;  // tick bounds in slots
-  ts.cnt[tid] = 0;
-  __syncthreads();
-  const unsigned long long base = (unsigned long long)blockIdx.x * kPartTile;
-  uint32_t m[kPartTile / 256], rank[kPartTile / 256];
-  uint8_t bn[kPartTile / 256];
+  const uint32_t units = L * w.nfine;
+  const uint32_t S = w.stride;
+  const uint32_t per_round = S * kExpandBlock <= kExpandSlots ? kExpandBlock : kExpandSlots / S;
+  const uint32_t c3drop = ctr3(K_DROP, w.key.trial);
+  if (tid < kMaxWindow * 2) (&sm.acc[0][0])[tid] = 0;
+  const unsigned long long rounds = (Tn + per_round - 1) / per_round;
+  for (unsigned long long rd = blockIdx.x; rd < rounds; rd += gridDim.x) {
+    sm.cnt[tid] = 0;
+    __syncthreads();
+    const unsigned long long g = rd * per_round + tid;
+    const bool active = tid < per_round && g < Tn;
+    uint32_t mm[MAXS], mt[MAXS];  // message, bin | rank << 8 (~0u = none)
 #pragma unroll
-  for (uint32_t r = 0; r < kPartTile / 256; ++r) {
-    const unsigned long long x = base + r * 256 + tid;
-    bn[r] = 0;
-    m[r] = kEmptyMsg;
-    if (x < T) {
-      const uint32_t u = w.amsg[x];
-      if (u != kEmptyMsg) {
-        uint32_t k = 0;
-        while (k + 1 < L && s_kb[k + 1] <= x) ++k;
-        bn[r] = (uint8_t)(u >> kCoarseShift);
-        m[r] = (u & ((1u << kCoarseShift) - 1)) | (k << kCoarseShift);
-        rank[r] = atomicAdd(&ts.cnt[bn[r]], 1u);
+    for (uint32_t j = 0; j < MAXS; ++j) mt[j] = ~0u;
+    if (active) {
+      const uint32_t u = unit_of(w, g, Tn, units);
+      const uint32_t k = u / w.nfine, f = u - k * w.nfine;
+      const uint32_t t = t0 + k;
+      const uint32_t s = t % w.R;
+      const uint32_t i = (uint32_t)(g - w.unit_off[u]);
+      const uint32_t v = (f << kFineLog) + w.flist[((size_t)s * w.nfine + f) * kFineNodes + i];
+      const uint32_t d = w.deg[v];
+      const uint32_t* row = w.ids + (size_t)v * S;
+#pragma unroll
+      for (uint32_t j = 0; j < MAXS; ++j) mm[j] = j < S ? row[j] : 0u;  // whole row in flight
+      uint32_t sent = 0;
+#pragma unroll
+      for (uint32_t jg = 0; jg < MAXS / 4; ++jg) {
+        if (jg * 4 >= d) break;
+        const u32x4 r = philox(v, t, jg, c3drop, w.key.k0, w.key.k1);   // :144, :172
+#pragma unroll
+        for (uint32_t jj = 0; jj < 4; ++jj) {
+          const uint32_t j = jg * 4 + jj;
+          if (j < d && (int32_t)uniform(lane_of(r, jj), 100u) >= w.kd) {   // kept: :145
+            const uint32_t bin = mm[j] >> kCoarseShift;
+            mt[j] = bin | (atomicAdd(&sm.cnt[bin], 1u) << 8);
+            mm[j] = (mm[j] & ((1u << kCoarseShift) - 1)) | (k << kCoarseShift);
+            ++sent;
+          }
+        }
       }
+      atomicAdd(&sm.acc[k][0], 1ull);
+      if (sent) atomicAdd(&sm.acc[k][1], (unsigned long long)sent);
+    }
+    __syncthreads();
+    if (!WRITE) {
+      if (sm.cnt[tid]) atomicAdd(&w.chist[tid], (unsigned long long)sm.cnt[tid]);
+      continue;  // the next round's first barrier orders the reuse of sm.cnt
+    }
+    block_scan256(sm.cnt, sm.off);
+    if (sm.cnt[tid]) {
+      const unsigned long long at = atomicAdd(&w.cfill[tid], (unsigned long long)sm.cnt[tid]);
+      if (at + sm.cnt[tid] > w.ccap[tid + 1] - w.ccap[tid]) atomicOr(w.err, kErrCoarse);
+      sm.gbase[tid] = w.ccap[tid] + at;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < MAXS; ++j)
+      if (mt[j] != ~0u) {
+        const uint32_t bin = mt[j] & 255, p = sm.off[bin] + (mt[j] >> 8);
+        sm.sorted[p] = mm[j];
+        sm.sbin[p] = (uint8_t)bin;
+      }
+    __syncthreads();
+    const uint32_t total = sm.off[256];
+    for (uint32_t p = tid; p < total; p += kExpandBlock) {
+      const uint32_t b = sm.sbin[p];
+      const unsigned long long pos = sm.gbase[b] + (p - sm.off[b]);
+      if (pos < w.ccap[b + 1]) w.cmsg[pos] = sm.sorted[p];
     }
   }
+  if (!WRITE || !add_stats) return;  // an exact redo must not count the window twice
   __syncthreads();
-  block_scan256(ts.cnt, ts.off);
-  if (ts.cnt[tid]) ts.gbase[tid] = w.cbase[tid] + atomicAdd(&w.cfill[tid], (unsigned long long)ts.cnt[tid]);
-  __syncthreads();
-#pragma unroll
-  for (uint32_t r = 0; r < kPartTile / 256; ++r)
-    if (m[r] != kEmptyMsg) {
-      const uint32_t p = ts.off[bn[r]] + rank[r];
-      ts.buf[p] = m[r];
-      ts.bin[p] = bn[r];
-    }
-  __syncthreads();
-  const uint32_t total = ts.off[256];
-  for (uint32_t p = tid; p < total; p += 256) {
-    const uint32_t b = ts.bin[p];
-    w.cmsg[ts.gbase[b] + (p - ts.off[b])] = ts.buf[p];
+  if (tid < L * 2) {
+    const uint32_t k = tid >> 1, fld = tid & 1;
+    const unsigned long long v = sm.acc[k][fld];
+    if (v) atomicAdd(&w.stats[(size_t)((t0 + k) % kStatSlots) * kStatFields + (fld ? ST_SENT : ST_FIRED)], v);
   }
 }
 
-// part2: coarse bucket tiles -> fine buckets; message = u_in_fine | k << 14
+// Fine regions inside each coarse region: capacity per fine bucket of coarse
+// c = cfill[c]*1.15/256 + 512 (fast path), or exact counts (fhist != null).
+__global__ void k_plan(const WinState w, bool exact) {
+  __shared__ unsigned long long s_base[257];
+  __shared__ unsigned long long s_cap[256];
+  __shared__ uint32_t s_tp[257];
+  const uint32_t tid = threadIdx.x;  // 256 threads per block
+  const unsigned long long cnt = w.cfill[tid] < w.ccap[tid + 1] - w.ccap[tid]
+                                     ? w.cfill[tid] : w.ccap[tid + 1] - w.ccap[tid];
+  const bool live = tid < w.ncoarse;
+  s_cap[tid] = live ? (cnt + cnt / 8 + 255) / 256 + 512 : 0;
+  s_base[tid + 1] = s_cap[tid] * 256;
+  s_tp[tid + 1] = live ? (uint32_t)((cnt + kPartTile - 1) / kPartTile) : 0;
+  if (tid == 0) { s_base[0] = 0; s_tp[0] = 0; }
+  __syncthreads();
+  if (tid == 0)
+    for (int i = 1; i <= 256; ++i) { s_base[i] += s_base[i - 1]; s_tp[i] += s_tp[i - 1]; }
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    w.tprefix[tid] = s_tp[tid];
+    if (tid == 0) w.tprefix[256] = s_tp[256];
+  }
+  if (exact) return;  // fstart comes from the exact count + scan instead
+  for (uint32_t f = blockIdx.x * blockDim.x + tid; f <= w.nfine; f += gridDim.x * blockDim.x) {
+    const uint32_t c = f >> 8, d = f & 255;
+    w.fstart[f] = f == w.nfine ? s_base[w.ncoarse] : s_base[c] + d * s_cap[c];
+  }
+}
+
+// LDS counting sort of one tile by an 8-bit digit, then coalesced runs out.
+struct TileSort {
+  uint32_t buf[kPartTile];
+  uint8_t bin[kPartTile];
+  uint32_t cnt[256];
+  uint32_t off[257];
+  unsigned long long gbase[256];
+};
+
+// part2: coarse tiles -> fine regions; message = u_in_fine | k << 14.
+// SCATTER=false counts per fine bucket (exact fallback).
 template <bool SCATTER>
 __global__ __launch_bounds__(256) void k_part2(const WinState w) {
   __shared__ TileSort ts;
@@ -246,7 +251,9 @@ __global__ __launch_bounds__(256) void k_part2(const WinState w) {
       if (s_tp[mid] <= g) lo = mid; else hi = mid - 1;
     }
     const uint32_t c = lo;
-    const unsigned long long cb = w.cbase[c], ce = w.cbase[c + 1];
+    const unsigned long long cb = w.ccap[c];
+    const unsigned long long fill = w.cfill[c] < w.ccap[c + 1] - cb ? w.cfill[c] : w.ccap[c + 1] - cb;
+    const unsigned long long ce = cb + fill;
     const unsigned long long base = cb + (unsigned long long)(g - s_tp[c]) * kPartTile;
     ts.cnt[tid] = 0;
     __syncthreads();
@@ -273,7 +280,9 @@ __global__ __launch_bounds__(256) void k_part2(const WinState w) {
     block_scan256(ts.cnt, ts.off);
     if (ts.cnt[tid]) {
       const uint32_t f = c * 256 + tid;
-      ts.gbase[tid] = w.fbase[f] + atomicAdd(&w.ffill[f], (unsigned long long)ts.cnt[tid]);
+      const unsigned long long at = atomicAdd(&w.ffill[f], (unsigned long long)ts.cnt[tid]);
+      if (at + ts.cnt[tid] > w.fstart[f + 1] - w.fstart[f]) atomicOr(w.err, kErrFine);
+      ts.gbase[tid] = w.fstart[f] + at;
     }
     __syncthreads();
 #pragma unroll
@@ -287,7 +296,8 @@ __global__ __launch_bounds__(256) void k_part2(const WinState w) {
     const uint32_t total = ts.off[256];
     for (uint32_t p = tid; p < total; p += 256) {
       const uint32_t b = ts.bin[p];
-      w.fmsg[ts.gbase[b] + (p - ts.off[b])] = ts.buf[p];
+      const unsigned long long pos = ts.gbase[b] + (p - ts.off[b]);
+      if (pos < w.fstart[c * 256 + b + 1]) w.fmsg[pos] = ts.buf[p];
     }
     __syncthreads();
   }
@@ -296,14 +306,67 @@ __global__ __launch_bounds__(256) void k_part2(const WinState w) {
 struct ResolveLds {
   uint32_t recv[kFineNodes / 32];
   uint32_t crash[kFineNodes / 32];
-  uint32_t cnt[kFineNodes / 2];  // two u16 arrival counters per word
+  uint32_t cnt[kFineNodes / 2];  // two u16 counters per word: arrivals, then offsets
   uint32_t fc[kWinMaxRing];      // fire-list lengths of this bucket, per ring slot
-  uint32_t tcnt[kMaxWindow];     // messages per tick of the window
-  uint32_t toff[kMaxWindow + 1];
   uint32_t st[kMaxWindow][4];    // msgs, recv, crash, sched per tick
+  uint32_t wsum[kResolveBlock / 64];
   uint32_t err;
-  uint32_t msg[kResolveMsgCap];  // the bucket's messages, sorted by tick
-};
+  uint32_t msg[kResolveMsgCap];  // the bucket's messages, sorted by node
+};  // ~69 KB: two workgroups per CU
+
+__device__ __forceinline__ uint32_t cnt16(const ResolveLds& sm, uint32_t i) {
+  return (sm.cnt[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
+}
+
+// Node-major resolve of one node: its messages sorted[b, e) (any tick order)
+// are replayed tick by tick, ordinals in order (simulator.go:107-123).
+__device__ __forceinline__ void resolve_node_major(const WinState& w, ResolveLds& sm, uint32_t f,
+                                                   uint32_t loc, uint32_t b, uint32_t e,
+                                                   uint32_t t0, uint32_t c3crash) {
+  uint32_t mask = 0;
+  for (uint32_t p = b; p < e; ++p) mask |= 1u << (sm.msg[p] >> kFineLog);
+  const uint32_t u = (f << kFineLog) + loc, bit = 1u << (loc & 31), wi = loc >> 5;
+  bool crashed = (sm.crash[wi] & bit) != 0;
+  const bool was_crashed = crashed;
+  bool received = (sm.recv[wi] & bit) != 0;
+  const bool was_received = received;
+  while (mask) {
+    const uint32_t k = __builtin_ctz(mask);
+    mask &= mask - 1;
+    uint32_t kk = 0;
+    for (uint32_t p = b; p < e; ++p) kk += (sm.msg[p] >> kFineLog) == k;
+    const uint32_t t = t0 + k;
+    uint32_t cm = 0, cr = 0, cc = 0, cs = 0;
+    u32x4 r{0, 0, 0, 0};
+    for (uint32_t i = 0; i < kk; ++i) {
+      if (crashed) break;                                          // :108
+      ++cm;                                                        // :111
+      if (w.kc > 0) {
+        if ((i & 3) == 0) r = philox(u, t, i >> 2, c3crash, w.key.k0, w.key.k1);
+        if ((int32_t)uniform(lane_of(r, i & 3), 100u) < w.kc) {   // :112-115
+          ++cc;
+          crashed = true;
+          break;
+        }
+      }
+      if (received) continue;                                      // :117
+      received = true;                                             // :120
+      ++cr;                                                        // :121
+      // Broadcast() (:122, :141-142): fire at t + off
+      const uint32_t off = fire_offset(w.delay_low, w.delay_span, draw0(w.key, K_DELAY, u, t, 0));
+      const uint32_t s = (t + off) % w.R;
+      const uint32_t pos = atomicAdd(&sm.fc[s], 1u);
+      w.flist[((size_t)s * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
+      ++cs;
+    }
+    if (cm) atomicAdd(&sm.st[k][0], cm);
+    if (cr) atomicAdd(&sm.st[k][1], cr);
+    if (cc) atomicAdd(&sm.st[k][2], cc);
+    if (cs) atomicAdd(&sm.st[k][3], cs);
+  }
+  if (crashed && !was_crashed) atomicOr(&sm.crash[wi], bit);
+  if (received && !was_received) atomicOr(&sm.recv[wi], bit);
+}
 
 // The receive case of Node.Start (simulator.go:107-123) for node `loc` of the
 // bucket with kk arrivals at tick t: ordinals 0..kk-1, keyed crash rolls.
@@ -372,11 +435,24 @@ __device__ __forceinline__ void resolve_tick(const WinState& w, ResolveLds& sm, 
 __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
   __shared__ ResolveLds sm;
   const uint32_t f = blockIdx.x, tid = threadIdx.x;
+  const unsigned long long mb = w.fstart[f];
+  const uint32_t M = (uint32_t)w.ffill[f];
+  if (M == 0) return;  // no receipt in this bucket during the window
   const uint32_t node0 = f << kFineLog;
   const uint64_t wbase = (uint64_t)node0 >> 5;  // u32 word index of the bucket's bits
   const uint32_t* rg = (const uint32_t*)w.recv;
   const uint32_t* cg = (const uint32_t*)w.crash;
   const uint64_t nw32 = w.W * 2;
+  const uint32_t* gm = w.fmsg + mb;
+  // issue every global load of the block up front: messages, bits, list lengths
+  constexpr uint32_t kPerThread = kResolveMsgCap / kResolveBlock;
+  uint32_t mr[kPerThread];
+  const bool small = M <= kResolveMsgCap;
+#pragma unroll
+  for (uint32_t i = 0; i < kPerThread; ++i) {
+    const uint32_t p = tid + i * kResolveBlock;
+    mr[i] = small && p < M ? gm[p] : ~0u;
+  }
   for (uint32_t i = tid; i < kFineNodes / 32; i += kResolveBlock) {
     const bool in = wbase + i < nw32;
     sm.recv[i] = in ? rg[wbase + i] : 0u;
@@ -385,30 +461,60 @@ __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uin
   for (uint32_t i = tid; i < kFineNodes / 2; i += kResolveBlock) sm.cnt[i] = 0;
   for (uint32_t s = tid; s < w.R; s += kResolveBlock) sm.fc[s] = w.fcount[(size_t)s * w.nfine + f];
   if (tid < kMaxWindow * 4) (&sm.st[0][0])[tid] = 0;
-  if (tid < kMaxWindow) sm.tcnt[tid] = 0;
   if (tid == 0) sm.err = 0;
-  const unsigned long long mb = w.fbase[f];
-  const uint32_t M = (uint32_t)(w.fbase[f + 1] - mb);
-  const uint32_t* gm = w.fmsg + mb;
   const uint32_t c3crash = ctr3(K_CRASH, w.key.trial);
   __syncthreads();
-  if (M <= kResolveMsgCap) {
-    // counting sort of the bucket's messages by tick, into LDS
-    for (uint32_t p = tid; p < M; p += kResolveBlock) atomicAdd(&sm.tcnt[gm[p] >> kFineLog], 1u);
+  if (small) {
+    // counting sort of the bucket's messages by node (u16 counters -> offsets)
+#pragma unroll
+    for (uint32_t i = 0; i < kPerThread; ++i)
+      if (mr[i] != ~0u) {
+        const uint32_t loc = mr[i] & (kFineNodes - 1);
+        atomicAdd(&sm.cnt[loc >> 1], 1u << ((loc & 1) * 16));
+      }
     __syncthreads();
-    if (tid == 0) {
-      uint32_t a = 0;
-      for (uint32_t k = 0; k < L; ++k) { sm.toff[k] = a; a += sm.tcnt[k]; sm.tcnt[k] = 0; }
-      sm.toff[L] = a;
+    {  // exclusive scan of 16384 u16 counters: 32 per thread (M <= 8192 fits u16)
+      constexpr uint32_t kPer = kFineNodes / kResolveBlock;  // 32
+      uint32_t* wp = &sm.cnt[tid * (kPer / 2)];
+      uint32_t sum = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < kPer / 2; ++i) sum += (wp[i] & 0xFFFFu) + (wp[i] >> 16);
+      const uint32_t lane = tid & 63, wv = tid >> 6;
+      uint32_t x = sum;
+#pragma unroll
+      for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (lane == 63) sm.wsum[wv] = x;
+      __syncthreads();
+      uint32_t base = x - sum;
+      for (uint32_t v = 0; v < wv; ++v) base += sm.wsum[v];
+#pragma unroll
+      for (uint32_t i = 0; i < kPer / 2; ++i) {
+        const uint32_t a = wp[i] & 0xFFFFu, b = wp[i] >> 16;
+        wp[i] = base | ((base + a) << 16);
+        base += a + b;
+      }
     }
     __syncthreads();
+#pragma unroll
+    for (uint32_t i = 0; i < kPerThread; ++i)
+      if (mr[i] != ~0u) {
+        const uint32_t m = mr[i], loc = m & (kFineNodes - 1), sh = (loc & 1) * 16;
+        const uint32_t pos = (atomicAdd(&sm.cnt[loc >> 1], 1u << sh) >> sh) & 0xFFFFu;
+        sm.msg[pos] = m;
+      }
+    __syncthreads();
+    // cnt now holds each node's END offset.  The lane holding the first
+    // message of a node's run (a "segment head") resolves that node: every
+    // lane sits on a message, and most messages head a run of their own.
     for (uint32_t p = tid; p < M; p += kResolveBlock) {
-      const uint32_t m = gm[p], k = m >> kFineLog;
-      sm.msg[sm.toff[k] + atomicAdd(&sm.tcnt[k], 1u)] = m;
+      const uint32_t loc = sm.msg[p] & (kFineNodes - 1);
+      if (p && (sm.msg[p - 1] & (kFineNodes - 1)) == loc) continue;
+      resolve_node_major(w, sm, f, loc, p, cnt16(sm, loc), t0, c3crash);
     }
     __syncthreads();
-    for (uint32_t k = 0; k < L; ++k)
-      resolve_tick(w, sm, f, sm.msg, sm.toff[k], sm.toff[k + 1], k, false, t0 + k, c3crash);
   } else {
     // large bucket: stream the messages from global memory once per pass
     for (uint32_t k = 0; k < L; ++k) resolve_tick(w, sm, f, gm, 0, M, k, true, t0 + k, c3crash);
@@ -425,7 +531,7 @@ __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uin
     if (v) atomicAdd(&w.stats[(size_t)((t0 + k) % kStatSlots) * kStatFields + field],
                      (unsigned long long)v);
   }
-  if (tid == 0 && sm.err) atomicOr(w.err, 4u);
+  if (tid == 0 && sm.err) atomicOr(w.err, kErrArrivals);
 }
 
 __global__ void k_schedule_one_win(const WinState w, uint32_t node, uint32_t t) {
@@ -439,28 +545,47 @@ __global__ void k_schedule_one_win(const WinState w, uint32_t node, uint32_t t) 
 }  // namespace
 
 hipError_t win_units(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s) {
-  const uint32_t units = std::max<uint32_t>(L * w.nfine + 1, w.ncoarse * 256 + 1);
+  const uint32_t units = std::max<uint32_t>(L * w.nfine + 1, w.nfine);
   const uint32_t blocks = std::min<uint32_t>((units + 255) / 256, 4096);
   hipLaunchKernelGGL(k_units, dim3(blocks), dim3(256), 0, s, w, t0, L);
   return hipGetLastError();
 }
 
-hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s, uint64_t Tn) {
-  const uint64_t waves = (Tn + kNodesPerWave - 1) / kNodesPerWave;
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((waves + 3) / 4, 16384);
-  hipLaunchKernelGGL(k_expand, dim3(blocks ? blocks : 1), dim3(kExpandBlock), 0, s, w, t0, L,
-                     (unsigned long long)Tn);
+hipError_t win_scan_units(const WinState& w, uint32_t L, void* tmp, size_t& tmp_bytes, hipStream_t s) {
+  return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, (const unsigned long long*)w.usize,
+                                          w.unit_off, (int)(L * w.nfine + 1), s);
+}
+
+hipError_t win_groupmap(const WinState& w, uint32_t L, hipStream_t s) {
+  const uint32_t units = L * w.nfine;
+  const uint32_t blocks = std::min<uint32_t>((units + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_groupmap, dim3(blocks ? blocks : 1), dim3(256), 0, s, w, L);
   return hipGetLastError();
 }
 
-hipError_t win_coarse_scan(const WinState& w, hipStream_t s) {
-  hipLaunchKernelGGL(k_coarse_scan, dim3(1), dim3(256), 0, s, w);
+// mode 0: count coarse buckets only; 1: write + per-tick stats; 2: write only
+hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, int mode,
+                      hipStream_t s) {
+  const uint32_t per_round =
+      w.stride * kExpandBlock <= kExpandSlots ? kExpandBlock : kExpandSlots / w.stride;
+  const uint64_t rounds = (Tn + per_round - 1) / per_round;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>(rounds, 8192);
+  const dim3 grid(blocks ? blocks : 1), blk(kExpandBlock);
+  const unsigned long long tn = Tn;
+  const int st = mode == 1 ? 1 : 0;
+  if (w.stride <= 8) {
+    if (mode) hipLaunchKernelGGL((k_expand<true, 8>), grid, blk, 0, s, w, t0, L, tn, st);
+    else hipLaunchKernelGGL((k_expand<false, 8>), grid, blk, 0, s, w, t0, L, tn, 0);
+  } else {
+    if (mode) hipLaunchKernelGGL((k_expand<true, kWinMaxStride>), grid, blk, 0, s, w, t0, L, tn, st);
+    else hipLaunchKernelGGL((k_expand<false, kWinMaxStride>), grid, blk, 0, s, w, t0, L, tn, 0);
+  }
   return hipGetLastError();
 }
 
-hipError_t win_part1(const WinState& w, uint64_t T, uint32_t L, hipStream_t s) {
-  const uint64_t tiles = (T + kPartTile - 1) / kPartTile;
-  hipLaunchKernelGGL(k_part1, dim3((uint32_t)tiles), dim3(256), 0, s, w, (unsigned long long)T, L);
+hipError_t win_plan(const WinState& w, bool exact, hipStream_t s) {
+  const uint32_t blocks = std::min<uint32_t>((w.nfine + 1 + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_plan, dim3(blocks), dim3(256), 0, s, w, exact);
   return hipGetLastError();
 }
 
@@ -472,6 +597,11 @@ hipError_t win_part2(const WinState& w, uint64_t T, bool scatter, hipStream_t s)
   return hipGetLastError();
 }
 
+hipError_t win_scan_fine(const WinState& w, void* tmp, size_t& tmp_bytes, hipStream_t s) {
+  return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, (const unsigned long long*)w.fhist,
+                                          w.fstart, (int)(w.nfine + 1), s);
+}
+
 hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s) {
   hipLaunchKernelGGL(k_resolve, dim3(w.nfine), dim3(kResolveBlock), 0, s, w, t0, L);
   return hipGetLastError();
@@ -480,16 +610,6 @@ hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s
 hipError_t win_schedule_one(const WinState& w, uint32_t node, uint32_t tick, hipStream_t s) {
   hipLaunchKernelGGL(k_schedule_one_win, dim3(1), dim3(1), 0, s, w, node, tick);
   return hipGetLastError();
-}
-
-hipError_t win_scan_units(const WinState& w, uint32_t L, void* tmp, size_t& tmp_bytes, hipStream_t s) {
-  return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, (const unsigned long long*)w.usize,
-                                          w.unit_off, (int)(L * w.nfine + 1), s);
-}
-
-hipError_t win_scan_fine(const WinState& w, void* tmp, size_t& tmp_bytes, hipStream_t s) {
-  return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, (const unsigned long long*)w.fhist,
-                                          w.fbase, (int)(w.nfine + 1), s);
 }
 
 }  // namespace gs

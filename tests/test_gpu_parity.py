@@ -135,6 +135,18 @@ def test_random_tables_bit_exact(gs, oracle, kw, stride, dlo, dhi):
     run_both(gs, oracle, kw, deg, ids)
 
 
+def test_skewed_targets_force_exact_partition(gs, oracle):
+    """Every friend of every node lies in [0, 16384): the window engine's
+    estimated coarse/fine regions overflow and the window is redone with exact
+    counts; the one hot bucket also takes k_resolve's global-streaming path."""
+    n = 5_000_000
+    rng = np.random.default_rng(7)
+    deg = np.full(n, 6, np.uint8)
+    ids = rng.integers(0, 16384, size=(n, 6)).astype(np.uint32)
+    kw = dict(BASE, n=n, delay_low=1, delay_high=2, drop_rate=0.0, crash_rate=0.02)
+    run_both(gs, oracle, kw, deg, ids, sender=10, ticks=8)
+
+
 def test_sender_argument_and_multi_tick_steps(gs, oracle):
     kw = dict(BASE, n=3000, crash_rate=0.02)
     deg, ids = random_table(3000, 6, 5, 6, seed=5)
