@@ -128,15 +128,21 @@ def main():
         tm = sim.timing()
         tot_r = sim.totals()
         kern_ms = tm["deliver_ms"] + tm["resolve_ms"]
-        launches = int(tm["deliver_launches"])
+        launches = int(tm["resolve_launches"])
         achieved = BYTES_PER_SEND * tot_r["sent"] / (kern_ms * 1e-3) / 1e9
+        per = {"k_expand": tm["expand_ms"], "k_plan+k_part2": tm["part_ms"],
+               "k_resolve": tm["resolve_ms"]}
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "kernel": "k_tick (COUNT+RESOLVE per tick)" if a.crashrate >= 0.01 else
-                          "k_tick (FLOOD per tick)",
+                "kernel": "window pipeline k_expand -> k_plan/k_part2 -> k_resolve "
+                          "(one launch of each per window)",
                 "avg_launch_us": round(kern_ms * 1e3 / max(launches, 1), 2),
-                "launches": launches, "bytes_per_launch": int(BYTES_PER_SEND * tot_r["sent"] /
-                                                              max(launches, 1))}
+                "launches": launches,
+                "bytes_per_launch": int(BYTES_PER_SEND * tot_r["sent"] / max(launches, 1)),
+                "kernels_avg_us": {k: round(v * 1e3 / max(launches, 1), 2) for k, v in per.items()},
+                "kernels_total_ms": {k: round(v, 3) for k, v in per.items()},
+                "exact_redos": int(tm["exact_redos"]),
+                "broadcast_device_ms": round(kern_ms, 3)}
         sim.set_flags(False)
 
     cpu = None

@@ -67,7 +67,8 @@ class Window(C.Structure):
 class Timing(C.Structure):
     _fields_ = [("deliver_ms", C.c_double), ("resolve_ms", C.c_double),
                 ("deliver_launches", C.c_uint64), ("resolve_launches", C.c_uint64),
-                ("overlay_ms", C.c_double)]
+                ("overlay_ms", C.c_double), ("expand_ms", C.c_double),
+                ("part_ms", C.c_double), ("windows", C.c_uint64), ("exact_redos", C.c_uint64)]
 
 
 _lib = None

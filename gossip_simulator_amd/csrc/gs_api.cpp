@@ -45,7 +45,6 @@ struct gs_ctx {
   struct Buf { void* p = nullptr; size_t bytes = 0; } gmap, cmsg, fmsg, tmp;
   unsigned long long* h_cap = nullptr;  // pinned [257] coarse region plan
   unsigned long long* h_misc = nullptr; // pinned scratch (counts, flags)
-  uint64_t exact_redos = 0;             // windows whose partition was redone exactly
 };
 
 namespace {
@@ -572,14 +571,22 @@ static int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing) {
     w.gmap = (uint32_t*)c->gmap.p;
     w.cmsg = (uint32_t*)c->cmsg.p;
     w.fmsg = (uint32_t*)c->fmsg.p;
-    hipEvent_t* e = timing ? &c->ev[(size_t)widx * 3] : nullptr;
-    if (e) CK(c, hipEventRecord(e[0], c->stream));
+    if (timing)
+      while (c->ev.size() < (size_t)(widx + 1) * 5) {
+        hipEvent_t ev;
+        CK(c, hipEventCreate(&ev));
+        c->ev.push_back(ev);
+      }
+    hipEvent_t* e = timing ? &c->ev[(size_t)widx * 5] : nullptr;
     if (T) {
       CK(c, hipMemcpyAsync(w.ccap, c->h_cap, 257 * 8, hipMemcpyHostToDevice, c->stream));
       CK(c, win_groupmap(w, L, c->stream));
+      if (e) CK(c, hipEventRecord(e[0], c->stream));
       CK(c, win_expand(w, t, L, Tn, 1, c->stream));
+      if (e) CK(c, hipEventRecord(e[1], c->stream));
       CK(c, win_plan(w, false, c->stream));
       CK(c, win_part2(w, T, true, c->stream));
+      if (e) CK(c, hipEventRecord(e[2], c->stream));
       // regions sized from estimates: check, and redo exactly on overflow
       CK(c, hipMemcpyAsync(c->h_misc, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
       CK(c, hipStreamSynchronize(c->stream));
@@ -607,19 +614,23 @@ static int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing) {
         CK(c, win_scan_fine(w, c->tmp.p, need2, c->stream));
         CK(c, hipMemsetAsync(w.ffill, 0, (size_t)w.nfine * 8, c->stream));
         CK(c, win_part2(w, T, true, c->stream));
-        ++c->exact_redos;
+        ++c->timing.exact_redos;
       }
+    } else if (e) {
+      CK(c, hipEventRecord(e[0], c->stream));
+      CK(c, hipEventRecord(e[1], c->stream));
+      CK(c, hipEventRecord(e[2], c->stream));
     }
     // the window's fire lists are consumed: later ticks t + R may reuse the slots
     const uint32_t s0 = t % w.R;
     const uint32_t first = std::min(L, w.R - s0);
     CK(c, hipMemsetAsync(w.fcount + (size_t)s0 * w.nfine, 0, (size_t)first * w.nfine * 4, c->stream));
     if (first < L) CK(c, hipMemsetAsync(w.fcount, 0, (size_t)(L - first) * w.nfine * 4, c->stream));
-    if (e) CK(c, hipEventRecord(e[1], c->stream));
+    if (e) CK(c, hipEventRecord(e[3], c->stream));
     if (T) CK(c, win_resolve(w, t, L, c->stream));
     if (e) {
-      CK(c, hipEventRecord(e[2], c->stream));
-      evs.emplace_back(widx * 3, T ? 1u : 0u);
+      CK(c, hipEventRecord(e[4], c->stream));
+      evs.emplace_back(widx * 5, T ? 1u : 0u);
     }
     ++widx;
     done += L;
@@ -630,11 +641,16 @@ static int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing) {
       hipEvent_t* e = &c->ev[pr.first];
       float ms = 0;
       CK(c, hipEventElapsedTime(&ms, e[0], e[1]));
+      c->timing.expand_ms += ms;
       c->timing.deliver_ms += ms;
       CK(c, hipEventElapsedTime(&ms, e[1], e[2]));
+      c->timing.part_ms += ms;
+      c->timing.deliver_ms += ms;
+      CK(c, hipEventElapsedTime(&ms, e[3], e[4]));
       c->timing.resolve_ms += ms;
       c->timing.deliver_launches += pr.second;
       c->timing.resolve_launches += pr.second;
+      c->timing.windows += 1;
     }
   }
   uint32_t err = 0;
@@ -661,7 +677,7 @@ int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
                          c->stream));
     if (first < batch)
       CK(c, hipMemsetAsync(c->st.stats, 0, (size_t)(batch - first) * kStatFields * 8, c->stream));
-    const uint32_t nev = timing ? batch * (c->win ? 3 : flood ? 2 : 4) : 0;
+    const uint32_t nev = timing && !c->win ? batch * (flood ? 2 : 4) : 0;
     while (c->ev.size() < nev) {
       hipEvent_t e;
       CK(c, hipEventCreate(&e));

@@ -205,7 +205,9 @@ __global__ void k_plan(const WinState w, bool exact) {
   const unsigned long long cnt = w.cfill[tid] < w.ccap[tid + 1] - w.ccap[tid]
                                      ? w.cfill[tid] : w.ccap[tid + 1] - w.ccap[tid];
   const bool live = tid < w.ncoarse;
-  s_cap[tid] = live ? (cnt + cnt / 8 + 255) / 256 + 512 : 0;
+  // the last coarse bucket may hold fewer than 256 fine buckets
+  const uint32_t nf = live ? min(256u, w.nfine - tid * 256) : 1u;
+  s_cap[tid] = live ? (cnt + cnt / 8 + nf - 1) / nf + 512 : 0;
   s_base[tid + 1] = s_cap[tid] * 256;
   s_tp[tid + 1] = live ? (uint32_t)((cnt + kPartTile - 1) / kPartTile) : 0;
   if (tid == 0) { s_base[0] = 0; s_tp[0] = 0; }

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 1
+#define GS_ABI_VERSION 2
 
 enum {
   GS_OK = 0,
@@ -81,13 +81,20 @@ typedef struct gs_window {
   uint64_t breakups;  /* BreakUps in the window (:77)                         */
 } gs_window;
 
-/* Device time spent in the broadcast tick kernels (GS_FLAG_TIMING). */
+/* Device time spent in the broadcast kernels (GS_FLAG_TIMING), from HIP
+ * events on the context's stream.  Tick engine: deliver = the per-tick
+ * delivery kernel, resolve = its second (kc > 0) pass.  Window engine:
+ * deliver = expand + partition (expand_ms + part_ms), resolve = k_resolve. */
 typedef struct gs_timing {
-  double deliver_ms;       /* sum over launches of the delivery kernel       */
-  double resolve_ms;       /* sum over launches of the resolve kernel (kc>0) */
+  double deliver_ms;       /* sum over launches of the delivery kernel(s)    */
+  double resolve_ms;       /* sum over launches of the resolve kernel        */
   uint64_t deliver_launches;
   uint64_t resolve_launches;
   double overlay_ms;       /* wall time of the last gs_build_overlay          */
+  double expand_ms;        /* window engine: k_expand (row gather + coarse partition) */
+  double part_ms;          /* window engine: k_plan + k_part2 (fine partition)        */
+  uint64_t windows;        /* window engine: windows processed                */
+  uint64_t exact_redos;    /* window engine: windows re-partitioned exactly   */
 } gs_timing;
 
 /* gs_run status */
