@@ -223,6 +223,15 @@ int validate_table(gs_ctx* c) {
   return GS_OK;
 }
 
+// The window engine reads friend rows without the length byte: slots past a
+// node's list are set to kEmptyMsg on the device copy.
+int seal_rows(gs_ctx* c) {
+  if (!c->win) return GS_OK;
+  CK(c, win_seal_rows(c->d_deg, c->d_ids, c->p.n, c->st.stride, c->stream));
+  CK(c, hipStreamSynchronize(c->stream));
+  return GS_OK;
+}
+
 bool covered(uint64_t recv, uint64_t n) {
   // simulator.go:246-248, in float32
   volatile float a = (float)recv, b = (float)n;
@@ -409,6 +418,8 @@ int gs_load_peers(gs_ctx* c, const uint8_t* deg, const uint32_t* ids, uint32_t s
   }
   rc = validate_table(c);
   if (rc) return rc;
+  rc = seal_rows(c);
+  if (rc) return rc;
   c->peers = true;
   return GS_OK;
 }
@@ -423,6 +434,8 @@ int gs_load_peers_device(gs_ctx* c, const void* d_deg, const void* d_ids, uint32
   CK(c, hipMemcpyAsync(c->d_deg, d_deg, c->p.n, hipMemcpyDeviceToDevice, c->stream));
   CK(c, hipMemcpyAsync(c->d_ids, d_ids, c->p.n * stride * 4ull, hipMemcpyDeviceToDevice, c->stream));
   rc = validate_table(c);
+  if (rc) return rc;
+  rc = seal_rows(c);
   if (rc) return rc;
   c->peers = true;
   return GS_OK;
@@ -474,6 +487,8 @@ int gs_build_overlay(gs_ctx* c, uint64_t max_ticks, gs_window* win, size_t cap, 
   if (nwin) *nwin = ws.n;
   if (final_tick) *final_tick = res.final_tick;
   if (rc) return fail(c, rc, res.msg);
+  rc = seal_rows(c);
+  if (rc) return rc;
   c->peers = true;
   return GS_OK;
 }

@@ -130,6 +130,8 @@ hipError_t win_plan(const WinState& w, bool exact, hipStream_t s);
 hipError_t win_scan_fine(const WinState& w, void* tmp, size_t& tmp_bytes, hipStream_t s);
 hipError_t win_part2(const WinState& w, uint64_t T, bool scatter, hipStream_t s);
 hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
+hipError_t win_seal_rows(const uint8_t* deg, uint32_t* ids, uint64_t n, uint32_t stride,
+                         hipStream_t s);
 hipError_t win_schedule_one(const WinState& w, uint32_t node, uint32_t tick, hipStream_t s);
 
 // Launchers (gs_broadcast.hip).

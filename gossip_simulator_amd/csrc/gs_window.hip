@@ -35,7 +35,8 @@ namespace gs {
 namespace {
 
 constexpr uint32_t kExpandBlock = 256;
-constexpr uint32_t kExpandSlots = 4096;   // LDS message slots per expand round
+constexpr uint32_t kExpandNpt = 4;        // firing nodes per thread per round (rows <= 8)
+constexpr uint32_t kExpandSlots = kExpandBlock * kExpandNpt * 8;  // LDS message slots per round
 constexpr uint32_t kResolveBlock = 512;
 constexpr uint32_t kResolveMsgCap = 8192;
 
@@ -107,51 +108,82 @@ __device__ __forceinline__ void block_scan256(uint32_t* cnt, uint32_t* off) {
   }
 }
 
-// Expand + coarse partition.  WRITE=false only counts (exact fallback).
-// Expand + coarse partition; a thread's messages stay in registers (MAXS >=
-// stride) so the LDS footprint is the 4096-entry sort buffer only.
-template <bool WRITE, uint32_t MAXS>
+// Friends row of v into registers; slots past the list hold kEmptyMsg (rows
+// are sealed by k_seal_rows, so the length byte is not read).
+template <uint32_t MAXS>
+__device__ __forceinline__ void load_row(const WinState& w, uint32_t v, uint32_t (&mm)[MAXS]) {
+  const uint32_t S = w.stride;
+  if ((S & 1) == 0) {
+    const uint2* row = reinterpret_cast<const uint2*>(w.ids + (size_t)v * S);
+#pragma unroll
+    for (uint32_t j = 0; j < MAXS; j += 2) {
+      const uint2 x = 2 * j < 2 * S ? row[j / 2] : make_uint2(kEmptyMsg, kEmptyMsg);
+      mm[j] = x.x;
+      if (j + 1 < MAXS) mm[j + 1] = x.y;
+    }
+  } else {
+    const uint32_t* row = w.ids + (size_t)v * S;
+#pragma unroll
+    for (uint32_t j = 0; j < MAXS; ++j) mm[j] = j < S ? row[j] : kEmptyMsg;
+  }
+}
+
+// Expand + coarse partition (Node.Broadcast, simulator.go:141-147).  Each
+// thread takes NPT firing nodes per round; their rows are all in flight before
+// any is used.  Kept targets are counting-sorted in LDS by coarse bucket and
+// leave as coalesced runs, one global reservation per (round, bucket).
+// WRITE=false only counts (exact fallback).
+template <bool WRITE, uint32_t MAXS, uint32_t NPT>
 __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint32_t t0, uint32_t L,
                                                          unsigned long long Tn, int add_stats) {
   __shared__ ExpandLds sm;
   const uint32_t tid = threadIdx.x;
   const uint32_t units = L * w.nfine;
-  const uint32_t S = w.stride;
-  const uint32_t per_round = S * kExpandBlock <= kExpandSlots ? kExpandBlock : kExpandSlots / S;
+  constexpr uint32_t per_round = kExpandBlock * NPT;
   const uint32_t c3drop = ctr3(K_DROP, w.key.trial);
   if (tid < kMaxWindow * 2) (&sm.acc[0][0])[tid] = 0;
   const unsigned long long rounds = (Tn + per_round - 1) / per_round;
   for (unsigned long long rd = blockIdx.x; rd < rounds; rd += gridDim.x) {
     sm.cnt[tid] = 0;
     __syncthreads();
-    const unsigned long long g = rd * per_round + tid;
-    const bool active = tid < per_round && g < Tn;
-    uint32_t mm[MAXS], mt[MAXS];  // message, bin | rank << 8 (~0u = none)
+    uint32_t mm[NPT][MAXS], mt[NPT][MAXS];  // message, bin | rank << 8 (~0u = none)
+    uint32_t vv[NPT], kk[NPT];
 #pragma unroll
-    for (uint32_t j = 0; j < MAXS; ++j) mt[j] = ~0u;
-    if (active) {
-      const uint32_t u = unit_of(w, g, Tn, units);
-      const uint32_t k = u / w.nfine, f = u - k * w.nfine;
-      const uint32_t t = t0 + k;
-      const uint32_t s = t % w.R;
-      const uint32_t i = (uint32_t)(g - w.unit_off[u]);
-      const uint32_t v = (f << kFineLog) + w.flist[((size_t)s * w.nfine + f) * kFineNodes + i];
-      const uint32_t d = w.deg[v];
-      const uint32_t* row = w.ids + (size_t)v * S;
+    for (uint32_t q = 0; q < NPT; ++q) {
+      const unsigned long long g = rd * per_round + q * kExpandBlock + tid;
+      vv[q] = ~0u;
+      kk[q] = 0;
+      if (g < Tn) {
+        const uint32_t u = unit_of(w, g, Tn, units);
+        const uint32_t k = u / w.nfine, f = u - k * w.nfine;
+        const uint32_t s = (t0 + k) % w.R;
+        const uint32_t i = (uint32_t)(g - w.unit_off[u]);
+        vv[q] = (f << kFineLog) + w.flist[((size_t)s * w.nfine + f) * kFineNodes + i];
+        kk[q] = k;
+      }
+    }
 #pragma unroll
-      for (uint32_t j = 0; j < MAXS; ++j) mm[j] = j < S ? row[j] : 0u;  // whole row in flight
+    for (uint32_t q = 0; q < NPT; ++q) {
+#pragma unroll
+      for (uint32_t j = 0; j < MAXS; ++j) { mm[q][j] = kEmptyMsg; mt[q][j] = ~0u; }
+      if (vv[q] != ~0u) load_row<MAXS>(w, vv[q], mm[q]);  // all rows in flight
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < NPT; ++q) {
+      if (vv[q] == ~0u) continue;
+      const uint32_t v = vv[q], k = kk[q], t = t0 + k;
       uint32_t sent = 0;
 #pragma unroll
       for (uint32_t jg = 0; jg < MAXS / 4; ++jg) {
-        if (jg * 4 >= d) break;
+        if (mm[q][jg * 4] == kEmptyMsg) break;
         const u32x4 r = philox(v, t, jg, c3drop, w.key.k0, w.key.k1);   // :144, :172
 #pragma unroll
         for (uint32_t jj = 0; jj < 4; ++jj) {
           const uint32_t j = jg * 4 + jj;
-          if (j < d && (int32_t)uniform(lane_of(r, jj), 100u) >= w.kd) {   // kept: :145
-            const uint32_t bin = mm[j] >> kCoarseShift;
-            mt[j] = bin | (atomicAdd(&sm.cnt[bin], 1u) << 8);
-            mm[j] = (mm[j] & ((1u << kCoarseShift) - 1)) | (k << kCoarseShift);
+          if (mm[q][j] != kEmptyMsg && (int32_t)uniform(lane_of(r, jj), 100u) >= w.kd) {  // kept: :145
+            const uint32_t bin = mm[q][j] >> kCoarseShift;
+            mt[q][j] = bin | (atomicAdd(&sm.cnt[bin], 1u) << 8);
+            mm[q][j] = (mm[q][j] & ((1u << kCoarseShift) - 1)) | (k << kCoarseShift);
             ++sent;
           }
         }
@@ -172,12 +204,14 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
     }
     __syncthreads();
 #pragma unroll
-    for (uint32_t j = 0; j < MAXS; ++j)
-      if (mt[j] != ~0u) {
-        const uint32_t bin = mt[j] & 255, p = sm.off[bin] + (mt[j] >> 8);
-        sm.sorted[p] = mm[j];
-        sm.sbin[p] = (uint8_t)bin;
-      }
+    for (uint32_t q = 0; q < NPT; ++q)
+#pragma unroll
+      for (uint32_t j = 0; j < MAXS; ++j)
+        if (mt[q][j] != ~0u) {
+          const uint32_t bin = mt[q][j] & 255, p = sm.off[bin] + (mt[q][j] >> 8);
+          sm.sorted[p] = mm[q][j];
+          sm.sbin[p] = (uint8_t)bin;
+        }
     __syncthreads();
     const uint32_t total = sm.off[256];
     for (uint32_t p = tid; p < total; p += kExpandBlock) {
@@ -192,6 +226,16 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
     const uint32_t k = tid >> 1, fld = tid & 1;
     const unsigned long long v = sm.acc[k][fld];
     if (v) atomicAdd(&w.stats[(size_t)((t0 + k) % kStatSlots) * kStatFields + (fld ? ST_SENT : ST_FIRED)], v);
+  }
+}
+
+// Slots past a node's friends list become kEmptyMsg (the window engine's
+// expand reads rows without the length byte).
+__global__ void k_seal_rows(const uint8_t* deg, uint32_t* ids, uint64_t n, uint32_t stride) {
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
+       v += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t d = deg[v];
+    for (uint32_t j = d; j < stride; ++j) ids[v * stride + j] = kEmptyMsg;
   }
 }
 
@@ -568,20 +612,27 @@ hipError_t win_groupmap(const WinState& w, uint32_t L, hipStream_t s) {
 // mode 0: count coarse buckets only; 1: write + per-tick stats; 2: write only
 hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, int mode,
                       hipStream_t s) {
-  const uint32_t per_round =
-      w.stride * kExpandBlock <= kExpandSlots ? kExpandBlock : kExpandSlots / w.stride;
+  const uint32_t per_round = w.stride <= 8 ? kExpandBlock * kExpandNpt : kExpandBlock;
   const uint64_t rounds = (Tn + per_round - 1) / per_round;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>(rounds, 8192);
   const dim3 grid(blocks ? blocks : 1), blk(kExpandBlock);
   const unsigned long long tn = Tn;
   const int st = mode == 1 ? 1 : 0;
   if (w.stride <= 8) {
-    if (mode) hipLaunchKernelGGL((k_expand<true, 8>), grid, blk, 0, s, w, t0, L, tn, st);
-    else hipLaunchKernelGGL((k_expand<false, 8>), grid, blk, 0, s, w, t0, L, tn, 0);
+    if (mode) hipLaunchKernelGGL((k_expand<true, 8, kExpandNpt>), grid, blk, 0, s, w, t0, L, tn, st);
+    else hipLaunchKernelGGL((k_expand<false, 8, kExpandNpt>), grid, blk, 0, s, w, t0, L, tn, 0);
   } else {
-    if (mode) hipLaunchKernelGGL((k_expand<true, kWinMaxStride>), grid, blk, 0, s, w, t0, L, tn, st);
-    else hipLaunchKernelGGL((k_expand<false, kWinMaxStride>), grid, blk, 0, s, w, t0, L, tn, 0);
+    if (mode) hipLaunchKernelGGL((k_expand<true, kWinMaxStride, 1>), grid, blk, 0, s, w, t0, L, tn, st);
+    else hipLaunchKernelGGL((k_expand<false, kWinMaxStride, 1>), grid, blk, 0, s, w, t0, L, tn, 0);
   }
+  return hipGetLastError();
+}
+
+hipError_t win_seal_rows(const uint8_t* deg, uint32_t* ids, uint64_t n, uint32_t stride,
+                         hipStream_t s) {
+  const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_seal_rows, dim3((uint32_t)(blocks ? blocks : 1)), dim3(256), 0, s, deg, ids, n,
+                     stride);
   return hipGetLastError();
 }
 
