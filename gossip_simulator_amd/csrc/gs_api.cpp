@@ -671,7 +671,7 @@ static int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing) {
   uint32_t err = 0;
   CK(c, hipMemcpyAsync(&err, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
   CK(c, hipStreamSynchronize(c->stream));
-  if (err & 4) return fail(c, GS_EOVERFLOW, "more than 65535 arrivals at one node in one tick");
+  if (err & 4) return fail(c, GS_EOVERFLOW, "too many arrivals at one node in one tick");
   return GS_OK;
 }
 

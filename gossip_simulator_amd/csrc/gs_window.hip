@@ -349,73 +349,48 @@ __global__ __launch_bounds__(256) void k_part2(const WinState w) {
   }
 }
 
+constexpr uint32_t kResolveWaves = kResolveBlock / 64;
+constexpr uint32_t kWaveNodesLog = kFineLog - 3;        // 2048 nodes owned per wave
+constexpr uint32_t kBins = kResolveWaves * kMaxWindow;   // (owner wave, tick) bins
+static_assert(kResolveWaves == 8, "wave ownership assumes 8 waves per workgroup");
+
 struct ResolveLds {
+  uint32_t cnt[kFineNodes / 2];     // u16 per node: arrival ordinal counter (cmin after a roll)
+  uint32_t rolled[kFineNodes / 32]; // node had a crash roll in the current tick
   uint32_t recv[kFineNodes / 32];
   uint32_t crash[kFineNodes / 32];
-  uint32_t cnt[kFineNodes / 2];  // two u16 counters per word: arrivals, then offsets
-  uint32_t fc[kWinMaxRing];      // fire-list lengths of this bucket, per ring slot
-  uint32_t st[kMaxWindow][4];    // msgs, recv, crash, sched per tick
+  uint32_t buf[kResolveMsgCap];     // messages sorted by (owner wave, tick)
+  uint32_t bstart[kBins + 1];
+  uint32_t bfill[kBins];
+  uint32_t fc[kWinMaxRing];         // fire-list lengths of this bucket, per ring slot
+  uint32_t st[kMaxWindow][4];       // msgs, recv, crash, sched per tick
   uint32_t wsum[kResolveBlock / 64];
   uint32_t err;
-  uint32_t msg[kResolveMsgCap];  // the bucket's messages, sorted by node
-};  // ~69 KB: two workgroups per CU
+};  // ~71 KB: two workgroups per CU
+
+// buf entry after the ordinal pass: loc | i << 14 | ROLL | DEAD | INF
+constexpr uint32_t kOrdShift = kFineLog;
+constexpr uint32_t kOrdMask = 0x1FFFu;       // ordinals < 8191 (kResolveMsgCap)
+constexpr uint32_t kRollBit = 1u << 27;
+constexpr uint32_t kDeadBit = 1u << 28;
+constexpr uint32_t kInfBit = 1u << 29;
 
 __device__ __forceinline__ uint32_t cnt16(const ResolveLds& sm, uint32_t i) {
   return (sm.cnt[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
 }
 
-// Node-major resolve of one node: its messages sorted[b, e) (any tick order)
-// are replayed tick by tick, ordinals in order (simulator.go:107-123).
-__device__ __forceinline__ void resolve_node_major(const WinState& w, ResolveLds& sm, uint32_t f,
-                                                   uint32_t loc, uint32_t b, uint32_t e,
-                                                   uint32_t t0, uint32_t c3crash) {
-  uint32_t mask = 0;
-  for (uint32_t p = b; p < e; ++p) mask |= 1u << (sm.msg[p] >> kFineLog);
-  const uint32_t u = (f << kFineLog) + loc, bit = 1u << (loc & 31), wi = loc >> 5;
-  bool crashed = (sm.crash[wi] & bit) != 0;
-  const bool was_crashed = crashed;
-  bool received = (sm.recv[wi] & bit) != 0;
-  const bool was_received = received;
-  while (mask) {
-    const uint32_t k = __builtin_ctz(mask);
-    mask &= mask - 1;
-    uint32_t kk = 0;
-    for (uint32_t p = b; p < e; ++p) kk += (sm.msg[p] >> kFineLog) == k;
-    const uint32_t t = t0 + k;
-    uint32_t cm = 0, cr = 0, cc = 0, cs = 0;
-    u32x4 r{0, 0, 0, 0};
-    for (uint32_t i = 0; i < kk; ++i) {
-      if (crashed) break;                                          // :108
-      ++cm;                                                        // :111
-      if (w.kc > 0) {
-        if ((i & 3) == 0) r = philox(u, t, i >> 2, c3crash, w.key.k0, w.key.k1);
-        if ((int32_t)uniform(lane_of(r, i & 3), 100u) < w.kc) {   // :112-115
-          ++cc;
-          crashed = true;
-          break;
-        }
-      }
-      if (received) continue;                                      // :117
-      received = true;                                             // :120
-      ++cr;                                                        // :121
-      // Broadcast() (:122, :141-142): fire at t + off
-      const uint32_t off = fire_offset(w.delay_low, w.delay_span, draw0(w.key, K_DELAY, u, t, 0));
-      const uint32_t s = (t + off) % w.R;
-      const uint32_t pos = atomicAdd(&sm.fc[s], 1u);
-      w.flist[((size_t)s * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
-      ++cs;
-    }
-    if (cm) atomicAdd(&sm.st[k][0], cm);
-    if (cr) atomicAdd(&sm.st[k][1], cr);
-    if (cc) atomicAdd(&sm.st[k][2], cc);
-    if (cs) atomicAdd(&sm.st[k][3], cs);
-  }
-  if (crashed && !was_crashed) atomicOr(&sm.crash[wi], bit);
-  if (received && !was_received) atomicOr(&sm.recv[wi], bit);
+// Orders one wave's LDS accesses between phases: the wave's lanes exchange
+// per-node state through LDS, and a wave's LDS operations complete in order.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
 }
+
+__device__ __forceinline__ uint32_t popc_ballot(bool x) { return (uint32_t)__popcll(__ballot(x)); }
 
 // The receive case of Node.Start (simulator.go:107-123) for node `loc` of the
 // bucket with kk arrivals at tick t: ordinals 0..kk-1, keyed crash rolls.
+// (Large-bucket path.)
 __device__ __forceinline__ void resolve_node(const WinState& w, ResolveLds& sm, uint32_t f,
                                              uint32_t loc, uint32_t kk, uint32_t t, uint32_t c3crash,
                                              uint32_t& cm, uint32_t& cr, uint32_t& cc, uint32_t& cs) {
@@ -448,8 +423,9 @@ __device__ __forceinline__ void resolve_node(const WinState& w, ResolveLds& sm, 
   }
 }
 
-// One tick's receipts over messages m[lo, hi): count arrivals per node, then
-// the lane whose atomicAnd takes a node's nonzero count resolves that node.
+// One tick's receipts over messages m[lo, hi) (large buckets, streamed from
+// global memory): count arrivals per node, then the lane whose atomicAnd takes
+// a node's nonzero count resolves that node.
 template <class Src>
 __device__ __forceinline__ void resolve_tick(const WinState& w, ResolveLds& sm, uint32_t f,
                                              const Src& src, uint32_t lo, uint32_t hi, uint32_t k,
@@ -478,6 +454,117 @@ __device__ __forceinline__ void resolve_tick(const WinState& w, ResolveLds& sm, 
   __syncthreads();
 }
 
+// One (owner wave, tick) bin of the receive case, lane per message
+// (simulator.go:107-123).  Rule A6: with k arrivals at node u in tick t the
+// ordinals i = 0..k-1 are processed in order; ordinal i is counted unless an
+// earlier ordinal crashed the node, rolls crash with U_100(u, t, i) < kc, and
+// ordinal 0 infects a node not yet received unless it crashes.  So every
+// message needs only its ordinal (an LDS atomic), its own roll and the node's
+// first crashing ordinal cmin: counted = i <= cmin, crash = i == cmin,
+// infect = i == 0 && !roll && !received.  The wave owns every node of its
+// messages, so the phases are ordered by wave_sync() alone.
+__device__ __forceinline__ void resolve_bin(const WinState& w, ResolveLds& sm, uint32_t f,
+                                            uint32_t b, uint32_t e, uint32_t k, uint32_t t,
+                                            uint32_t c3crash, uint32_t c3delay) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t node0 = f << kFineLog;
+  bool any_roll = false;
+  // A: ordinal and crash roll of each message at a live node
+  for (uint32_t p = b + lane; p < e; p += 64) {
+    const uint32_t loc = sm.buf[p] & (kFineNodes - 1), bit = 1u << (loc & 31);
+    if (sm.crash[loc >> 5] & bit) { sm.buf[p] = kDeadBit; continue; }   // :108
+    const uint32_t sh = (loc & 1) * 16;
+    uint32_t i = (atomicAdd(&sm.cnt[loc >> 1], 1u << sh) >> sh) & 0xFFFFu;
+    if (i >= kOrdMask) { sm.err = 1; i = kOrdMask - 1; }
+    bool roll = false;
+    if (w.kc > 0) {
+      const u32x4 r = philox(node0 + loc, t, i >> 2, c3crash, w.key.k0, w.key.k1);
+      roll = (int32_t)uniform(lane_of(r, i & 3), 100u) < w.kc;              // :112
+    }
+    sm.buf[p] = loc | (i << kOrdShift) | (roll ? kRollBit : 0u);
+    any_roll |= roll;
+  }
+  wave_sync();
+  // B (rare): the node's count becomes the minimum crashing ordinal
+  if (__ballot(any_roll)) {
+    for (uint32_t p = b + lane; p < e; p += 64) {
+      const uint32_t m = sm.buf[p];
+      if (!(m & kRollBit)) continue;
+      const uint32_t loc = m & (kFineNodes - 1);
+      atomicOr(&sm.cnt[loc >> 1], 0xFFFFu << ((loc & 1) * 16));
+      atomicOr(&sm.rolled[loc >> 5], 1u << (loc & 31));
+    }
+    wave_sync();
+    for (uint32_t p = b + lane; p < e; p += 64) {
+      const uint32_t m = sm.buf[p];
+      if (!(m & kRollBit)) continue;
+      const uint32_t loc = m & (kFineNodes - 1), sh = (loc & 1) * 16;
+      const uint32_t i = (m >> kOrdShift) & kOrdMask;
+      uint32_t old = sm.cnt[loc >> 1];
+      while (((old >> sh) & 0xFFFFu) > i) {
+        const uint32_t nw = (old & ~(0xFFFFu << sh)) | (i << sh);
+        const uint32_t got = atomicCAS(&sm.cnt[loc >> 1], old, nw);
+        if (got == old) break;
+        old = got;
+      }
+    }
+    wave_sync();
+  }
+  // C: counted / crash / infect
+  uint32_t cm = 0, cc = 0, cr = 0;
+  for (uint32_t p = b + lane; p < e; p += 64) {
+    const uint32_t m = sm.buf[p];
+    const bool live = !(m & kDeadBit);
+    const uint32_t loc = m & (kFineNodes - 1), bit = 1u << (loc & 31);
+    const uint32_t i = (m >> kOrdShift) & kOrdMask;
+    const bool roll = (m & kRollBit) != 0;
+    uint32_t cmin = 0xFFFFu;
+    if (live && (sm.rolled[loc >> 5] & bit)) cmin = cnt16(sm, loc);
+    const bool counted = live && i <= cmin;                                  // :111
+    const bool crashm = live && roll && i == cmin;                           // :113-115
+    const bool infect = live && i == 0 && !roll && !(sm.recv[loc >> 5] & bit);  // :117-121
+    cm += popc_ballot(counted);
+    cc += popc_ballot(crashm);
+    cr += popc_ballot(infect);
+    if (crashm) atomicOr(&sm.crash[loc >> 5], bit);
+    if (infect) {
+      atomicOr(&sm.recv[loc >> 5], bit);
+      sm.buf[p] = m | kInfBit;
+    }
+  }
+  wave_sync();
+  // D: clear the per-node tick state; compact the infections to the bin's front
+  uint32_t ninf = 0;
+  for (uint32_t p0 = b; p0 < e; p0 += 64) {
+    const uint32_t p = p0 + lane;
+    const uint32_t m = p < e ? sm.buf[p] : kDeadBit;
+    const uint32_t loc = m & (kFineNodes - 1);
+    if (!(m & kDeadBit)) {
+      atomicAnd(&sm.cnt[loc >> 1], ~(0xFFFFu << ((loc & 1) * 16)));
+      if (m & kRollBit) atomicAnd(&sm.rolled[loc >> 5], ~(1u << (loc & 31)));
+    }
+    const bool inf = (m & kInfBit) != 0;
+    const unsigned long long bal = __ballot(inf);
+    if (inf) sm.buf[b + ninf + (uint32_t)__popcll(bal & ((1ull << lane) - 1))] = loc;
+    ninf += (uint32_t)__popcll(bal);
+  }
+  wave_sync();
+  // E: Broadcast() of each infected node (:122, :141-142): fire at t + off
+  for (uint32_t q = lane; q < ninf; q += 64) {
+    const uint32_t loc = sm.buf[b + q];
+    const uint32_t off = fire_offset(w.delay_low, w.delay_span,
+                                     philox(node0 + loc, t, 0, c3delay, w.key.k0, w.key.k1).x);
+    const uint32_t s = (t + off) % w.R;
+    const uint32_t pos = atomicAdd(&sm.fc[s], 1u);
+    w.flist[((size_t)s * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
+  }
+  if (lane == 0) {
+    if (cm) atomicAdd(&sm.st[k][0], cm);
+    if (cr) { atomicAdd(&sm.st[k][1], cr); atomicAdd(&sm.st[k][3], cr); }
+    if (cc) atomicAdd(&sm.st[k][2], cc);
+  }
+}
+
 __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
   __shared__ ResolveLds sm;
   const uint32_t f = blockIdx.x, tid = threadIdx.x;
@@ -490,75 +577,63 @@ __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uin
   const uint32_t* cg = (const uint32_t*)w.crash;
   const uint64_t nw32 = w.W * 2;
   const uint32_t* gm = w.fmsg + mb;
-  // issue every global load of the block up front: messages, bits, list lengths
   constexpr uint32_t kPerThread = kResolveMsgCap / kResolveBlock;
+  static_assert(kFineNodes / 32 == kResolveBlock, "one bit word per thread");
   uint32_t mr[kPerThread];
-  const bool small = M <= kResolveMsgCap;
+  const bool small = M < kResolveMsgCap;
 #pragma unroll
   for (uint32_t i = 0; i < kPerThread; ++i) {
     const uint32_t p = tid + i * kResolveBlock;
     mr[i] = small && p < M ? gm[p] : ~0u;
   }
-  for (uint32_t i = tid; i < kFineNodes / 32; i += kResolveBlock) {
-    const bool in = wbase + i < nw32;
-    sm.recv[i] = in ? rg[wbase + i] : 0u;
-    sm.crash[i] = in ? cg[wbase + i] : 0u;
+  const bool in = wbase + tid < nw32;
+  const uint32_t recv0 = in ? rg[wbase + tid] : 0u, crash0 = in ? cg[wbase + tid] : 0u;
+  sm.recv[tid] = recv0;
+  sm.crash[tid] = crash0;
+  sm.rolled[tid] = 0;
+  {
+    uint4* c4 = reinterpret_cast<uint4*>(sm.cnt);
+    for (uint32_t i = tid; i < kFineNodes / 8; i += kResolveBlock) c4[i] = make_uint4(0, 0, 0, 0);
   }
-  for (uint32_t i = tid; i < kFineNodes / 2; i += kResolveBlock) sm.cnt[i] = 0;
   for (uint32_t s = tid; s < w.R; s += kResolveBlock) sm.fc[s] = w.fcount[(size_t)s * w.nfine + f];
   if (tid < kMaxWindow * 4) (&sm.st[0][0])[tid] = 0;
+  if (tid < kBins) sm.bfill[tid] = 0;
   if (tid == 0) sm.err = 0;
-  const uint32_t c3crash = ctr3(K_CRASH, w.key.trial);
+  const uint32_t c3crash = ctr3(K_CRASH, w.key.trial), c3delay = ctr3(K_DELAY, w.key.trial);
   __syncthreads();
   if (small) {
-    // counting sort of the bucket's messages by node (u16 counters -> offsets)
+    // counting sort by (owner wave, tick)
 #pragma unroll
     for (uint32_t i = 0; i < kPerThread; ++i)
-      if (mr[i] != ~0u) {
-        const uint32_t loc = mr[i] & (kFineNodes - 1);
-        atomicAdd(&sm.cnt[loc >> 1], 1u << ((loc & 1) * 16));
-      }
+      if (mr[i] != ~0u)
+        atomicAdd(&sm.bfill[((mr[i] & (kFineNodes - 1)) >> kWaveNodesLog) * kMaxWindow + (mr[i] >> kFineLog)], 1u);
     __syncthreads();
-    {  // exclusive scan of 16384 u16 counters: 32 per thread (M <= 8192 fits u16)
-      constexpr uint32_t kPer = kFineNodes / kResolveBlock;  // 32
-      uint32_t* wp = &sm.cnt[tid * (kPer / 2)];
-      uint32_t sum = 0;
-#pragma unroll
-      for (uint32_t i = 0; i < kPer / 2; ++i) sum += (wp[i] & 0xFFFFu) + (wp[i] >> 16);
-      const uint32_t lane = tid & 63, wv = tid >> 6;
-      uint32_t x = sum;
+    if (tid < 64) {  // exclusive scan of the 128 bins, 2 per lane
+      const uint32_t a = sm.bfill[2 * tid], c = sm.bfill[2 * tid + 1];
+      uint32_t x = a + c;
 #pragma unroll
       for (uint32_t o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
+        if (tid >= o) x += y;
       }
-      if (lane == 63) sm.wsum[wv] = x;
-      __syncthreads();
-      uint32_t base = x - sum;
-      for (uint32_t v = 0; v < wv; ++v) base += sm.wsum[v];
-#pragma unroll
-      for (uint32_t i = 0; i < kPer / 2; ++i) {
-        const uint32_t a = wp[i] & 0xFFFFu, b = wp[i] >> 16;
-        wp[i] = base | ((base + a) << 16);
-        base += a + b;
-      }
+      sm.bstart[2 * tid] = x - a - c;
+      sm.bstart[2 * tid + 1] = x - c;
+      if (tid == 63) sm.bstart[kBins] = x;
+      sm.bfill[2 * tid] = x - a - c;
+      sm.bfill[2 * tid + 1] = x - c;
     }
     __syncthreads();
 #pragma unroll
     for (uint32_t i = 0; i < kPerThread; ++i)
       if (mr[i] != ~0u) {
-        const uint32_t m = mr[i], loc = m & (kFineNodes - 1), sh = (loc & 1) * 16;
-        const uint32_t pos = (atomicAdd(&sm.cnt[loc >> 1], 1u << sh) >> sh) & 0xFFFFu;
-        sm.msg[pos] = m;
+        const uint32_t bin = ((mr[i] & (kFineNodes - 1)) >> kWaveNodesLog) * kMaxWindow + (mr[i] >> kFineLog);
+        sm.buf[atomicAdd(&sm.bfill[bin], 1u)] = mr[i] & (kFineNodes - 1);
       }
     __syncthreads();
-    // cnt now holds each node's END offset.  The lane holding the first
-    // message of a node's run (a "segment head") resolves that node: every
-    // lane sits on a message, and most messages head a run of their own.
-    for (uint32_t p = tid; p < M; p += kResolveBlock) {
-      const uint32_t loc = sm.msg[p] & (kFineNodes - 1);
-      if (p && (sm.msg[p - 1] & (kFineNodes - 1)) == loc) continue;
-      resolve_node_major(w, sm, f, loc, p, cnt16(sm, loc), t0, c3crash);
+    const uint32_t wv = tid >> 6;
+    for (uint32_t k = 0; k < L; ++k) {
+      const uint32_t b = sm.bstart[wv * kMaxWindow + k], e = sm.bstart[wv * kMaxWindow + k + 1];
+      if (b < e) resolve_bin(w, sm, f, b, e, k, t0 + k, c3crash, c3delay);
     }
     __syncthreads();
   } else {
@@ -567,8 +642,10 @@ __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uin
   }
   uint32_t* rw = (uint32_t*)w.recv;
   uint32_t* cw = (uint32_t*)w.crash;
-  for (uint32_t i = tid; i < kFineNodes / 32; i += kResolveBlock)
-    if (wbase + i < nw32) { rw[wbase + i] = sm.recv[i]; cw[wbase + i] = sm.crash[i]; }
+  if (in) {
+    if (sm.recv[tid] != recv0) rw[wbase + tid] = sm.recv[tid];
+    if (sm.crash[tid] != crash0) cw[wbase + tid] = sm.crash[tid];
+  }
   for (uint32_t s = tid; s < w.R; s += kResolveBlock) w.fcount[(size_t)s * w.nfine + f] = sm.fc[s];
   if (tid < L * 4) {
     const uint32_t k = tid >> 2, fld = tid & 3;
