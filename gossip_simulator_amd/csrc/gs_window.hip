@@ -352,7 +352,7 @@ __global__ __launch_bounds__(256) void k_part2(const WinState w) {
 constexpr uint32_t kResolveWaves = kResolveBlock / 64;
 constexpr uint32_t kWaveNodesLog = kFineLog - 3;        // 2048 nodes owned per wave
 constexpr uint32_t kBins = kResolveWaves * kMaxWindow;   // (owner wave, tick) bins
-static_assert(kResolveWaves == 8, "wave ownership assumes 8 waves per workgroup");
+static_assert((kFineNodes >> kWaveNodesLog) == kResolveWaves && kBins % 64 == 0, "wave ownership");
 
 struct ResolveLds {
   uint32_t cnt[kFineNodes / 2];     // u16 per node: arrival ordinal counter (cmin after a roll)
@@ -373,7 +373,6 @@ constexpr uint32_t kOrdShift = kFineLog;
 constexpr uint32_t kOrdMask = 0x1FFFu;       // ordinals < 8191 (kResolveMsgCap)
 constexpr uint32_t kRollBit = 1u << 27;
 constexpr uint32_t kDeadBit = 1u << 28;
-constexpr uint32_t kInfBit = 1u << 29;
 
 __device__ __forceinline__ uint32_t cnt16(const ResolveLds& sm, uint32_t i) {
   return (sm.cnt[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
@@ -510,7 +509,8 @@ __device__ __forceinline__ void resolve_bin(const WinState& w, ResolveLds& sm, u
     }
     wave_sync();
   }
-  // C: counted / crash / infect
+  // C: counted / crash / infect; an infected node's Broadcast() (:122,
+  // :141-142) fires at t + off
   uint32_t cm = 0, cc = 0, cr = 0;
   for (uint32_t p = b + lane; p < e; p += 64) {
     const uint32_t m = sm.buf[p];
@@ -529,35 +529,23 @@ __device__ __forceinline__ void resolve_bin(const WinState& w, ResolveLds& sm, u
     if (crashm) atomicOr(&sm.crash[loc >> 5], bit);
     if (infect) {
       atomicOr(&sm.recv[loc >> 5], bit);
-      sm.buf[p] = m | kInfBit;
+      const uint32_t off = fire_offset(w.delay_low, w.delay_span,
+                                       philox(node0 + loc, t, 0, c3delay, w.key.k0, w.key.k1).x);
+      const uint32_t s = (t + off) % w.R;
+      const uint32_t pos = atomicAdd(&sm.fc[s], 1u);
+      w.flist[((size_t)s * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
     }
   }
   wave_sync();
-  // D: clear the per-node tick state; compact the infections to the bin's front
-  uint32_t ninf = 0;
-  for (uint32_t p0 = b; p0 < e; p0 += 64) {
-    const uint32_t p = p0 + lane;
-    const uint32_t m = p < e ? sm.buf[p] : kDeadBit;
+  // D: clear the per-node tick state
+  for (uint32_t p = b + lane; p < e; p += 64) {
+    const uint32_t m = sm.buf[p];
+    if (m & kDeadBit) continue;
     const uint32_t loc = m & (kFineNodes - 1);
-    if (!(m & kDeadBit)) {
-      atomicAnd(&sm.cnt[loc >> 1], ~(0xFFFFu << ((loc & 1) * 16)));
-      if (m & kRollBit) atomicAnd(&sm.rolled[loc >> 5], ~(1u << (loc & 31)));
-    }
-    const bool inf = (m & kInfBit) != 0;
-    const unsigned long long bal = __ballot(inf);
-    if (inf) sm.buf[b + ninf + (uint32_t)__popcll(bal & ((1ull << lane) - 1))] = loc;
-    ninf += (uint32_t)__popcll(bal);
+    atomicAnd(&sm.cnt[loc >> 1], ~(0xFFFFu << ((loc & 1) * 16)));
+    if (m & kRollBit) atomicAnd(&sm.rolled[loc >> 5], ~(1u << (loc & 31)));
   }
   wave_sync();
-  // E: Broadcast() of each infected node (:122, :141-142): fire at t + off
-  for (uint32_t q = lane; q < ninf; q += 64) {
-    const uint32_t loc = sm.buf[b + q];
-    const uint32_t off = fire_offset(w.delay_low, w.delay_span,
-                                     philox(node0 + loc, t, 0, c3delay, w.key.k0, w.key.k1).x);
-    const uint32_t s = (t + off) % w.R;
-    const uint32_t pos = atomicAdd(&sm.fc[s], 1u);
-    w.flist[((size_t)s * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
-  }
   if (lane == 0) {
     if (cm) atomicAdd(&sm.st[k][0], cm);
     if (cr) { atomicAdd(&sm.st[k][1], cr); atomicAdd(&sm.st[k][3], cr); }
@@ -578,7 +566,7 @@ __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uin
   const uint64_t nw32 = w.W * 2;
   const uint32_t* gm = w.fmsg + mb;
   constexpr uint32_t kPerThread = kResolveMsgCap / kResolveBlock;
-  static_assert(kFineNodes / 32 == kResolveBlock, "one bit word per thread");
+  constexpr uint32_t kBitWords = kFineNodes / 32;  // 512: threads below it own one word each
   uint32_t mr[kPerThread];
   const bool small = M < kResolveMsgCap;
 #pragma unroll
@@ -586,11 +574,14 @@ __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uin
     const uint32_t p = tid + i * kResolveBlock;
     mr[i] = small && p < M ? gm[p] : ~0u;
   }
-  const bool in = wbase + tid < nw32;
+  const bool own = tid < kBitWords;
+  const bool in = own && wbase + tid < nw32;
   const uint32_t recv0 = in ? rg[wbase + tid] : 0u, crash0 = in ? cg[wbase + tid] : 0u;
-  sm.recv[tid] = recv0;
-  sm.crash[tid] = crash0;
-  sm.rolled[tid] = 0;
+  if (own) {
+    sm.recv[tid] = recv0;
+    sm.crash[tid] = crash0;
+    sm.rolled[tid] = 0;
+  }
   {
     uint4* c4 = reinterpret_cast<uint4*>(sm.cnt);
     for (uint32_t i = tid; i < kFineNodes / 8; i += kResolveBlock) c4[i] = make_uint4(0, 0, 0, 0);
@@ -608,19 +599,25 @@ __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uin
       if (mr[i] != ~0u)
         atomicAdd(&sm.bfill[((mr[i] & (kFineNodes - 1)) >> kWaveNodesLog) * kMaxWindow + (mr[i] >> kFineLog)], 1u);
     __syncthreads();
-    if (tid < 64) {  // exclusive scan of the 128 bins, 2 per lane
-      const uint32_t a = sm.bfill[2 * tid], c = sm.bfill[2 * tid + 1];
-      uint32_t x = a + c;
+    if (tid < 64) {  // exclusive scan of the bins, kBins / 64 per lane
+      constexpr uint32_t kPer = kBins / 64;
+      uint32_t a[kPer], sum = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < kPer; ++j) { a[j] = sm.bfill[kPer * tid + j]; sum += a[j]; }
+      uint32_t x = sum;
 #pragma unroll
       for (uint32_t o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(x, o, 64);
         if (tid >= o) x += y;
       }
-      sm.bstart[2 * tid] = x - a - c;
-      sm.bstart[2 * tid + 1] = x - c;
+      uint32_t ex = x - sum;
+#pragma unroll
+      for (uint32_t j = 0; j < kPer; ++j) {
+        sm.bstart[kPer * tid + j] = ex;
+        sm.bfill[kPer * tid + j] = ex;
+        ex += a[j];
+      }
       if (tid == 63) sm.bstart[kBins] = x;
-      sm.bfill[2 * tid] = x - a - c;
-      sm.bfill[2 * tid + 1] = x - c;
     }
     __syncthreads();
 #pragma unroll

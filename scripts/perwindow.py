@@ -1,0 +1,29 @@
+"""Per-window kernel durations (us) of the last broadcast in a rocprofv3 .db:
+expand, part2, resolve in dispatch order.  Usage: python scripts/perwindow.py <db> [nwin]"""
+import re
+import sqlite3
+import sys
+
+db = sqlite3.connect(sys.argv[1])
+rows = db.execute("select name, start, end from kernels order by start").fetchall()
+
+
+def s(n):
+    m = re.search(r"gs::(?:\(anonymous namespace\)::)?(\w+)", n)
+    return m.group(1) if m else ""
+
+
+seq = [(s(n), (e - b) / 1e3) for n, b, e in rows if s(n) in ("k_expand", "k_part2", "k_resolve")]
+wins, cur = [], {}
+for name, us in seq:
+    cur[name] = cur.get(name, 0) + us
+    if name == "k_resolve":
+        wins.append(cur)
+        cur = {}
+nwin = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+tot = {}
+for i, w in enumerate(wins[-nwin:]):
+    print(f"{i:3d} expand {w.get('k_expand', 0):8.1f}  part2 {w.get('k_part2', 0):8.1f}  resolve {w.get('k_resolve', 0):8.1f}")
+    for k, v in w.items():
+        tot[k] = tot.get(k, 0) + v
+print("sum(ms)", {k: round(v / 1e3, 2) for k, v in tot.items()})
