@@ -39,6 +39,10 @@ constexpr uint32_t kExpandNpt = 4;        // firing nodes per thread per round (
 constexpr uint32_t kExpandSlots = kExpandBlock * kExpandNpt * 8;  // LDS message slots per round
 constexpr uint32_t kResolveBlock = 512;
 constexpr uint32_t kResolveMsgCap = 8192;
+// Messages: coarse = u_in_coarse | k << 22 | roll0 << 26; fine = loc | k << 14 |
+// roll0 << 18, where roll0 is the receiver's crash roll for ordinal 0.
+constexpr uint32_t kRoll0Coarse = kCoarseShift + 4;
+constexpr uint32_t kRoll0Fine = kFineLog + 4;
 
 // Units = (tick k, fine bucket f); usize = fires.  Also zeroes the window's
 // counters (one launch instead of several memsets).
@@ -140,7 +144,7 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
   const uint32_t tid = threadIdx.x;
   const uint32_t units = L * w.nfine;
   constexpr uint32_t per_round = kExpandBlock * NPT;
-  const uint32_t c3drop = ctr3(K_DROP, w.key.trial);
+  const uint32_t c3drop = ctr3(K_DROP, w.key.trial), c3crash = ctr3(K_CRASH, w.key.trial);
   if (tid < kMaxWindow * 2) (&sm.acc[0][0])[tid] = 0;
   const unsigned long long rounds = (Tn + per_round - 1) / per_round;
   for (unsigned long long rd = blockIdx.x; rd < rounds; rd += gridDim.x) {
@@ -181,9 +185,13 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
         for (uint32_t jj = 0; jj < 4; ++jj) {
           const uint32_t j = jg * 4 + jj;
           if (mm[q][j] != kEmptyMsg && (int32_t)uniform(lane_of(r, jj), 100u) >= w.kd) {  // kept: :145
-            const uint32_t bin = mm[q][j] >> kCoarseShift;
+            const uint32_t tgt = mm[q][j], bin = tgt >> kCoarseShift;
+            // the receiver's crash roll for ordinal 0 (:112, key (u, t, 0)) rides along
+            uint32_t roll0 = 0;
+            if (w.kc > 0)
+              roll0 = (int32_t)uniform(philox(tgt, t, 0, c3crash, w.key.k0, w.key.k1).x, 100u) < w.kc;
             mt[q][j] = bin | (atomicAdd(&sm.cnt[bin], 1u) << 8);
-            mm[q][j] = (mm[q][j] & ((1u << kCoarseShift) - 1)) | (k << kCoarseShift);
+            mm[q][j] = (tgt & ((1u << kCoarseShift) - 1)) | (k << kCoarseShift) | (roll0 << kRoll0Coarse);
             ++sent;
           }
         }
@@ -432,7 +440,7 @@ __device__ __forceinline__ void resolve_tick(const WinState& w, ResolveLds& sm, 
   const uint32_t tid = threadIdx.x;
   for (uint32_t p = lo + tid; p < hi; p += kResolveBlock) {
     const uint32_t m = src[p];
-    if (filter && (m >> kFineLog) != k) continue;
+    if (filter && ((m >> kFineLog) & (kMaxWindow - 1)) != k) continue;
     const uint32_t loc = m & (kFineNodes - 1), sh = (loc & 1) * 16;
     const uint32_t old = atomicAdd(&sm.cnt[loc >> 1], 1u << sh);
     if (((old >> sh) & 0xFFFFu) == 0xFFFFu) sm.err = 1;
@@ -441,7 +449,7 @@ __device__ __forceinline__ void resolve_tick(const WinState& w, ResolveLds& sm, 
   uint32_t cm = 0, cr = 0, cc = 0, cs = 0;
   for (uint32_t p = lo + tid; p < hi; p += kResolveBlock) {
     const uint32_t m = src[p];
-    if (filter && (m >> kFineLog) != k) continue;
+    if (filter && ((m >> kFineLog) & (kMaxWindow - 1)) != k) continue;
     const uint32_t loc = m & (kFineNodes - 1), sh = (loc & 1) * 16;
     const uint32_t kk = (atomicAnd(&sm.cnt[loc >> 1], ~(0xFFFFu << sh)) >> sh) & 0xFFFFu;
     if (kk) resolve_node(w, sm, f, loc, kk, t, c3crash, cm, cr, cc, cs);
@@ -468,17 +476,19 @@ __device__ __forceinline__ void resolve_bin(const WinState& w, ResolveLds& sm, u
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t node0 = f << kFineLog;
   bool any_roll = false;
-  // A: ordinal and crash roll of each message at a live node
+  // A: ordinal and crash roll of each message at a live node (ordinal 0's
+  // roll came with the message; later ordinals draw their own)
   for (uint32_t p = b + lane; p < e; p += 64) {
-    const uint32_t loc = sm.buf[p] & (kFineNodes - 1), bit = 1u << (loc & 31);
+    const uint32_t m0 = sm.buf[p];
+    const uint32_t loc = m0 & (kFineNodes - 1), bit = 1u << (loc & 31);
     if (sm.crash[loc >> 5] & bit) { sm.buf[p] = kDeadBit; continue; }   // :108
     const uint32_t sh = (loc & 1) * 16;
     uint32_t i = (atomicAdd(&sm.cnt[loc >> 1], 1u << sh) >> sh) & 0xFFFFu;
     if (i >= kOrdMask) { sm.err = 1; i = kOrdMask - 1; }
-    bool roll = false;
-    if (w.kc > 0) {
+    bool roll = (m0 >> kRoll0Fine) & 1;                                     // :112
+    if (i > 0 && w.kc > 0) {
       const u32x4 r = philox(node0 + loc, t, i >> 2, c3crash, w.key.k0, w.key.k1);
-      roll = (int32_t)uniform(lane_of(r, i & 3), 100u) < w.kc;              // :112
+      roll = (int32_t)uniform(lane_of(r, i & 3), 100u) < w.kc;
     }
     sm.buf[p] = loc | (i << kOrdShift) | (roll ? kRollBit : 0u);
     any_roll |= roll;
@@ -597,7 +607,7 @@ __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uin
 #pragma unroll
     for (uint32_t i = 0; i < kPerThread; ++i)
       if (mr[i] != ~0u)
-        atomicAdd(&sm.bfill[((mr[i] & (kFineNodes - 1)) >> kWaveNodesLog) * kMaxWindow + (mr[i] >> kFineLog)], 1u);
+        atomicAdd(&sm.bfill[((mr[i] & (kFineNodes - 1)) >> kWaveNodesLog) * kMaxWindow + ((mr[i] >> kFineLog) & (kMaxWindow - 1))], 1u);
     __syncthreads();
     if (tid < 64) {  // exclusive scan of the bins, kBins / 64 per lane
       constexpr uint32_t kPer = kBins / 64;
@@ -623,8 +633,8 @@ __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uin
 #pragma unroll
     for (uint32_t i = 0; i < kPerThread; ++i)
       if (mr[i] != ~0u) {
-        const uint32_t bin = ((mr[i] & (kFineNodes - 1)) >> kWaveNodesLog) * kMaxWindow + (mr[i] >> kFineLog);
-        sm.buf[atomicAdd(&sm.bfill[bin], 1u)] = mr[i] & (kFineNodes - 1);
+        const uint32_t bin = ((mr[i] & (kFineNodes - 1)) >> kWaveNodesLog) * kMaxWindow + ((mr[i] >> kFineLog) & (kMaxWindow - 1));
+        sm.buf[atomicAdd(&sm.bfill[bin], 1u)] = (mr[i] & (kFineNodes - 1)) | (mr[i] & (1u << kRoll0Fine));
       }
     __syncthreads();
     const uint32_t wv = tid >> 6;
