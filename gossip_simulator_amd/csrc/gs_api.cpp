@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -85,8 +86,9 @@ int alloc_window(gs_ctx* c) {
   const size_t b_fc = al((size_t)w.R * w.nfine * 4), b_units = al(units * 8),
                b_small = al(256 * 8) * 3 + al(257 * 4) + al(257 * 8),
                b_fhist = al(((size_t)w.ncoarse * 256 + 1) * 8), b_fbase = al(((size_t)w.nfine + 1) * 8),
-               b_ffill = al((size_t)w.nfine * 8);
-  const size_t total = b_fc + 2 * b_units + b_small + b_fhist + b_fbase + b_ffill;
+               b_ffill = al((size_t)w.nfine * 8),
+               b_sst = al((size_t)kStatShards * kMaxWindow * kStatFields * 8);
+  const size_t total = b_fc + 2 * b_units + b_small + b_fhist + b_fbase + b_ffill + b_sst;
   if (hipMalloc(&c->d_win, total) != hipSuccess)
     return fail(c, GS_ENOMEM, "cannot allocate window-engine buffers");
   const size_t flist = (size_t)w.R * w.nfine * kFineNodes * 2;
@@ -104,6 +106,10 @@ int alloc_window(gs_ctx* c) {
   w.fhist = (unsigned long long*)q; q += b_fhist;
   w.fstart = (unsigned long long*)q; q += b_fbase;
   w.ffill = (unsigned long long*)q; q += b_ffill;
+  w.sstats = (unsigned long long*)q; q += b_sst;
+  w.dbg = nullptr;
+  if (getenv("GS_STAMPS") && hipMalloc(&w.dbg, 2 * kStampPhases * 8) == hipSuccess)
+    (void)hipMemset(w.dbg, 0, 2 * kStampPhases * 8);
   w.flist = (uint16_t*)c->d_flist;
   c->fcount_bytes = (size_t)w.R * w.nfine * 4;
   if (hipMemsetAsync(c->d_win, 0, total, c->stream) != hipSuccess)
@@ -381,6 +387,19 @@ int gs_create(const gs_params* params, gs_ctx** out) {
 void gs_destroy(gs_ctx* c) {
   if (!c) return;
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->ws.dbg) {
+    unsigned long long h[2 * kStampPhases];
+    if (hipMemcpy(h, c->ws.dbg, sizeof h, hipMemcpyDeviceToHost) == hipSuccess)
+      for (int cls = 0; cls < 2; ++cls) {
+        const unsigned long long* d = h + cls * kStampPhases;
+        fprintf(stderr, "[stamps] k_resolve %s: %llu workgroups, mean us per phase:", cls ? "M>=2048" : "M<2048",
+                d[0]);
+        for (uint32_t i = 1; i < kStampPhases; ++i)
+          fprintf(stderr, " %.2f", d[0] ? d[i] * 0.01 / d[0] : 0.0);
+        fprintf(stderr, "\n");
+      }
+    (void)hipFree(c->ws.dbg);
+  }
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->d_deg) (void)hipFree(c->d_deg);
   if (c->d_ids) (void)hipFree(c->d_ids);
@@ -643,6 +662,7 @@ static int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing) {
     if (first < L) CK(c, hipMemsetAsync(w.fcount, 0, (size_t)(L - first) * w.nfine * 4, c->stream));
     if (e) CK(c, hipEventRecord(e[3], c->stream));
     if (T) CK(c, win_resolve(w, t, L, c->stream));
+    if (T) CK(c, win_stats_reduce(w, t, L, c->stream));
     if (e) {
       CK(c, hipEventRecord(e[4], c->stream));
       evs.emplace_back(widx * 5, T ? 1u : 0u);

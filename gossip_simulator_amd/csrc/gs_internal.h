@@ -107,6 +107,7 @@ struct WinState {
   unsigned long long* fhist;     // [ncoarse*256 + 1] exact fine counts (fallback)
   unsigned long long* fstart;    // [nfine + 1] fine region starts
   unsigned long long* ffill;     // [nfine] fine region fill
+  unsigned long long* sstats;    // [kStatShards][kMaxWindow][kStatFields] per-window partial counters
   unsigned long long* dbg;       // diagnostic phase stamps (GS_STAMPS=1), else null
   uint64_t n, W;
   uint32_t nfine, ncoarse, R, stride, stride_magic;
@@ -115,7 +116,8 @@ struct WinState {
   int32_t kd, kc;
   Key key;
 };
-constexpr uint32_t kStampPhases = 8;
+constexpr uint32_t kStatShards = 256;
+constexpr uint32_t kStampPhases = 9;
 
 constexpr uint32_t kErrArrivals = 4;  // > 65535 arrivals at one node in one tick
 constexpr uint32_t kErrCoarse = 8;    // a coarse region overflowed its estimate
@@ -132,6 +134,7 @@ hipError_t win_part2(const WinState& w, uint64_t T, bool scatter, hipStream_t s)
 hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
 hipError_t win_seal_rows(const uint8_t* deg, uint32_t* ids, uint64_t n, uint32_t stride,
                          hipStream_t s);
+hipError_t win_stats_reduce(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
 hipError_t win_schedule_one(const WinState& w, uint32_t node, uint32_t tick, hipStream_t s);
 
 // Launchers (gs_broadcast.hip).

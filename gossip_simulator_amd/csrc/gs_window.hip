@@ -82,6 +82,27 @@ __device__ __forceinline__ uint32_t unit_of(const WinState& w, unsigned long lon
   return lo;
 }
 
+// Per-tick counters are added into one of kStatShards copies (by workgroup)
+// and summed into the stats ring by k_stats_reduce: tens of thousands of
+// workgroups adding into the same few lines would serialise at the memory-side
+// atomic unit.
+__device__ __forceinline__ unsigned long long* shard_row(const WinState& w, uint32_t k) {
+  return w.sstats + ((size_t)(blockIdx.x & (kStatShards - 1)) * kMaxWindow + k) * kStatFields;
+}
+
+__global__ void k_stats_reduce(const WinState w, uint32_t t0, uint32_t L) {
+  const uint32_t tid = threadIdx.x;  // one (tick, field) pair per thread
+  const uint32_t k = tid / kStatFields, fld = tid % kStatFields;
+  if (k >= L) return;
+  unsigned long long sum = 0;
+  for (uint32_t sh = 0; sh < kStatShards; ++sh) {
+    unsigned long long* x = &w.sstats[((size_t)sh * kMaxWindow + k) * kStatFields + fld];
+    sum += *x;
+    *x = 0;
+  }
+  if (sum) w.stats[(size_t)((t0 + k) % kStatSlots) * kStatFields + fld] += sum;
+}
+
 struct ExpandLds {
   uint32_t sorted[kExpandSlots];
   uint8_t sbin[kExpandSlots];
@@ -233,7 +254,10 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
   if (tid < L * 2) {
     const uint32_t k = tid >> 1, fld = tid & 1;
     const unsigned long long v = sm.acc[k][fld];
-    if (v) atomicAdd(&w.stats[(size_t)((t0 + k) % kStatSlots) * kStatFields + (fld ? ST_SENT : ST_FIRED)], v);
+    unsigned long long* row = shard_row(w, k);
+    if (v) atomicAdd(&row[fld ? ST_SENT : ST_FIRED], v);
+    // every delivered send is a receipt; k_resolve subtracts the uncounted ones
+    if (v && fld) atomicAdd(&row[ST_MSGS], v);
   }
 }
 
@@ -357,43 +381,28 @@ __global__ __launch_bounds__(256) void k_part2(const WinState w) {
   }
 }
 
-constexpr uint32_t kResolveWaves = kResolveBlock / 64;
-constexpr uint32_t kWaveNodesLog = kFineLog - 3;        // 2048 nodes owned per wave
-constexpr uint32_t kBins = kResolveWaves * kMaxWindow;   // (owner wave, tick) bins
-static_assert((kFineNodes >> kWaveNodesLog) == kResolveWaves && kBins % 64 == 0, "wave ownership");
-
 struct ResolveLds {
-  uint32_t cnt[kFineNodes / 2];     // u16 per node: arrival ordinal counter (cmin after a roll)
-  uint32_t rolled[kFineNodes / 32]; // node had a crash roll in the current tick
-  uint32_t recv[kFineNodes / 32];
+  uint32_t cnt[kFineNodes / 2];     // u16 per node: counting sort (then the infection list)
+  uint32_t recv[kFineNodes / 32];   // bits at the window start
   uint32_t crash[kFineNodes / 32];
-  uint32_t buf[kResolveMsgCap];     // messages sorted by (owner wave, tick)
-  uint32_t bstart[kBins + 1];
-  uint32_t bfill[kBins];
+  uint32_t nrecv[kFineNodes / 32];  // bits set during the window
+  uint32_t ncrash[kFineNodes / 32];
+  uint32_t buf[kResolveMsgCap];     // the bucket's messages sorted by node
   uint32_t fc[kWinMaxRing];         // fire-list lengths of this bucket, per ring slot
-  uint32_t st[kMaxWindow][4];       // msgs, recv, crash, sched per tick
+  uint32_t st[kMaxWindow][4];       // dead (not counted), recv, crash, sched per tick
   uint32_t wsum[kResolveBlock / 64];
+  uint32_t ninf;
   uint32_t err;
-};  // ~71 KB: two workgroups per CU
+};  // ~77 KB: two workgroups per CU
 
-// buf entry after the ordinal pass: loc | i << 14 | ROLL | DEAD | INF
-constexpr uint32_t kOrdShift = kFineLog;
-constexpr uint32_t kOrdMask = 0x1FFFu;       // ordinals < 8191 (kResolveMsgCap)
-constexpr uint32_t kRollBit = 1u << 27;
-constexpr uint32_t kDeadBit = 1u << 28;
+// buf entry (sorted path): loc | k << 14 | roll0 << 18 | roll << 19 | o << 20,
+// o = the message's place in its node's (tick, ordinal) processing order.
+constexpr uint32_t kRollBit = 1u << 19;
+constexpr uint32_t kOrdShift = 20;
+constexpr uint32_t kMaxSeg = 4095;  // o < 4096; a node with more receipts takes the large path
 
-__device__ __forceinline__ uint32_t cnt16(const ResolveLds& sm, uint32_t i) {
-  return (sm.cnt[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
-}
-
-// Orders one wave's LDS accesses between phases: the wave's lanes exchange
-// per-node state through LDS, and a wave's LDS operations complete in order.
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
-__device__ __forceinline__ uint32_t popc_ballot(bool x) { return (uint32_t)__popcll(__ballot(x)); }
+__device__ __forceinline__ uint32_t msg_loc(uint32_t m) { return m & (kFineNodes - 1); }
+__device__ __forceinline__ uint32_t msg_tick(uint32_t m) { return (m >> kFineLog) & (kMaxWindow - 1); }
 
 // The receive case of Node.Start (simulator.go:107-123) for node `loc` of the
 // bucket with kk arrivals at tick t: ordinals 0..kk-1, keyed crash rolls.
@@ -436,131 +445,131 @@ __device__ __forceinline__ void resolve_node(const WinState& w, ResolveLds& sm, 
 template <class Src>
 __device__ __forceinline__ void resolve_tick(const WinState& w, ResolveLds& sm, uint32_t f,
                                              const Src& src, uint32_t lo, uint32_t hi, uint32_t k,
-                                             bool filter, uint32_t t, uint32_t c3crash) {
+                                             uint32_t t, uint32_t c3crash) {
   const uint32_t tid = threadIdx.x;
   for (uint32_t p = lo + tid; p < hi; p += kResolveBlock) {
     const uint32_t m = src[p];
-    if (filter && ((m >> kFineLog) & (kMaxWindow - 1)) != k) continue;
-    const uint32_t loc = m & (kFineNodes - 1), sh = (loc & 1) * 16;
+    if (msg_tick(m) != k) continue;
+    const uint32_t loc = msg_loc(m), sh = (loc & 1) * 16;
     const uint32_t old = atomicAdd(&sm.cnt[loc >> 1], 1u << sh);
     if (((old >> sh) & 0xFFFFu) == 0xFFFFu) sm.err = 1;
   }
   __syncthreads();
-  uint32_t cm = 0, cr = 0, cc = 0, cs = 0;
+  uint32_t arr = 0, cm = 0, cr = 0, cc = 0, cs = 0;
   for (uint32_t p = lo + tid; p < hi; p += kResolveBlock) {
     const uint32_t m = src[p];
-    if (filter && ((m >> kFineLog) & (kMaxWindow - 1)) != k) continue;
-    const uint32_t loc = m & (kFineNodes - 1), sh = (loc & 1) * 16;
+    if (msg_tick(m) != k) continue;
+    const uint32_t loc = msg_loc(m), sh = (loc & 1) * 16;
     const uint32_t kk = (atomicAnd(&sm.cnt[loc >> 1], ~(0xFFFFu << sh)) >> sh) & 0xFFFFu;
+    arr += kk;
     if (kk) resolve_node(w, sm, f, loc, kk, t, c3crash, cm, cr, cc, cs);
   }
-  if (cm) atomicAdd(&sm.st[k][0], cm);
+  if (arr != cm) atomicAdd(&sm.st[k][0], arr - cm);
   if (cr) atomicAdd(&sm.st[k][1], cr);
   if (cc) atomicAdd(&sm.st[k][2], cc);
   if (cs) atomicAdd(&sm.st[k][3], cs);
   __syncthreads();
 }
 
-// One (owner wave, tick) bin of the receive case, lane per message
-// (simulator.go:107-123).  Rule A6: with k arrivals at node u in tick t the
-// ordinals i = 0..k-1 are processed in order; ordinal i is counted unless an
-// earlier ordinal crashed the node, rolls crash with U_100(u, t, i) < kc, and
-// ordinal 0 infects a node not yet received unless it crashes.  So every
-// message needs only its ordinal (an LDS atomic), its own roll and the node's
-// first crashing ordinal cmin: counted = i <= cmin, crash = i == cmin,
-// infect = i == 0 && !roll && !received.  The wave owns every node of its
-// messages, so the phases are ordered by wave_sync() alone.
-__device__ __forceinline__ void resolve_bin(const WinState& w, ResolveLds& sm, uint32_t f,
-                                            uint32_t b, uint32_t e, uint32_t k, uint32_t t,
-                                            uint32_t c3crash, uint32_t c3delay) {
-  const uint32_t lane = threadIdx.x & 63;
+// Segment of the node of buf[p] (messages are sorted by node).
+__device__ __forceinline__ void segment_of(const ResolveLds& sm, uint32_t p, uint32_t M,
+                                           uint32_t loc, uint32_t& s, uint32_t& e) {
+  s = p;
+  while (s > 0 && msg_loc(sm.buf[s - 1]) == loc) --s;
+  e = p + 1;
+  while (e < M && msg_loc(sm.buf[e]) == loc) ++e;
+}
+
+// The receive case (simulator.go:107-123) for a whole window, lane per
+// message.  A node's receipts are processed in (tick, ordinal) order (rule
+// A6); message p's place o in that order and its crash roll
+// U_100(u, t, i) < kc (i = its ordinal within the tick; ordinal 0's roll came
+// with the message) are computed independently per lane.  With c* = the
+// first crashing place: counted = o <= c*, crash = o == c*, and the node is
+// infected at o == 0 unless that receipt crashes it or it was received
+// before; a node crashed before the window counts nothing (:108).
+__device__ void resolve_sorted(const WinState& w, ResolveLds& sm, uint32_t f, uint32_t M,
+                               uint32_t t0, uint32_t c3crash, bool stamp,
+                               unsigned long long (&ts)[kStampPhases]) {
+  const uint32_t tid = threadIdx.x;
   const uint32_t node0 = f << kFineLog;
-  bool any_roll = false;
-  // A: ordinal and crash roll of each message at a live node (ordinal 0's
-  // roll came with the message; later ordinals draw their own)
-  for (uint32_t p = b + lane; p < e; p += 64) {
-    const uint32_t m0 = sm.buf[p];
-    const uint32_t loc = m0 & (kFineNodes - 1), bit = 1u << (loc & 31);
-    if (sm.crash[loc >> 5] & bit) { sm.buf[p] = kDeadBit; continue; }   // :108
-    const uint32_t sh = (loc & 1) * 16;
-    uint32_t i = (atomicAdd(&sm.cnt[loc >> 1], 1u << sh) >> sh) & 0xFFFFu;
-    if (i >= kOrdMask) { sm.err = 1; i = kOrdMask - 1; }
-    bool roll = (m0 >> kRoll0Fine) & 1;                                     // :112
+  constexpr uint32_t kPerThread = kResolveMsgCap / kResolveBlock;
+  // 1: place and roll of every message
+  uint32_t add[kPerThread];
+#pragma unroll
+  for (uint32_t j = 0; j < kPerThread; ++j) {
+    const uint32_t p = tid + j * kResolveBlock;
+    add[j] = 0;
+    if (p >= M) continue;
+    const uint32_t m = sm.buf[p], loc = msg_loc(m), k = msg_tick(m);
+    uint32_t s, e;
+    segment_of(sm, p, M, loc, s, e);
+    uint32_t i = 0, before = 0;
+    for (uint32_t q = s; q < e; ++q) {
+      const uint32_t kq = msg_tick(sm.buf[q]);
+      before += kq < k;
+      i += (kq == k) & (q < p);
+    }
+    bool roll = (m >> kRoll0Fine) & 1;                                      // :112
     if (i > 0 && w.kc > 0) {
-      const u32x4 r = philox(node0 + loc, t, i >> 2, c3crash, w.key.k0, w.key.k1);
+      const u32x4 r = philox(node0 + loc, t0 + k, i >> 2, c3crash, w.key.k0, w.key.k1);
       roll = (int32_t)uniform(lane_of(r, i & 3), 100u) < w.kc;
     }
-    sm.buf[p] = loc | (i << kOrdShift) | (roll ? kRollBit : 0u);
-    any_roll |= roll;
+    add[j] = (roll ? kRollBit : 0u) | ((before + i) << kOrdShift);
   }
-  wave_sync();
-  // B (rare): the node's count becomes the minimum crashing ordinal
-  if (__ballot(any_roll)) {
-    for (uint32_t p = b + lane; p < e; p += 64) {
-      const uint32_t m = sm.buf[p];
-      if (!(m & kRollBit)) continue;
-      const uint32_t loc = m & (kFineNodes - 1);
-      atomicOr(&sm.cnt[loc >> 1], 0xFFFFu << ((loc & 1) * 16));
-      atomicOr(&sm.rolled[loc >> 5], 1u << (loc & 31));
-    }
-    wave_sync();
-    for (uint32_t p = b + lane; p < e; p += 64) {
-      const uint32_t m = sm.buf[p];
-      if (!(m & kRollBit)) continue;
-      const uint32_t loc = m & (kFineNodes - 1), sh = (loc & 1) * 16;
-      const uint32_t i = (m >> kOrdShift) & kOrdMask;
-      uint32_t old = sm.cnt[loc >> 1];
-      while (((old >> sh) & 0xFFFFu) > i) {
-        const uint32_t nw = (old & ~(0xFFFFu << sh)) | (i << sh);
-        const uint32_t got = atomicCAS(&sm.cnt[loc >> 1], old, nw);
-        if (got == old) break;
-        old = got;
+#pragma unroll
+  for (uint32_t j = 0; j < kPerThread; ++j) {
+    const uint32_t p = tid + j * kResolveBlock;
+    if (p < M) atomicOr(&sm.buf[p], add[j]);  // other lanes read only loc and tick meanwhile
+  }
+  __syncthreads();
+  if (stamp) ts[5] = __builtin_amdgcn_s_memrealtime();
+  // 2: counted / crash / infect
+  uint32_t* inf = sm.cnt;  // the counting-sort array is free now
+#pragma unroll
+  for (uint32_t j = 0; j < kPerThread; ++j) {
+    const uint32_t p = tid + j * kResolveBlock;
+    if (p >= M) continue;
+    const uint32_t m = sm.buf[p], loc = msg_loc(m), k = msg_tick(m), bit = 1u << (loc & 31);
+    const uint32_t o = m >> kOrdShift;
+    const bool roll = (m & kRollBit) != 0;
+    const bool crashed0 = (sm.crash[loc >> 5] & bit) != 0;
+    uint32_t cstar = 0xFFFFu;
+    if (!crashed0) {
+      uint32_t s, e;
+      segment_of(sm, p, M, loc, s, e);
+      for (uint32_t q = s; q < e; ++q) {
+        const uint32_t mq = sm.buf[q];
+        if (mq & kRollBit) cstar = min(cstar, mq >> kOrdShift);
       }
     }
-    wave_sync();
-  }
-  // C: counted / crash / infect; an infected node's Broadcast() (:122,
-  // :141-142) fires at t + off
-  uint32_t cm = 0, cc = 0, cr = 0;
-  for (uint32_t p = b + lane; p < e; p += 64) {
-    const uint32_t m = sm.buf[p];
-    const bool live = !(m & kDeadBit);
-    const uint32_t loc = m & (kFineNodes - 1), bit = 1u << (loc & 31);
-    const uint32_t i = (m >> kOrdShift) & kOrdMask;
-    const bool roll = (m & kRollBit) != 0;
-    uint32_t cmin = 0xFFFFu;
-    if (live && (sm.rolled[loc >> 5] & bit)) cmin = cnt16(sm, loc);
-    const bool counted = live && i <= cmin;                                  // :111
-    const bool crashm = live && roll && i == cmin;                           // :113-115
-    const bool infect = live && i == 0 && !roll && !(sm.recv[loc >> 5] & bit);  // :117-121
-    cm += popc_ballot(counted);
-    cc += popc_ballot(crashm);
-    cr += popc_ballot(infect);
-    if (crashm) atomicOr(&sm.crash[loc >> 5], bit);
+    const bool dead = crashed0 || o > cstar;                                 // :108, :111
+    const bool crashm = !crashed0 && roll && o == cstar;                     // :113-115
+    const bool infect = !crashed0 && o == 0 && !roll && !(sm.recv[loc >> 5] & bit);  // :117-121
+    if (dead) atomicAdd(&sm.st[k][0], 1u);
+    if (crashm) {
+      atomicAdd(&sm.st[k][2], 1u);
+      atomicOr(&sm.ncrash[loc >> 5], bit);
+    }
     if (infect) {
-      atomicOr(&sm.recv[loc >> 5], bit);
-      const uint32_t off = fire_offset(w.delay_low, w.delay_span,
-                                       philox(node0 + loc, t, 0, c3delay, w.key.k0, w.key.k1).x);
-      const uint32_t s = (t + off) % w.R;
-      const uint32_t pos = atomicAdd(&sm.fc[s], 1u);
-      w.flist[((size_t)s * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
+      atomicAdd(&sm.st[k][1], 1u);
+      atomicOr(&sm.nrecv[loc >> 5], bit);
+      inf[atomicAdd(&sm.ninf, 1u)] = loc | (k << kFineLog);
     }
   }
-  wave_sync();
-  // D: clear the per-node tick state
-  for (uint32_t p = b + lane; p < e; p += 64) {
-    const uint32_t m = sm.buf[p];
-    if (m & kDeadBit) continue;
-    const uint32_t loc = m & (kFineNodes - 1);
-    atomicAnd(&sm.cnt[loc >> 1], ~(0xFFFFu << ((loc & 1) * 16)));
-    if (m & kRollBit) atomicAnd(&sm.rolled[loc >> 5], ~(1u << (loc & 31)));
+  __syncthreads();
+  if (stamp) ts[6] = __builtin_amdgcn_s_memrealtime();
+  // 3: Broadcast() of every infected node (:122, :141-142): fire at t + off
+  const uint32_t c3delay = ctr3(K_DELAY, w.key.trial);
+  for (uint32_t q = tid; q < sm.ninf; q += kResolveBlock) {
+    const uint32_t x = inf[q], loc = msg_loc(x), t = t0 + msg_tick(x);
+    const uint32_t off = fire_offset(w.delay_low, w.delay_span,
+                                     philox(node0 + loc, t, 0, c3delay, w.key.k0, w.key.k1).x);
+    const uint32_t slot = (t + off) % w.R;
+    const uint32_t pos = atomicAdd(&sm.fc[slot], 1u);
+    w.flist[((size_t)slot * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
   }
-  wave_sync();
-  if (lane == 0) {
-    if (cm) atomicAdd(&sm.st[k][0], cm);
-    if (cr) { atomicAdd(&sm.st[k][1], cr); atomicAdd(&sm.st[k][3], cr); }
-    if (cc) atomicAdd(&sm.st[k][2], cc);
-  }
+  if (tid < kMaxWindow) sm.st[tid][3] = sm.st[tid][1];
 }
 
 __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
@@ -569,6 +578,11 @@ __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uin
   const unsigned long long mb = w.fstart[f];
   const uint32_t M = (uint32_t)w.ffill[f];
   if (M == 0) return;  // no receipt in this bucket during the window
+  // diagnostic phase stamps (GS_STAMPS=1): every 64th workgroup
+  const bool stamp = w.dbg != nullptr && (f & 63) == 0;
+  unsigned long long ts[kStampPhases];
+#define GS_STAMP(i) if (stamp) ts[i] = __builtin_amdgcn_s_memrealtime()
+  GS_STAMP(0);
   const uint32_t node0 = f << kFineLog;
   const uint64_t wbase = (uint64_t)node0 >> 5;  // u32 word index of the bucket's bits
   const uint32_t* rg = (const uint32_t*)w.recv;
@@ -576,92 +590,125 @@ __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uin
   const uint64_t nw32 = w.W * 2;
   const uint32_t* gm = w.fmsg + mb;
   constexpr uint32_t kPerThread = kResolveMsgCap / kResolveBlock;
-  constexpr uint32_t kBitWords = kFineNodes / 32;  // 512: threads below it own one word each
+  constexpr uint32_t kBitWords = kFineNodes / 32;
+  static_assert(kBitWords == kResolveBlock, "one bit word per thread");
   uint32_t mr[kPerThread];
-  const bool small = M < kResolveMsgCap;
+  bool small = M < kResolveMsgCap;
 #pragma unroll
   for (uint32_t i = 0; i < kPerThread; ++i) {
     const uint32_t p = tid + i * kResolveBlock;
     mr[i] = small && p < M ? gm[p] : ~0u;
   }
-  const bool own = tid < kBitWords;
-  const bool in = own && wbase + tid < nw32;
+  const bool in = wbase + tid < nw32;
   const uint32_t recv0 = in ? rg[wbase + tid] : 0u, crash0 = in ? cg[wbase + tid] : 0u;
-  if (own) {
-    sm.recv[tid] = recv0;
-    sm.crash[tid] = crash0;
-    sm.rolled[tid] = 0;
-  }
+  sm.recv[tid] = recv0;
+  sm.crash[tid] = crash0;
+  sm.nrecv[tid] = 0;
+  sm.ncrash[tid] = 0;
   {
     uint4* c4 = reinterpret_cast<uint4*>(sm.cnt);
     for (uint32_t i = tid; i < kFineNodes / 8; i += kResolveBlock) c4[i] = make_uint4(0, 0, 0, 0);
   }
   for (uint32_t s = tid; s < w.R; s += kResolveBlock) sm.fc[s] = w.fcount[(size_t)s * w.nfine + f];
   if (tid < kMaxWindow * 4) (&sm.st[0][0])[tid] = 0;
-  if (tid < kBins) sm.bfill[tid] = 0;
-  if (tid == 0) sm.err = 0;
-  const uint32_t c3crash = ctr3(K_CRASH, w.key.trial), c3delay = ctr3(K_DELAY, w.key.trial);
+  if (tid == 0) { sm.err = 0; sm.ninf = 0; }
+  const uint32_t c3crash = ctr3(K_CRASH, w.key.trial);
   __syncthreads();
+  GS_STAMP(1);
   if (small) {
-    // counting sort by (owner wave, tick)
+    // counting sort of the bucket's messages by node (u16 counters -> offsets)
 #pragma unroll
     for (uint32_t i = 0; i < kPerThread; ++i)
-      if (mr[i] != ~0u)
-        atomicAdd(&sm.bfill[((mr[i] & (kFineNodes - 1)) >> kWaveNodesLog) * kMaxWindow + ((mr[i] >> kFineLog) & (kMaxWindow - 1))], 1u);
+      if (mr[i] != ~0u) {
+        const uint32_t loc = msg_loc(mr[i]);
+        atomicAdd(&sm.cnt[loc >> 1], 1u << ((loc & 1) * 16));
+      }
     __syncthreads();
-    if (tid < 64) {  // exclusive scan of the bins, kBins / 64 per lane
-      constexpr uint32_t kPer = kBins / 64;
-      uint32_t a[kPer], sum = 0;
+    GS_STAMP(2);
+    {  // exclusive scan of 16384 u16 counters: 32 per thread (M < 8192 fits u16)
+      constexpr uint32_t kPer = kFineNodes / kResolveBlock;  // 32
+      uint32_t* wp = &sm.cnt[tid * (kPer / 2)];
+      uint32_t sum = 0;
+      bool big = false;
 #pragma unroll
-      for (uint32_t j = 0; j < kPer; ++j) { a[j] = sm.bfill[kPer * tid + j]; sum += a[j]; }
+      for (uint32_t i = 0; i < kPer / 2; ++i) {
+        const uint32_t a = wp[i] & 0xFFFFu, b = wp[i] >> 16;
+        sum += a + b;
+        big |= a > kMaxSeg || b > kMaxSeg;
+      }
+      if (big) sm.err = 2;
+      const uint32_t lane = tid & 63, wv = tid >> 6;
       uint32_t x = sum;
 #pragma unroll
       for (uint32_t o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(x, o, 64);
-        if (tid >= o) x += y;
+        if (lane >= o) x += y;
       }
-      uint32_t ex = x - sum;
+      if (lane == 63) sm.wsum[wv] = x;
+      __syncthreads();
+      uint32_t base = x - sum;
+      for (uint32_t v = 0; v < wv; ++v) base += sm.wsum[v];
 #pragma unroll
-      for (uint32_t j = 0; j < kPer; ++j) {
-        sm.bstart[kPer * tid + j] = ex;
-        sm.bfill[kPer * tid + j] = ex;
-        ex += a[j];
+      for (uint32_t i = 0; i < kPer / 2; ++i) {
+        const uint32_t a = wp[i] & 0xFFFFu, b = wp[i] >> 16;
+        wp[i] = base | ((base + a) << 16);
+        base += a + b;
       }
-      if (tid == 63) sm.bstart[kBins] = x;
     }
     __syncthreads();
+    GS_STAMP(3);
+    if (sm.err == 2) {
+      // a node with more than kMaxSeg receipts: take the large path instead
+      small = false;
+      __syncthreads();
+      uint4* c4 = reinterpret_cast<uint4*>(sm.cnt);
+      for (uint32_t i = tid; i < kFineNodes / 8; i += kResolveBlock) c4[i] = make_uint4(0, 0, 0, 0);
+      if (tid == 0) sm.err = 0;
+      __syncthreads();
+    } else {
 #pragma unroll
-    for (uint32_t i = 0; i < kPerThread; ++i)
-      if (mr[i] != ~0u) {
-        const uint32_t bin = ((mr[i] & (kFineNodes - 1)) >> kWaveNodesLog) * kMaxWindow + ((mr[i] >> kFineLog) & (kMaxWindow - 1));
-        sm.buf[atomicAdd(&sm.bfill[bin], 1u)] = (mr[i] & (kFineNodes - 1)) | (mr[i] & (1u << kRoll0Fine));
-      }
-    __syncthreads();
-    const uint32_t wv = tid >> 6;
-    for (uint32_t k = 0; k < L; ++k) {
-      const uint32_t b = sm.bstart[wv * kMaxWindow + k], e = sm.bstart[wv * kMaxWindow + k + 1];
-      if (b < e) resolve_bin(w, sm, f, b, e, k, t0 + k, c3crash, c3delay);
+      for (uint32_t i = 0; i < kPerThread; ++i)
+        if (mr[i] != ~0u) {
+          const uint32_t loc = msg_loc(mr[i]), sh = (loc & 1) * 16;
+          const uint32_t pos = (atomicAdd(&sm.cnt[loc >> 1], 1u << sh) >> sh) & 0xFFFFu;
+          sm.buf[pos] = mr[i] & ((1u << (kRoll0Fine + 1)) - 1);
+        }
+      __syncthreads();
+      GS_STAMP(4);
+      resolve_sorted(w, sm, f, M, t0, c3crash, stamp, ts);
+      __syncthreads();
+      GS_STAMP(7);
     }
-    __syncthreads();
-  } else {
-    // large bucket: stream the messages from global memory once per pass
-    for (uint32_t k = 0; k < L; ++k) resolve_tick(w, sm, f, gm, 0, M, k, true, t0 + k, c3crash);
+  }
+  if (!small) {
+    // large bucket: stream the messages from global memory once per tick
+    for (uint32_t k = 0; k < L; ++k) resolve_tick(w, sm, f, gm, 0, M, k, t0 + k, c3crash);
   }
   uint32_t* rw = (uint32_t*)w.recv;
   uint32_t* cw = (uint32_t*)w.crash;
   if (in) {
-    if (sm.recv[tid] != recv0) rw[wbase + tid] = sm.recv[tid];
-    if (sm.crash[tid] != crash0) cw[wbase + tid] = sm.crash[tid];
+    const uint32_t r = sm.recv[tid] | sm.nrecv[tid], c = sm.crash[tid] | sm.ncrash[tid];
+    if (r != recv0) rw[wbase + tid] = r;
+    if (c != crash0) cw[wbase + tid] = c;
   }
   for (uint32_t s = tid; s < w.R; s += kResolveBlock) w.fcount[(size_t)s * w.nfine + f] = sm.fc[s];
   if (tid < L * 4) {
     const uint32_t k = tid >> 2, fld = tid & 3;
     const uint32_t v = sm.st[k][fld];
     const uint32_t field = fld == 0 ? ST_MSGS : fld == 1 ? ST_RECV : fld == 2 ? ST_CRASH : ST_SCHED;
-    if (v) atomicAdd(&w.stats[(size_t)((t0 + k) % kStatSlots) * kStatFields + field],
-                     (unsigned long long)v);
+    // field 0 counts receipts that were NOT counted (:108, after a crash):
+    // the expand added every delivered send to ST_MSGS
+    const unsigned long long add = fld == 0 ? 0ull - (unsigned long long)v : (unsigned long long)v;
+    if (v) atomicAdd(&shard_row(w, k)[field], add);
   }
   if (tid == 0 && sm.err) atomicOr(w.err, kErrArrivals);
+  GS_STAMP(8);
+  if (stamp && tid == 0 && small) {
+    unsigned long long* d = w.dbg + (M >= 2048 ? kStampPhases : 0);
+    atomicAdd(&d[0], 1ull);
+    for (uint32_t i = 1; i < kStampPhases; ++i) atomicAdd(&d[i], ts[i] - ts[i - 1]);
+  }
+#undef GS_STAMP
 }
 
 __global__ void k_schedule_one_win(const WinState w, uint32_t node, uint32_t t) {
@@ -741,6 +788,11 @@ hipError_t win_scan_fine(const WinState& w, void* tmp, size_t& tmp_bytes, hipStr
 
 hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s) {
   hipLaunchKernelGGL(k_resolve, dim3(w.nfine), dim3(kResolveBlock), 0, s, w, t0, L);
+  return hipGetLastError();
+}
+
+hipError_t win_stats_reduce(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s) {
+  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(kMaxWindow * kStatFields), 0, s, w, t0, L);
   return hipGetLastError();
 }
 
