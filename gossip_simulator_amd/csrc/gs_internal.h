@@ -83,8 +83,8 @@ constexpr uint32_t kWinMaxRing = 256;
 constexpr uint32_t kWinMaxStride = 32;          // friends-row length the window engine takes
 constexpr uint32_t kEmptyMsg = 0xFFFFFFFFu;
 constexpr uint32_t kPartTile = 4096;            // messages per partition tile
-constexpr uint32_t kWinSlotsPerBucket = 7168;   // window cut: friend slots per fine bucket
-                                                // (k_resolve keeps <= 8192 receipts in LDS)
+constexpr uint32_t kWinSlotsPerBucket = 6144;   // window cut: friend slots per fine bucket
+                                                // (k_resolve keeps <= 7168 receipts in LDS)
 
 struct WinState {
   const uint8_t* deg;

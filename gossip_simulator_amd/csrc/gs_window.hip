@@ -38,7 +38,7 @@ constexpr uint32_t kExpandBlock = 256;
 constexpr uint32_t kExpandNpt = 4;        // firing nodes per thread per round (rows <= 8)
 constexpr uint32_t kExpandSlots = kExpandBlock * kExpandNpt * 8;  // LDS message slots per round
 constexpr uint32_t kResolveBlock = 512;
-constexpr uint32_t kResolveMsgCap = 8192;
+constexpr uint32_t kResolveMsgCap = 7168;   // receipts of one bucket held in LDS
 // Messages: coarse = u_in_coarse | k << 22 | roll0 << 26; fine = loc | k << 14 |
 // roll0 << 18, where roll0 is the receiver's crash roll for ordinal 0.
 constexpr uint32_t kRoll0Coarse = kCoarseShift + 4;
@@ -382,27 +382,32 @@ __global__ __launch_bounds__(256) void k_part2(const WinState w) {
 }
 
 struct ResolveLds {
-  uint32_t cnt[kFineNodes / 2];     // u16 per node: counting sort (then the infection list)
+  uint32_t cnt[kFineNodes / 2];     // u16 per node: receipts in the window, then list heads
   uint32_t recv[kFineNodes / 32];   // bits at the window start
   uint32_t crash[kFineNodes / 32];
   uint32_t nrecv[kFineNodes / 32];  // bits set during the window
   uint32_t ncrash[kFineNodes / 32];
-  uint32_t buf[kResolveMsgCap];     // the bucket's messages sorted by node
+  uint32_t buf[kResolveMsgCap];     // the bucket's messages (arrival order) + list links
   uint32_t fc[kWinMaxRing];         // fire-list lengths of this bucket, per ring slot
   uint32_t st[kMaxWindow][4];       // dead (not counted), recv, crash, sched per tick
-  uint32_t wsum[kResolveBlock / 64];
+  uint16_t own[kResolveMsgCap / 2]; // nodes with several receipts (<= half the receipts)
+  uint32_t nown;
   uint32_t ninf;
   uint32_t err;
-};  // ~77 KB: two workgroups per CU
+};  // ~78 KB: two workgroups per CU
 
-// buf entry (sorted path): loc | k << 14 | roll0 << 18 | roll << 19 | o << 20,
-// o = the message's place in its node's (tick, ordinal) processing order.
-constexpr uint32_t kRollBit = 1u << 19;
-constexpr uint32_t kOrdShift = 20;
-constexpr uint32_t kMaxSeg = 4095;  // o < 4096; a node with more receipts takes the large path
+// buf entry: loc | k << 14 | roll0 << 18 | link << 19 (link = index + 1 of the
+// next receipt of the same node, 0 = end); list heads are kHeadFlag | (index+1)
+constexpr uint32_t kMsgBits = kRoll0Fine + 1;
+constexpr uint32_t kLinkShift = kMsgBits;
+constexpr uint32_t kHeadFlag = 0x8000u;
+constexpr uint32_t kInfMark = 0x4000u;    // replayed node infected: kInfMark | tick
 
 __device__ __forceinline__ uint32_t msg_loc(uint32_t m) { return m & (kFineNodes - 1); }
 __device__ __forceinline__ uint32_t msg_tick(uint32_t m) { return (m >> kFineLog) & (kMaxWindow - 1); }
+__device__ __forceinline__ uint32_t half_of(uint32_t word, uint32_t loc) {
+  return (word >> ((loc & 1) * 16)) & 0xFFFFu;
+}
 
 // The receive case of Node.Start (simulator.go:107-123) for node `loc` of the
 // bucket with kk arrivals at tick t: ordinals 0..kk-1, keyed crash rolls.
@@ -471,81 +476,132 @@ __device__ __forceinline__ void resolve_tick(const WinState& w, ResolveLds& sm, 
   __syncthreads();
 }
 
-// Segment of the node of buf[p] (messages are sorted by node).
-__device__ __forceinline__ void segment_of(const ResolveLds& sm, uint32_t p, uint32_t M,
-                                           uint32_t loc, uint32_t& s, uint32_t& e) {
-  s = p;
-  while (s > 0 && msg_loc(sm.buf[s - 1]) == loc) --s;
-  e = p + 1;
-  while (e < M && msg_loc(sm.buf[e]) == loc) ++e;
+// A node with several receipts in the window: walk its list and replay the
+// receive case (simulator.go:107-123) tick by tick, ordinals in order (rule
+// A6).  Ordinal 0's crash roll came with the message (all receipts of one
+// (node, tick) carry the same one); later ordinals draw U_100(u, t, i).
+// Returns the infection tick + 1 (0 = none).
+__device__ __forceinline__ uint32_t replay_multi(const WinState& w, ResolveLds& sm, uint32_t f,
+                                                 uint32_t loc, uint32_t t0, uint32_t c3crash) {
+  const uint32_t bit = 1u << (loc & 31), wi = loc >> 5;
+  // per-tick receipt counts (8 bits each) and ordinal-0 rolls
+  unsigned long long h0 = 0, h1 = 0;
+  uint32_t rollmask = 0, tickmask = 0;
+  for (uint32_t q = half_of(sm.cnt[loc >> 1], loc) & ~kHeadFlag; q != 0;) {
+    const uint32_t m = sm.buf[q - 1], k = msg_tick(m);
+    if (k < 8) h0 += 1ull << (8 * k); else h1 += 1ull << (8 * (k - 8));
+    tickmask |= 1u << k;
+    rollmask |= ((m >> kRoll0Fine) & 1u) << k;
+    q = m >> kLinkShift;
+  }
+  const bool crashed0 = (sm.crash[wi] & bit) != 0;
+  bool crashed = crashed0, received = (sm.recv[wi] & bit) != 0;
+  uint32_t inf = 0;
+  const uint32_t u = (f << kFineLog) + loc;
+  while (tickmask) {
+    const uint32_t k = __builtin_ctz(tickmask);
+    tickmask &= tickmask - 1;
+    const uint32_t kk = (uint32_t)(((k < 8 ? h0 >> (8 * k) : h1 >> (8 * (k - 8)))) & 255u);
+    if (crashed) {                                                // :108
+      atomicAdd(&sm.st[k][0], kk);
+      continue;
+    }
+    const uint32_t t = t0 + k;
+    for (uint32_t i = 0; i < kk; ++i) {
+      bool roll = (rollmask >> k) & 1;                            // :112
+      if (i > 0 && w.kc > 0) {
+        const u32x4 r = philox(u, t, i >> 2, c3crash, w.key.k0, w.key.k1);
+        roll = (int32_t)uniform(lane_of(r, i & 3), 100u) < w.kc;
+      }
+      if (roll) {                                                 // :113-115
+        crashed = true;
+        atomicAdd(&sm.st[k][2], 1u);
+        if (kk - i - 1) atomicAdd(&sm.st[k][0], kk - i - 1);      // the rest of the tick
+        break;
+      }
+      if (!received) {                                            // :117-121
+        received = true;
+        inf = k + 1;
+        atomicAdd(&sm.st[k][1], 1u);
+      }
+    }
+  }
+  if (crashed && !crashed0) atomicOr(&sm.ncrash[wi], bit);
+  if (inf) atomicOr(&sm.nrecv[wi], bit);
+  return inf;
 }
 
-// The receive case (simulator.go:107-123) for a whole window, lane per
-// message.  A node's receipts are processed in (tick, ordinal) order (rule
-// A6); message p's place o in that order and its crash roll
-// U_100(u, t, i) < kc (i = its ordinal within the tick; ordinal 0's roll came
-// with the message) are computed independently per lane.  With c* = the
-// first crashing place: counted = o <= c*, crash = o == c*, and the node is
-// infected at o == 0 unless that receipt crashes it or it was received
-// before; a node crashed before the window counts nothing (:108).
-__device__ void resolve_sorted(const WinState& w, ResolveLds& sm, uint32_t f, uint32_t M,
-                               uint32_t t0, uint32_t c3crash, bool stamp,
-                               unsigned long long (&ts)[kStampPhases]) {
+// Wave-aggregated append: one LDS atomic per wave, lanes with `take` get
+// consecutive slots of the list whose fill counter is *n.
+__device__ __forceinline__ uint32_t wave_append(uint32_t* n, bool take) {
+  const unsigned long long bal = __ballot(take);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t leader = bal ? (uint32_t)__ffsll((long long)bal) - 1 : 0;
+  uint32_t base = 0;
+  if (take && lane == leader) base = atomicAdd(n, (uint32_t)__popcll(bal));
+  base = __shfl(base, leader, 64);
+  return base + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+}
+
+// The receive case (simulator.go:107-123) for one bucket and a whole window.
+// Most receiving nodes get exactly one receipt: ordinal 0 of its tick, whose
+// crash roll rode with the message, so it resolves in its own lane.  Nodes
+// with several receipts are linked into per-node lists and replayed one node
+// per lane.  Every phase issues its LDS reads for all of a thread's receipts
+// before it uses them.
+// Returns false (state untouched but the counters) if a node has more than
+// 255 receipts: the caller then takes the large path.
+__device__ bool resolve_window(const WinState& w, ResolveLds& sm, uint32_t f, uint32_t M,
+                               uint32_t t0, uint32_t c3crash, const uint32_t* mr, bool stamp,
+                               unsigned long long* ts) {
+#define GS_STAMPW(i) if (stamp) ts[i] = __builtin_amdgcn_s_memrealtime()
   const uint32_t tid = threadIdx.x;
   const uint32_t node0 = f << kFineLog;
   constexpr uint32_t kPerThread = kResolveMsgCap / kResolveBlock;
-  // 1: place and roll of every message
-  uint32_t add[kPerThread];
+  // 1: receipts per node; arrival index a of every message
+  uint32_t a[kPerThread];
 #pragma unroll
   for (uint32_t j = 0; j < kPerThread; ++j) {
-    const uint32_t p = tid + j * kResolveBlock;
-    add[j] = 0;
-    if (p >= M) continue;
-    const uint32_t m = sm.buf[p], loc = msg_loc(m), k = msg_tick(m);
-    uint32_t s, e;
-    segment_of(sm, p, M, loc, s, e);
-    uint32_t i = 0, before = 0;
-    for (uint32_t q = s; q < e; ++q) {
-      const uint32_t kq = msg_tick(sm.buf[q]);
-      before += kq < k;
-      i += (kq == k) & (q < p);
-    }
-    bool roll = (m >> kRoll0Fine) & 1;                                      // :112
-    if (i > 0 && w.kc > 0) {
-      const u32x4 r = philox(node0 + loc, t0 + k, i >> 2, c3crash, w.key.k0, w.key.k1);
-      roll = (int32_t)uniform(lane_of(r, i & 3), 100u) < w.kc;
-    }
-    add[j] = (roll ? kRollBit : 0u) | ((before + i) << kOrdShift);
+    a[j] = 0;
+    if (mr[j] == ~0u) continue;
+    const uint32_t loc = msg_loc(mr[j]), sh = (loc & 1) * 16;
+    a[j] = (atomicAdd(&sm.cnt[loc >> 1], 1u << sh) >> sh) & 0xFFFFu;
   }
 #pragma unroll
-  for (uint32_t j = 0; j < kPerThread; ++j) {
-    const uint32_t p = tid + j * kResolveBlock;
-    if (p < M) atomicOr(&sm.buf[p], add[j]);  // other lanes read only loc and tick meanwhile
-  }
+  for (uint32_t j = 0; j < kPerThread; ++j)
+    if (mr[j] != ~0u) sm.buf[tid + j * kResolveBlock] = mr[j];
   __syncthreads();
-  if (stamp) ts[5] = __builtin_amdgcn_s_memrealtime();
-  // 2: counted / crash / infect
-  uint32_t* inf = sm.cnt;  // the counting-sort array is free now
+  GS_STAMPW(2);
+  uint32_t cw[kPerThread], crw[kPerThread], rcw[kPerThread];
+  bool big = false;
 #pragma unroll
   for (uint32_t j = 0; j < kPerThread; ++j) {
-    const uint32_t p = tid + j * kResolveBlock;
-    if (p >= M) continue;
-    const uint32_t m = sm.buf[p], loc = msg_loc(m), k = msg_tick(m), bit = 1u << (loc & 31);
-    const uint32_t o = m >> kOrdShift;
-    const bool roll = (m & kRollBit) != 0;
-    const bool crashed0 = (sm.crash[loc >> 5] & bit) != 0;
-    uint32_t cstar = 0xFFFFu;
-    if (!crashed0) {
-      uint32_t s, e;
-      segment_of(sm, p, M, loc, s, e);
-      for (uint32_t q = s; q < e; ++q) {
-        const uint32_t mq = sm.buf[q];
-        if (mq & kRollBit) cstar = min(cstar, mq >> kOrdShift);
-      }
-    }
-    const bool dead = crashed0 || o > cstar;                                 // :108, :111
-    const bool crashm = !crashed0 && roll && o == cstar;                     // :113-115
-    const bool infect = !crashed0 && o == 0 && !roll && !(sm.recv[loc >> 5] & bit);  // :117-121
+    const uint32_t loc = msg_loc(mr[j]);
+    const bool v = mr[j] != ~0u;
+    cw[j] = v ? sm.cnt[loc >> 1] : 0u;
+    crw[j] = v ? sm.crash[loc >> 5] : 0u;
+    rcw[j] = v ? sm.recv[loc >> 5] : 0u;
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kPerThread; ++j) {
+    cw[j] = mr[j] == ~0u ? 0u : half_of(cw[j], msg_loc(mr[j]));  // receipts of the node
+    big |= cw[j] > 255;  // a replayed node keeps 8-bit per-tick counts
+  }
+  if (big) sm.err = 2;
+  __syncthreads();
+  GS_STAMPW(3);
+  if (sm.err == 2) return false;
+  // 2: singletons resolve in their lane; multi nodes are linked and listed
+  uint32_t infmask = 0;            // slot j infected its node (singletons)
+  unsigned long long infk = 0;     // slot j: 4-bit infection tick
+#pragma unroll
+  for (uint32_t j = 0; j < kPerThread; ++j) {
+    const uint32_t m = mr[j], loc = msg_loc(m), k = msg_tick(m), bit = 1u << (loc & 31);
+    const bool single = m != ~0u && cw[j] == 1;
+    const bool crashed0 = (crw[j] & bit) != 0, roll = (m >> kRoll0Fine) & 1;
+    const bool dead = single && crashed0;                                     // :108
+    const bool crashm = single && !crashed0 && roll;                          // :113-115
+    const bool infect = single && !crashed0 && !roll && !(rcw[j] & bit);      // :117-121
     if (dead) atomicAdd(&sm.st[k][0], 1u);
     if (crashm) {
       atomicAdd(&sm.st[k][2], 1u);
@@ -554,12 +610,72 @@ __device__ void resolve_sorted(const WinState& w, ResolveLds& sm, uint32_t f, ui
     if (infect) {
       atomicAdd(&sm.st[k][1], 1u);
       atomicOr(&sm.nrecv[loc >> 5], bit);
-      inf[atomicAdd(&sm.ninf, 1u)] = loc | (k << kFineLog);
+      infmask |= 1u << j;
+      infk |= (unsigned long long)k << (4 * j);
+    }
+    const bool owner = m != ~0u && cw[j] > 1 && a[j] == 0;
+    const uint32_t at = wave_append(&sm.nown, owner);
+    if (owner) sm.own[at] = (uint16_t)loc;
+  }
+  // link the receipts of multi nodes: head = kHeadFlag | (index + 1)
+  uint32_t old[kPerThread];
+#pragma unroll
+  for (uint32_t j = 0; j < kPerThread; ++j) {
+    const uint32_t loc = msg_loc(mr[j]), sh = (loc & 1) * 16;
+    const uint32_t p = tid + j * kResolveBlock;
+    if (mr[j] == ~0u || cw[j] < 2) continue;
+    uint32_t o = sm.cnt[loc >> 1];
+    for (;;) {
+      const uint32_t nw = (o & ~(0xFFFFu << sh)) | ((kHeadFlag | (p + 1)) << sh);
+      const uint32_t got = atomicCAS(&sm.cnt[loc >> 1], o, nw);
+      if (got == o) break;
+      o = got;
+    }
+    old[j] = (o >> sh) & 0xFFFFu;
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kPerThread; ++j) {
+    if (mr[j] == ~0u || cw[j] < 2) continue;
+    const uint32_t link = (old[j] & kHeadFlag) ? (old[j] & ~kHeadFlag) : 0u;
+    sm.buf[tid + j * kResolveBlock] = mr[j] | (link << kLinkShift);
+  }
+  __syncthreads();
+  GS_STAMPW(4);
+  // 3: one multi node per lane; an infection is left in the node's head half
+  // (0x4000 | tick) for phase 4
+  const uint32_t nown = sm.nown;
+  for (uint32_t q = tid; q < nown; q += kResolveBlock) {
+    const uint32_t loc = sm.own[q], sh = (loc & 1) * 16;
+    const uint32_t x = replay_multi(w, sm, f, loc, t0, c3crash);
+    if (x) {
+      atomicAnd(&sm.cnt[loc >> 1], ~(0xFFFFu << sh));
+      atomicOr(&sm.cnt[loc >> 1], (kInfMark | (x - 1)) << sh);
     }
   }
   __syncthreads();
-  if (stamp) ts[6] = __builtin_amdgcn_s_memrealtime();
-  // 3: Broadcast() of every infected node (:122, :141-142): fire at t + off
+  GS_STAMPW(5);
+  // 4: infection list (the receipt buffer is free now)
+  uint32_t* inf = sm.buf;
+#pragma unroll
+  for (uint32_t j = 0; j < kPerThread; ++j) {
+    const bool x = (infmask >> j) & 1;
+    const uint32_t at = wave_append(&sm.ninf, x);
+    if (x) inf[at] = msg_loc(mr[j]) | ((uint32_t)((infk >> (4 * j)) & 15u) << kFineLog);
+  }
+  for (uint32_t q0 = 0; q0 < nown; q0 += kResolveBlock) {
+    const uint32_t q = q0 + tid;
+    uint32_t loc = 0, h = 0;
+    if (q < nown) {
+      loc = sm.own[q];
+      h = half_of(sm.cnt[loc >> 1], loc);
+    }
+    const bool x = q < nown && (h & (kHeadFlag | kInfMark)) == kInfMark;
+    const uint32_t at = wave_append(&sm.ninf, x);
+    if (x) inf[at] = loc | ((h & (kMaxWindow - 1)) << kFineLog);
+  }
+  __syncthreads();
+  GS_STAMPW(6);
+  // 5: Broadcast() of each infected node (:122, :141-142): fire at t + off
   const uint32_t c3delay = ctr3(K_DELAY, w.key.trial);
   for (uint32_t q = tid; q < sm.ninf; q += kResolveBlock) {
     const uint32_t x = inf[q], loc = msg_loc(x), t = t0 + msg_tick(x);
@@ -570,6 +686,8 @@ __device__ void resolve_sorted(const WinState& w, ResolveLds& sm, uint32_t f, ui
     w.flist[((size_t)slot * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
   }
   if (tid < kMaxWindow) sm.st[tid][3] = sm.st[tid][1];
+  return true;
+#undef GS_STAMPW
 }
 
 __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
@@ -590,14 +708,15 @@ __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uin
   const uint64_t nw32 = w.W * 2;
   const uint32_t* gm = w.fmsg + mb;
   constexpr uint32_t kPerThread = kResolveMsgCap / kResolveBlock;
+  static_assert(kResolveMsgCap % kResolveBlock == 0, "whole messages per thread");
   constexpr uint32_t kBitWords = kFineNodes / 32;
   static_assert(kBitWords == kResolveBlock, "one bit word per thread");
   uint32_t mr[kPerThread];
-  bool small = M < kResolveMsgCap;
+  bool small = M <= kResolveMsgCap;
 #pragma unroll
   for (uint32_t i = 0; i < kPerThread; ++i) {
     const uint32_t p = tid + i * kResolveBlock;
-    mr[i] = small && p < M ? gm[p] : ~0u;
+    mr[i] = small && p < M ? gm[p] & ((1u << kMsgBits) - 1) : ~0u;
   }
   const bool in = wbase + tid < nw32;
   const uint32_t recv0 = in ? rg[wbase + tid] : 0u, crash0 = in ? cg[wbase + tid] : 0u;
@@ -611,79 +730,24 @@ __global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uin
   }
   for (uint32_t s = tid; s < w.R; s += kResolveBlock) sm.fc[s] = w.fcount[(size_t)s * w.nfine + f];
   if (tid < kMaxWindow * 4) (&sm.st[0][0])[tid] = 0;
-  if (tid == 0) { sm.err = 0; sm.ninf = 0; }
+  if (tid == 0) { sm.err = 0; sm.ninf = 0; sm.nown = 0; }
   const uint32_t c3crash = ctr3(K_CRASH, w.key.trial);
   __syncthreads();
   GS_STAMP(1);
-  if (small) {
-    // counting sort of the bucket's messages by node (u16 counters -> offsets)
-#pragma unroll
-    for (uint32_t i = 0; i < kPerThread; ++i)
-      if (mr[i] != ~0u) {
-        const uint32_t loc = msg_loc(mr[i]);
-        atomicAdd(&sm.cnt[loc >> 1], 1u << ((loc & 1) * 16));
-      }
+  if (small && !resolve_window(w, sm, f, M, t0, c3crash, mr, stamp, ts)) {
+    small = false;  // a node with > 255 receipts in the window
     __syncthreads();
-    GS_STAMP(2);
-    {  // exclusive scan of 16384 u16 counters: 32 per thread (M < 8192 fits u16)
-      constexpr uint32_t kPer = kFineNodes / kResolveBlock;  // 32
-      uint32_t* wp = &sm.cnt[tid * (kPer / 2)];
-      uint32_t sum = 0;
-      bool big = false;
-#pragma unroll
-      for (uint32_t i = 0; i < kPer / 2; ++i) {
-        const uint32_t a = wp[i] & 0xFFFFu, b = wp[i] >> 16;
-        sum += a + b;
-        big |= a > kMaxSeg || b > kMaxSeg;
-      }
-      if (big) sm.err = 2;
-      const uint32_t lane = tid & 63, wv = tid >> 6;
-      uint32_t x = sum;
-#pragma unroll
-      for (uint32_t o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-      }
-      if (lane == 63) sm.wsum[wv] = x;
-      __syncthreads();
-      uint32_t base = x - sum;
-      for (uint32_t v = 0; v < wv; ++v) base += sm.wsum[v];
-#pragma unroll
-      for (uint32_t i = 0; i < kPer / 2; ++i) {
-        const uint32_t a = wp[i] & 0xFFFFu, b = wp[i] >> 16;
-        wp[i] = base | ((base + a) << 16);
-        base += a + b;
-      }
-    }
+    uint4* c4 = reinterpret_cast<uint4*>(sm.cnt);
+    for (uint32_t i = tid; i < kFineNodes / 8; i += kResolveBlock) c4[i] = make_uint4(0, 0, 0, 0);
+    if (tid == 0) sm.err = 0;
     __syncthreads();
-    GS_STAMP(3);
-    if (sm.err == 2) {
-      // a node with more than kMaxSeg receipts: take the large path instead
-      small = false;
-      __syncthreads();
-      uint4* c4 = reinterpret_cast<uint4*>(sm.cnt);
-      for (uint32_t i = tid; i < kFineNodes / 8; i += kResolveBlock) c4[i] = make_uint4(0, 0, 0, 0);
-      if (tid == 0) sm.err = 0;
-      __syncthreads();
-    } else {
-#pragma unroll
-      for (uint32_t i = 0; i < kPerThread; ++i)
-        if (mr[i] != ~0u) {
-          const uint32_t loc = msg_loc(mr[i]), sh = (loc & 1) * 16;
-          const uint32_t pos = (atomicAdd(&sm.cnt[loc >> 1], 1u << sh) >> sh) & 0xFFFFu;
-          sm.buf[pos] = mr[i] & ((1u << (kRoll0Fine + 1)) - 1);
-        }
-      __syncthreads();
-      GS_STAMP(4);
-      resolve_sorted(w, sm, f, M, t0, c3crash, stamp, ts);
-      __syncthreads();
-      GS_STAMP(7);
-    }
   }
   if (!small) {
     // large bucket: stream the messages from global memory once per tick
     for (uint32_t k = 0; k < L; ++k) resolve_tick(w, sm, f, gm, 0, M, k, t0 + k, c3crash);
   }
+  __syncthreads();
+  GS_STAMP(7);
   uint32_t* rw = (uint32_t*)w.recv;
   uint32_t* cw = (uint32_t*)w.crash;
   if (in) {
