@@ -390,12 +390,12 @@ void gs_destroy(gs_ctx* c) {
   if (c->ws.dbg) {
     unsigned long long h[2 * kStampPhases];
     if (hipMemcpy(h, c->ws.dbg, sizeof h, hipMemcpyDeviceToHost) == hipSuccess)
-      for (int cls = 0; cls < 2; ++cls) {
+      for (int cls = 0; cls < 2; ++cls) {  // k_resolve phases (GS_STAMPS=1), thread 0 of every workgroup
         const unsigned long long* d = h + cls * kStampPhases;
-        fprintf(stderr, "[stamps] k_resolve %s: %llu workgroups, mean us per phase:", cls ? "M>=2048" : "M<2048",
-                d[0]);
-        for (uint32_t i = 1; i < kStampPhases; ++i)
-          fprintf(stderr, " %.2f", d[0] ? d[i] * 0.01 / d[0] : 0.0);
+        if (!d[0]) continue;
+        fprintf(stderr, "[stamps] k_resolve %s: %llu buckets, mean kcycles per bucket per phase:",
+                cls ? "M>=1024" : "M<1024", d[0]);
+        for (uint32_t i = 1; i < kStampPhases; ++i) fprintf(stderr, " %.2f", d[i] * 1e-3 / d[0]);
         fprintf(stderr, "\n");
       }
     (void)hipFree(c->ws.dbg);

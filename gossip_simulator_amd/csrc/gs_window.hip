@@ -28,6 +28,7 @@
 // partition is redone with exact counts (expand and part2 are idempotent).
 // Fire lists: fcount[R][nfine] + flist[R][nfine][16384] (u16 local ids).
 #include <hipcub/hipcub.hpp>
+#include <cstdlib>
 
 #include "gs_internal.h"
 
@@ -381,20 +382,37 @@ __global__ __launch_bounds__(256) void k_part2(const WinState w) {
   }
 }
 
+constexpr uint32_t kResolveMaxBuckets = 256;  // buckets one persistent workgroup may own
+
 struct ResolveLds {
-  uint32_t cnt[kFineNodes / 2];     // u16 per node: receipts in the window, then list heads
+  uint32_t cnt[kFineNodes / 2];     // u16 per node: receipts in the window, then list heads;
+                                    // all zero between buckets (cleared where touched)
   uint32_t recv[kFineNodes / 32];   // bits at the window start
   uint32_t crash[kFineNodes / 32];
   uint32_t nrecv[kFineNodes / 32];  // bits set during the window
   uint32_t ncrash[kFineNodes / 32];
   uint32_t buf[kResolveMsgCap];     // the bucket's messages (arrival order) + list links
   uint32_t fc[kWinMaxRing];         // fire-list lengths of this bucket, per ring slot
-  uint32_t st[kMaxWindow][4];       // dead (not counted), recv, crash, sched per tick
+  uint32_t st[kMaxWindow][4];       // dead (not counted), recv, crash per tick: whole launch
   uint16_t own[kResolveMsgCap / 2]; // nodes with several receipts (<= half the receipts)
+  uint32_t blist[kResolveMaxBuckets];  // this workgroup's non-empty buckets
   uint32_t nown;
   uint32_t ninf;
   uint32_t err;
-};  // ~78 KB: two workgroups per CU
+  uint32_t nb;
+  unsigned long long stamp[2][kStampPhases];  // GS_STAMPS: [M >= 1024][phase] cycles (thread 0)
+  unsigned long long tlast;
+  uint32_t cls;
+};  // ~79 KB: two workgroups per CU
+
+// GS_STAMPS diagnostics: thread 0 adds the cycles since the last stamp to phase i.
+__device__ __forceinline__ void stamp(const WinState& w, ResolveLds& sm, uint32_t i) {
+  if (w.dbg && threadIdx.x == 0) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    if (i) sm.stamp[sm.cls][i] += t - sm.tlast;
+    sm.tlast = t;
+  }
+}
 
 // buf entry: loc | k << 14 | roll0 << 18 | link << 19 (link = index + 1 of the
 // next receipt of the same node, 0 = end); list heads are kHeadFlag | (index+1)
@@ -472,7 +490,7 @@ __device__ __forceinline__ void resolve_tick(const WinState& w, ResolveLds& sm, 
   if (arr != cm) atomicAdd(&sm.st[k][0], arr - cm);
   if (cr) atomicAdd(&sm.st[k][1], cr);
   if (cc) atomicAdd(&sm.st[k][2], cc);
-  if (cs) atomicAdd(&sm.st[k][3], cs);
+  (void)cs;  // every infection schedules one Broadcast: ST_SCHED = ST_RECV
   __syncthreads();
 }
 
@@ -507,10 +525,11 @@ __device__ __forceinline__ uint32_t replay_multi(const WinState& w, ResolveLds& 
       continue;
     }
     const uint32_t t = t0 + k;
+    u32x4 r{0, 0, 0, 0};
     for (uint32_t i = 0; i < kk; ++i) {
       bool roll = (rollmask >> k) & 1;                            // :112
       if (i > 0 && w.kc > 0) {
-        const u32x4 r = philox(u, t, i >> 2, c3crash, w.key.k0, w.key.k1);
+        if (i == 1 || (i & 3) == 0) r = philox(u, t, i >> 2, c3crash, w.key.k0, w.key.k1);
         roll = (int32_t)uniform(lane_of(r, i & 3), 100u) < w.kc;
       }
       if (roll) {                                                 // :113-115
@@ -531,99 +550,151 @@ __device__ __forceinline__ uint32_t replay_multi(const WinState& w, ResolveLds& 
   return inf;
 }
 
+__device__ __forceinline__ uint32_t lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+__device__ __forceinline__ uint32_t mbcnt(unsigned long long b) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+}
+
 // Wave-aggregated append: one LDS atomic per wave, lanes with `take` get
-// consecutive slots of the list whose fill counter is *n.
+// consecutive slots of the list whose fill counter is *n (all lanes active).
 __device__ __forceinline__ uint32_t wave_append(uint32_t* n, bool take) {
   const unsigned long long bal = __ballot(take);
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t leader = bal ? (uint32_t)__ffsll((long long)bal) - 1 : 0;
   uint32_t base = 0;
-  if (take && lane == leader) base = atomicAdd(n, (uint32_t)__popcll(bal));
-  base = __shfl(base, leader, 64);
-  return base + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+  if (bal && lane_id() == 0) base = atomicAdd(n, (uint32_t)__popcll(bal));
+  return __builtin_amdgcn_readfirstlane(base) + mbcnt(bal);
 }
+
+// As wave_append for c < 16 items per lane: the lane's first slot.
+__device__ __forceinline__ uint32_t wave_reserve(uint32_t* n, uint32_t c) {
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (uint32_t b = 0; b < 4; ++b) {
+    const unsigned long long bal = __ballot((c >> b) & 1u);
+    pre += mbcnt(bal) << b;
+    tot += (uint32_t)__popcll(bal) << b;
+  }
+  uint32_t base = 0;
+  if (tot && lane_id() == 0) base = atomicAdd(n, tot);
+  return __builtin_amdgcn_readfirstlane(base) + pre;
+}
+
+// Per-tick counters: one LDS atomic per (wave, tick, field) instead of one
+// per lane; a wave's receipts span one or two ticks (all lanes active).
+__device__ __forceinline__ void wave_stats(ResolveLds& sm, uint32_t k, bool dead, bool crashm,
+                                           bool infect) {
+  unsigned long long m = __ballot(dead || crashm || infect);
+  const uint32_t lane = lane_id();
+  while (m) {
+    const uint32_t kl = __builtin_amdgcn_readlane(k, (uint32_t)__builtin_ctzll(m));
+    const bool mine = k == kl;
+    const unsigned long long sd = __ballot(mine && dead), si = __ballot(mine && infect),
+                             sc = __ballot(mine && crashm);
+    const unsigned long long s = lane == 0 ? sd : lane == 1 ? si : sc;
+    if (lane < 3 && s) atomicAdd(&sm.st[kl][lane], (uint32_t)__popcll(s));
+    m &= ~(sd | si | sc);
+  }
+}
+
+constexpr uint32_t kPerThread = kResolveMsgCap / kResolveBlock;
+static_assert(kResolveMsgCap % kResolveBlock == 0, "whole messages per thread");
+static_assert(kPerThread < 16, "per-lane counts fit wave_reserve");
 
 // The receive case (simulator.go:107-123) for one bucket and a whole window.
 // Most receiving nodes get exactly one receipt: ordinal 0 of its tick, whose
 // crash roll rode with the message, so it resolves in its own lane.  Nodes
 // with several receipts are linked into per-node lists and replayed one node
-// per lane.  Every phase issues its LDS reads for all of a thread's receipts
-// before it uses them.
-// Returns false (state untouched but the counters) if a node has more than
-// 255 receipts: the caller then takes the large path.
-__device__ bool resolve_window(const WinState& w, ResolveLds& sm, uint32_t f, uint32_t M,
-                               uint32_t t0, uint32_t c3crash, const uint32_t* mr, bool stamp,
-                               unsigned long long* ts) {
-#define GS_STAMPW(i) if (stamp) ts[i] = __builtin_amdgcn_s_memrealtime()
+// per lane.  Returns false (nothing changed but sm.cnt) if a node has more
+// than 255 receipts: the caller then takes the large path.
+template <int PROBE>
+__device__ bool resolve_window(const WinState& w, ResolveLds& sm, uint32_t f, uint32_t t0,
+                               uint32_t c3crash, const uint32_t (&mr)[kPerThread], uint32_t nj) {
   const uint32_t tid = threadIdx.x;
   const uint32_t node0 = f << kFineLog;
-  constexpr uint32_t kPerThread = kResolveMsgCap / kResolveBlock;
-  // 1: receipts per node; arrival index a of every message
-  uint32_t a[kPerThread];
+  // 1: receipts per node; first arrival of every node
+  uint32_t firstm = 0;
 #pragma unroll
   for (uint32_t j = 0; j < kPerThread; ++j) {
-    a[j] = 0;
+    if (j >= nj) continue;  // nj = ceil(M / 512): slots past it hold no message
     if (mr[j] == ~0u) continue;
     const uint32_t loc = msg_loc(mr[j]), sh = (loc & 1) * 16;
-    a[j] = (atomicAdd(&sm.cnt[loc >> 1], 1u << sh) >> sh) & 0xFFFFu;
+    const uint32_t a = (atomicAdd(&sm.cnt[loc >> 1], 1u << sh) >> sh) & 0xFFFFu;
+    firstm |= (a == 0 ? 1u : 0u) << j;
   }
 #pragma unroll
-  for (uint32_t j = 0; j < kPerThread; ++j)
+  for (uint32_t j = 0; j < kPerThread; ++j) {
+    if (j >= nj) continue;
     if (mr[j] != ~0u) sm.buf[tid + j * kResolveBlock] = mr[j];
-  __syncthreads();
-  GS_STAMPW(2);
-  uint32_t cw[kPerThread], crw[kPerThread], rcw[kPerThread];
-  bool big = false;
-#pragma unroll
-  for (uint32_t j = 0; j < kPerThread; ++j) {
-    const uint32_t loc = msg_loc(mr[j]);
-    const bool v = mr[j] != ~0u;
-    cw[j] = v ? sm.cnt[loc >> 1] : 0u;
-    crw[j] = v ? sm.crash[loc >> 5] : 0u;
-    rcw[j] = v ? sm.recv[loc >> 5] : 0u;
   }
+  __syncthreads();
+  stamp(w, sm, 2);
+  // 2: classify: singletons resolve in their lane, multi nodes are listed
+  uint32_t singlem = 0, multim = 0, crashedm = 0, recvm = 0;
+  bool big = false;
+  constexpr uint32_t kHalf = (kPerThread + 1) / 2;  // reads in flight per step (VGPR budget)
 #pragma unroll
-  for (uint32_t j = 0; j < kPerThread; ++j) {
-    cw[j] = mr[j] == ~0u ? 0u : half_of(cw[j], msg_loc(mr[j]));  // receipts of the node
-    big |= cw[j] > 255;  // a replayed node keeps 8-bit per-tick counts
+  for (uint32_t j0 = 0; j0 < kPerThread; j0 += kHalf) {
+    uint32_t cw[kHalf], crw[kHalf], rcw[kHalf];
+#pragma unroll
+    for (uint32_t jj = 0; jj < kHalf; ++jj) {
+      const uint32_t j = j0 + jj;
+      if (j >= kPerThread || j >= nj) continue;
+      // unconditional (an empty slot reads node 16383's words): no exec-masked load chain
+      const uint32_t loc = msg_loc(mr[j]);
+      cw[jj] = sm.cnt[loc >> 1];
+      crw[jj] = sm.crash[loc >> 5];
+      rcw[jj] = sm.recv[loc >> 5];
+    }
+#pragma unroll
+    for (uint32_t jj = 0; jj < kHalf; ++jj) {
+      const uint32_t j = j0 + jj;
+      if (j >= kPerThread || j >= nj) continue;
+      const uint32_t loc = msg_loc(mr[j]), bit = 1u << (loc & 31);
+      const uint32_t c = mr[j] == ~0u ? 0u : half_of(cw[jj], loc);  // receipts of the node
+      big |= c > 255;  // a replayed node keeps 8-bit per-tick counts
+      singlem |= (c == 1 ? 1u : 0u) << j;
+      multim |= (c > 1 ? 1u : 0u) << j;
+      crashedm |= ((crw[jj] & bit) ? 1u : 0u) << j;
+      recvm |= ((rcw[jj] & bit) ? 1u : 0u) << j;
+    }
   }
   if (big) sm.err = 2;
   __syncthreads();
-  GS_STAMPW(3);
+  stamp(w, sm, 3);
   if (sm.err == 2) return false;
-  // 2: singletons resolve in their lane; multi nodes are linked and listed
   uint32_t infmask = 0;            // slot j infected its node (singletons)
-  unsigned long long infk = 0;     // slot j: 4-bit infection tick
 #pragma unroll
   for (uint32_t j = 0; j < kPerThread; ++j) {
+    if (j >= nj) continue;
     const uint32_t m = mr[j], loc = msg_loc(m), k = msg_tick(m), bit = 1u << (loc & 31);
-    const bool single = m != ~0u && cw[j] == 1;
-    const bool crashed0 = (crw[j] & bit) != 0, roll = (m >> kRoll0Fine) & 1;
+    const bool single = (singlem >> j) & 1, crashed0 = (crashedm >> j) & 1;
+    const bool roll = (m >> kRoll0Fine) & 1;
     const bool dead = single && crashed0;                                     // :108
     const bool crashm = single && !crashed0 && roll;                          // :113-115
-    const bool infect = single && !crashed0 && !roll && !(rcw[j] & bit);      // :117-121
-    if (dead) atomicAdd(&sm.st[k][0], 1u);
-    if (crashm) {
-      atomicAdd(&sm.st[k][2], 1u);
-      atomicOr(&sm.ncrash[loc >> 5], bit);
-    }
-    if (infect) {
-      atomicAdd(&sm.st[k][1], 1u);
-      atomicOr(&sm.nrecv[loc >> 5], bit);
-      infmask |= 1u << j;
-      infk |= (unsigned long long)k << (4 * j);
-    }
-    const bool owner = m != ~0u && cw[j] > 1 && a[j] == 0;
-    const uint32_t at = wave_append(&sm.nown, owner);
-    if (owner) sm.own[at] = (uint16_t)loc;
+    const bool infect = single && !crashed0 && !roll && !((recvm >> j) & 1);  // :117-121
+    wave_stats(sm, k, dead, crashm, infect);
+    if (crashm) atomicOr(&sm.ncrash[loc >> 5], bit);
+    if (infect) atomicOr(&sm.nrecv[loc >> 5], bit);
+    infmask |= (infect ? 1u : 0u) << j;
   }
-  // link the receipts of multi nodes: head = kHeadFlag | (index + 1)
-  uint32_t old[kPerThread];
+  // owners (first receipt of a multi node) are listed; receipts are linked:
+  // head = kHeadFlag | (index + 1)
+  const uint32_t ownm = multim & firstm;
+  {
+    uint32_t at = wave_reserve(&sm.nown, (uint32_t)__popc(ownm));
+#pragma unroll
+    for (uint32_t j = 0; j < kPerThread; ++j) {
+      if (j >= nj) continue;
+      if ((ownm >> j) & 1) sm.own[at++] = (uint16_t)msg_loc(mr[j]);
+    }
+  }
 #pragma unroll
   for (uint32_t j = 0; j < kPerThread; ++j) {
+    if (j >= nj) continue;
+    if (!((multim >> j) & 1)) continue;
     const uint32_t loc = msg_loc(mr[j]), sh = (loc & 1) * 16;
     const uint32_t p = tid + j * kResolveBlock;
-    if (mr[j] == ~0u || cw[j] < 2) continue;
     uint32_t o = sm.cnt[loc >> 1];
     for (;;) {
       const uint32_t nw = (o & ~(0xFFFFu << sh)) | ((kHeadFlag | (p + 1)) << sh);
@@ -631,18 +702,14 @@ __device__ bool resolve_window(const WinState& w, ResolveLds& sm, uint32_t f, ui
       if (got == o) break;
       o = got;
     }
-    old[j] = (o >> sh) & 0xFFFFu;
-  }
-#pragma unroll
-  for (uint32_t j = 0; j < kPerThread; ++j) {
-    if (mr[j] == ~0u || cw[j] < 2) continue;
-    const uint32_t link = (old[j] & kHeadFlag) ? (old[j] & ~kHeadFlag) : 0u;
-    sm.buf[tid + j * kResolveBlock] = mr[j] | (link << kLinkShift);
+    const uint32_t old = (o >> sh) & 0xFFFFu;
+    const uint32_t link = (old & kHeadFlag) ? (old & ~kHeadFlag) : 0u;
+    sm.buf[p] = mr[j] | (link << kLinkShift);
   }
   __syncthreads();
-  GS_STAMPW(4);
+  stamp(w, sm, 4);
   // 3: one multi node per lane; an infection is left in the node's head half
-  // (0x4000 | tick) for phase 4
+  // (kInfMark | tick) for phase 4
   const uint32_t nown = sm.nown;
   for (uint32_t q = tid; q < nown; q += kResolveBlock) {
     const uint32_t loc = sm.own[q], sh = (loc & 1) * 16;
@@ -653,14 +720,16 @@ __device__ bool resolve_window(const WinState& w, ResolveLds& sm, uint32_t f, ui
     }
   }
   __syncthreads();
-  GS_STAMPW(5);
+  stamp(w, sm, 5);
   // 4: infection list (the receipt buffer is free now)
   uint32_t* inf = sm.buf;
+  {
+    uint32_t at = wave_reserve(&sm.ninf, (uint32_t)__popc(infmask));
 #pragma unroll
-  for (uint32_t j = 0; j < kPerThread; ++j) {
-    const bool x = (infmask >> j) & 1;
-    const uint32_t at = wave_append(&sm.ninf, x);
-    if (x) inf[at] = msg_loc(mr[j]) | ((uint32_t)((infk >> (4 * j)) & 15u) << kFineLog);
+    for (uint32_t j = 0; j < kPerThread; ++j) {
+      if (j >= nj) continue;
+      if ((infmask >> j) & 1) inf[at++] = msg_loc(mr[j]) | (msg_tick(mr[j]) << kFineLog);
+    }
   }
   for (uint32_t q0 = 0; q0 < nown; q0 += kResolveBlock) {
     const uint32_t q = q0 + tid;
@@ -674,105 +743,150 @@ __device__ bool resolve_window(const WinState& w, ResolveLds& sm, uint32_t f, ui
     if (x) inf[at] = loc | ((h & (kMaxWindow - 1)) << kFineLog);
   }
   __syncthreads();
-  GS_STAMPW(6);
+  stamp(w, sm, 6);
+  if (PROBE == 3) return true;
   // 5: Broadcast() of each infected node (:122, :141-142): fire at t + off
   const uint32_t c3delay = ctr3(K_DELAY, w.key.trial);
-  for (uint32_t q = tid; q < sm.ninf; q += kResolveBlock) {
+  const uint32_t ninf = sm.ninf;
+  for (uint32_t q = tid; q < ninf; q += kResolveBlock) {
     const uint32_t x = inf[q], loc = msg_loc(x), t = t0 + msg_tick(x);
     const uint32_t off = fire_offset(w.delay_low, w.delay_span,
                                      philox(node0 + loc, t, 0, c3delay, w.key.k0, w.key.k1).x);
     const uint32_t slot = (t + off) % w.R;
     const uint32_t pos = atomicAdd(&sm.fc[slot], 1u);
-    w.flist[((size_t)slot * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
+    if (!PROBE) w.flist[((size_t)slot * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
   }
-  if (tid < kMaxWindow) sm.st[tid][3] = sm.st[tid][1];
   return true;
-#undef GS_STAMPW
 }
 
-__global__ __launch_bounds__(kResolveBlock) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
-  __shared__ ResolveLds sm;
-  const uint32_t f = blockIdx.x, tid = threadIdx.x;
-  const unsigned long long mb = w.fstart[f];
-  const uint32_t M = (uint32_t)w.ffill[f];
-  if (M == 0) return;  // no receipt in this bucket during the window
-  // diagnostic phase stamps (GS_STAMPS=1): every 64th workgroup
-  const bool stamp = w.dbg != nullptr && (f & 63) == 0;
-  unsigned long long ts[kStampPhases];
-#define GS_STAMP(i) if (stamp) ts[i] = __builtin_amdgcn_s_memrealtime()
-  GS_STAMP(0);
-  const uint32_t node0 = f << kFineLog;
-  const uint64_t wbase = (uint64_t)node0 >> 5;  // u32 word index of the bucket's bits
-  const uint32_t* rg = (const uint32_t*)w.recv;
-  const uint32_t* cg = (const uint32_t*)w.crash;
-  const uint64_t nw32 = w.W * 2;
+// Bucket f's messages (arrival order), bit words and fire-list lengths into
+// registers.
+__device__ __forceinline__ void fetch_bucket(const WinState& w, uint32_t f, unsigned long long mb,
+                                             uint32_t M, uint32_t (&mr)[kPerThread], uint32_t& r0,
+                                             uint32_t& c0, uint32_t& fcv) {
+  const uint32_t tid = threadIdx.x;
   const uint32_t* gm = w.fmsg + mb;
-  constexpr uint32_t kPerThread = kResolveMsgCap / kResolveBlock;
-  static_assert(kResolveMsgCap % kResolveBlock == 0, "whole messages per thread");
-  constexpr uint32_t kBitWords = kFineNodes / 32;
-  static_assert(kBitWords == kResolveBlock, "one bit word per thread");
-  uint32_t mr[kPerThread];
-  bool small = M <= kResolveMsgCap;
+  const bool small = M <= kResolveMsgCap;
+  // branch-free: every lane loads (index clamped into the bucket, M >= 1), so
+  // the loads issue back to back instead of one exec-masked load at a time
+  const uint32_t nj = small ? (M + kResolveBlock - 1) / kResolveBlock : 0u;
+#pragma unroll
+  for (uint32_t i = 0; i < kPerThread; ++i) mr[i] = ~0u;
 #pragma unroll
   for (uint32_t i = 0; i < kPerThread; ++i) {
+    if (i >= nj) continue;
     const uint32_t p = tid + i * kResolveBlock;
-    mr[i] = small && p < M ? gm[p] & ((1u << kMsgBits) - 1) : ~0u;
+    const uint32_t x = gm[p < M ? p : M - 1];
+    mr[i] = p < M ? x & ((1u << kMsgBits) - 1) : ~0u;
   }
-  const bool in = wbase + tid < nw32;
-  const uint32_t recv0 = in ? rg[wbase + tid] : 0u, crash0 = in ? cg[wbase + tid] : 0u;
-  sm.recv[tid] = recv0;
-  sm.crash[tid] = crash0;
-  sm.nrecv[tid] = 0;
-  sm.ncrash[tid] = 0;
+  const uint64_t wi = ((uint64_t)f << kFineLog >> 5) + tid;
+  const bool in = wi < w.W * 2;
+  r0 = in ? ((const uint32_t*)w.recv)[wi] : 0u;
+  c0 = in ? ((const uint32_t*)w.crash)[wi] : 0u;
+  fcv = tid < w.R ? w.fcount[(size_t)tid * w.nfine + f] : 0u;
+}
+
+// Persistent: workgroup g owns buckets g, g + G, g + 2G, ... (G = gridDim.x),
+// resolves its non-empty ones in turn, and adds its per-tick counters once at
+// the end.
+// PROBE > 0 (timing diagnostics, GS_PROBE): no global writes; 1 = skeleton
+// only, 2 = through classification, 3 = through the replay, 4 = all phases.
+template <int PROBE>
+__global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
+  __shared__ ResolveLds sm;
+  const uint32_t tid = threadIdx.x, G = gridDim.x;
+  static_assert(kFineNodes / 32 == kResolveBlock, "one bit word per thread");
+  static_assert(kWinMaxRing <= kResolveBlock, "one ring slot per thread");
+  const uint32_t c3crash = ctr3(K_CRASH, w.key.trial);
   {
     uint4* c4 = reinterpret_cast<uint4*>(sm.cnt);
     for (uint32_t i = tid; i < kFineNodes / 8; i += kResolveBlock) c4[i] = make_uint4(0, 0, 0, 0);
   }
-  for (uint32_t s = tid; s < w.R; s += kResolveBlock) sm.fc[s] = w.fcount[(size_t)s * w.nfine + f];
   if (tid < kMaxWindow * 4) (&sm.st[0][0])[tid] = 0;
-  if (tid == 0) { sm.err = 0; sm.ninf = 0; sm.nown = 0; }
-  const uint32_t c3crash = ctr3(K_CRASH, w.key.trial);
+  if (tid == 0) sm.nb = 0;
+  if (tid < 2 * kStampPhases) (&sm.stamp[0][0])[tid] = 0;
+  if (tid == 0) sm.cls = 0;
   __syncthreads();
-  GS_STAMP(1);
-  if (small && !resolve_window(w, sm, f, M, t0, c3crash, mr, stamp, ts)) {
-    small = false;  // a node with > 255 receipts in the window
-    __syncthreads();
-    uint4* c4 = reinterpret_cast<uint4*>(sm.cnt);
-    for (uint32_t i = tid; i < kFineNodes / 8; i += kResolveBlock) c4[i] = make_uint4(0, 0, 0, 0);
-    if (tid == 0) sm.err = 0;
-    __syncthreads();
-  }
-  if (!small) {
-    // large bucket: stream the messages from global memory once per tick
-    for (uint32_t k = 0; k < L; ++k) resolve_tick(w, sm, f, gm, 0, M, k, t0 + k, c3crash);
+  {
+    const uint32_t f = blockIdx.x + tid * G;
+    const bool ne = tid < kResolveMaxBuckets && f < w.nfine && w.ffill[f] != 0;
+    const uint32_t at = wave_append(&sm.nb, ne);
+    if (ne) sm.blist[at] = f;
   }
   __syncthreads();
-  GS_STAMP(7);
+  const uint32_t nb = sm.nb;
+  stamp(w, sm, 0);
+  // bucket i+1's header is in flight while bucket i is resolved (prefetching
+  // its messages as well would need more VGPRs than two workgroups per CU leave)
+  uint32_t fB = 0, MB = 0;
+  unsigned long long mbB = 0;
+  if (nb > 0) { fB = sm.blist[0]; mbB = w.fstart[fB]; MB = (uint32_t)w.ffill[fB]; }
   uint32_t* rw = (uint32_t*)w.recv;
-  uint32_t* cw = (uint32_t*)w.crash;
-  if (in) {
-    const uint32_t r = sm.recv[tid] | sm.nrecv[tid], c = sm.crash[tid] | sm.ncrash[tid];
-    if (r != recv0) rw[wbase + tid] = r;
-    if (c != crash0) cw[wbase + tid] = c;
+  uint32_t* cwg = (uint32_t*)w.crash;
+  for (uint32_t i = 0; i < nb; ++i) {
+    const uint32_t f = fB, M = MB;
+    const unsigned long long mb = mbB;
+    uint32_t mr[kPerThread], recv0, crash0, fcv;
+    fetch_bucket(w, f, mb, M, mr, recv0, crash0, fcv);
+    if (i + 1 < nb) { fB = sm.blist[i + 1]; mbB = w.fstart[fB]; MB = (uint32_t)w.ffill[fB]; }
+    sm.recv[tid] = recv0;
+    sm.crash[tid] = crash0;
+    sm.nrecv[tid] = 0;
+    sm.ncrash[tid] = 0;
+    if (tid < w.R) sm.fc[tid] = fcv;
+    if (tid == 0) { sm.nown = 0; sm.ninf = 0; sm.err = 0; }
+    __syncthreads();
+    stamp(w, sm, 1);
+    if (tid == 0) sm.cls = M >= 1024 ? 1 : 0;
+    bool small = M <= kResolveMsgCap;
+    if (PROBE == 1) small = true;
+    else if (small && !resolve_window<PROBE>(w, sm, f, t0, c3crash, mr,
+                                              (M + kResolveBlock - 1) / kResolveBlock)) {
+      small = false;  // a node with > 255 receipts in the window
+      __syncthreads();
+      uint4* c4 = reinterpret_cast<uint4*>(sm.cnt);
+      for (uint32_t q = tid; q < kFineNodes / 8; q += kResolveBlock) c4[q] = make_uint4(0, 0, 0, 0);
+      if (tid == 0) sm.err = 0;
+      __syncthreads();
+#pragma unroll
+      for (uint32_t j = 0; j < kPerThread; ++j) mr[j] = ~0u;  // sm.cnt is clean after the large path
+    }
+    if (!small && !PROBE)  // large bucket: stream the messages from global memory once per tick
+      for (uint32_t k = 0; k < L; ++k) resolve_tick(w, sm, f, w.fmsg + mb, 0, M, k, t0 + k, c3crash);
+    __syncthreads();
+    stamp(w, sm, 7);
+    const uint64_t wi = ((uint64_t)f << kFineLog >> 5) + tid;
+    if (!PROBE && wi < w.W * 2) {
+      // the large path (resolve_node) sets sm.recv/sm.crash directly
+      const uint32_t r = sm.recv[tid] | sm.nrecv[tid], c = sm.crash[tid] | sm.ncrash[tid];
+      if (r != recv0) rw[wi] = r;
+      if (c != crash0) cwg[wi] = c;
+    }
+    if (!PROBE && tid < w.R) w.fcount[(size_t)tid * w.nfine + f] = sm.fc[tid];
+#pragma unroll
+    for (uint32_t j = 0; j < kPerThread; ++j) {
+      if (j * kResolveBlock >= M) continue;
+      if (mr[j] != ~0u) sm.cnt[msg_loc(mr[j]) >> 1] = 0;
+    }
+    if (!PROBE && tid == 0 && sm.err) atomicOr(w.err, kErrArrivals);
+    stamp(w, sm, 8);
+    if (w.dbg && tid == 0) sm.stamp[sm.cls][0] += 1;
   }
-  for (uint32_t s = tid; s < w.R; s += kResolveBlock) w.fcount[(size_t)s * w.nfine + f] = sm.fc[s];
-  if (tid < L * 4) {
-    const uint32_t k = tid >> 2, fld = tid & 3;
+  if (w.dbg && tid < 2 * kStampPhases) atomicAdd(&w.dbg[tid], (&sm.stamp[0][0])[tid]);
+  __syncthreads();
+  if (!PROBE && tid < L * 3) {
+    const uint32_t k = tid / 3, fld = tid - k * 3;
     const uint32_t v = sm.st[k][fld];
-    const uint32_t field = fld == 0 ? ST_MSGS : fld == 1 ? ST_RECV : fld == 2 ? ST_CRASH : ST_SCHED;
     // field 0 counts receipts that were NOT counted (:108, after a crash):
     // the expand added every delivered send to ST_MSGS
-    const unsigned long long add = fld == 0 ? 0ull - (unsigned long long)v : (unsigned long long)v;
-    if (v) atomicAdd(&shard_row(w, k)[field], add);
+    unsigned long long* row = shard_row(w, k);
+    if (v && fld == 0) atomicAdd(&row[ST_MSGS], 0ull - (unsigned long long)v);
+    if (v && fld == 1) {
+      atomicAdd(&row[ST_RECV], (unsigned long long)v);
+      atomicAdd(&row[ST_SCHED], (unsigned long long)v);  // every infection schedules one Broadcast
+    }
+    if (v && fld == 2) atomicAdd(&row[ST_CRASH], (unsigned long long)v);
   }
-  if (tid == 0 && sm.err) atomicOr(w.err, kErrArrivals);
-  GS_STAMP(8);
-  if (stamp && tid == 0 && small) {
-    unsigned long long* d = w.dbg + (M >= 2048 ? kStampPhases : 0);
-    atomicAdd(&d[0], 1ull);
-    for (uint32_t i = 1; i < kStampPhases; ++i) atomicAdd(&d[i], ts[i] - ts[i - 1]);
-  }
-#undef GS_STAMP
 }
 
 __global__ void k_schedule_one_win(const WinState w, uint32_t node, uint32_t t) {
@@ -851,7 +965,24 @@ hipError_t win_scan_fine(const WinState& w, void* tmp, size_t& tmp_bytes, hipStr
 }
 
 hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s) {
-  hipLaunchKernelGGL(k_resolve, dim3(w.nfine), dim3(kResolveBlock), 0, s, w, t0, L);
+  // persistent: two workgroups per CU (the LDS holds two), each owning <= 256 buckets
+  static uint32_t cus = 0;
+  if (!cus) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      cus = (uint32_t)v;
+    else
+      cus = 256;
+  }
+  uint32_t G = std::min<uint32_t>(w.nfine, 2 * cus);
+  G = std::max<uint32_t>(G, (w.nfine + kResolveMaxBuckets - 1) / kResolveMaxBuckets);
+  static const int probe = getenv("GS_PROBE") ? atoi(getenv("GS_PROBE")) : 0;
+  if (probe == 1) hipLaunchKernelGGL(k_resolve<1>, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
+  if (probe == 2) hipLaunchKernelGGL(k_resolve<2>, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
+  if (probe == 3) hipLaunchKernelGGL(k_resolve<3>, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
+  if (probe == 4) hipLaunchKernelGGL(k_resolve<4>, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
+  hipLaunchKernelGGL(k_resolve<0>, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
   return hipGetLastError();
 }
 

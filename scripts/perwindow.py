@@ -1,5 +1,6 @@
 """Per-window kernel durations (us) of the last broadcast in a rocprofv3 .db:
-expand, part2, resolve in dispatch order.  Usage: python scripts/perwindow.py <db> [nwin]"""
+expand, part2, resolve (and a GS_PROBE diagnostic resolve, if any) in dispatch
+order.  Usage: python scripts/perwindow.py <db> [nwin]"""
 import re
 import sqlite3
 import sys
@@ -9,11 +10,15 @@ rows = db.execute("select name, start, end from kernels order by start").fetchal
 
 
 def s(n):
-    m = re.search(r"gs::(?:\(anonymous namespace\)::)?(\w+)", n)
-    return m.group(1) if m else ""
+    m = re.search(r"gs::(?:\(anonymous namespace\)::)?(\w+)(<\d+>)?", n)
+    if not m:
+        return ""
+    if m.group(1) == "k_resolve" and m.group(2) and m.group(2) != "<0>":
+        return "probe"
+    return m.group(1)
 
 
-seq = [(s(n), (e - b) / 1e3) for n, b, e in rows if s(n) in ("k_expand", "k_part2", "k_resolve")]
+seq = [(s(n), (e - b) / 1e3) for n, b, e in rows if s(n) in ("k_expand", "k_part2", "k_resolve", "probe")]
 wins, cur = [], {}
 for name, us in seq:
     cur[name] = cur.get(name, 0) + us
@@ -23,7 +28,9 @@ for name, us in seq:
 nwin = int(sys.argv[2]) if len(sys.argv) > 2 else 40
 tot = {}
 for i, w in enumerate(wins[-nwin:]):
-    print(f"{i:3d} expand {w.get('k_expand', 0):8.1f}  part2 {w.get('k_part2', 0):8.1f}  resolve {w.get('k_resolve', 0):8.1f}")
+    extra = f"  probe {w['probe']:8.1f}" if "probe" in w else ""
+    print(f"{i:3d} expand {w.get('k_expand', 0):8.1f}  part2 {w.get('k_part2', 0):8.1f}  "
+          f"resolve {w.get('k_resolve', 0):8.1f}{extra}")
     for k, v in w.items():
         tot[k] = tot.get(k, 0) + v
 print("sum(ms)", {k: round(v / 1e3, 2) for k, v in tot.items()})
