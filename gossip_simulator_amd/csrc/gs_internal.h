@@ -82,7 +82,7 @@ constexpr uint32_t kMaxWindow = 16;             // tick offset in 4 bits
 constexpr uint32_t kWinMaxRing = 256;
 constexpr uint32_t kWinMaxStride = 32;          // friends-row length the window engine takes
 constexpr uint32_t kEmptyMsg = 0xFFFFFFFFu;
-constexpr uint32_t kPartTile = 4096;            // messages per partition tile
+constexpr uint32_t kPartTile = 8192;            // messages per partition tile (runs of ~32 per fine bucket)
 constexpr uint32_t kWinSlotsPerBucket = 6144;   // window cut: friend slots per fine bucket
                                                 // (k_resolve keeps <= 7168 receipts in LDS)
 

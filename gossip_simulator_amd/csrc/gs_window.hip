@@ -304,6 +304,9 @@ __global__ void k_plan(const WinState w, bool exact) {
 }
 
 // LDS counting sort of one tile by an 8-bit digit, then coalesced runs out.
+constexpr uint32_t kPartBlock = 512;  // threads per partition tile (16 messages each)
+static_assert(kPartTile % kPartBlock == 0, "whole messages per thread");
+
 struct TileSort {
   uint32_t buf[kPartTile];
   uint8_t bin[kPartTile];
@@ -315,12 +318,11 @@ struct TileSort {
 // part2: coarse tiles -> fine regions; message = u_in_fine | k << 14.
 // SCATTER=false counts per fine bucket (exact fallback).
 template <bool SCATTER>
-__global__ __launch_bounds__(256) void k_part2(const WinState w) {
+__global__ __launch_bounds__(kPartBlock) void k_part2(const WinState w) {
   __shared__ TileSort ts;
   __shared__ uint32_t s_tp[257];
   const uint32_t tid = threadIdx.x;
-  s_tp[tid] = w.tprefix[tid];
-  if (tid == 0) s_tp[256] = w.tprefix[256];
+  if (tid <= 256) s_tp[tid] = w.tprefix[tid];
   __syncthreads();
   const uint32_t ntiles = s_tp[256];
   for (uint32_t g = blockIdx.x; g < ntiles; g += gridDim.x) {
@@ -334,17 +336,19 @@ __global__ __launch_bounds__(256) void k_part2(const WinState w) {
     const unsigned long long fill = w.cfill[c] < w.ccap[c + 1] - cb ? w.cfill[c] : w.ccap[c + 1] - cb;
     const unsigned long long ce = cb + fill;
     const unsigned long long base = cb + (unsigned long long)(g - s_tp[c]) * kPartTile;
-    ts.cnt[tid] = 0;
+    if (tid < 256) ts.cnt[tid] = 0;
     __syncthreads();
-    uint32_t m[kPartTile / 256], rank[kPartTile / 256];
-    uint8_t bn[kPartTile / 256];
+    constexpr uint32_t kPer = kPartTile / kPartBlock;
+    uint32_t m[kPer], rank[kPer];
+    uint8_t bn[kPer];
 #pragma unroll
-    for (uint32_t r = 0; r < kPartTile / 256; ++r) {
-      const unsigned long long x = base + r * 256 + tid;
+    for (uint32_t r = 0; r < kPer; ++r) {
+      const unsigned long long x = base + r * kPartBlock + tid;
+      // branch-free load (index clamped into the tile's region: base < ce)
+      const uint32_t m1 = w.cmsg[x < ce ? x : ce - 1];
       m[r] = kEmptyMsg;
       bn[r] = 0;
       if (x < ce) {
-        const uint32_t m1 = w.cmsg[x];
         bn[r] = (uint8_t)((m1 >> kFineLog) & 255);
         m[r] = (m1 & (kFineNodes - 1)) | ((m1 >> kCoarseShift) << kFineLog);
         rank[r] = atomicAdd(&ts.cnt[bn[r]], 1u);
@@ -352,12 +356,12 @@ __global__ __launch_bounds__(256) void k_part2(const WinState w) {
     }
     __syncthreads();
     if (!SCATTER) {
-      if (ts.cnt[tid]) atomicAdd(&w.fhist[c * 256 + tid], (unsigned long long)ts.cnt[tid]);
+      if (tid < 256 && ts.cnt[tid]) atomicAdd(&w.fhist[c * 256 + tid], (unsigned long long)ts.cnt[tid]);
       __syncthreads();
       continue;
     }
     block_scan256(ts.cnt, ts.off);
-    if (ts.cnt[tid]) {
+    if (tid < 256 && ts.cnt[tid]) {
       const uint32_t f = c * 256 + tid;
       const unsigned long long at = atomicAdd(&w.ffill[f], (unsigned long long)ts.cnt[tid]);
       if (at + ts.cnt[tid] > w.fstart[f + 1] - w.fstart[f]) atomicOr(w.err, kErrFine);
@@ -365,7 +369,7 @@ __global__ __launch_bounds__(256) void k_part2(const WinState w) {
     }
     __syncthreads();
 #pragma unroll
-    for (uint32_t r = 0; r < kPartTile / 256; ++r)
+    for (uint32_t r = 0; r < kPer; ++r)
       if (m[r] != kEmptyMsg) {
         const uint32_t p = ts.off[bn[r]] + rank[r];
         ts.buf[p] = m[r];
@@ -373,7 +377,7 @@ __global__ __launch_bounds__(256) void k_part2(const WinState w) {
       }
     __syncthreads();
     const uint32_t total = ts.off[256];
-    for (uint32_t p = tid; p < total; p += 256) {
+    for (uint32_t p = tid; p < total; p += kPartBlock) {
       const uint32_t b = ts.bin[p];
       const unsigned long long pos = ts.gbase[b] + (p - ts.off[b]);
       if (pos < w.fstart[c * 256 + b + 1]) w.fmsg[pos] = ts.buf[p];
@@ -919,8 +923,11 @@ hipError_t win_groupmap(const WinState& w, uint32_t L, hipStream_t s) {
 }
 
 // mode 0: count coarse buckets only; 1: write + per-tick stats; 2: write only
-hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, int mode,
+hipError_t win_expand(const WinState& w0, uint32_t t0, uint32_t L, uint64_t Tn, int mode,
                       hipStream_t s) {
+  static const int xprobe = getenv("GS_XPROBE") ? atoi(getenv("GS_XPROBE")) : 0;
+  WinState w = w0;
+  if (xprobe == 1) w.kc = 0;  // timing diagnostic only: no ordinal-0 crash roll in the expand
   const uint32_t per_round = w.stride <= 8 ? kExpandBlock * kExpandNpt : kExpandBlock;
   const uint64_t rounds = (Tn + per_round - 1) / per_round;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>(rounds, 8192);
@@ -954,8 +961,8 @@ hipError_t win_plan(const WinState& w, bool exact, hipStream_t s) {
 hipError_t win_part2(const WinState& w, uint64_t T, bool scatter, hipStream_t s) {
   const uint64_t tiles = (T + kPartTile - 1) / kPartTile + 256;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>(tiles, 8192);
-  if (scatter) hipLaunchKernelGGL(k_part2<true>, dim3(blocks), dim3(256), 0, s, w);
-  else hipLaunchKernelGGL(k_part2<false>, dim3(blocks), dim3(256), 0, s, w);
+  if (scatter) hipLaunchKernelGGL(k_part2<true>, dim3(blocks), dim3(kPartBlock), 0, s, w);
+  else hipLaunchKernelGGL(k_part2<false>, dim3(blocks), dim3(kPartBlock), 0, s, w);
   return hipGetLastError();
 }
 
