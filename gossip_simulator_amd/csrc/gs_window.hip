@@ -37,7 +37,6 @@ namespace {
 
 constexpr uint32_t kExpandBlock = 256;
 constexpr uint32_t kExpandNpt = 4;        // firing nodes per thread per round (rows <= 8)
-constexpr uint32_t kExpandSlots = kExpandBlock * kExpandNpt * 8;  // LDS message slots per round
 constexpr uint32_t kResolveBlock = 512;
 constexpr uint32_t kResolveMsgCap = 7168;   // receipts of one bucket held in LDS
 // Messages: coarse = u_in_coarse | k << 22 | roll0 << 26; fine = loc | k << 14 |
@@ -104,9 +103,10 @@ __global__ void k_stats_reduce(const WinState w, uint32_t t0, uint32_t L) {
   if (sum) w.stats[(size_t)((t0 + k) % kStatSlots) * kStatFields + fld] += sum;
 }
 
+template <uint32_t SLOTS>  // LDS message slots per round: block * nodes per thread * row length
 struct ExpandLds {
-  uint32_t sorted[kExpandSlots];
-  uint8_t sbin[kExpandSlots];
+  uint32_t sorted[SLOTS];
+  uint8_t sbin[SLOTS];
   uint32_t cnt[256];
   uint32_t off[257];
   unsigned long long gbase[256];
@@ -162,7 +162,7 @@ __device__ __forceinline__ void load_row(const WinState& w, uint32_t v, uint32_t
 template <bool WRITE, uint32_t MAXS, uint32_t NPT>
 __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint32_t t0, uint32_t L,
                                                          unsigned long long Tn, int add_stats) {
-  __shared__ ExpandLds sm;
+  __shared__ ExpandLds<kExpandBlock * NPT * MAXS> sm;
   const uint32_t tid = threadIdx.x;
   const uint32_t units = L * w.nfine;
   constexpr uint32_t per_round = kExpandBlock * NPT;
