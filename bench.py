@@ -132,8 +132,10 @@ def main():
         achieved = BYTES_PER_SEND * tot_r["sent"] / (kern_ms * 1e-3) / 1e9
         per = {"k_expand": tm["expand_ms"], "k_plan+k_part2": tm["part_ms"],
                "k_resolve": tm["resolve_ms"]}
+        traffic, tnote = pmc_traffic()
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "traffic_note": tnote,
                 "kernel": "window pipeline k_expand -> k_plan/k_part2 -> k_resolve "
                           "(one launch of each per window)",
                 "avg_launch_us": round(kern_ms * 1e3 / max(launches, 1), 2),
@@ -177,6 +179,19 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def pmc_traffic():
+    """HBM bytes per window launch (k_expand + k_part2 + k_resolve) from the
+    committed PMC pass (scripts/pmc.sh + scripts/pmc_traffic.py, FETCH_SIZE
+    doubled per MI355X_MICROARCH.md); counters cannot be read from inside the
+    timed process, so this is the profile of the same workload, not this run."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None, "no PMC profile committed"
+    d = json.load(open(path))
+    return int(d["bytes_per_launch"]), (f"{os.path.relpath(path, ROOT)}: FETCH_SIZE*2 + WRITE_SIZE "
+                                        f"over {d['launches']} window launches of one broadcast")
 
 
 def cpu_baseline(a, gs):
