@@ -574,7 +574,7 @@ int gs_frontier_import(gs_ctx* c, uint64_t tick, const void* src) {
 // ticks (gs_window.hip).  One host sync per window reads its task count.
 static int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing) {
   WinState& w = c->ws;
-  const uint32_t Lmax = std::min<uint32_t>(std::max<int32_t>(c->p.delay_low, 1), kMaxWindow);
+  const uint32_t Lmax = std::min<uint32_t>(std::max<int32_t>(c->p.delay_low, 1), kBitTicks);
   uint32_t done = 0, widx = 0;
   std::vector<std::pair<uint32_t, uint32_t>> evs;
   // Receipts per fine bucket are ~density * 16384 whatever N is; a window whose

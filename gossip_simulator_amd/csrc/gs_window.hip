@@ -28,7 +28,6 @@
 // partition is redone with exact counts (expand and part2 are idempotent).
 // Fire lists: fcount[R][nfine] + flist[R][nfine][16384] (u16 local ids).
 #include <hipcub/hipcub.hpp>
-#include <cstdlib>
 
 #include "gs_internal.h"
 
@@ -38,7 +37,6 @@ namespace {
 constexpr uint32_t kExpandBlock = 256;
 constexpr uint32_t kExpandNpt = 4;        // firing nodes per thread per round (rows <= 8)
 constexpr uint32_t kResolveBlock = 512;
-constexpr uint32_t kResolveMsgCap = 7168;   // receipts of one bucket held in LDS
 // Messages: coarse = u_in_coarse | k << 22 | roll0 << 26; fine = loc | k << 14 |
 // roll0 << 18, where roll0 is the receiver's crash roll for ordinal 0.
 constexpr uint32_t kRoll0Coarse = kCoarseShift + 4;
@@ -388,26 +386,43 @@ __global__ __launch_bounds__(kPartBlock) void k_part2(const WinState w) {
 
 constexpr uint32_t kResolveMaxBuckets = 256;  // buckets one persistent workgroup may own
 
+// Bit-parallel resolve (k_resolve): per tick k of the window, b1 = nodes with
+// >= 1 receipt, b2 = nodes with >= 2, rl = nodes whose ordinal-0 crash roll
+// fired; receipts beyond the first of a (node, tick) are listed per 32-node
+// word (dlist, chained from dhead).  The large path (resolve_tick) reuses the
+// same LDS for per-node counters and bit words.
+constexpr uint32_t kBitWords = kFineNodes / 32;
+constexpr uint32_t kDupCap = 3072;     // repeat receipts per bucket (more: large path)
 struct ResolveLds {
-  uint32_t cnt[kFineNodes / 2];     // u16 per node: receipts in the window, then list heads;
-                                    // all zero between buckets (cleared where touched)
-  uint32_t recv[kFineNodes / 32];   // bits at the window start
-  uint32_t crash[kFineNodes / 32];
-  uint32_t nrecv[kFineNodes / 32];  // bits set during the window
-  uint32_t ncrash[kFineNodes / 32];
-  uint32_t buf[kResolveMsgCap];     // the bucket's messages (arrival order) + list links
+  union {
+    struct {                            // b1 .. dlist, then the infection list
+      uint32_t b1[kBitTicks][kBitWords];
+      uint32_t b2[kBitTicks][kBitWords];
+      uint32_t rl[kBitTicks][kBitWords];
+      uint32_t dlist[kDupCap];          // loc | k << 14 | next << 18 (next = index + 1, 0 = end)
+      uint32_t dhead[kBitWords];
+    };
+    struct {                            // large path
+      uint32_t cnt[kFineNodes / 2];     // u16 per node: arrivals at the current tick
+      uint32_t recv[kBitWords];
+      uint32_t crash[kBitWords];
+      uint32_t nrecv[kBitWords];
+      uint32_t ncrash[kBitWords];
+    };
+  };
   uint32_t fc[kWinMaxRing];         // fire-list lengths of this bucket, per ring slot
   uint32_t st[kMaxWindow][4];       // dead (not counted), recv, crash per tick: whole launch
-  uint16_t own[kResolveMsgCap / 2]; // nodes with several receipts (<= half the receipts)
   uint32_t blist[kResolveMaxBuckets];  // this workgroup's non-empty buckets
-  uint32_t nown;
+  uint32_t ndup;
   uint32_t ninf;
   uint32_t err;
   uint32_t nb;
+  uint32_t cls;
   unsigned long long stamp[2][kStampPhases];  // GS_STAMPS: [M >= 1024][phase] cycles (thread 0)
   unsigned long long tlast;
-  uint32_t cls;
-};  // ~79 KB: two workgroups per CU
+};  // ~77 KB: two workgroups per CU
+static_assert(kBitTicks <= kMaxWindow, "window ticks fit the message format");
+static_assert((3 * kBitTicks * kBitWords + kDupCap) >= kFineNodes, "the infection list fits the bitmaps");
 
 // GS_STAMPS diagnostics: thread 0 adds the cycles since the last stamp to phase i.
 __device__ __forceinline__ void stamp(const WinState& w, ResolveLds& sm, uint32_t i) {
@@ -418,18 +433,10 @@ __device__ __forceinline__ void stamp(const WinState& w, ResolveLds& sm, uint32_
   }
 }
 
-// buf entry: loc | k << 14 | roll0 << 18 | link << 19 (link = index + 1 of the
-// next receipt of the same node, 0 = end); list heads are kHeadFlag | (index+1)
-constexpr uint32_t kMsgBits = kRoll0Fine + 1;
-constexpr uint32_t kLinkShift = kMsgBits;
-constexpr uint32_t kHeadFlag = 0x8000u;
-constexpr uint32_t kInfMark = 0x4000u;    // replayed node infected: kInfMark | tick
+// receipt (fine message): loc | k << 14 | roll0 << 18
 
 __device__ __forceinline__ uint32_t msg_loc(uint32_t m) { return m & (kFineNodes - 1); }
 __device__ __forceinline__ uint32_t msg_tick(uint32_t m) { return (m >> kFineLog) & (kMaxWindow - 1); }
-__device__ __forceinline__ uint32_t half_of(uint32_t word, uint32_t loc) {
-  return (word >> ((loc & 1) * 16)) & 0xFFFFu;
-}
 
 // The receive case of Node.Start (simulator.go:107-123) for node `loc` of the
 // bucket with kk arrivals at tick t: ordinals 0..kk-1, keyed crash rolls.
@@ -498,62 +505,6 @@ __device__ __forceinline__ void resolve_tick(const WinState& w, ResolveLds& sm, 
   __syncthreads();
 }
 
-// A node with several receipts in the window: walk its list and replay the
-// receive case (simulator.go:107-123) tick by tick, ordinals in order (rule
-// A6).  Ordinal 0's crash roll came with the message (all receipts of one
-// (node, tick) carry the same one); later ordinals draw U_100(u, t, i).
-// Returns the infection tick + 1 (0 = none).
-__device__ __forceinline__ uint32_t replay_multi(const WinState& w, ResolveLds& sm, uint32_t f,
-                                                 uint32_t loc, uint32_t t0, uint32_t c3crash) {
-  const uint32_t bit = 1u << (loc & 31), wi = loc >> 5;
-  // per-tick receipt counts (8 bits each) and ordinal-0 rolls
-  unsigned long long h0 = 0, h1 = 0;
-  uint32_t rollmask = 0, tickmask = 0;
-  for (uint32_t q = half_of(sm.cnt[loc >> 1], loc) & ~kHeadFlag; q != 0;) {
-    const uint32_t m = sm.buf[q - 1], k = msg_tick(m);
-    if (k < 8) h0 += 1ull << (8 * k); else h1 += 1ull << (8 * (k - 8));
-    tickmask |= 1u << k;
-    rollmask |= ((m >> kRoll0Fine) & 1u) << k;
-    q = m >> kLinkShift;
-  }
-  const bool crashed0 = (sm.crash[wi] & bit) != 0;
-  bool crashed = crashed0, received = (sm.recv[wi] & bit) != 0;
-  uint32_t inf = 0;
-  const uint32_t u = (f << kFineLog) + loc;
-  while (tickmask) {
-    const uint32_t k = __builtin_ctz(tickmask);
-    tickmask &= tickmask - 1;
-    const uint32_t kk = (uint32_t)(((k < 8 ? h0 >> (8 * k) : h1 >> (8 * (k - 8)))) & 255u);
-    if (crashed) {                                                // :108
-      atomicAdd(&sm.st[k][0], kk);
-      continue;
-    }
-    const uint32_t t = t0 + k;
-    u32x4 r{0, 0, 0, 0};
-    for (uint32_t i = 0; i < kk; ++i) {
-      bool roll = (rollmask >> k) & 1;                            // :112
-      if (i > 0 && w.kc > 0) {
-        if (i == 1 || (i & 3) == 0) r = philox(u, t, i >> 2, c3crash, w.key.k0, w.key.k1);
-        roll = (int32_t)uniform(lane_of(r, i & 3), 100u) < w.kc;
-      }
-      if (roll) {                                                 // :113-115
-        crashed = true;
-        atomicAdd(&sm.st[k][2], 1u);
-        if (kk - i - 1) atomicAdd(&sm.st[k][0], kk - i - 1);      // the rest of the tick
-        break;
-      }
-      if (!received) {                                            // :117-121
-        received = true;
-        inf = k + 1;
-        atomicAdd(&sm.st[k][1], 1u);
-      }
-    }
-  }
-  if (crashed && !crashed0) atomicOr(&sm.ncrash[wi], bit);
-  if (inf) atomicOr(&sm.nrecv[wi], bit);
-  return inf;
-}
-
 __device__ __forceinline__ uint32_t lane_id() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
@@ -570,246 +521,68 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* n, bool take) {
   return __builtin_amdgcn_readfirstlane(base) + mbcnt(bal);
 }
 
-// As wave_append for c < 16 items per lane: the lane's first slot.
-__device__ __forceinline__ uint32_t wave_reserve(uint32_t* n, uint32_t c) {
-  uint32_t pre = 0, tot = 0;
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
-  for (uint32_t b = 0; b < 4; ++b) {
-    const unsigned long long bal = __ballot((c >> b) & 1u);
-    pre += mbcnt(bal) << b;
-    tot += (uint32_t)__popcll(bal) << b;
-  }
-  uint32_t base = 0;
-  if (tot && lane_id() == 0) base = atomicAdd(n, tot);
-  return __builtin_amdgcn_readfirstlane(base) + pre;
+  for (uint32_t o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
 }
 
-// Per-tick counters: one LDS atomic per (wave, tick, field) instead of one
-// per lane; a wave's receipts span one or two ticks (all lanes active).
-__device__ __forceinline__ void wave_stats(ResolveLds& sm, uint32_t k, bool dead, bool crashm,
-                                           bool infect) {
-  unsigned long long m = __ballot(dead || crashm || infect);
-  const uint32_t lane = lane_id();
-  while (m) {
-    const uint32_t kl = __builtin_amdgcn_readlane(k, (uint32_t)__builtin_ctzll(m));
-    const bool mine = k == kl;
-    const unsigned long long sd = __ballot(mine && dead), si = __ballot(mine && infect),
-                             sc = __ballot(mine && crashm);
-    const unsigned long long s = lane == 0 ? sd : lane == 1 ? si : sc;
-    if (lane < 3 && s) atomicAdd(&sm.st[kl][lane], (uint32_t)__popcll(s));
-    m &= ~(sd | si | sc);
+// Receipt ordinals of one node with c >= 2 receipts at tick t (rule A6,
+// simulator.go:107-123): counted -> crash roll (ordinal 0 rode with the
+// message, later ordinals draw U_100(u, t, i)) -> first receipt infects.
+__device__ __forceinline__ void replay_node(const WinState& w, uint32_t u, uint32_t t, uint32_t c,
+                                            uint32_t bit, bool roll0, uint32_t c3crash, uint32_t& cw,
+                                            uint32_t& rw, uint32_t& infS, uint32_t& nd, uint32_t& nc,
+                                            uint32_t& ni) {
+  if (cw & bit) {  // crashed before this tick: nothing is counted (:108)
+    nd += c;
+    return;
   }
-}
-
-constexpr uint32_t kPerThread = kResolveMsgCap / kResolveBlock;
-static_assert(kResolveMsgCap % kResolveBlock == 0, "whole messages per thread");
-static_assert(kPerThread < 16, "per-lane counts fit wave_reserve");
-
-// The receive case (simulator.go:107-123) for one bucket and a whole window.
-// Most receiving nodes get exactly one receipt: ordinal 0 of its tick, whose
-// crash roll rode with the message, so it resolves in its own lane.  Nodes
-// with several receipts are linked into per-node lists and replayed one node
-// per lane.  Returns false (nothing changed but sm.cnt) if a node has more
-// than 255 receipts: the caller then takes the large path.
-template <int PROBE>
-__device__ bool resolve_window(const WinState& w, ResolveLds& sm, uint32_t f, uint32_t t0,
-                               uint32_t c3crash, const uint32_t (&mr)[kPerThread], uint32_t nj) {
-  const uint32_t tid = threadIdx.x;
-  const uint32_t node0 = f << kFineLog;
-  // 1: receipts per node; first arrival of every node
-  uint32_t firstm = 0;
-#pragma unroll
-  for (uint32_t j = 0; j < kPerThread; ++j) {
-    if (j >= nj) continue;  // nj = ceil(M / 512): slots past it hold no message
-    if (mr[j] == ~0u) continue;
-    const uint32_t loc = msg_loc(mr[j]), sh = (loc & 1) * 16;
-    const uint32_t a = (atomicAdd(&sm.cnt[loc >> 1], 1u << sh) >> sh) & 0xFFFFu;
-    firstm |= (a == 0 ? 1u : 0u) << j;
-  }
-#pragma unroll
-  for (uint32_t j = 0; j < kPerThread; ++j) {
-    if (j >= nj) continue;
-    if (mr[j] != ~0u) sm.buf[tid + j * kResolveBlock] = mr[j];
-  }
-  __syncthreads();
-  stamp(w, sm, 2);
-  // 2: classify: singletons resolve in their lane, multi nodes are listed
-  uint32_t singlem = 0, multim = 0, crashedm = 0, recvm = 0;
-  bool big = false;
-  constexpr uint32_t kHalf = (kPerThread + 1) / 2;  // reads in flight per step (VGPR budget)
-#pragma unroll
-  for (uint32_t j0 = 0; j0 < kPerThread; j0 += kHalf) {
-    uint32_t cw[kHalf], crw[kHalf], rcw[kHalf];
-#pragma unroll
-    for (uint32_t jj = 0; jj < kHalf; ++jj) {
-      const uint32_t j = j0 + jj;
-      if (j >= kPerThread || j >= nj) continue;
-      // unconditional (an empty slot reads node 16383's words): no exec-masked load chain
-      const uint32_t loc = msg_loc(mr[j]);
-      cw[jj] = sm.cnt[loc >> 1];
-      crw[jj] = sm.crash[loc >> 5];
-      rcw[jj] = sm.recv[loc >> 5];
+  u32x4 r{0, 0, 0, 0};
+  for (uint32_t i = 0; i < c; ++i) {                              // :111 counted
+    bool roll = roll0;                                            // :112
+    if (i > 0) {
+      roll = false;
+      if (w.kc > 0) {
+        if (i == 1 || (i & 3) == 0) r = philox(u, t, i >> 2, c3crash, w.key.k0, w.key.k1);
+        roll = (int32_t)uniform(lane_of(r, i & 3), 100u) < w.kc;
+      }
     }
-#pragma unroll
-    for (uint32_t jj = 0; jj < kHalf; ++jj) {
-      const uint32_t j = j0 + jj;
-      if (j >= kPerThread || j >= nj) continue;
-      const uint32_t loc = msg_loc(mr[j]), bit = 1u << (loc & 31);
-      const uint32_t c = mr[j] == ~0u ? 0u : half_of(cw[jj], loc);  // receipts of the node
-      big |= c > 255;  // a replayed node keeps 8-bit per-tick counts
-      singlem |= (c == 1 ? 1u : 0u) << j;
-      multim |= (c > 1 ? 1u : 0u) << j;
-      crashedm |= ((crw[jj] & bit) ? 1u : 0u) << j;
-      recvm |= ((rcw[jj] & bit) ? 1u : 0u) << j;
+    if (roll) {                                                   // :113-115
+      cw |= bit;
+      ++nc;
+      nd += c - 1 - i;                                            // the rest of the tick
+      return;
+    }
+    if (!(rw & bit)) {                                            // :117-121
+      rw |= bit;
+      infS |= bit;
+      ++ni;
     }
   }
-  if (big) sm.err = 2;
-  __syncthreads();
-  stamp(w, sm, 3);
-  if (sm.err == 2) return false;
-  uint32_t infmask = 0;            // slot j infected its node (singletons)
-#pragma unroll
-  for (uint32_t j = 0; j < kPerThread; ++j) {
-    if (j >= nj) continue;
-    const uint32_t m = mr[j], loc = msg_loc(m), k = msg_tick(m), bit = 1u << (loc & 31);
-    const bool single = (singlem >> j) & 1, crashed0 = (crashedm >> j) & 1;
-    const bool roll = (m >> kRoll0Fine) & 1;
-    const bool dead = single && crashed0;                                     // :108
-    const bool crashm = single && !crashed0 && roll;                          // :113-115
-    const bool infect = single && !crashed0 && !roll && !((recvm >> j) & 1);  // :117-121
-    wave_stats(sm, k, dead, crashm, infect);
-    if (crashm) atomicOr(&sm.ncrash[loc >> 5], bit);
-    if (infect) atomicOr(&sm.nrecv[loc >> 5], bit);
-    infmask |= (infect ? 1u : 0u) << j;
-  }
-  // owners (first receipt of a multi node) are listed; receipts are linked:
-  // head = kHeadFlag | (index + 1)
-  const uint32_t ownm = multim & firstm;
-  {
-    uint32_t at = wave_reserve(&sm.nown, (uint32_t)__popc(ownm));
-#pragma unroll
-    for (uint32_t j = 0; j < kPerThread; ++j) {
-      if (j >= nj) continue;
-      if ((ownm >> j) & 1) sm.own[at++] = (uint16_t)msg_loc(mr[j]);
-    }
-  }
-#pragma unroll
-  for (uint32_t j = 0; j < kPerThread; ++j) {
-    if (j >= nj) continue;
-    if (!((multim >> j) & 1)) continue;
-    const uint32_t loc = msg_loc(mr[j]), sh = (loc & 1) * 16;
-    const uint32_t p = tid + j * kResolveBlock;
-    uint32_t o = sm.cnt[loc >> 1];
-    for (;;) {
-      const uint32_t nw = (o & ~(0xFFFFu << sh)) | ((kHeadFlag | (p + 1)) << sh);
-      const uint32_t got = atomicCAS(&sm.cnt[loc >> 1], o, nw);
-      if (got == o) break;
-      o = got;
-    }
-    const uint32_t old = (o >> sh) & 0xFFFFu;
-    const uint32_t link = (old & kHeadFlag) ? (old & ~kHeadFlag) : 0u;
-    sm.buf[p] = mr[j] | (link << kLinkShift);
-  }
-  __syncthreads();
-  stamp(w, sm, 4);
-  // 3: one multi node per lane; an infection is left in the node's head half
-  // (kInfMark | tick) for phase 4
-  const uint32_t nown = sm.nown;
-  for (uint32_t q = tid; q < nown; q += kResolveBlock) {
-    const uint32_t loc = sm.own[q], sh = (loc & 1) * 16;
-    const uint32_t x = replay_multi(w, sm, f, loc, t0, c3crash);
-    if (x) {
-      atomicAnd(&sm.cnt[loc >> 1], ~(0xFFFFu << sh));
-      atomicOr(&sm.cnt[loc >> 1], (kInfMark | (x - 1)) << sh);
-    }
-  }
-  __syncthreads();
-  stamp(w, sm, 5);
-  // 4: infection list (the receipt buffer is free now)
-  uint32_t* inf = sm.buf;
-  {
-    uint32_t at = wave_reserve(&sm.ninf, (uint32_t)__popc(infmask));
-#pragma unroll
-    for (uint32_t j = 0; j < kPerThread; ++j) {
-      if (j >= nj) continue;
-      if ((infmask >> j) & 1) inf[at++] = msg_loc(mr[j]) | (msg_tick(mr[j]) << kFineLog);
-    }
-  }
-  for (uint32_t q0 = 0; q0 < nown; q0 += kResolveBlock) {
-    const uint32_t q = q0 + tid;
-    uint32_t loc = 0, h = 0;
-    if (q < nown) {
-      loc = sm.own[q];
-      h = half_of(sm.cnt[loc >> 1], loc);
-    }
-    const bool x = q < nown && (h & (kHeadFlag | kInfMark)) == kInfMark;
-    const uint32_t at = wave_append(&sm.ninf, x);
-    if (x) inf[at] = loc | ((h & (kMaxWindow - 1)) << kFineLog);
-  }
-  __syncthreads();
-  stamp(w, sm, 6);
-  if (PROBE == 3) return true;
-  // 5: Broadcast() of each infected node (:122, :141-142): fire at t + off
-  const uint32_t c3delay = ctr3(K_DELAY, w.key.trial);
-  const uint32_t ninf = sm.ninf;
-  for (uint32_t q = tid; q < ninf; q += kResolveBlock) {
-    const uint32_t x = inf[q], loc = msg_loc(x), t = t0 + msg_tick(x);
-    const uint32_t off = fire_offset(w.delay_low, w.delay_span,
-                                     philox(node0 + loc, t, 0, c3delay, w.key.k0, w.key.k1).x);
-    const uint32_t slot = (t + off) % w.R;
-    const uint32_t pos = atomicAdd(&sm.fc[slot], 1u);
-    if (!PROBE) w.flist[((size_t)slot * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
-  }
-  return true;
-}
-
-// Bucket f's messages (arrival order), bit words and fire-list lengths into
-// registers.
-__device__ __forceinline__ void fetch_bucket(const WinState& w, uint32_t f, unsigned long long mb,
-                                             uint32_t M, uint32_t (&mr)[kPerThread], uint32_t& r0,
-                                             uint32_t& c0, uint32_t& fcv) {
-  const uint32_t tid = threadIdx.x;
-  const uint32_t* gm = w.fmsg + mb;
-  const bool small = M <= kResolveMsgCap;
-  // branch-free: every lane loads (index clamped into the bucket, M >= 1), so
-  // the loads issue back to back instead of one exec-masked load at a time
-  const uint32_t nj = small ? (M + kResolveBlock - 1) / kResolveBlock : 0u;
-#pragma unroll
-  for (uint32_t i = 0; i < kPerThread; ++i) mr[i] = ~0u;
-#pragma unroll
-  for (uint32_t i = 0; i < kPerThread; ++i) {
-    if (i >= nj) continue;
-    const uint32_t p = tid + i * kResolveBlock;
-    const uint32_t x = gm[p < M ? p : M - 1];
-    mr[i] = p < M ? x & ((1u << kMsgBits) - 1) : ~0u;
-  }
-  const uint64_t wi = ((uint64_t)f << kFineLog >> 5) + tid;
-  const bool in = wi < w.W * 2;
-  r0 = in ? ((const uint32_t*)w.recv)[wi] : 0u;
-  c0 = in ? ((const uint32_t*)w.crash)[wi] : 0u;
-  fcv = tid < w.R ? w.fcount[(size_t)tid * w.nfine + f] : 0u;
 }
 
 // Persistent: workgroup g owns buckets g, g + G, g + 2G, ... (G = gridDim.x),
 // resolves its non-empty ones in turn, and adds its per-tick counters once at
-// the end.
-// PROBE > 0 (timing diagnostics, GS_PROBE): no global writes; 1 = skeleton
-// only, 2 = through classification, 3 = through the replay, 4 = all phases.
-template <int PROBE>
+// the end.  Per bucket:
+//   stage    thread w owns bit word w (32 nodes): its recv/crash words in
+//            registers, its b1/b2/rl words and dup-chain head zeroed
+//   receipts every message sets its (tick, node) bit in b1 (atomicOr); a
+//            repeat sets b2 and is chained under its word; a fired ordinal-0
+//            roll sets rl
+//   ticks    per tick, thread w resolves its 32 nodes at once with bit ops
+//            (single receipts), walking its chain only for b2 nodes; the
+//            infections of the tick are Broadcast() in the lane (:122, :141)
+// A bucket with more repeats than kDupCap takes the per-tick large path.
 __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
   __shared__ ResolveLds sm;
   const uint32_t tid = threadIdx.x, G = gridDim.x;
-  static_assert(kFineNodes / 32 == kResolveBlock, "one bit word per thread");
+  static_assert(kBitWords == kResolveBlock, "one bit word per thread");
   static_assert(kWinMaxRing <= kResolveBlock, "one ring slot per thread");
-  const uint32_t c3crash = ctr3(K_CRASH, w.key.trial);
-  {
-    uint4* c4 = reinterpret_cast<uint4*>(sm.cnt);
-    for (uint32_t i = tid; i < kFineNodes / 8; i += kResolveBlock) c4[i] = make_uint4(0, 0, 0, 0);
-  }
+  const uint32_t c3crash = ctr3(K_CRASH, w.key.trial), c3delay = ctr3(K_DELAY, w.key.trial);
   if (tid < kMaxWindow * 4) (&sm.st[0][0])[tid] = 0;
-  if (tid == 0) sm.nb = 0;
+  if (tid == 0) { sm.nb = 0; sm.cls = 0; }
   if (tid < 2 * kStampPhases) (&sm.stamp[0][0])[tid] = 0;
-  if (tid == 0) sm.cls = 0;
   __syncthreads();
   {
     const uint32_t f = blockIdx.x + tid * G;
@@ -820,65 +593,162 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
   __syncthreads();
   const uint32_t nb = sm.nb;
   stamp(w, sm, 0);
-  // bucket i+1's header is in flight while bucket i is resolved (prefetching
-  // its messages as well would need more VGPRs than two workgroups per CU leave)
   uint32_t fB = 0, MB = 0;
   unsigned long long mbB = 0;
   if (nb > 0) { fB = sm.blist[0]; mbB = w.fstart[fB]; MB = (uint32_t)w.ffill[fB]; }
-  uint32_t* rw = (uint32_t*)w.recv;
+  uint32_t* rwg = (uint32_t*)w.recv;
   uint32_t* cwg = (uint32_t*)w.crash;
   for (uint32_t i = 0; i < nb; ++i) {
     const uint32_t f = fB, M = MB;
     const unsigned long long mb = mbB;
-    uint32_t mr[kPerThread], recv0, crash0, fcv;
-    fetch_bucket(w, f, mb, M, mr, recv0, crash0, fcv);
+    const uint32_t node0 = f << kFineLog;
+    const uint64_t wi = ((uint64_t)node0 >> 5) + tid;
+    const bool in = wi < w.W * 2;
+    const uint32_t recv0 = in ? rwg[wi] : 0u, crash0 = in ? cwg[wi] : 0u;
+    const uint32_t fcv = tid < w.R ? w.fcount[(size_t)tid * w.nfine + f] : 0u;
     if (i + 1 < nb) { fB = sm.blist[i + 1]; mbB = w.fstart[fB]; MB = (uint32_t)w.ffill[fB]; }
-    sm.recv[tid] = recv0;
-    sm.crash[tid] = crash0;
-    sm.nrecv[tid] = 0;
-    sm.ncrash[tid] = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kBitTicks; ++k)
+      if (k < L) { sm.b1[k][tid] = 0; sm.b2[k][tid] = 0; sm.rl[k][tid] = 0; }
+    sm.dhead[tid] = 0;
     if (tid < w.R) sm.fc[tid] = fcv;
-    if (tid == 0) { sm.nown = 0; sm.ninf = 0; sm.err = 0; }
+    if (tid == 0) { sm.ndup = 0; sm.ninf = 0; sm.err = 0; sm.cls = M >= 1024 ? 1 : 0; }
     __syncthreads();
     stamp(w, sm, 1);
-    if (tid == 0) sm.cls = M >= 1024 ? 1 : 0;
-    bool small = M <= kResolveMsgCap;
-    if (PROBE == 1) small = true;
-    else if (small && !resolve_window<PROBE>(w, sm, f, t0, c3crash, mr,
-                                              (M + kResolveBlock - 1) / kResolveBlock)) {
-      small = false;  // a node with > 255 receipts in the window
+    // receipts: (tick, node) bits; repeats chained under their word
+    const uint32_t* gm = w.fmsg + mb;
+    constexpr uint32_t kU = 8;  // loads in flight per lane
+    for (uint32_t p0 = 0; p0 < M; p0 += kResolveBlock * kU) {
+      uint32_t m[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t p = p0 + u * kResolveBlock + tid;
+        const uint32_t x = gm[p < M ? p : M - 1];  // branch-free (M >= 1)
+        m[u] = p < M ? x : ~0u;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        bool dup = false;
+        uint32_t loc = 0, k = 0;
+        if (m[u] != ~0u) {
+          loc = msg_loc(m[u]);
+          k = msg_tick(m[u]);
+          const uint32_t bit = 1u << (loc & 31);
+          dup = (atomicOr(&sm.b1[k][loc >> 5], bit) & bit) != 0;
+          if ((m[u] >> kRoll0Fine) & 1) atomicOr(&sm.rl[k][loc >> 5], bit);
+          if (dup) atomicOr(&sm.b2[k][loc >> 5], bit);
+        }
+        const uint32_t at = wave_append(&sm.ndup, dup);
+        if (dup) {
+          if (at < kDupCap) {
+            const uint32_t prev = atomicExch(&sm.dhead[loc >> 5], at + 1);
+            sm.dlist[at] = loc | (k << kFineLog) | (prev << 18);
+          } else {
+            sm.err = 3;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    stamp(w, sm, 2);
+    uint32_t rw = recv0, cw = crash0;
+    if (sm.err != 3) {
+      // ticks: thread tid resolves nodes 32*tid .. 32*tid+31, tick by tick
+      const uint32_t ubase = node0 + tid * 32;
+      uint32_t infk[kBitTicks], ninf = 0;  // infections per tick of this word
+#pragma unroll
+      for (uint32_t k = 0; k < kBitTicks; ++k) {
+        infk[k] = 0;
+        if (k >= L) continue;
+        const uint32_t A = sm.b1[k][tid], D = sm.b2[k][tid], R = sm.rl[k][tid];
+        const uint32_t S = A & ~D;                       // one receipt at this tick
+        const uint32_t deadS = S & cw;                   // :108 crashed: not counted
+        const uint32_t crS = S & ~cw & R;                // :112-115
+        uint32_t infS = S & ~cw & ~R & ~rw;              // :117-121
+        cw |= crS;
+        rw |= infS;
+        uint32_t nd = __popc(deadS), nc = __popc(crS), ni = __popc(infS);
+        const uint32_t t = t0 + k;
+        for (uint32_t dm = D; dm; dm &= dm - 1) {        // nodes with repeats at this tick
+          const uint32_t b = __builtin_ctz(dm), loc = tid * 32 + b;
+          uint32_t c = 1;
+          for (uint32_t q = sm.dhead[tid]; q;) {
+            const uint32_t e = sm.dlist[q - 1];
+            c += (e & ((1u << 18) - 1)) == (loc | (k << kFineLog)) ? 1u : 0u;
+            q = e >> 18;
+          }
+          replay_node(w, ubase + b, t, c, 1u << b, (R >> b) & 1, c3crash, cw, rw, infS, nd, nc, ni);
+        }
+        // per-tick counters: one LDS atomic per wave and field
+        if (__ballot((nd | nc | ni) != 0)) {
+          const uint32_t sd = wave_sum(nd), sr = wave_sum(ni), sc = wave_sum(nc);
+          const uint32_t lane = lane_id();
+          const uint32_t v = lane == 0 ? sd : lane == 1 ? sr : sc;
+          if (lane < 3 && v) atomicAdd(&sm.st[k][lane], v);
+        }
+        infk[k] = infS;
+        ninf += ni;
+      }
+      stamp(w, sm, 3);
+      // infection list (loc | tick << 14) over the bitmaps, dead from here on
+      __syncthreads();
+      uint32_t* inf = &sm.b1[0][0];
+      {
+        uint32_t pre = 0, tot = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < 9; ++b) {  // ninf <= 32 * kBitTicks < 512
+          const unsigned long long bal = __ballot((ninf >> b) & 1u);
+          pre += mbcnt(bal) << b;
+          tot += (uint32_t)__popcll(bal) << b;
+        }
+        uint32_t base = 0;
+        if (tot && lane_id() == 0) base = atomicAdd(&sm.ninf, tot);
+        uint32_t at = __builtin_amdgcn_readfirstlane(base) + pre;
+#pragma unroll
+        for (uint32_t k = 0; k < kBitTicks; ++k)
+          for (uint32_t x = k < L ? infk[k] : 0u; x; x &= x - 1)
+            inf[at++] = (tid * 32 + __builtin_ctz(x)) | (k << kFineLog);
+      }
+      __syncthreads();
+      stamp(w, sm, 4);
+      // Broadcast() of each infected node (:122, :141-142): fire at t + off
+      const uint32_t ni_all = sm.ninf;
+      for (uint32_t q = tid; q < ni_all; q += kResolveBlock) {
+        const uint32_t x = inf[q], loc = msg_loc(x), t = t0 + msg_tick(x);
+        const uint32_t off = fire_offset(w.delay_low, w.delay_span,
+                                         philox(node0 + loc, t, 0, c3delay, w.key.k0, w.key.k1).x);
+        const uint32_t slot = (t + off) % w.R;
+        const uint32_t pos = atomicAdd(&sm.fc[slot], 1u);
+        w.flist[((size_t)slot * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
+      }
+    } else {
+      // large path: per-node counters, the messages streamed once per tick
       __syncthreads();
       uint4* c4 = reinterpret_cast<uint4*>(sm.cnt);
       for (uint32_t q = tid; q < kFineNodes / 8; q += kResolveBlock) c4[q] = make_uint4(0, 0, 0, 0);
-      if (tid == 0) sm.err = 0;
+      sm.recv[tid] = recv0;
+      sm.crash[tid] = crash0;
+      sm.nrecv[tid] = 0;
+      sm.ncrash[tid] = 0;
       __syncthreads();
-#pragma unroll
-      for (uint32_t j = 0; j < kPerThread; ++j) mr[j] = ~0u;  // sm.cnt is clean after the large path
+      for (uint32_t k = 0; k < L; ++k) resolve_tick(w, sm, f, gm, 0, M, k, t0 + k, c3crash);
+      rw = sm.recv[tid] | sm.nrecv[tid];
+      cw = sm.crash[tid] | sm.ncrash[tid];
+      if (tid == 0 && sm.err == 1) atomicOr(w.err, kErrArrivals);
     }
-    if (!small && !PROBE)  // large bucket: stream the messages from global memory once per tick
-      for (uint32_t k = 0; k < L; ++k) resolve_tick(w, sm, f, w.fmsg + mb, 0, M, k, t0 + k, c3crash);
     __syncthreads();
     stamp(w, sm, 7);
-    const uint64_t wi = ((uint64_t)f << kFineLog >> 5) + tid;
-    if (!PROBE && wi < w.W * 2) {
-      // the large path (resolve_node) sets sm.recv/sm.crash directly
-      const uint32_t r = sm.recv[tid] | sm.nrecv[tid], c = sm.crash[tid] | sm.ncrash[tid];
-      if (r != recv0) rw[wi] = r;
-      if (c != crash0) cwg[wi] = c;
+    if (in) {
+      if (rw != recv0) rwg[wi] = rw;
+      if (cw != crash0) cwg[wi] = cw;
     }
-    if (!PROBE && tid < w.R) w.fcount[(size_t)tid * w.nfine + f] = sm.fc[tid];
-#pragma unroll
-    for (uint32_t j = 0; j < kPerThread; ++j) {
-      if (j * kResolveBlock >= M) continue;
-      if (mr[j] != ~0u) sm.cnt[msg_loc(mr[j]) >> 1] = 0;
-    }
-    if (!PROBE && tid == 0 && sm.err) atomicOr(w.err, kErrArrivals);
+    if (tid < w.R) w.fcount[(size_t)tid * w.nfine + f] = sm.fc[tid];
     stamp(w, sm, 8);
     if (w.dbg && tid == 0) sm.stamp[sm.cls][0] += 1;
   }
   if (w.dbg && tid < 2 * kStampPhases) atomicAdd(&w.dbg[tid], (&sm.stamp[0][0])[tid]);
   __syncthreads();
-  if (!PROBE && tid < L * 3) {
+  if (tid < L * 3) {
     const uint32_t k = tid / 3, fld = tid - k * 3;
     const uint32_t v = sm.st[k][fld];
     // field 0 counts receipts that were NOT counted (:108, after a crash):
@@ -923,11 +793,8 @@ hipError_t win_groupmap(const WinState& w, uint32_t L, hipStream_t s) {
 }
 
 // mode 0: count coarse buckets only; 1: write + per-tick stats; 2: write only
-hipError_t win_expand(const WinState& w0, uint32_t t0, uint32_t L, uint64_t Tn, int mode,
+hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, int mode,
                       hipStream_t s) {
-  static const int xprobe = getenv("GS_XPROBE") ? atoi(getenv("GS_XPROBE")) : 0;
-  WinState w = w0;
-  if (xprobe == 1) w.kc = 0;  // timing diagnostic only: no ordinal-0 crash roll in the expand
   const uint32_t per_round = w.stride <= 8 ? kExpandBlock * kExpandNpt : kExpandBlock;
   const uint64_t rounds = (Tn + per_round - 1) / per_round;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>(rounds, 8192);
@@ -984,12 +851,7 @@ hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s
   }
   uint32_t G = std::min<uint32_t>(w.nfine, 2 * cus);
   G = std::max<uint32_t>(G, (w.nfine + kResolveMaxBuckets - 1) / kResolveMaxBuckets);
-  static const int probe = getenv("GS_PROBE") ? atoi(getenv("GS_PROBE")) : 0;
-  if (probe == 1) hipLaunchKernelGGL(k_resolve<1>, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
-  if (probe == 2) hipLaunchKernelGGL(k_resolve<2>, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
-  if (probe == 3) hipLaunchKernelGGL(k_resolve<3>, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
-  if (probe == 4) hipLaunchKernelGGL(k_resolve<4>, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
-  hipLaunchKernelGGL(k_resolve<0>, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
+  hipLaunchKernelGGL(k_resolve, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
   return hipGetLastError();
 }
 
