@@ -598,6 +598,11 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
   if (nb > 0) { fB = sm.blist[0]; mbB = w.fstart[fB]; MB = (uint32_t)w.ffill[fB]; }
   uint32_t* rwg = (uint32_t*)w.recv;
   uint32_t* cwg = (uint32_t*)w.crash;
+  // this lane's per-tick counters over all its buckets: infected | crashed << 16
+  // (each <= 32 per bucket and tick, <= 256 buckets), and receipts not counted
+  uint32_t acc_rc[kBitTicks], acc_d[kBitTicks];
+#pragma unroll
+  for (uint32_t k = 0; k < kBitTicks; ++k) { acc_rc[k] = 0; acc_d[k] = 0; }
   for (uint32_t i = 0; i < nb; ++i) {
     const uint32_t f = fB, M = MB;
     const unsigned long long mb = mbB;
@@ -638,6 +643,7 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
           if ((m[u] >> kRoll0Fine) & 1) atomicOr(&sm.rl[k][loc >> 5], bit);
           if (dup) atomicOr(&sm.b2[k][loc >> 5], bit);
         }
+        if (!__ballot(dup)) continue;  // no repeat receipt in this wave
         const uint32_t at = wave_append(&sm.ndup, dup);
         if (dup) {
           if (at < kDupCap) {
@@ -679,13 +685,9 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
           }
           replay_node(w, ubase + b, t, c, 1u << b, (R >> b) & 1, c3crash, cw, rw, infS, nd, nc, ni);
         }
-        // per-tick counters: one LDS atomic per wave and field
-        if (__ballot((nd | nc | ni) != 0)) {
-          const uint32_t sd = wave_sum(nd), sr = wave_sum(ni), sc = wave_sum(nc);
-          const uint32_t lane = lane_id();
-          const uint32_t v = lane == 0 ? sd : lane == 1 ? sr : sc;
-          if (lane < 3 && v) atomicAdd(&sm.st[k][lane], v);
-        }
+        // per-tick counters stay in the lane until the launch ends
+        acc_rc[k] += ni | (nc << 16);
+        acc_d[k] += nd;
         infk[k] = infS;
         ninf += ni;
       }
@@ -747,6 +749,15 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
     if (w.dbg && tid == 0) sm.stamp[sm.cls][0] += 1;
   }
   if (w.dbg && tid < 2 * kStampPhases) atomicAdd(&w.dbg[tid], (&sm.stamp[0][0])[tid]);
+#pragma unroll
+  for (uint32_t k = 0; k < kBitTicks; ++k) {
+    if (k >= L) continue;
+    const uint32_t rc = acc_rc[k];
+    const uint32_t sd = wave_sum(acc_d[k]), sr = wave_sum(rc & 0xFFFFu), sc = wave_sum(rc >> 16);
+    const uint32_t lane = lane_id();
+    const uint32_t v = lane == 0 ? sd : lane == 1 ? sr : sc;
+    if (lane < 3 && v) atomicAdd(&sm.st[k][lane], v);
+  }
   __syncthreads();
   if (tid < L * 3) {
     const uint32_t k = tid / 3, fld = tid - k * 3;
