@@ -84,7 +84,7 @@ int alloc_window(gs_ctx* c) {
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t units = (size_t)kMaxWindow * w.nfine + 1;
   const size_t b_fc = al((size_t)w.R * w.nfine * 4), b_units = al(units * 8),
-               b_small = al(256 * 8) * 3 + al(257 * 4) + al(257 * 8),
+               b_small = al(256 * 8) * 3 + al(257 * 4) + al(257 * 8) + al(kMaxWindow * 8),
                b_fhist = al(((size_t)w.ncoarse * 256 + 1) * 8), b_fbase = al(((size_t)w.nfine + 1) * 8),
                b_ffill = al((size_t)w.nfine * 8),
                b_sst = al((size_t)kStatShards * kMaxWindow * kStatFields * 8);
@@ -101,7 +101,8 @@ int alloc_window(gs_ctx* c) {
   w.chist = (unsigned long long*)q; q += al(256 * 8);
   w.cfill = (unsigned long long*)q; q += al(256 * 8);
   w.ccap = (unsigned long long*)q; q += al(257 * 8);
-  w.tprefix = (uint32_t*)q;
+  w.tprefix = (uint32_t*)q; q += al(257 * 4);
+  w.tfires = (unsigned long long*)q;
   q = (char*)c->d_win + b_fc + 2 * b_units + b_small;
   w.fhist = (unsigned long long*)q; q += b_fhist;
   w.fstart = (unsigned long long*)q; q += b_fbase;
@@ -583,19 +584,26 @@ static int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing) {
   while (done < n) {
     const uint32_t Lw = std::min(Lmax, n - done);
     const uint32_t t = (uint32_t)(t0 + done);
-    CK(c, win_units(w, t, Lw, c->stream));
-    size_t need = 0;
-    CK(c, win_scan_units(w, Lw, nullptr, need, c->stream));
-    if (!grow(c->tmp, need)) return fail(c, GS_ENOMEM, "cannot allocate scan scratch");
-    need = c->tmp.bytes;
-    CK(c, win_scan_units(w, Lw, c->tmp.p, need, c->stream));
-    // firing index at the start of every tick of the window (units are tick-major)
-    CK(c, hipMemcpy2DAsync(c->h_misc, 8, w.unit_off, (size_t)w.nfine * 8, 8, Lw + 1,
-                           hipMemcpyDeviceToHost, c->stream));
-    CK(c, hipStreamSynchronize(c->stream));
+    auto units = [&](uint32_t Lu) -> int {
+      CK(c, hipMemsetAsync(w.tfires, 0, kMaxWindow * 8, c->stream));
+      CK(c, win_units(w, t, Lu, c->stream));
+      size_t need = 0;
+      CK(c, win_scan_units(w, Lu, nullptr, need, c->stream));
+      if (!grow(c->tmp, need)) return fail(c, GS_ENOMEM, "cannot allocate scan scratch");
+      need = c->tmp.bytes;
+      CK(c, win_scan_units(w, Lu, c->tmp.p, need, c->stream));
+      CK(c, hipMemcpyAsync(c->h_misc, w.tfires, kMaxWindow * 8, hipMemcpyDeviceToHost, c->stream));
+      CK(c, hipStreamSynchronize(c->stream));
+      return GS_OK;
+    };
+    if (int rc = units(Lw)) return rc;
+    // fires per tick -> the window's length under the slot budget
     uint32_t L = 1;
-    while (L < Lw && c->h_misc[L + 1] * w.stride <= slot_budget) ++L;
-    const unsigned long long Tn = c->h_misc[L];  // broadcasts firing in the window
+    unsigned long long Tn = c->h_misc[0];  // broadcasts firing in the window
+    while (L < Lw && (Tn + c->h_misc[L]) * w.stride <= slot_budget) Tn += c->h_misc[L++];
+    // units are bucket-major: a cut window is laid out again for its L ticks
+    if (L < Lw)
+      if (int rc = units(L)) return rc;
     const unsigned long long T = Tn * w.stride;  // friend slots of the firing nodes
     plan_coarse(c, T, nullptr);
     const uint64_t fcap = T + T / 8 + (uint64_t)w.ncoarse * 256 * 513 + 16;

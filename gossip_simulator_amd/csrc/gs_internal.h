@@ -96,8 +96,9 @@ struct WinState {
   uint32_t* err;
   uint32_t* fcount;              // [R][nfine] fire-list lengths
   uint16_t* flist;               // [R][nfine][16384] local ids of firing nodes
-  unsigned long long* usize;     // [L*nfine + 1] fires per (tick, bucket) unit
+  unsigned long long* usize;     // [L*nfine + 1] fires per unit (bucket f, tick k), u = f*L + k
   unsigned long long* unit_off;  // [L*nfine + 1] exclusive scan of usize
+  unsigned long long* tfires;    // [kMaxWindow] fires per tick of the window (host-zeroed)
   uint32_t* gmap;                // [ceil(fires/64)] unit of every 64th firing index
   uint32_t* cmsg;                // coarse regions: u_in_coarse | k << 22
   uint32_t* fmsg;                // fine regions:   u_in_fine   | k << 14

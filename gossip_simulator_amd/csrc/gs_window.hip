@@ -8,7 +8,8 @@
 // receipts of each tick are still resolved in tick order per node.
 //
 // Pipeline of one window:
-//   units     fires per (tick k, fine bucket f); hipcub scan -> firing index
+//   units     fires per (fine bucket f, tick k), bucket-major; hipcub scan ->
+//             firing index
 //   groupmap  first unit of every 64-node group of firing indices
 //   expand    one thread per firing node (Node.Broadcast, :141-147): row read
 //             once, keyed RandomDrop per slot (one Philox per 4 slots), kept
@@ -42,17 +43,27 @@ constexpr uint32_t kResolveBlock = 512;
 constexpr uint32_t kRoll0Coarse = kCoarseShift + 4;
 constexpr uint32_t kRoll0Fine = kFineLog + 4;
 
-// Units = (tick k, fine bucket f); usize = fires.  Also zeroes the window's
+// Units = (fine bucket f, tick k), bucket-major (u = f*L + k): the L fire lists
+// of one bucket are expanded back to back, so friends-row lines that several
+// ticks of the window share are fetched once into the XCD's L2.  usize = fires;
+// tfires[k] = fires per tick (the host's window cut).  Also zeroes the window's
 // counters (one launch instead of several memsets).
 __global__ void k_units(const WinState w, uint32_t t0, uint32_t L) {
+  __shared__ uint32_t s_t[kMaxWindow];
   const uint32_t units = L * w.nfine;
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+  if (threadIdx.x < kMaxWindow) s_t[threadIdx.x] = 0;
+  __syncthreads();
   for (uint32_t u = tid; u <= units; u += nth) {
     if (u == units) { w.usize[u] = 0; continue; }
-    const uint32_t k = u / w.nfine, f = u - k * w.nfine;
+    const uint32_t f = u / L, k = u - f * L;
     const uint32_t s = (t0 + k) % w.R;
-    w.usize[u] = w.fcount[(size_t)s * w.nfine + f];
+    const uint32_t c = w.fcount[(size_t)s * w.nfine + f];
+    w.usize[u] = c;
+    if (c) atomicAdd(&s_t[k], c);
   }
+  __syncthreads();
+  if (threadIdx.x < L && s_t[threadIdx.x]) atomicAdd(&w.tfires[threadIdx.x], (unsigned long long)s_t[threadIdx.x]);
   for (uint32_t i = tid; i < 256; i += nth) { w.chist[i] = 0; w.cfill[i] = 0; }
   for (uint32_t i = tid; i < w.nfine; i += nth) w.ffill[i] = 0;
   if (tid == 0) *w.err &= ~(kErrCoarse | kErrFine);
@@ -167,7 +178,12 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
   const uint32_t c3drop = ctr3(K_DROP, w.key.trial), c3crash = ctr3(K_CRASH, w.key.trial);
   if (tid < kMaxWindow * 2) (&sm.acc[0][0])[tid] = 0;
   const unsigned long long rounds = (Tn + per_round - 1) / per_round;
-  for (unsigned long long rd = blockIdx.x; rd < rounds; rd += gridDim.x) {
+  // XCD-aware: workgroups are dealt to the 8 XCDs round-robin, so logical
+  // workgroup ids are remapped to give each XCD a contiguous run of rounds
+  // (one bucket's fire lists share friends-row lines in that XCD's L2)
+  const uint32_t B = gridDim.x;
+  const uint32_t lb = (B & 7) == 0 ? (blockIdx.x & 7) * (B >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  for (unsigned long long rd = lb; rd < rounds; rd += B) {
     sm.cnt[tid] = 0;
     __syncthreads();
     uint32_t mm[NPT][MAXS], mt[NPT][MAXS];  // message, bin | rank << 8 (~0u = none)
@@ -179,7 +195,7 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
       kk[q] = 0;
       if (g < Tn) {
         const uint32_t u = unit_of(w, g, Tn, units);
-        const uint32_t k = u / w.nfine, f = u - k * w.nfine;
+        const uint32_t f = u / L, k = u - f * L;
         const uint32_t s = (t0 + k) % w.R;
         const uint32_t i = (uint32_t)(g - w.unit_off[u]);
         vv[q] = (f << kFineLog) + w.flist[((size_t)s * w.nfine + f) * kFineNodes + i];
@@ -388,11 +404,11 @@ constexpr uint32_t kResolveMaxBuckets = 256;  // buckets one persistent workgrou
 
 // Bit-parallel resolve (k_resolve): per tick k of the window, b1 = nodes with
 // >= 1 receipt, b2 = nodes with >= 2, rl = nodes whose ordinal-0 crash roll
-// fired; receipts beyond the first of a (node, tick) are listed per 32-node
+// fired; receipts beyond the second of a (node, tick) are listed per 32-node
 // word (dlist, chained from dhead).  The large path (resolve_tick) reuses the
 // same LDS for per-node counters and bit words.
 constexpr uint32_t kBitWords = kFineNodes / 32;
-constexpr uint32_t kDupCap = 3072;     // repeat receipts per bucket (more: large path)
+constexpr uint32_t kDupCap = 3072;     // third+ receipts per bucket (more: large path)
 struct ResolveLds {
   union {
     struct {                            // b1 .. dlist, then the infection list
@@ -568,10 +584,10 @@ __device__ __forceinline__ void replay_node(const WinState& w, uint32_t u, uint3
 //   stage    thread w owns bit word w (32 nodes): its recv/crash words in
 //            registers, its b1/b2/rl words and dup-chain head zeroed
 //   receipts every message sets its (tick, node) bit in b1 (atomicOr); a
-//            repeat sets b2 and is chained under its word; a fired ordinal-0
-//            roll sets rl
+//            second receipt sets b2, later ones are chained under their
+//            word; a fired ordinal-0 roll sets rl
 //   ticks    per tick, thread w resolves its 32 nodes at once with bit ops
-//            (single receipts), walking its chain only for b2 nodes; the
+//            (single receipts), counting chain entries only for b2 nodes; the
 //            infections of the tick are Broadcast() in the lane (:122, :141)
 // A bucket with more repeats than kDupCap takes the per-tick large path.
 __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
@@ -639,11 +655,13 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
           loc = msg_loc(m[u]);
           k = msg_tick(m[u]);
           const uint32_t bit = 1u << (loc & 31);
-          dup = (atomicOr(&sm.b1[k][loc >> 5], bit) & bit) != 0;
           if ((m[u] >> kRoll0Fine) & 1) atomicOr(&sm.rl[k][loc >> 5], bit);
-          if (dup) atomicOr(&sm.b2[k][loc >> 5], bit);
+          // thermometer: b1 = >= 1 receipt, b2 = >= 2; the third and later
+          // receipts of a (node, tick) are chained under their word
+          if (atomicOr(&sm.b1[k][loc >> 5], bit) & bit)
+            dup = (atomicOr(&sm.b2[k][loc >> 5], bit) & bit) != 0;
         }
-        if (!__ballot(dup)) continue;  // no repeat receipt in this wave
+        if (!__ballot(dup)) continue;  // no third receipt in this wave
         const uint32_t at = wave_append(&sm.ndup, dup);
         if (dup) {
           if (at < kDupCap) {
@@ -677,7 +695,7 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
         const uint32_t t = t0 + k;
         for (uint32_t dm = D; dm; dm &= dm - 1) {        // nodes with repeats at this tick
           const uint32_t b = __builtin_ctz(dm), loc = tid * 32 + b;
-          uint32_t c = 1;
+          uint32_t c = 2;
           for (uint32_t q = sm.dhead[tid]; q;) {
             const uint32_t e = sm.dlist[q - 1];
             c += (e & ((1u << 18) - 1)) == (loc | (k << kFineLog)) ? 1u : 0u;
