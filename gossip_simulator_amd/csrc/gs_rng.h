@@ -33,13 +33,29 @@ __host__ __device__ __forceinline__ uint32_t mulhi32(uint32_t a, uint32_t b) {
 #endif
 }
 
+// hi:lo of a * b.  On gfx950 one v_mad_u64_u32 instead of the v_mul_hi_u32 +
+// v_mul_lo_u32 pair the compiler emits (Philox +24 %, scripts/micro/philox_bench2).
+__host__ __device__ __forceinline__ void mul64(uint32_t a, uint32_t b, uint32_t& hi, uint32_t& lo) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t p;
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(p) : "v"(a), "v"(b) : "vcc");
+  hi = (uint32_t)(p >> 32);
+  lo = (uint32_t)p;
+#else
+  const uint64_t p = (uint64_t)a * b;
+  hi = (uint32_t)(p >> 32);
+  lo = (uint32_t)p;
+#endif
+}
+
 // Philox4x32-10 (Random123 round and key schedule).
 __host__ __device__ __forceinline__ u32x4 philox(uint32_t c0, uint32_t c1, uint32_t c2,
                                                  uint32_t c3, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t h0 = mulhi32(0xD2511F53u, c0), l0 = 0xD2511F53u * c0;
-    const uint32_t h1 = mulhi32(0xCD9E8D57u, c2), l1 = 0xCD9E8D57u * c2;
+    uint32_t h0, l0, h1, l1;
+    mul64(0xD2511F53u, c0, h0, l0);
+    mul64(0xCD9E8D57u, c2, h1, l1);
     const uint32_t n0 = h1 ^ c1 ^ k0, n2 = h0 ^ c3 ^ k1;
     c0 = n0; c1 = l1; c2 = n2; c3 = l0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;

@@ -318,12 +318,13 @@ __global__ void k_plan(const WinState w, bool exact) {
 }
 
 // LDS counting sort of one tile by an 8-bit digit, then coalesced runs out.
-constexpr uint32_t kPartBlock = 512;  // threads per partition tile (16 messages each)
+constexpr uint32_t kPartBlock = 1024;  // threads per partition tile (16 messages each)
 static_assert(kPartTile % kPartBlock == 0, "whole messages per thread");
 
+// The tile holds coarse messages as they came: the fine digit (bits 14..21) is
+// re-read at write-out, so there is no per-slot bin byte (64 KB: two tiles/CU).
 struct TileSort {
   uint32_t buf[kPartTile];
-  uint8_t bin[kPartTile];
   uint32_t cnt[256];
   uint32_t off[257];
   unsigned long long gbase[256];
@@ -354,20 +355,16 @@ __global__ __launch_bounds__(kPartBlock) void k_part2(const WinState w) {
     __syncthreads();
     constexpr uint32_t kPer = kPartTile / kPartBlock;
     uint32_t m[kPer], rank[kPer];
-    uint8_t bn[kPer];
 #pragma unroll
     for (uint32_t r = 0; r < kPer; ++r) {
       const unsigned long long x = base + r * kPartBlock + tid;
       // branch-free load (index clamped into the tile's region: base < ce)
       const uint32_t m1 = w.cmsg[x < ce ? x : ce - 1];
-      m[r] = kEmptyMsg;
-      bn[r] = 0;
-      if (x < ce) {
-        bn[r] = (uint8_t)((m1 >> kFineLog) & 255);
-        m[r] = (m1 & (kFineNodes - 1)) | ((m1 >> kCoarseShift) << kFineLog);
-        rank[r] = atomicAdd(&ts.cnt[bn[r]], 1u);
-      }
+      m[r] = x < ce ? m1 : kEmptyMsg;
     }
+#pragma unroll
+    for (uint32_t r = 0; r < kPer; ++r)
+      if (m[r] != kEmptyMsg) rank[r] = atomicAdd(&ts.cnt[(m[r] >> kFineLog) & 255], 1u);
     __syncthreads();
     if (!SCATTER) {
       if (tid < 256 && ts.cnt[tid]) atomicAdd(&w.fhist[c * 256 + tid], (unsigned long long)ts.cnt[tid]);
@@ -384,17 +381,14 @@ __global__ __launch_bounds__(kPartBlock) void k_part2(const WinState w) {
     __syncthreads();
 #pragma unroll
     for (uint32_t r = 0; r < kPer; ++r)
-      if (m[r] != kEmptyMsg) {
-        const uint32_t p = ts.off[bn[r]] + rank[r];
-        ts.buf[p] = m[r];
-        ts.bin[p] = bn[r];
-      }
+      if (m[r] != kEmptyMsg) ts.buf[ts.off[(m[r] >> kFineLog) & 255] + rank[r]] = m[r];
     __syncthreads();
     const uint32_t total = ts.off[256];
     for (uint32_t p = tid; p < total; p += kPartBlock) {
-      const uint32_t b = ts.bin[p];
+      const uint32_t m1 = ts.buf[p], b = (m1 >> kFineLog) & 255;
       const unsigned long long pos = ts.gbase[b] + (p - ts.off[b]);
-      if (pos < w.fstart[c * 256 + b + 1]) w.fmsg[pos] = ts.buf[p];
+      if (pos < w.fstart[c * 256 + b + 1])
+        w.fmsg[pos] = (m1 & (kFineNodes - 1)) | ((m1 >> kCoarseShift) << kFineLog);
     }
     __syncthreads();
   }
@@ -408,14 +402,17 @@ constexpr uint32_t kResolveMaxBuckets = 256;  // buckets one persistent workgrou
 // word (dlist, chained from dhead).  The large path (resolve_tick) reuses the
 // same LDS for per-node counters and bit words.
 constexpr uint32_t kBitWords = kFineNodes / 32;
-constexpr uint32_t kDupCap = 3072;     // third+ receipts per bucket (more: large path)
+constexpr uint32_t kDupCap = 3840;     // third+ receipts per bucket (more: large path); the
+                                       // slots after them hold the batched crash rolls
 struct ResolveLds {
   union {
     struct {                            // b1 .. dlist, then the infection list
       uint32_t b1[kBitTicks][kBitWords];
       uint32_t b2[kBitTicks][kBitWords];
       uint32_t rl[kBitTicks][kBitWords];
-      uint32_t dlist[kDupCap];          // loc | k << 14 | next << 18 (next = index + 1, 0 = end)
+      uint32_t dlist[kDupCap];          // [0, ndup): loc | k << 14 | next << 18 (next = index + 1,
+                                        // 0 = end); then roll entries word << 9 | k << 5 | bit,
+                                        // with the ordinal 1..3 crash rolls in bits 18..20
       uint32_t dhead[kBitWords];
     };
     struct {                            // large path
@@ -430,6 +427,7 @@ struct ResolveLds {
   uint32_t st[kMaxWindow][4];       // dead (not counted), recv, crash per tick: whole launch
   uint32_t blist[kResolveMaxBuckets];  // this workgroup's non-empty buckets
   uint32_t ndup;
+  uint32_t nroll;
   uint32_t ninf;
   uint32_t err;
   uint32_t nb;
@@ -546,10 +544,11 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 // Receipt ordinals of one node with c >= 2 receipts at tick t (rule A6,
 // simulator.go:107-123): counted -> crash roll (ordinal 0 rode with the
 // message, later ordinals draw U_100(u, t, i)) -> first receipt infects.
+// roll123 = the rolls of ordinals 1..3 when `have` (batched), else drawn here.
 __device__ __forceinline__ void replay_node(const WinState& w, uint32_t u, uint32_t t, uint32_t c,
-                                            uint32_t bit, bool roll0, uint32_t c3crash, uint32_t& cw,
-                                            uint32_t& rw, uint32_t& infS, uint32_t& nd, uint32_t& nc,
-                                            uint32_t& ni) {
+                                            uint32_t bit, bool roll0, bool have, uint32_t roll123,
+                                            uint32_t c3crash, uint32_t& cw, uint32_t& rw,
+                                            uint32_t& infS, uint32_t& nd, uint32_t& nc, uint32_t& ni) {
   if (cw & bit) {  // crashed before this tick: nothing is counted (:108)
     nd += c;
     return;
@@ -560,8 +559,12 @@ __device__ __forceinline__ void replay_node(const WinState& w, uint32_t u, uint3
     if (i > 0) {
       roll = false;
       if (w.kc > 0) {
-        if (i == 1 || (i & 3) == 0) r = philox(u, t, i >> 2, c3crash, w.key.k0, w.key.k1);
-        roll = (int32_t)uniform(lane_of(r, i & 3), 100u) < w.kc;
+        if (have && i <= 3) {
+          roll = (roll123 >> (i - 1)) & 1;
+        } else {
+          if ((!have && i == 1) || (i & 3) == 0) r = philox(u, t, i >> 2, c3crash, w.key.k0, w.key.k1);
+          roll = (int32_t)uniform(lane_of(r, i & 3), 100u) < w.kc;
+        }
       }
     }
     if (roll) {                                                   // :113-115
@@ -677,8 +680,46 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
     stamp(w, sm, 2);
     uint32_t rw = recv0, cw = crash0;
     if (sm.err != 3) {
-      // ticks: thread tid resolves nodes 32*tid .. 32*tid+31, tick by tick
       const uint32_t ubase = node0 + tid * 32;
+      // crash rolls of ordinals 1..3 for every (node, tick) with >= 2 receipts,
+      // one lane per entry (in the tick loop they would serialise the wave);
+      // this word's entries are contiguous from rcur, in tick loop order
+      uint32_t rcur = kDupCap;
+      if (w.kc > 0) {
+        uint32_t cnt = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kBitTicks; ++k)
+          if (k < L) cnt += __popc(sm.b2[k][tid]);
+        uint32_t x = cnt;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_up(x, o, 64);
+          if (lane_id() >= o) x += y;
+        }
+        if (tid == 0) sm.nroll = sm.ndup < kDupCap ? sm.ndup : kDupCap;
+        __syncthreads();
+        uint32_t base = 0;
+        if (lane_id() == 63 && x) base = atomicAdd(&sm.nroll, x);
+        rcur = __shfl(base, 63, 64) + x - cnt;
+        uint32_t j = rcur;
+#pragma unroll
+        for (uint32_t k = 0; k < kBitTicks; ++k)
+          for (uint32_t d = k < L ? sm.b2[k][tid] : 0u; d; d &= d - 1, ++j)
+            if (j < kDupCap) sm.dlist[j] = (tid << 9) | (k << 5) | __builtin_ctz(d);
+        __syncthreads();
+        const uint32_t r0 = sm.ndup < kDupCap ? sm.ndup : kDupCap;
+        const uint32_t r1 = sm.nroll < kDupCap ? sm.nroll : kDupCap;
+        for (uint32_t q = r0 + tid; q < r1; q += kResolveBlock) {
+          const uint32_t e = sm.dlist[q];
+          const uint32_t u = node0 + (e >> 9) * 32 + (e & 31), t = t0 + ((e >> 5) & 15);
+          const u32x4 r = philox(u, t, 0, c3crash, w.key.k0, w.key.k1);  // :180, ordinals 0..3
+          const uint32_t b1 = (int32_t)uniform(r.y, 100u) < w.kc, b2 = (int32_t)uniform(r.z, 100u) < w.kc,
+                         b3 = (int32_t)uniform(r.w, 100u) < w.kc;
+          sm.dlist[q] = e | (b1 << 18) | (b2 << 19) | (b3 << 20);
+        }
+        __syncthreads();
+      }
+      // ticks: thread tid resolves nodes 32*tid .. 32*tid+31, tick by tick
       uint32_t infk[kBitTicks], ninf = 0;  // infections per tick of this word
 #pragma unroll
       for (uint32_t k = 0; k < kBitTicks; ++k) {
@@ -701,7 +742,11 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
             c += (e & ((1u << 18) - 1)) == (loc | (k << kFineLog)) ? 1u : 0u;
             q = e >> 18;
           }
-          replay_node(w, ubase + b, t, c, 1u << b, (R >> b) & 1, c3crash, cw, rw, infS, nd, nc, ni);
+          const bool have = rcur < kDupCap;
+          const uint32_t r123 = have ? (sm.dlist[rcur] >> 18) & 7 : 0u;
+          ++rcur;
+          replay_node(w, ubase + b, t, c, 1u << b, (R >> b) & 1, have, r123, c3crash, cw, rw, infS, nd,
+                      nc, ni);
         }
         // per-tick counters stay in the lane until the launch ends
         acc_rc[k] += ni | (nc << 16);
