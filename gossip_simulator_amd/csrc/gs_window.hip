@@ -214,12 +214,13 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
       const uint32_t v = vv[q], k = kk[q], t = t0 + k;
       uint32_t sent = 0;
 #pragma unroll
-      for (uint32_t jg = 0; jg < MAXS / 4; ++jg) {
+      for (uint32_t jg = 0; jg < (MAXS + 3) / 4; ++jg) {
         if (mm[q][jg * 4] == kEmptyMsg) break;
         const u32x4 r = philox(v, t, jg, c3drop, w.key.k0, w.key.k1);   // :144, :172
 #pragma unroll
         for (uint32_t jj = 0; jj < 4; ++jj) {
           const uint32_t j = jg * 4 + jj;
+          if (j >= MAXS) break;
           if (mm[q][j] != kEmptyMsg && (int32_t)uniform(lane_of(r, jj), 100u) >= w.kd) {  // kept: :145
             const uint32_t tgt = mm[q][j], bin = tgt >> kCoarseShift;
             // the receiver's crash roll for ordinal 0 (:112, key (u, t, 0)) rides along
@@ -869,13 +870,18 @@ hipError_t win_groupmap(const WinState& w, uint32_t L, hipStream_t s) {
 // mode 0: count coarse buckets only; 1: write + per-tick stats; 2: write only
 hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, int mode,
                       hipStream_t s) {
+  // rows of <= 6 (C5's fanin 6) and <= 8 slots: 4 nodes per thread; LDS holds
+  // block * 4 * row slots, so 6-slot rows fit four workgroups per CU
   const uint32_t per_round = w.stride <= 8 ? kExpandBlock * kExpandNpt : kExpandBlock;
   const uint64_t rounds = (Tn + per_round - 1) / per_round;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>(rounds, 8192);
   const dim3 grid(blocks ? blocks : 1), blk(kExpandBlock);
   const unsigned long long tn = Tn;
   const int st = mode == 1 ? 1 : 0;
-  if (w.stride <= 8) {
+  if (w.stride <= 6) {
+    if (mode) hipLaunchKernelGGL((k_expand<true, 6, kExpandNpt>), grid, blk, 0, s, w, t0, L, tn, st);
+    else hipLaunchKernelGGL((k_expand<false, 6, kExpandNpt>), grid, blk, 0, s, w, t0, L, tn, 0);
+  } else if (w.stride <= 8) {
     if (mode) hipLaunchKernelGGL((k_expand<true, 8, kExpandNpt>), grid, blk, 0, s, w, t0, L, tn, st);
     else hipLaunchKernelGGL((k_expand<false, 8, kExpandNpt>), grid, blk, 0, s, w, t0, L, tn, 0);
   } else {
