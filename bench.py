@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--cpu-n", type=int, default=10_000_000,
                     help="nodes in the bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-extensions", action="store_true",
+                    help="skip the C5 extension runs (1%% failed mask, push-pull)")
     return ap.parse_args()
 
 
@@ -105,6 +107,7 @@ def main():
         tot, status = one_step()
         sent += tot["sent"]
         ticks.append(tot["tick"])
+    recv_last = tot["received"]
     barrier()
     elapsed = time.perf_counter() - t1
     msgs = tot["messages"]
@@ -147,11 +150,17 @@ def main():
                 "broadcast_device_ms": round(kern_ms, 3)}
         sim.set_flags(False)
 
+    ext = None
+    if not a.no_extensions:
+        ext = {"flood_failed_1pct": flood_failed(a, sim)}
+    sim.close()
+    if not a.no_extensions:
+        ext.update(pushpull_runs(a, gs, rank, local))
+
     cpu = None
     if rank == 0 and world == 1 and a.cpu_n > 0:
         cpu = cpu_baseline(a, gs)
 
-    sim.close()
     if rank == 0:
         line = {
             "metric": "gossip messages delivered/sec (node) at N=1e9; rounds-to-coverage parity",
@@ -170,15 +179,107 @@ def main():
                        "n": a.n, "fanout": a.fanout, "fanin": a.fanin,
                        "delaylow": a.delaylow, "delayhigh": a.delayhigh,
                        "droprate": a.droprate, "crashrate": a.crashrate,
-                       "ticks_to_99": ticks[-1], "delivered_per_step": sent // a.steps,
+                       # a step ends at the first 10-tick poll with float32 coverage
+                       # >= 99 % (covered) or with no broadcast pending (quiescent:
+                       # with crashrate 0.01 about 1 % of the nodes crash on their
+                       # first receipt, so 99 % can be out of reach)
+                       "ticks": ticks[-1], "status": STATUS[status],
+                       "coverage": round(recv_last / a.n, 6),
+                       "delivered_per_step": sent // a.steps,
                        "messages_per_step": msgs, "overlay_s": round(overlay_s, 3),
                        "overlay_stabilised_ms": stab, "parallelism": f"trials{world}"},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "extensions": ext,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def failed_mask(n, frac, seed):
+    """Pre-failed node mask: round(frac * n) node ids drawn uniformly (with
+    replacement, so slightly fewer distinct nodes), as ceil(n/64) words."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    idx = rng.integers(0, n, size=int(round(frac * n)), dtype=np.int64)
+    w = np.zeros((n + 63) // 64, dtype=np.uint64)
+    np.bitwise_or.at(w, idx >> 6, np.left_shift(np.uint64(1), (idx & 63).astype(np.uint64)))
+    return w
+
+
+def timed_broadcast(sim, poll=10):
+    import torch
+    sim.reset()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sim.broadcast_begin(-1)
+    _, status = sim.run(poll=poll)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    tot = sim.totals()
+    return tot, status, dt
+
+
+STATUS = {0: "covered", 1: "quiescent", 2: "max_ticks"}
+
+
+def flood_failed(a, sim):
+    """C5 extension: the reference's flood with 1 % of the nodes pre-failed
+    (gs_set_failed); the crashrate still applies, so 99 % is out of reach and
+    the run ends when no broadcast is pending."""
+    sim.reset()
+    sim.set_failed(failed_mask(a.n, 0.01, a.seed + 1))
+    tot, status, dt = timed_broadcast(sim)
+    log(f"flood+1% failed: ticks={tot['tick']} sent={tot['sent']} {dt * 1e3:.1f} ms {STATUS[status]}")
+    return {"value": round(tot["sent"] / dt, 1), "unit": "msgs/s", "ms": round(dt * 1e3, 3),
+            "ticks": tot["tick"], "delivered": tot["sent"], "received": tot["received"],
+            "status": STATUS[status]}
+
+
+def pushpull_runs(a, gs, rank, local):
+    """C5 extension: push-pull gossip over the same
+    overlay (same seed -> the same table, rebuilt in a push-pull context),
+    without and with 1 % pre-failed nodes.  value = delivered transmissions / s
+    (calls not lost, whose receiver is live); k_pp_round roofline at 12
+    algorithmic bytes per call (4-B friend id + 8-B peer state word)."""
+    cfg = gs.Config(n=a.n, fanout=a.fanout, fanin=a.fanin, delaylow=a.delaylow,
+                    delayhigh=a.delayhigh, droprate=a.droprate, crashrate=a.crashrate,
+                    seed=a.seed, trial=rank, device=local, model="pushpull")
+    out = {}
+    with gs.Simulator(cfg) as sim:
+        sim.build_overlay()
+        timed_broadcast(sim)  # warmup
+        runs = [timed_broadcast(sim) for _ in range(max(a.steps, 1))]
+        dt = sum(r[2] for r in runs)
+        tot, status, _ = runs[-1]
+        sim.set_flags(True)
+        timed_broadcast(sim)
+        tm = sim.timing()
+        sim.set_flags(False)
+        rounds = int(tm["deliver_launches"])
+        ms = tm["deliver_ms"]
+        calls = tot["fired"]
+        ach = 12 * calls / (ms * 1e-3) / 1e9
+        log(f"push-pull: rounds={tot['tick']} sent={tot['sent']} {dt * 1e3 / len(runs):.1f} ms/run")
+        out["pushpull"] = {
+            "value": round(sum(r[0]["messages"] for r in runs) / dt, 1), "unit": "msgs/s",
+            "ms_per_step": round(dt * 1e3 / len(runs), 3), "rounds_to_99": tot["tick"],
+            "calls_per_s": round(sum(r[0]["fired"] for r in runs) / dt, 1),
+            "messages_per_step": tot["messages"], "received": tot["received"],
+            "status": STATUS[status],
+            "roofline": {"bound": "hbm", "kernel": "k_pp_round (one launch per round)",
+                         "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 5),
+                         "avg_launch_us": round(ms * 1e3 / max(rounds, 1), 2), "launches": rounds}}
+        sim.reset()
+        sim.set_failed(failed_mask(a.n, 0.01, a.seed + 1))
+        tot, status, dt = timed_broadcast(sim)
+        log(f"push-pull+1% failed: rounds={tot['tick']} {dt * 1e3:.1f} ms {STATUS[status]}")
+        out["pushpull_failed_1pct"] = {
+            "value": round(tot["messages"] / dt, 1), "unit": "msgs/s", "ms": round(dt * 1e3, 3),
+            "rounds": tot["tick"], "received": tot["received"], "status": STATUS[status]}
+    return out
 
 
 def pmc_traffic():

@@ -48,7 +48,7 @@ class Params(C.Structure):
         ("trial", C.c_uint32),
         ("device", C.c_int32),
         ("flags", C.c_uint32),
-        ("reserved0_", C.c_uint32),
+        ("model", C.c_uint32),  # GS_MODEL_FLOOD = 0 (reference), GS_MODEL_PUSHPULL = 1
         ("node_lo", C.c_uint64),
         ("node_hi", C.c_uint64),
         ("reserved_", C.c_uint64 * 4),

@@ -188,6 +188,8 @@ int main(int argc, char** argv) {
       {"trial", "uint", "Philox trial index", "0", false, "0"},
       {"device", "int", "HIP device ordinal", "0", false, "0"},
       {"peers", "string", "injected peer-table file (skips overlay construction)", "", false, ""},
+      {"model", "string", "dissemination model: flood (the reference) or pushpull (extension)",
+       "flood", false, "flood"},
       {"maxticks", "int", "give up after this many simulated ms per phase", "10000000", false,
        "10000000"},
   };
@@ -216,6 +218,12 @@ int main(int argc, char** argv) {
   p.seed = strtoull(find("seed")->val.c_str(), nullptr, 10);
   p.trial = (uint32_t)strtoull(find("trial")->val.c_str(), nullptr, 10);
   p.device = (int32_t)ival("device");
+  const std::string model = find("model")->val;
+  if (model != "flood" && model != "pushpull") {
+    fprintf(stderr, "invalid value \"%s\" for flag -model: want flood or pushpull\n", model.c_str());
+    return 2;
+  }
+  p.model = model == "pushpull" ? GS_MODEL_PUSHPULL : GS_MODEL_FLOOD;
   const uint64_t max_ticks = (uint64_t)ival("maxticks");
   if (ival("n") <= 0) {
     fprintf(stderr, "panic: invalid argument to Intn\n");  // simulator.go:240 with N=0

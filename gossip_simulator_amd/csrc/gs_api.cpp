@@ -37,6 +37,10 @@ struct gs_ctx {
   uint64_t t = 0, fired = 0, sent = 0, msgs = 0, recv = 0, crashed = 0, pending = 0;
   std::vector<hipEvent_t> ev;
   gs_timing timing{};
+  // push-pull extension (gs_pushpull.hip)
+  bool pp = false;
+  unsigned long long* d_next = nullptr;  // informed set being built (state block)
+  uint32_t* d_flag = nullptr;
   // window engine (gs_window.hip)
   bool win = false;
   WinState ws{};
@@ -171,6 +175,11 @@ int check_params(const gs_params* p, std::string& why) {
     return GS_EINVAL;
   }
   if (ring_slots(*p) > 4096) { why = "delayhigh must be <= 4096"; return GS_EINVAL; }
+  if (p->model > GS_MODEL_PUSHPULL) { why = "model must be GS_MODEL_FLOOD or GS_MODEL_PUSHPULL"; return GS_EINVAL; }
+  if (p->model == GS_MODEL_PUSHPULL && !(p->node_lo == 0 && (p->node_hi == 0 || p->node_hi == p->n))) {
+    why = "push-pull runs are not node-range sharded (shard trials instead)";
+    return GS_EINVAL;
+  }
   return GS_OK;
 }
 
@@ -331,18 +340,21 @@ int gs_create(const gs_params* params, gs_ctx** out) {
   s.key = Key{(uint32_t)c->p.seed, (uint32_t)(c->p.seed >> 32), c->p.trial};
   // Engine: the window engine (gs_window.hip) unless the run is node-range
   // sharded (per-tick frontier exchange) or its ring is too long for LDS.
-  c->win = !s.sharded && s.R <= kWinMaxRing && !(c->p.flags & GS_FLAG_TICK_ENGINE) &&
+  // Push-pull has its own round kernels (gs_pushpull.hip).
+  c->pp = c->p.model == GS_MODEL_PUSHPULL;
+  c->win = !c->pp && !s.sharded && s.R <= kWinMaxRing && !(c->p.flags & GS_FLAG_TICK_ENGINE) &&
            (uint32_t)std::max(c->p.fanout, c->p.fanin) <= kWinMaxStride;
   // One state allocation, 256-B aligned sub-buffers; everything before
   // `stats` is per-broadcast state that gs_reset clears.
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  const bool tick = !c->win;
+  const bool tick = !c->win && !c->pp;
+  const size_t b_next = c->pp ? al(s.W * 8) : 0;
   const size_t b_bits = al(s.W * 8), b_ring = tick ? al((size_t)s.R * s.W * 8) : 0,
                b_cflag = tick ? al((size_t)s.R * s.C * 4) : 0,
                b_clist = tick ? al((size_t)s.R * kShards * s.CS * 4) : 0,
                b_ccount = tick ? al((size_t)s.R * kShards * kCounterStride * 4) : 0,
                b_stats = al((size_t)kStatSlots * kStatFields * 8);
-  const size_t total = 2 * b_bits + b_ring + b_cflag + b_clist + b_ccount + b_stats + 256;
+  const size_t total = 2 * b_bits + b_next + b_ring + b_cflag + b_clist + b_ccount + b_stats + 256;
   c->state_bytes = total;
   if (hipMalloc(&c->d_state, total) != hipSuccess) {
     fprintf(stderr, "gs_create: cannot allocate %zu bytes of device state\n", total);
@@ -352,12 +364,14 @@ int gs_create(const gs_params* params, gs_ctx** out) {
   char* q = (char*)c->d_state;
   s.recv = (unsigned long long*)q; q += b_bits;
   s.crash = (unsigned long long*)q; q += b_bits;
+  c->d_next = b_next ? (unsigned long long*)q : nullptr; q += b_next;
   s.ring = (unsigned long long*)q; q += b_ring;
   s.cflag = (uint32_t*)q; q += b_cflag;
   s.clist = (uint32_t*)q; q += b_clist;
   s.ccount = (uint32_t*)q; q += b_ccount;
   s.stats = (unsigned long long*)q; q += b_stats;
   c->d_err = (uint32_t*)q;
+  c->d_flag = c->d_err + 1;
   if (tick && s.kc > 0) {
     if (hipMalloc(&c->d_cnt, s.n * 4) != hipSuccess) {
       fprintf(stderr, "gs_create: cannot allocate arrival counters\n");
@@ -537,6 +551,16 @@ int gs_broadcast_begin(gs_ctx* c, int64_t sender) {
                           : (uint64_t)sender;
   if (s >= c->p.n) return fail(c, GS_EINVAL, "sender out of range");
   CK(c, hipSetDevice(c->dev));
+  if (c->pp) {  // push-pull: the sender is informed (unless failed)
+    CK(c, pp_seed(c->st, c->d_next, (uint32_t)s, c->d_flag, c->stream));
+    uint32_t ok = 0;
+    CK(c, hipMemcpyAsync(&ok, c->d_flag, 4, hipMemcpyDeviceToHost, c->stream));
+    CK(c, hipStreamSynchronize(c->stream));
+    c->t = 0;
+    c->recv = c->pending = ok;
+    c->begun = true;
+    return GS_OK;
+  }
   const bool mine = s >= c->st.lo && s < c->st.hi;  // only the sender's owner schedules it
   if (mine && c->win) CK(c, win_schedule_one(c->ws, (uint32_t)s, 0, c->stream));
   else if (mine) CK(c, launch_schedule_one(c->st, (uint32_t)s, 0, c->stream));
@@ -720,7 +744,7 @@ int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
                          c->stream));
     if (first < batch)
       CK(c, hipMemsetAsync(c->st.stats, 0, (size_t)(batch - first) * kStatFields * 8, c->stream));
-    const uint32_t nev = timing && !c->win ? batch * (flood ? 2 : 4) : 0;
+    const uint32_t nev = timing && !c->win ? batch * (flood || c->pp ? 2 : 4) : 0;
     while (c->ev.size() < nev) {
       hipEvent_t e;
       CK(c, hipEventCreate(&e));
@@ -730,7 +754,15 @@ int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
       int rc = run_windows(c, t0, batch, timing);
       if (rc) return rc;
     }
-    for (uint32_t i = 0; i < batch && !c->win; ++i) {
+    for (uint32_t i = 0; i < batch && c->pp; ++i) {  // push-pull rounds
+      const uint32_t tt = (uint32_t)(t0 + i);
+      hipEvent_t* e = timing ? &c->ev[(size_t)i * 2] : nullptr;
+      if (e) CK(c, hipEventRecord(e[0], c->stream));
+      CK(c, pp_round(c->st, c->d_next, tt, c->stream));
+      if (e) CK(c, hipEventRecord(e[1], c->stream));
+      CK(c, pp_commit(c->st, c->d_next, tt, c->stream));
+    }
+    for (uint32_t i = 0; i < batch && !c->win && !c->pp; ++i) {
       const uint32_t tt = (uint32_t)(t0 + i);
       hipEvent_t* e = timing ? &c->ev[(size_t)i * (flood ? 2 : 4)] : nullptr;
       if (e) CK(c, hipEventRecord(e[0], c->stream));
@@ -751,12 +783,12 @@ int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
     CK(c, hipStreamSynchronize(c->stream));
     if (timing && !c->win) {
       for (uint32_t i = 0; i < batch; ++i) {
-        hipEvent_t* e = &c->ev[(size_t)i * (flood ? 2 : 4)];
+        hipEvent_t* e = &c->ev[(size_t)i * (flood || c->pp ? 2 : 4)];
         float ms = 0;
         CK(c, hipEventElapsedTime(&ms, e[0], e[1]));
         c->timing.deliver_ms += ms;
         c->timing.deliver_launches++;
-        if (!flood) {
+        if (!flood && !c->pp) {
           CK(c, hipEventElapsedTime(&ms, e[2], e[3]));
           c->timing.resolve_ms += ms;
           c->timing.resolve_launches++;
@@ -771,7 +803,8 @@ int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
       c->msgs += s[ST_MSGS];
       c->recv += s[ST_RECV];
       c->crashed += s[ST_CRASH];
-      c->pending = c->pending + s[ST_SCHED] - s[ST_FIRED];
+      // push-pull: every informed node keeps calling
+      c->pending = c->pp ? c->recv : c->pending + s[ST_SCHED] - s[ST_FIRED];
       if (out) {
         gs_tick_stats& o = out[done + i];
         o.tick = c->t;
@@ -794,7 +827,7 @@ int gs_run(gs_ctx* c, uint32_t poll, uint64_t max_ticks, gs_tick_stats* out, siz
   size_t k = 0;
   int32_t st = GS_RUN_MAX_TICKS;
   for (;;) {
-    const uint64_t f0 = c->fired, s0 = c->sent, m0 = c->msgs;
+    const uint64_t f0 = c->fired, s0 = c->sent, m0 = c->msgs, r0 = c->recv;
     int rc = gs_step(c, poll, nullptr);
     if (rc) return rc;
     if (out && k < cap)
@@ -802,7 +835,9 @@ int gs_run(gs_ctx* c, uint32_t poll, uint64_t max_ticks, gs_tick_stats* out, siz
                              c->pending};
     ++k;
     if (covered(c->recv, c->p.n)) { st = GS_RUN_COVERED; break; }
-    if (c->pending == 0) { st = GS_RUN_QUIESCENT; break; }
+    // push-pull: informed nodes call forever, so a poll window that informs
+    // nobody new (or an empty informed set) ends the run instead
+    if (c->pending == 0 || (c->pp && c->recv == r0)) { st = GS_RUN_QUIESCENT; break; }
     if (c->t >= max_ticks) { st = GS_RUN_MAX_TICKS; break; }
   }
   if (nout) *nout = k;

@@ -139,6 +139,13 @@ hipError_t win_seal_rows(const uint8_t* deg, uint32_t* ids, uint64_t n, uint32_t
 hipError_t win_stats_reduce(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
 hipError_t win_schedule_one(const WinState& w, uint32_t node, uint32_t tick, hipStream_t s);
 
+// Push-pull extension (gs_pushpull.hip): one round per tick; `next` is the
+// informed set being built (equal to recv at the start of every round).
+hipError_t pp_round(const DevState& s, unsigned long long* next, uint32_t t, hipStream_t st);
+hipError_t pp_commit(const DevState& s, const unsigned long long* next, uint32_t t, hipStream_t st);
+hipError_t pp_seed(const DevState& s, unsigned long long* next, uint32_t node, uint32_t* flag,
+                   hipStream_t st);
+
 // Launchers (gs_broadcast.hip).
 hipError_t launch_tick(const DevState& st, uint32_t tick, int mode, hipStream_t s);
 hipError_t launch_slot_reset(const DevState& st, uint32_t slot, hipStream_t s);

@@ -1,0 +1,148 @@
+// gs_pushpull.hip -- push-pull gossip rounds (extension, config C5).
+//
+// The reference only floods (simulator.go:140-149: every receipt re-broadcasts
+// to every friend).  Config C5 asks for push-pull gossip as well; it has no
+// reference semantics, so the model is the one oracle/gsoracle.h states (and
+// DESIGN.md section 4.5): one tick = one synchronous round; every live node v with a
+// non-empty friends list draws r = Philox{v, t, 0, PUSHPULL}, calls
+// u = friends[v][U_deg(r.x)], and the call is lost iff U_100(r.y) < kd
+// (the -droprate quantisation of simulator.go:172).  With I = informed set at
+// the start of the round: v in I pushes to u (u informed iff live); v not in I
+// pulls from u in I.  Failed nodes (gs_set_failed) never call or answer.
+//
+// Layout: one lane per node, one wave per 64-bit word of the bitsets, so a
+// wave's pulls land in its own word with one atomicOr of the ballot.  Pushes
+// scatter into `next` (atomicOr, only when u is neither informed nor failed);
+// `next` starts every round equal to `recv`, and k_pp_commit makes
+// recv = next and counts the newly informed.  Per round at N = 1e9: the
+// friends table is streamed once (a wave's 64 rows are contiguous), the
+// 125-MB recv bitset is gathered once per call (Infinity-Cache resident).
+#include <algorithm>
+
+#include "gs_internal.h"
+
+namespace gs {
+namespace {
+
+constexpr uint32_t kPPBlock = 256;
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (uint32_t o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Per-block sums of up to 3 counters into stats[slot][f0..], one atomic each.
+__device__ __forceinline__ void block_add(uint64_t* sh, const uint64_t (&v)[3], uint32_t nf,
+                                          unsigned long long* row, const uint32_t (&fld)[3]) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid < 3 * (kPPBlock / 64)) sh[tid] = 0;
+  __syncthreads();
+  for (uint32_t i = 0; i < nf; ++i) {
+    const uint64_t s = wave_sum64(v[i]);
+    if (lane == 0) sh[i * (kPPBlock / 64) + wv] = s;
+  }
+  __syncthreads();
+  if (tid < nf) {
+    uint64_t s = 0;
+    for (uint32_t k = 0; k < kPPBlock / 64; ++k) s += sh[tid * (kPPBlock / 64) + k];
+    if (s) atomicAdd(&row[fld[tid]], (unsigned long long)s);
+  }
+}
+
+__global__ __launch_bounds__(kPPBlock) void k_pp_round(const DevState s,
+                                                       unsigned long long* __restrict__ next,
+                                                       uint32_t t) {
+  __shared__ uint64_t sh[3 * (kPPBlock / 64)];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t c3 = ctr3(K_PUSHPULL, s.key.trial);
+  uint64_t fired = 0, sent = 0, msgs = 0;
+  const uint64_t step = (uint64_t)gridDim.x * kPPBlock;
+  for (uint64_t base = (uint64_t)blockIdx.x * kPPBlock + (threadIdx.x & ~63u); base < s.n; base += step) {
+    const uint64_t word = base >> 6;  // this wave's word (wave-uniform)
+    const uint64_t v = base + lane;
+    const unsigned long long Iw = s.recv[word], Fw = s.crash[word];
+    const bool live = v < s.n && !((Fw >> lane) & 1);
+    const uint32_t d = live ? s.deg[v] : 0u;
+    bool pulled = false;
+    if (d > 0) {
+      const u32x4 r = philox((uint32_t)v, t, 0, c3, s.key.k0, s.key.k1);
+      const uint32_t u = s.ids[v * s.stride + uniform(r.x, d)];
+      const bool kept = (int32_t)uniform(r.y, 100u) >= s.kd;
+      const unsigned long long ubit = 1ull << (u & 63);
+      ++fired;
+      if ((Iw >> lane) & 1) {  // push
+        if (kept) {
+          ++sent;
+          const unsigned long long Iu = s.recv[u >> 6], Fu = s.crash[u >> 6];
+          if (!(Fu & ubit)) {
+            ++msgs;
+            if (!(Iu & ubit)) atomicOr(&next[u >> 6], ubit);
+          }
+        }
+      } else if (s.recv[u >> 6] & ubit) {  // pull (u informed => u live)
+        if (kept) {
+          ++sent;
+          ++msgs;
+          pulled = true;
+        }
+      }
+    }
+    const unsigned long long bal = __ballot(pulled);
+    if (lane == 0 && bal) atomicOr(&next[word], bal);
+  }
+  const uint64_t v3[3] = {fired, sent, msgs};
+  const uint32_t f3[3] = {ST_FIRED, ST_SENT, ST_MSGS};
+  block_add(sh, v3, 3, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
+}
+
+__global__ __launch_bounds__(kPPBlock) void k_pp_commit(const DevState s,
+                                                        const unsigned long long* __restrict__ next,
+                                                        uint32_t t) {
+  __shared__ uint64_t sh[3 * (kPPBlock / 64)];
+  uint64_t newly = 0;
+  for (uint64_t w = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; w < s.W;
+       w += (uint64_t)gridDim.x * kPPBlock) {
+    const unsigned long long nx = next[w], old = s.recv[w];
+    newly += (uint64_t)__popcll(nx & ~old);
+    if (nx != old) s.recv[w] = nx;
+  }
+  const uint64_t v3[3] = {newly, 0, 0};
+  const uint32_t f3[3] = {ST_RECV, 0, 0};
+  block_add(sh, v3, 1, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
+}
+
+// Sender (simulator.go:239-241 for the flood model): informed at begin unless
+// failed; flag[0] = 1 if it was informed.
+__global__ void k_pp_seed(const DevState s, unsigned long long* next, uint32_t node, uint32_t* flag) {
+  const unsigned long long bit = 1ull << (node & 63);
+  const bool ok = !(s.crash[node >> 6] & bit);
+  if (ok) {
+    s.recv[node >> 6] |= bit;
+    next[node >> 6] |= bit;
+  }
+  *flag = ok ? 1u : 0u;
+}
+
+}  // namespace
+
+hipError_t pp_round(const DevState& s, unsigned long long* next, uint32_t t, hipStream_t st) {
+  const uint64_t waves = (s.n + 63) / 64;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((waves + 3) / 4, 8192);
+  hipLaunchKernelGGL(k_pp_round, dim3(blocks), dim3(kPPBlock), 0, st, s, next, t);
+  return hipGetLastError();
+}
+
+hipError_t pp_commit(const DevState& s, const unsigned long long* next, uint32_t t, hipStream_t st) {
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.W + kPPBlock - 1) / kPPBlock, 2048);
+  hipLaunchKernelGGL(k_pp_commit, dim3(blocks), dim3(kPPBlock), 0, st, s, next, t);
+  return hipGetLastError();
+}
+
+hipError_t pp_seed(const DevState& s, unsigned long long* next, uint32_t node, uint32_t* flag,
+                   hipStream_t st) {
+  hipLaunchKernelGGL(k_pp_seed, dim3(1), dim3(1), 0, st, s, next, node, flag);
+  return hipGetLastError();
+}
+
+}  // namespace gs

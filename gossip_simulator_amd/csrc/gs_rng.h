@@ -11,6 +11,7 @@
 //   kind OVDELAY simulator.go:153,160 ctr {u, t, k, .}          out[0] -> U_(high-low)
 //   kind VICTIM  simulator.go:71    ctr {u, t, k, .}            out[0] -> U_deg
 //   kind REPLACE simulator.go:86-88 ctr {u, t, k*64+a/4, .}     out[a%4] -> U_n
+//   kind PUSHPULL (extension)        ctr {v, t, 0, .}            out[0] -> U_deg, out[1] -> U_100
 // with counter word 3 = kind << 24 | trial.  U_m(r) = floor(r*m / 2^32).
 #pragma once
 #include <stdint.h>
@@ -20,7 +21,8 @@ namespace gs {
 
 enum Kind : uint32_t {
   K_SENDER = 1, K_DELAY = 2, K_DROP = 3, K_CRASH = 4,
-  K_PICK = 5, K_OVDELAY = 6, K_VICTIM = 7, K_REPLACE = 8
+  K_PICK = 5, K_OVDELAY = 6, K_VICTIM = 7, K_REPLACE = 8,
+  K_PUSHPULL = 9  // push-pull extension: peer pick + loss per (node, round)
 };
 
 struct u32x4 { uint32_t x, y, z, w; };

@@ -33,6 +33,7 @@ class Config:
     device: int = 0
     timing: bool = False
     engine: str = "window"  # "window" (default) or "tick" (per-tick atomic engine)
+    model: str = "flood"    # "flood" (the reference) or "pushpull" (extension)
 
     def to_params(self) -> Params:
         p = Params()
@@ -40,6 +41,9 @@ class Config:
         p.delay_low, p.delay_high = self.delaylow, self.delayhigh
         p.drop_rate, p.crash_rate = self.droprate, self.crashrate
         p.seed, p.trial, p.device = self.seed, self.trial, self.device
+        if self.model not in ("flood", "pushpull"):
+            raise ValueError(f"model must be 'flood' or 'pushpull', not {self.model!r}")
+        p.model = 1 if self.model == "pushpull" else 0
         p.flags = (_lib.GS_FLAG_TIMING if self.timing else 0) | \
             (_lib.GS_FLAG_TICK_ENGINE if self.engine == "tick" else 0)
         return p

@@ -42,6 +42,14 @@ enum {
 #define GS_FLAG_TIMING 1u /* time every tick kernel with HIP events (gs_timing) */
 #define GS_FLAG_TICK_ENGINE 2u /* force the per-tick atomic engine (default: window engine) */
 
+/* Dissemination model (gs_params.model). */
+#define GS_MODEL_FLOOD 0u    /* the reference: every receipt re-broadcasts to all friends (simulator.go:107-149) */
+#define GS_MODEL_PUSHPULL 1u /* extension (config C5), no reference counterpart: one synchronous
+                              * round per tick; each live node calls one Philox-picked friend,
+                              * informed callers push, uninformed callers pull; -droprate loses
+                              * calls, -crashrate is unused, gs_set_failed masks nodes
+                              * (oracle/gsoracle.h) */
+
 /* simulator.go:11-20 (Parameters) + the additive -seed/-trial knobs. */
 typedef struct gs_params {
   uint64_t n;          /* -n          simulator.go:187                       */
@@ -55,7 +63,7 @@ typedef struct gs_params {
   uint32_t trial;      /* Philox counter word 3, low 24 bits                  */
   int32_t device;      /* HIP device ordinal                                  */
   uint32_t flags;      /* GS_FLAG_*                                           */
-  uint32_t reserved0_;
+  uint32_t model;      /* GS_MODEL_* (0 = the reference's push flooding)      */
   /* Node-range sharding (config C4): this context owns nodes [node_lo,
    * node_hi); both multiples of 4096 except node_hi == n.  0,0 = all nodes. */
   uint64_t node_lo, node_hi;
@@ -140,8 +148,8 @@ int gs_broadcast_begin(gs_ctx* ctx, int64_t sender);
 int gs_step(gs_ctx* ctx, uint32_t ticks, gs_tick_stats* out);
 /* Replaces the poll loop simulator.go:243-251: steps `poll` ticks at a time
  * until float32(received)/float32(n) >= 0.99 at a poll (GS_RUN_COVERED), no
- * broadcast is pending (GS_RUN_QUIESCENT; the reference would spin forever),
- * or max_ticks.  out (may be NULL) receives one gs_tick_stats per poll. */
+ * broadcast is pending (GS_RUN_QUIESCENT; the reference would spin forever;
+ * push-pull: a poll window informed nobody new), or max_ticks.  out (may be NULL) receives one gs_tick_stats per poll. */
 int gs_run(gs_ctx* ctx, uint32_t poll, uint64_t max_ticks, gs_tick_stats* out,
            size_t cap, size_t* nout, int32_t* status);
 /* Cumulative totals so far (tick, fired/sent/messages summed). */

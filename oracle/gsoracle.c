@@ -93,6 +93,7 @@ static int check_params(const or_params* p) {
   if (p->delay_high <= p->delay_low) return -1;          /* :167 Intn(<=0) panics */
   if (p->fanin < 0 || p->fanout < 0) return -1;
   if (p->fanin > 255 || p->fanout > 255) return -1;
+  if (p->model > OR_MODEL_PUSHPULL) return -1;
   return 0;
 }
 
@@ -335,6 +336,16 @@ int or_engine_begin(or_engine* e, int64_t sender) {
   uint64_t s = sender < 0 ? or_pick_sender(&e->p) : (uint64_t)sender;
   if (s >= e->n) return -1;
   e->t = 0;
+  if (e->p.model == OR_MODEL_PUSHPULL) {
+    if (e->lo != 0 || e->hi != e->n) return -1;  /* not sharded */
+    if (!BIT(e->crashed, s)) {                    /* a failed sender informs nobody */
+      SETBIT(e->received, s);
+      e->recv = 1;
+    }
+    e->pending = e->recv;
+    e->begun = 1;
+    return 0;
+  }
   if (s >= e->lo && s < e->hi)   /* only the owner of the sender schedules it */
     schedule(e, (uint32_t)s, 0); /* simulator.go:241; sender NOT marked received */
   e->begun = 1;
@@ -348,8 +359,55 @@ int or_engine_set_failed(or_engine* e, const uint64_t* words, size_t nwords) {
   return 0;
 }
 
+/* Push-pull extension: one synchronous round per tick (see gsoracle.h).  The
+ * next informed set is built from the round's starting set only, so the
+ * result does not depend on the order nodes are visited in. */
+static int pushpull_step(or_engine* e, uint32_t ticks, or_tick_stats* out) {
+  uint64_t* next = (uint64_t*)malloc(e->W * 8);
+  if (!next) return -1;
+  for (uint32_t s = 0; s < ticks; ++s) {
+    uint64_t t = ++e->t;
+    uint64_t fired = 0, sent = 0, msgs = 0;
+    memcpy(next, e->received, e->W * 8);
+    for (uint64_t v = 0; v < e->n; ++v) {
+      uint32_t d = e->deg[v];
+      if (BIT(e->crashed, v) || d == 0) continue;
+      uint32_t ctr[4] = {(uint32_t)v, (uint32_t)t, 0, c3of(OR_K_PUSHPULL, e->p.trial)}, rnd[4];
+      or_philox(ctr, e->key, rnd);
+      uint32_t u = e->ids[v * e->stride + or_uniform(rnd[0], d)];
+      int kept = (int32_t)or_uniform(rnd[1], 100) >= e->kd;
+      ++fired;
+      if (BIT(e->received, v)) {              /* push */
+        if (!kept) continue;
+        ++sent;
+        if (BIT(e->crashed, u)) continue;
+        ++msgs;
+        SETBIT(next, u);
+      } else if (BIT(e->received, u)) {       /* pull (u informed => u live) */
+        if (!kept) continue;
+        ++sent;
+        ++msgs;
+        SETBIT(next, v);
+      }
+    }
+    for (uint64_t w = 0; w < e->W; ++w) {
+      e->recv += (uint64_t)__builtin_popcountll(next[w] & ~e->received[w]);
+      e->received[w] = next[w];
+    }
+    e->pending = e->recv;
+    if (out) {
+      out[s].tick = t; out[s].fired = fired; out[s].sent = sent;
+      out[s].messages = msgs; out[s].received = e->recv;
+      out[s].crashed = e->crashed_cnt; out[s].pending = e->pending;
+    }
+  }
+  free(next);
+  return 0;
+}
+
 int or_engine_step(or_engine* e, uint32_t ticks, or_tick_stats* out) {
   if (!e || !e->begun) return -1;
+  if (e->p.model == OR_MODEL_PUSHPULL) return pushpull_step(e, ticks, out);
   for (uint32_t s = 0; s < ticks; ++s) {
     uint64_t t = ++e->t;
     uint64_t* ring = e->ring + (t % e->R) * e->W;

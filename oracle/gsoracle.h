@@ -44,7 +44,14 @@ enum {
   OR_K_PICK = 5,    /* simulator.go:97   new-friend pick                      */
   OR_K_OVDELAY = 6, /* simulator.go:153,160 Breakup/Makeup delay              */
   OR_K_VICTIM = 7,  /* simulator.go:71   victim slot                          */
-  OR_K_REPLACE = 8  /* simulator.go:86-89 replacement friend (rejection)      */
+  OR_K_REPLACE = 8, /* simulator.go:86-89 replacement friend (rejection)      */
+  OR_K_PUSHPULL = 9 /* push-pull extension: peer pick + loss, per (node, round) */
+};
+
+/* Dissemination models (or_params.model). */
+enum {
+  OR_MODEL_FLOOD = 0,    /* the reference: push flooding (simulator.go:107-149)  */
+  OR_MODEL_PUSHPULL = 1  /* extension (config C5), no reference counterpart      */
 };
 
 typedef struct or_params {
@@ -57,7 +64,7 @@ typedef struct or_params {
   double crash_rate;   /* -crashrate simulator.go:193 */
   uint64_t seed;       /* Philox key (additive flag -seed) */
   uint32_t trial;      /* Philox counter word 3 low 24 bits */
-  uint32_t pad_;
+  uint32_t model;      /* OR_MODEL_* */
 } or_params;
 
 typedef struct or_tick_stats {
@@ -95,6 +102,16 @@ int or_overlay(const or_params* p, uint8_t* deg, uint32_t* ids, or_window* win,
                uint64_t* final_tick);
 
 /* ---- broadcast tick engine (simulator.go:107-123,140-149,237-253) ------- */
+/* model OR_MODEL_PUSHPULL (extension; the reference only floods): one tick is
+ * one synchronous round.  Every live node v with a non-empty friends list
+ * draws r = Philox{v, t, 0, PUSHPULL}: peer u = friends[U_deg(r.x)], call lost
+ * iff U_100(r.y) < int(droprate*100).  With I = the informed set at the start
+ * of the round: v in I pushes to u (sent; delivered and u informed iff u is
+ * live); v not in I pulls from u in I (sent, delivered, v informed).  Failed
+ * nodes (or_engine_set_failed) never call, answer or become informed; the
+ * crash rate is not used.  The sender is informed at begin (if live).
+ * Per tick: fired = calls, sent = rumour transmissions not lost, messages =
+ * those delivered to a live node, received = |I|, pending = |I|. */
 typedef struct or_engine or_engine;
 or_engine* or_engine_new(const or_params* p, const uint8_t* deg,
                          const uint32_t* ids, uint32_t stride);

@@ -34,7 +34,7 @@ class Params(C.Structure):
         ("crash_rate", C.c_double),
         ("seed", C.c_uint64),
         ("trial", C.c_uint32),
-        ("pad_", C.c_uint32),
+        ("model", C.c_uint32),  # 0 flood (reference), 1 push-pull (extension)
     ]
 
 
@@ -96,10 +96,13 @@ def lib():
     return _lib
 
 
+MODEL_FLOOD, MODEL_PUSHPULL = 0, 1
+
+
 def make_params(n=50000, fanout=5, fanin=6, delay_low=10, delay_high=20,
-                drop_rate=0.1, crash_rate=0.001, seed=0x5EED, trial=0) -> Params:
+                drop_rate=0.1, crash_rate=0.001, seed=0x5EED, trial=0, model=0) -> Params:
     return Params(n, fanout, fanin, delay_low, delay_high, drop_rate, crash_rate,
-                  seed, trial, 0)
+                  seed, trial, model)
 
 
 def threshold(rate: float) -> int:
@@ -220,12 +223,16 @@ def run_to_coverage(p: Params, deg, ids, sender=-1, poll=10, max_ticks=100000,
         e.set_failed(failed)
     e.begin(sender)
     rows = []
+    r0 = int(sum(bin(int(x)).count("1") for x in e.received()))  # informed at begin (push-pull)
     while True:
         s = e.step(poll)
         rows.append(s)
         last = s[-1]
         if covered(int(last[4]), p.n) or int(last[6]) == 0 or int(last[0]) >= max_ticks:
             break
+        if p.model == MODEL_PUSHPULL and int(last[4]) == r0:  # gs_run's push-pull quiescence
+            break
+        r0 = int(last[4])
     return np.concatenate(rows), e
 
 

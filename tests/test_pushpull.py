@@ -1,0 +1,213 @@
+"""Push-pull extension (config C5): no reference semantics exist
+(simulator.go only floods, :140-149), so the CPU restatement in
+oracle/gsoracle.c (pushpull_step) is pinned here by a second, independent
+pure-Python restatement and by hand-derived answers, and the HIP rounds
+(gs_pushpull.hip) must match it bit-exactly per round.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import masked, random_table, sha
+
+PP = dict(fanout=5, fanin=6, delay_low=10, delay_high=20, drop_rate=0.1, crash_rate=0.0,
+          seed=0x5EED, trial=0, model=1)
+
+
+def py_pushpull(oracle, p, deg, ids, sender, rounds, failed=None):
+    """Independent restatement: one synchronous round per tick, all draws keyed
+    Philox{v, t, 0, kind 9 << 24 | trial}."""
+    n = int(p.n)
+    key = [int(p.seed) & 0xFFFFFFFF, int(p.seed) >> 32]
+    kd = oracle.threshold(p.drop_rate)
+    dead = np.zeros(n, bool) if failed is None else failed
+    inf = np.zeros(n, bool)
+    recv = 0
+    if not dead[sender]:
+        inf[sender] = True
+        recv = 1
+    out = []
+    for t in range(1, rounds + 1):
+        nxt = inf.copy()
+        fired = sent = msgs = 0
+        for v in range(n):
+            d = int(deg[v])
+            if dead[v] or d == 0:
+                continue
+            r = oracle.philox([v, t, 0, (9 << 24) | int(p.trial)], key)
+            u = int(ids[v, (r[0] * d) >> 32])
+            kept = ((r[1] * 100) >> 32) >= kd
+            fired += 1
+            if inf[v]:
+                if kept:
+                    sent += 1
+                    if not dead[u]:
+                        msgs += 1
+                        nxt[u] = True
+            elif inf[u] and kept:
+                sent += 1
+                msgs += 1
+                nxt[v] = True
+        recv += int((nxt & ~inf).sum())
+        inf = nxt
+        out.append([t, fired, sent, msgs, recv, 0, recv])
+    return np.array(out, dtype=np.uint64), inf
+
+
+def words_of(bits):
+    n = bits.size
+    w = np.zeros((n + 63) // 64, dtype=np.uint64)
+    idx = np.nonzero(bits)[0]
+    np.bitwise_or.at(w, idx // 64, np.left_shift(np.uint64(1), (idx % 64).astype(np.uint64)))
+    return w
+
+
+@pytest.mark.parametrize("n,drop,fail_frac", [(1, 0.1, 0.0), (2, 0.0, 0.0), (300, 0.1, 0.0),
+                                              (257, 0.3, 0.05), (500, 1.0, 0.0)])
+def test_oracle_matches_python_restatement(oracle, n, drop, fail_frac):
+    deg, ids = random_table(n, 6, 0 if n > 2 else 1, 6, seed=n + 1)
+    p = oracle.make_params(**dict(PP, n=n, drop_rate=drop))
+    rng = np.random.default_rng(n)
+    dead = rng.random(n) < fail_frac
+    sender = int(oracle.pick_sender(p))
+    rounds = 25
+    ref, inf = py_pushpull(oracle, p, deg, masked(deg, ids), sender, rounds, dead)
+    e = oracle.Engine(p, deg, ids)
+    if fail_frac:
+        e.set_failed(words_of(dead))
+    e.begin(-1)
+    got = e.step(rounds)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(e.received(), words_of(inf))
+
+
+def test_oracle_known_answers(oracle):
+    n = 4000
+    deg, ids = random_table(n, 6, 5, 6, seed=3)
+    # every call lost: only the sender is ever informed, nothing is sent
+    e = oracle.Engine(oracle.make_params(**dict(PP, n=n, drop_rate=1.0)), deg, ids)
+    e.begin(7)
+    s = e.step(10)
+    assert (s[:, 4] == 1).all() and (s[:, 2] == 0).all() and (s[:, 1] == n).all()
+    # a failed sender informs nobody, and a failed node is never informed
+    failed = np.zeros(n, bool)
+    failed[[7, 100, 2000]] = True
+    e = oracle.Engine(oracle.make_params(**dict(PP, n=n)), deg, ids)
+    e.set_failed(words_of(failed))
+    e.begin(7)
+    assert (e.step(5)[:, 4] == 0).all()
+    e = oracle.Engine(oracle.make_params(**dict(PP, n=n, drop_rate=0.0)), deg, ids)
+    e.set_failed(words_of(failed))
+    e.begin(8)
+    s = e.step(40)
+    rec = e.received()
+    for v in (7, 100, 2000):
+        assert not (int(rec[v // 64]) >> (v % 64)) & 1
+    assert (np.diff(s[:, 4].astype(np.int64)) >= 0).all() and (s[:, 6] == s[:, 4]).all()
+    assert int(s[-1, 4]) == n - 3  # a connected table: everyone live is reached
+    # complete graph, no loss: round 1 informs the sender's pick and every
+    # node that picked the sender
+    n = 64
+    deg = np.full(n, n - 1, np.uint8)
+    ids = np.array([[u for u in range(n) if u != v] for v in range(n)], np.uint32)
+    p = oracle.make_params(**dict(PP, n=n, fanout=n - 1, fanin=n - 1, drop_rate=0.0))
+    e = oracle.Engine(p, deg, ids)
+    e.begin(0)
+    s = e.step(1)[0]
+    key = [int(p.seed) & 0xFFFFFFFF, int(p.seed) >> 32]
+    picks = [int(ids[v, (oracle.philox([v, 1, 0, 9 << 24], key)[0] * (n - 1)) >> 32]) for v in range(n)]
+    expect = {0, picks[0]} | {v for v in range(n) if picks[v] == 0}
+    assert int(s[4]) == len(expect)
+    assert int(s[2]) == 1 + sum(1 for v in range(1, n) if picks[v] == 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw,stride,dlo,dhi,fail_frac", [
+    (dict(PP, n=1), 2, 1, 2, 0.0),
+    (dict(PP, n=2, drop_rate=0.0), 3, 0, 3, 0.0),
+    (dict(PP, n=777), 6, 0, 6, 0.0),                        # ragged words, zero degrees
+    (dict(PP, n=20000), 6, 5, 6, 0.01),                     # C5 shape, 1 % failed
+    (dict(PP, n=20000, drop_rate=1.0), 6, 5, 6, 0.0),       # every call lost
+    (dict(PP, n=65536 + 77, drop_rate=0.29, trial=5), 19, 18, 19, 0.03),  # wide rows
+])
+def test_gpu_pushpull_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac):
+    import gossip_simulator_amd as gs
+    gs.load()
+    n = kw["n"]
+    deg, ids = random_table(n, stride, dlo, dhi, seed=n)
+    p = oracle.make_params(**kw)
+    e = oracle.Engine(p, deg, ids)
+    failed = words_of(np.random.default_rng(1).random(n) < fail_frac) if fail_frac else None
+    if failed is not None:
+        e.set_failed(failed)
+    e.begin(-1)
+    cfg = gs.Config(n=n, fanout=kw["fanout"], fanin=kw["fanin"], delaylow=kw["delay_low"],
+                    delayhigh=kw["delay_high"], droprate=kw["drop_rate"], crashrate=kw["crash_rate"],
+                    seed=kw["seed"], trial=kw["trial"], model="pushpull")
+    with gs.Simulator(cfg) as sim:
+        sim.load_peers(deg, ids)
+        if failed is not None:
+            sim.set_failed(failed)
+        sim.broadcast_begin(-1)
+        for r in range(60):
+            a, b = e.step(1), sim.step(1)
+            assert np.array_equal(a, b), f"round {r + 1}:\n{a}\n{b}"
+            assert sha(e.received()) == sha(sim.received()), f"informed set differs at round {r + 1}"
+            if oracle.covered(int(a[0, 4]), n) or int(a[0, 4]) == 0:
+                break
+
+
+@pytest.mark.gpu
+def test_gpu_pushpull_c5_shape_1e6(oracle):
+    """N = 1e6 over the GPU-built overlay (fanout 5, fanin 6), 0.5 % failed nodes:
+    bit-exact to the oracle at every round until 99 % coverage."""
+    import gossip_simulator_amd as gs
+    gs.load()
+    n = 1_000_000
+    cfg = gs.Config(n=n, fanout=5, fanin=6, droprate=0.1, crashrate=0.0, seed=0x5EED,
+                    model="pushpull")
+    with gs.Simulator(cfg) as sim:
+        sim.build_overlay()
+        deg, ids = sim.read_peers()
+        failed = words_of(np.random.default_rng(2).random(n) < 0.005)
+        sim.set_failed(failed)
+        p = oracle.make_params(n=n, drop_rate=0.1, crash_rate=0.0, model=1)
+        e = oracle.Engine(p, deg, ids)
+        e.set_failed(failed)
+        e.begin(-1)
+        sim.broadcast_begin(-1)
+        for r in range(200):
+            a, b = e.step(1), sim.step(1)
+            assert np.array_equal(a, b), f"round {r + 1}"
+            if oracle.covered(int(a[0, 4]), n):
+                break
+        assert oracle.covered(int(a[0, 4]), n)
+        assert sha(e.received()) == sha(sim.received())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fail_frac", [0.0, 0.02])
+def test_gpu_pushpull_run_polls_like_oracle(oracle, fail_frac):
+    """gs_run: 10-round polls, stop at 99 % (float32 rule) or after a poll
+    window that informed nobody new (2 % failed nodes cannot reach 99 %)."""
+    import gossip_simulator_amd as gs
+    gs.load()
+    n = 30000
+    deg, ids = random_table(n, 6, 5, 6, seed=4)
+    kw = dict(PP, n=n)
+    p = oracle.make_params(**kw)
+    failed = words_of(np.random.default_rng(3).random(n) < fail_frac) if fail_frac else None
+    rows, e = oracle.run_to_coverage(p, deg, ids, failed=failed)
+    cfg = gs.Config(n=n, droprate=kw["drop_rate"], crashrate=0.0, seed=kw["seed"], model="pushpull")
+    with gs.Simulator(cfg) as sim:
+        sim.load_peers(deg, ids)
+        if failed is not None:
+            sim.set_failed(failed)
+        sim.broadcast_begin(-1)
+        polls, status = sim.run(poll=10)
+        assert int(polls[-1][0]) == int(rows[-1][0])
+        assert int(polls[-1][4]) == int(rows[-1][4])
+        assert int(sim.totals()["messages"]) == int(rows[:, 3].sum())
+        assert status == (gs.GS_RUN_COVERED if oracle.covered(int(rows[-1][4]), n) else gs.GS_RUN_QUIESCENT)
+        assert sha(sim.received()) == sha(e.received())
