@@ -920,15 +920,13 @@ hipError_t win_scan_fine(const WinState& w, void* tmp, size_t& tmp_bytes, hipStr
 
 hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s) {
   // persistent: two workgroups per CU (the LDS holds two), each owning <= 256 buckets
-  static uint32_t cus = 0;
-  if (!cus) {
+  static const uint32_t cus = [] {  // thread-safe one-time query (contexts may run in threads)
     int dev = 0, v = 0;
     if (hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-      cus = (uint32_t)v;
-    else
-      cus = 256;
-  }
+      return (uint32_t)v;
+    return 256u;
+  }();
   uint32_t G = std::min<uint32_t>(w.nfine, 2 * cus);
   G = std::max<uint32_t>(G, (w.nfine + kResolveMaxBuckets - 1) / kResolveMaxBuckets);
   hipLaunchKernelGGL(k_resolve, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);

@@ -81,18 +81,34 @@ def run_one_trial(sim, n: int, poll: int = 10, max_ticks: int = 100000) -> list:
 
 
 def run_trials(make_sim, cfg: Config, total: int, rank: int = 0, world: int = 1,
-               device: str = "cpu", poll: int = 10) -> np.ndarray:
+               device: str = "cpu", poll: int = 10, concurrency: int = 1) -> np.ndarray:
     """Run trials rank, rank+world, ...; returns the full [total, 8] table on
-    every rank (one all-reduce of the per-rank rows at the end)."""
+    every rank (one all-reduce of the per-rank rows at the end).
+
+    concurrency > 1 runs that many trials at once on the rank's GPU, one
+    context (own HIP stream) per host thread: a trial at N = 1e5 launches
+    small grids, so one stream alone leaves most CUs idle.  ctypes releases
+    the GIL inside every C-ABI call, so the threads overlap on the device."""
     out = torch.zeros((total, len(TRIAL_FIELDS)), dtype=torch.int64)
-    for t in trials_of(total, rank, world):
+
+    def one(t):
         sim = make_sim(replace(cfg, trial=t))
         try:
-            out[t] = torch.tensor([t] + run_one_trial(sim, cfg.n, poll), dtype=torch.int64)
+            return t, [t] + run_one_trial(sim, cfg.n, poll)
         finally:
             close = getattr(sim, "close", None)
             if close:
                 close()
+
+    mine = list(trials_of(total, rank, world))
+    if concurrency > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max_workers=concurrency) as ex:
+            rows = list(ex.map(one, mine))
+    else:
+        rows = [one(t) for t in mine]
+    for t, row in rows:
+        out[t] = torch.tensor(row, dtype=torch.int64)
     if world > 1:
         buf = out.to(device)
         dist.all_reduce(buf, op=dist.ReduceOp.SUM)

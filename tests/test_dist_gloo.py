@@ -156,6 +156,9 @@ def test_trial_sharding_world2_matches_serial(oracle, tmp_path):
     serial = gd.run_trials(lambda c: OracleSim(oracle, c), Config(n=3000, crashrate=0.01, seed=5),
                            total=7)
     assert np.array_equal(a, serial)
+    threaded = gd.run_trials(lambda c: OracleSim(oracle, c), Config(n=3000, crashrate=0.01, seed=5),
+                             total=7, concurrency=3)
+    assert np.array_equal(threaded, serial)
     assert list(a[:, 0]) == list(range(7))
     assert set(a[:, 7]) <= {0, 1}  # covered, or the flood died out (crash 1 %)
     assert (a[a[:, 7] == 0, 1] > 0).all()
