@@ -261,7 +261,7 @@ int overlay_build(uint64_t n, int32_t fanout, int32_t fanin, int32_t delay_low,
   DevBuf scratch, outb, oslotb, heads, cub_tmp, meta;
   // meta layout: counts[R] | fill[R] | ptrs[R] | nheads | TickCounters
   uint64_t pending = 0, wm = 0, wb = 0;
-  std::vector<unsigned long long> h_counts(R);
+  std::vector<unsigned long long> h_counts(R), hfill(R);
   std::vector<uint64_t*> h_ptrs(R, nullptr);
   unsigned long long *d_counts = nullptr, *d_fill = nullptr;
   uint64_t** d_ptrs = nullptr;
@@ -387,12 +387,13 @@ int overlay_build(uint64_t n, int32_t fanout, int32_t fanin, int32_t delay_low,
       if (moved)
         OVCHK(hipMemcpyAsync(d_ptrs, h_ptrs.data(), R * 8, hipMemcpyHostToDevice, stream));
       {
-        std::vector<unsigned long long> hf(fill.begin(), fill.end());
-        OVCHK(hipMemcpyAsync(d_fill, hf.data(), R * 8, hipMemcpyHostToDevice, stream));
+        // hfill is rewritten only after the next tick's count sync, which
+        // orders it after this copy: no host sync after the scatter
+        hfill.assign(fill.begin(), fill.end());
+        OVCHK(hipMemcpyAsync(d_fill, hfill.data(), R * 8, hipMemcpyHostToDevice, stream));
         hipLaunchKernelGGL((k_scatter<true, OutSource>), dim3(blocks), dim3(kScatterBlock), 0,
                            stream, osrc, m, R, d_counts, d_fill, (uint64_t* const*)d_ptrs);
         OVCHK(hipGetLastError());
-        OVCHK(hipStreamSynchronize(stream));
       }
       for (uint32_t q = 0; q < R; ++q) { fill[q] += h_counts[q]; pending += h_counts[q]; }
       wm += h_tc.makeups;

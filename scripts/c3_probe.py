@@ -9,6 +9,7 @@ import gossip_simulator_amd as gs  # noqa: E402
 from gossip_simulator_amd import dist  # noqa: E402
 
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+CONC = [int(x) for x in sys.argv[2:]] or [16]
 cfg = gs.Config(n=100_000, crashrate=0.001, seed=0x5EED)
 t_ov = t_bc = 0.0
 for t in range(K):
@@ -25,3 +26,10 @@ for t in range(K):
         t_bc += t2 - t1
 print(f"C3 probe: {K - 1} trials, overlay {t_ov / (K - 1) * 1e3:.2f} ms/trial, "
       f"broadcast {t_bc / (K - 1) * 1e3:.2f} ms/trial")
+for conc in CONC:
+    cfg1 = gs.Config(n=100_000, seed=0x5EED)
+    dist.run_trials(gs.Simulator, cfg1, total=conc, concurrency=conc)
+    t0 = time.perf_counter()
+    dist.run_trials(gs.Simulator, cfg1, total=4 * conc, concurrency=conc)
+    dt = time.perf_counter() - t0
+    print(f"C3 probe: concurrency {conc}: {4 * conc / dt:.1f} trials/s")
