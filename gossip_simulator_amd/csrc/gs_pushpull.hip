@@ -74,8 +74,9 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_round(const DevState s,
       if ((Iw >> lane) & 1) {  // push
         if (kept) {
           ++sent;
-          const unsigned long long Iu = s.recv[u >> 6], Fu = s.crash[u >> 6];
-          if (!(Fu & ubit)) {
+          // the failed-mask gather only when a mask was set (gs_set_failed)
+          const unsigned long long Iu = s.recv[u >> 6];
+          if (!s.check_crashed || !(s.crash[u >> 6] & ubit)) {
             ++msgs;
             if (!(Iu & ubit)) atomicOr(&next[u >> 6], ubit);
           }
