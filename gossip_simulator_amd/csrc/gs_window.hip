@@ -119,6 +119,7 @@ struct ExpandLds {
   uint32_t cnt[256];
   uint32_t off[257];
   unsigned long long gbase[256];
+  unsigned long long cend[256];           // end of coarse region b (ccap[b + 1])
   unsigned long long acc[kMaxWindow][2];  // fired, sent per tick
 };
 
@@ -177,6 +178,9 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
   constexpr uint32_t per_round = kExpandBlock * NPT;
   const uint32_t c3drop = ctr3(K_DROP, w.key.trial), c3crash = ctr3(K_CRASH, w.key.trial);
   if (tid < kMaxWindow * 2) (&sm.acc[0][0])[tid] = 0;
+  static_assert(kExpandBlock == 256, "thread b owns coarse bin b");
+  const unsigned long long cbase = w.ccap[tid], cend = w.ccap[tid + 1];  // bin tid's region
+  sm.cend[tid] = cend;
   const unsigned long long rounds = (Tn + per_round - 1) / per_round;
   // XCD-aware: workgroups are dealt to the 8 XCDs round-robin, so logical
   // workgroup ids are remapped to give each XCD a contiguous run of rounds
@@ -242,11 +246,11 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
       continue;  // the next round's first barrier orders the reuse of sm.cnt
     }
     block_scan256(sm.cnt, sm.off);
-    if (sm.cnt[tid]) {
-      const unsigned long long at = atomicAdd(&w.cfill[tid], (unsigned long long)sm.cnt[tid]);
-      if (at + sm.cnt[tid] > w.ccap[tid + 1] - w.ccap[tid]) atomicOr(w.err, kErrCoarse);
-      sm.gbase[tid] = w.ccap[tid] + at;
-    }
+    // thread b reserves bin b's run; the atomic's return latency overlaps the
+    // LDS scatter below (which needs only off[] from the scan)
+    const uint32_t mycnt = sm.cnt[tid];
+    unsigned long long at = 0;
+    if (mycnt) at = atomicAdd(&w.cfill[tid], (unsigned long long)mycnt);
     __syncthreads();
 #pragma unroll
     for (uint32_t q = 0; q < NPT; ++q)
@@ -257,12 +261,16 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
           sm.sorted[p] = mm[q][j];
           sm.sbin[p] = (uint8_t)bin;
         }
+    if (mycnt) {
+      if (at + mycnt > cend - cbase) atomicOr(w.err, kErrCoarse);
+      sm.gbase[tid] = cbase + at;
+    }
     __syncthreads();
     const uint32_t total = sm.off[256];
     for (uint32_t p = tid; p < total; p += kExpandBlock) {
       const uint32_t b = sm.sbin[p];
       const unsigned long long pos = sm.gbase[b] + (p - sm.off[b]);
-      if (pos < w.ccap[b + 1]) w.cmsg[pos] = sm.sorted[p];
+      if (pos < sm.cend[b]) w.cmsg[pos] = sm.sorted[p];
     }
   }
   if (!WRITE || !add_stats) return;  // an exact redo must not count the window twice
