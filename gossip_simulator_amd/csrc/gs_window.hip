@@ -337,12 +337,13 @@ struct TileSort {
   uint32_t cnt[256];
   uint32_t off[257];
   unsigned long long gbase[256];
+  unsigned long long gend[256];  // end of fine region b (fstart[c*256 + b + 1])
 };
 
 // part2: coarse tiles -> fine regions; message = u_in_fine | k << 14.
 // SCATTER=false counts per fine bucket (exact fallback).
 template <bool SCATTER>
-__global__ __launch_bounds__(kPartBlock) void k_part2(const WinState w) {
+__global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_part2(const WinState w) {
   __shared__ TileSort ts;
   __shared__ uint32_t s_tp[257];
   const uint32_t tid = threadIdx.x;
@@ -363,7 +364,8 @@ __global__ __launch_bounds__(kPartBlock) void k_part2(const WinState w) {
     if (tid < 256) ts.cnt[tid] = 0;
     __syncthreads();
     constexpr uint32_t kPer = kPartTile / kPartBlock;
-    uint32_t m[kPer], rank[kPer];
+    static_assert(kPartTile <= 65536 && kPer % 2 == 0, "two 16-bit ranks per register");
+    uint32_t m[kPer], rank[kPer / 2] = {};
 #pragma unroll
     for (uint32_t r = 0; r < kPer; ++r) {
       const unsigned long long x = base + r * kPartBlock + tid;
@@ -373,7 +375,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part2(const WinState w) {
     }
 #pragma unroll
     for (uint32_t r = 0; r < kPer; ++r)
-      if (m[r] != kEmptyMsg) rank[r] = atomicAdd(&ts.cnt[(m[r] >> kFineLog) & 255], 1u);
+      if (m[r] != kEmptyMsg) rank[r / 2] |= atomicAdd(&ts.cnt[(m[r] >> kFineLog) & 255], 1u) << (16 * (r & 1));
     __syncthreads();
     if (!SCATTER) {
       if (tid < 256 && ts.cnt[tid]) atomicAdd(&w.fhist[c * 256 + tid], (unsigned long long)ts.cnt[tid]);
@@ -381,23 +383,32 @@ __global__ __launch_bounds__(kPartBlock) void k_part2(const WinState w) {
       continue;
     }
     block_scan256(ts.cnt, ts.off);
-    if (tid < 256 && ts.cnt[tid]) {
-      const uint32_t f = c * 256 + tid;
-      const unsigned long long at = atomicAdd(&w.ffill[f], (unsigned long long)ts.cnt[tid]);
-      if (at + ts.cnt[tid] > w.fstart[f + 1] - w.fstart[f]) atomicOr(w.err, kErrFine);
-      ts.gbase[tid] = w.fstart[f] + at;
+    // thread b < 256 reserves fine bucket c*256+b's run; the atomic's return
+    // latency overlaps the LDS scatter (which needs only off[] from the scan)
+    const uint32_t mycnt = tid < 256 ? ts.cnt[tid] : 0u;
+    const uint32_t myf = c * 256 + (tid & 255);
+    unsigned long long at = 0, fb = 0, fe = 0;
+    if (mycnt) {
+      at = atomicAdd(&w.ffill[myf], (unsigned long long)mycnt);
+      fb = w.fstart[myf];
+      fe = w.fstart[myf + 1];
     }
     __syncthreads();
 #pragma unroll
     for (uint32_t r = 0; r < kPer; ++r)
-      if (m[r] != kEmptyMsg) ts.buf[ts.off[(m[r] >> kFineLog) & 255] + rank[r]] = m[r];
+      if (m[r] != kEmptyMsg)
+        ts.buf[ts.off[(m[r] >> kFineLog) & 255] + ((rank[r / 2] >> (16 * (r & 1))) & 0xFFFFu)] = m[r];
+    if (mycnt) {
+      if (at + mycnt > fe - fb) atomicOr(w.err, kErrFine);
+      ts.gbase[tid] = fb + at;
+      ts.gend[tid] = fe;
+    }
     __syncthreads();
     const uint32_t total = ts.off[256];
     for (uint32_t p = tid; p < total; p += kPartBlock) {
       const uint32_t m1 = ts.buf[p], b = (m1 >> kFineLog) & 255;
       const unsigned long long pos = ts.gbase[b] + (p - ts.off[b]);
-      if (pos < w.fstart[c * 256 + b + 1])
-        w.fmsg[pos] = (m1 & (kFineNodes - 1)) | ((m1 >> kCoarseShift) << kFineLog);
+      if (pos < ts.gend[b]) w.fmsg[pos] = (m1 & (kFineNodes - 1)) | ((m1 >> kCoarseShift) << kFineLog);
     }
     __syncthreads();
   }
