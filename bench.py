@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--cpu-n", type=int, default=10_000_000,
                     help="nodes in the bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-c3", action="store_true",
+                    help="skip the C3 concurrent-trials sample (its host threads crash rocprofv3's tracer)")
     ap.add_argument("--no-extensions", action="store_true",
                     help="skip the C5 extension runs (1%% failed mask, push-pull)")
     return ap.parse_args()
@@ -156,7 +158,8 @@ def main():
     sim.close()
     if not a.no_extensions:
         ext.update(pushpull_runs(a, gs, rank, local))
-        ext["c3_trials"] = c3_trials(a, gs, rank, local)
+        if not a.no_c3:
+            ext["c3_trials"] = c3_trials(a, gs, rank, local)
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_n > 0:

@@ -9,6 +9,6 @@ tail -1 $o/tests.log
 timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --cpu-n 0 "$@" > $o/bench.json 2> $o/bench.err || { tail -20 $o/bench.err; exit 1; }
 python3 scripts/showbench.py $o/bench.json
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof -o run -- python3 bench.py --steps 1 --warmup 0 --cpu-n 0 --no-roofline "$@" > $o/prof.log 2>&1 || { tail -20 $o/prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof -o run -- python3 bench.py --steps 1 --warmup 0 --cpu-n 0 --no-roofline --no-extensions "$@" > $o/prof.log 2>&1 || { tail -20 $o/prof.log; exit 1; }
 f=$(find $o/prof -name '*.db' | head -1)
 python3 tools_profsummary.py "$f" 12 > $o/kernel_summary.txt && python3 scripts/perwindow.py "$f" 40 > $o/perwindow.txt && tail -1 $o/perwindow.txt && head -8 $o/kernel_summary.txt

@@ -11,6 +11,6 @@ tail -1 $o/smoke.log
 timeout -k 10 600 python -u bench.py > $o/bench.json 2> $o/bench.err || { tail -20 $o/bench.err; exit 1; }
 cut -c1-400 $o/bench.json
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $o/prof -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-n 0 > $o/prof.log 2>&1 || { tail -20 $o/prof.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $o/prof -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-n 0 --no-c3 > $o/prof.log 2>&1 || { tail -20 $o/prof.log; exit 1; }
 f=$(find $o/prof -name '*.db' | head -1)
 python3 tools_profsummary.py "$f" 20 > $o/kernel_summary.txt && python3 scripts/perwindow.py "$f" 50 > $o/perwindow.txt && cat $o/kernel_summary.txt
