@@ -415,7 +415,7 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8
 }
 
 constexpr uint32_t kResolveMaxBuckets = 256;  // buckets one persistent workgroup may own
-constexpr uint32_t kSmallMax = 64;            // buckets with <= this many receipts: k_resolve_small
+constexpr uint32_t kSmallMax = 256;           // buckets with <= this many receipts: k_resolve_small
 constexpr uint32_t kSmallBlock = 1024;        // k_resolve_small: 16 waves, one bucket each
 
 // Bit-parallel resolve (k_resolve): per tick k of the window, b1 = nodes with
@@ -861,84 +861,113 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
 
 // Small buckets (1..kSmallMax receipts in the window): one wave per bucket.
 // In the sparse windows at the start and end of a broadcast nearly every
-// bucket holds a few dozen receipts, and the bit-parallel k_resolve's fixed
-// cost per bucket (512 bit words x L ticks, a chain of block barriers) is what
-// the window pays.  Here a wave sorts its <= 64 receipts by (node, tick, roll0)
-// in registers (bitonic network over shuffles), the first lane of every node's
-// run replays the receive case (simulator.go:107-123, rule A6) along the run,
-// and infected nodes Broadcast() (:122, :141-142) into the bucket's fire lists.
-// k_resolve skips these buckets; the two launches touch disjoint buckets.
+// bucket holds a few dozen or hundred receipts, and the bit-parallel
+// k_resolve's fixed cost per bucket (512 bit words x L ticks, a chain of block
+// barriers) is what the window pays.  Here a wave holds the bucket's
+// receipts as E keys per lane (element r*64 + lane in register r), sorts them
+// by (node, tick, roll0) with a bitonic network (shuffles across lanes,
+// swaps across registers), and the first element of every node's run replays
+// the receive case (simulator.go:107-123, rule A6) along the run; infected
+// nodes Broadcast() (:122, :141-142) into the bucket's fire lists.
+// Instance E takes buckets with 64*(E/4) < M <= 64*E receipts (E = 1, 4);
+// k_resolve takes the rest.  The launches touch disjoint buckets.
+template <uint32_t E>
 __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w, uint32_t t0, uint32_t L) {
+  constexpr uint32_t N = 64 * E, kWaves = kSmallBlock / 64;
   __shared__ uint32_t st[kMaxWindow][4];  // dead (not counted), recv, crash per tick
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  __shared__ uint32_t sk[kWaves][N];      // each wave's sorted keys
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid < kMaxWindow * 4) (&st[0][0])[tid] = 0;
   __syncthreads();
-  const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * (kSmallBlock / 64) + (tid >> 6));
+  const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
   const unsigned long long M = f < w.nfine ? w.ffill[f] : 0ull;
-  if (M != 0 && M <= kSmallMax) {
+  if (M > (E == 1 ? 0ull : 64ull * (E / 4)) && M <= N) {
     const uint32_t c3crash = ctr3(K_CRASH, w.key.trial), c3delay = ctr3(K_DELAY, w.key.trial);
-    uint32_t key = ~0u;  // loc << 5 | k << 1 | roll0; ~0u sorts last
-    if (lane < M) {
-      const uint32_t m = w.fmsg[w.fstart[f] + lane];
-      key = (msg_loc(m) << 5) | (msg_tick(m) << 1) | ((m >> kRoll0Fine) & 1u);
+    const uint32_t* gm = w.fmsg + w.fstart[f];
+    uint32_t key[E];  // loc << 5 | k << 1 | roll0; ~0u sorts last
+#pragma unroll
+    for (uint32_t r = 0; r < E; ++r) {
+      const uint32_t i = r * 64 + lane;
+      key[r] = ~0u;
+      if (i < M) {
+        const uint32_t m = gm[i];
+        key[r] = (msg_loc(m) << 5) | (msg_tick(m) << 1) | ((m >> kRoll0Fine) & 1u);
+      }
     }
 #pragma unroll
-    for (uint32_t k = 2; k <= 64; k <<= 1)
+    for (uint32_t k = 2; k <= N; k <<= 1)
 #pragma unroll
       for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-        const uint32_t o = __shfl_xor(key, j, 64);
-        const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
-        key = keep_min ? min(key, o) : max(key, o);
+        if (j < 64) {
+#pragma unroll
+          for (uint32_t r = 0; r < E; ++r) {
+            const uint32_t i = r * 64 + lane;
+            const uint32_t o = __shfl_xor(key[r], j, 64);
+            const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+            key[r] = keep_min ? min(key[r], o) : max(key[r], o);
+          }
+        } else {
+          const uint32_t rj = j / 64;
+#pragma unroll
+          for (uint32_t r = 0; r < E; ++r) {
+            if (r & rj) continue;
+            const bool up = ((r * 64 + lane) & k) == 0;
+            const uint32_t a = key[r], b = key[r | rj];
+            key[r] = up ? min(a, b) : max(a, b);
+            key[r | rj] = up ? max(a, b) : min(a, b);
+          }
+        }
       }
-    const uint32_t prev = __shfl_up(key, 1, 64);
-    const uint32_t loc = key >> 5;
-    const bool head = key != ~0u && (lane == 0 || (prev >> 5) != loc);
-    const uint32_t u = (f << kFineLog) + loc, wi = u >> 5, bit = 1u << (u & 31);
+#pragma unroll
+    for (uint32_t r = 0; r < E; ++r) sk[wv][r * 64 + lane] = key[r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     uint32_t* rwg = (uint32_t*)w.recv;
     uint32_t* cwg = (uint32_t*)w.crash;
-    uint32_t rw = 0, cw = 0;
-    if (head) { rw = rwg[wi]; cw = cwg[wi]; }
-    bool rv = (rw & bit) != 0, cr = (cw & bit) != 0, inf = false, act = head;
-    uint32_t ktick = ~0u, ord = 0, tinf = 0;
-    // all lanes step along the runs together (the shuffle needs every lane)
-    for (uint32_t d = 0; d < 64; ++d) {
-      const uint32_t e = __shfl(key, (lane + d) & 63, 64);
-      if (act && (lane + d >= 64 || (e >> 5) != loc)) act = false;  // ~0u never matches a loc
-      if (act) {
+#pragma unroll
+    for (uint32_t r = 0; r < E; ++r) {
+      const uint32_t i = r * 64 + lane;
+      const uint32_t loc = key[r] >> 5;
+      if (key[r] == ~0u || (i > 0 && (sk[wv][i - 1] >> 5) == loc)) continue;  // not a run head
+      const uint32_t u = (f << kFineLog) + loc, wi = u >> 5, bit = 1u << (u & 31);
+      const uint32_t cw = cwg[wi];
+      bool rv = (rwg[wi] & bit) != 0, cr = (cw & bit) != 0, inf = false;
+      uint32_t ktick = ~0u, ord = 0, tinf = 0;
+      for (uint32_t q = i; q < N; ++q) {  // along the run (~0u never matches a loc)
+        const uint32_t e = sk[wv][q];
+        if ((e >> 5) != loc) break;
         const uint32_t k = (e >> 1) & (kMaxWindow - 1), t = t0 + k;
         if (k != ktick) { ktick = k; ord = 0; } else { ++ord; }
         if (cr) {                                                   // :108 not counted
           atomicAdd(&st[k][0], 1u);
-        } else {                                                    // :111 counted
-          bool roll = e & 1u;                                       // :112 ordinal 0 rode along
-          if (ord > 0) {
-            roll = false;
-            if (w.kc > 0)
-              roll = (int32_t)uniform(lane_of(philox(u, t, ord >> 2, c3crash, w.key.k0, w.key.k1), ord & 3),
-                                      100u) < w.kc;
-          }
-          if (roll) {                                               // :113-115
-            cr = true;
-            atomicAdd(&st[k][2], 1u);
-          } else if (!rv) {                                         // :117-121
-            rv = inf = true;
-            tinf = t;
-            atomicAdd(&st[k][1], 1u);
-          }
+          continue;
+        }
+        bool roll = e & 1u;                                         // :111-112, ordinal 0 rode along
+        if (ord > 0) {
+          roll = false;
+          if (w.kc > 0)
+            roll = (int32_t)uniform(lane_of(philox(u, t, ord >> 2, c3crash, w.key.k0, w.key.k1), ord & 3),
+                                    100u) < w.kc;
+        }
+        if (roll) {                                                 // :113-115
+          cr = true;
+          atomicAdd(&st[k][2], 1u);
+        } else if (!rv) {                                           // :117-121
+          rv = inf = true;
+          tinf = t;
+          atomicAdd(&st[k][1], 1u);
         }
       }
-      if (!__any(act)) break;
-    }
-    if (head) {
-      if (inf) atomicOr(&rwg[wi], bit);
       if (cr && !(cw & bit)) atomicOr(&cwg[wi], bit);
-    }
-    if (inf) {  // Broadcast() (:122, :141-142): fire at tinf + off
-      const uint32_t off = fire_offset(w.delay_low, w.delay_span,
-                                       philox(u, tinf, 0, c3delay, w.key.k0, w.key.k1).x);
-      const uint32_t slot = (tinf + off) % w.R;
-      const uint32_t pos = atomicAdd(&w.fcount[(size_t)slot * w.nfine + f], 1u);
-      w.flist[((size_t)slot * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
+      if (inf) {  // Broadcast() (:122, :141-142): fire at tinf + off
+        atomicOr(&rwg[wi], bit);
+        const uint32_t off = fire_offset(w.delay_low, w.delay_span,
+                                         philox(u, tinf, 0, c3delay, w.key.k0, w.key.k1).x);
+        const uint32_t slot = (tinf + off) % w.R;
+        const uint32_t pos = atomicAdd(&w.fcount[(size_t)slot * w.nfine + f], 1u);
+        w.flist[((size_t)slot * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
+      }
     }
   }
   __syncthreads();
@@ -1047,7 +1076,9 @@ hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s
   uint32_t G = std::min<uint32_t>(w.nfine, 2 * cus);
   G = std::max<uint32_t>(G, (w.nfine + kResolveMaxBuckets - 1) / kResolveMaxBuckets);
   const uint32_t gs = (w.nfine + kSmallBlock / 64 - 1) / (kSmallBlock / 64);
-  hipLaunchKernelGGL(k_resolve_small, dim3(gs), dim3(kSmallBlock), 0, s, w, t0, L);
+  hipLaunchKernelGGL(k_resolve_small<1>, dim3(gs), dim3(kSmallBlock), 0, s, w, t0, L);
+  hipLaunchKernelGGL(k_resolve_small<4>, dim3(gs), dim3(kSmallBlock), 0, s, w, t0, L);
+  static_assert(kSmallMax == 64 * 4, "the two instances cover 1..kSmallMax");
   hipLaunchKernelGGL(k_resolve, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
   return hipGetLastError();
 }

@@ -18,7 +18,8 @@ def s(n):
     return m.group(1)
 
 
-seq = [(s(n), (e - b) / 1e3) for n, b, e in rows if s(n) in ("k_expand", "k_part2", "k_resolve", "probe")]
+seq = [(s(n), (e - b) / 1e3) for n, b, e in rows
+       if s(n) in ("k_expand", "k_part2", "k_resolve_small", "k_resolve", "probe")]
 wins, cur = [], {}
 for name, us in seq:
     cur[name] = cur.get(name, 0) + us
@@ -30,7 +31,7 @@ tot = {}
 for i, w in enumerate(wins[-nwin:]):
     extra = f"  probe {w['probe']:8.1f}" if "probe" in w else ""
     print(f"{i:3d} expand {w.get('k_expand', 0):8.1f}  part2 {w.get('k_part2', 0):8.1f}  "
-          f"resolve {w.get('k_resolve', 0):8.1f}{extra}")
+          f"resolve {w.get('k_resolve', 0):8.1f}  small {w.get('k_resolve_small', 0):6.1f}{extra}")
     for k, v in w.items():
         tot[k] = tot.get(k, 0) + v
 print("sum(ms)", {k: round(v / 1e3, 2) for k, v in tot.items()})
