@@ -1,4 +1,4 @@
-"""HBM traffic of the window pipeline from a PMC summary (scripts/pmc.sh ->
+"""HBM traffic of the window pipeline (k_expand, k_part2, k_resolve_small, k_resolve) from a PMC summary (scripts/pmc.sh ->
 summary.csv over ONE broadcast: bench.py --steps 1 --warmup 0).
 
 rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB.  MI355X_MICROARCH.md (HBM
@@ -10,7 +10,7 @@ import csv
 import json
 import sys
 
-KERNELS = ("gs::k_expand", "gs::k_part2", "gs::k_resolve")
+KERNELS = ("gs::k_expand", "gs::k_part2", "gs::k_resolve_small", "gs::k_resolve")
 
 
 def main():
@@ -19,6 +19,8 @@ def main():
            "kernels": {}}
     total = 0.0
     for k in KERNELS:
+        if k not in rows:
+            continue
         r = rows[k]
         fetch = float(r["FETCH_SIZE"]) * 1024 * 2.0
         write = float(r["WRITE_SIZE"]) * 1024
