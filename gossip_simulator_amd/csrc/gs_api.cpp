@@ -40,6 +40,7 @@ struct gs_ctx {
   // push-pull extension (gs_pushpull.hip)
   bool pp = false;
   unsigned long long* d_next = nullptr;  // informed set being built (state block)
+  unsigned long long* d_ppsum = nullptr;  // push-pull word summaries (state block)
   uint32_t* d_flag = nullptr;
   // window engine (gs_window.hip)
   bool win = false;
@@ -348,7 +349,7 @@ int gs_create(const gs_params* params, gs_ctx** out) {
   // `stats` is per-broadcast state that gs_reset clears.
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const bool tick = !c->win && !c->pp;
-  const size_t b_next = c->pp ? al(s.W * 8) : 0;
+  const size_t b_next = c->pp ? al(s.W * 8) + al(2 * pp_summary_words(s.W) * 8) : 0;
   const size_t b_bits = al(s.W * 8), b_ring = tick ? al((size_t)s.R * s.W * 8) : 0,
                b_cflag = tick ? al((size_t)s.R * s.C * 4) : 0,
                b_clist = tick ? al((size_t)s.R * kShards * s.CS * 4) : 0,
@@ -364,7 +365,9 @@ int gs_create(const gs_params* params, gs_ctx** out) {
   char* q = (char*)c->d_state;
   s.recv = (unsigned long long*)q; q += b_bits;
   s.crash = (unsigned long long*)q; q += b_bits;
-  c->d_next = b_next ? (unsigned long long*)q : nullptr; q += b_next;
+  c->d_next = b_next ? (unsigned long long*)q : nullptr;
+  c->d_ppsum = b_next ? (unsigned long long*)(q + al(s.W * 8)) : nullptr;
+  q += b_next;
   s.ring = (unsigned long long*)q; q += b_ring;
   s.cflag = (uint32_t*)q; q += b_cflag;
   s.clist = (uint32_t*)q; q += b_clist;
@@ -758,7 +761,7 @@ int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
       const uint32_t tt = (uint32_t)(t0 + i);
       hipEvent_t* e = timing ? &c->ev[(size_t)i * 2] : nullptr;
       if (e) CK(c, hipEventRecord(e[0], c->stream));
-      CK(c, pp_round(c->st, c->d_next, tt, c->stream));
+      CK(c, pp_round(c->st, c->d_next, c->d_ppsum, tt, c->stream));
       if (e) CK(c, hipEventRecord(e[1], c->stream));
       CK(c, pp_commit(c->st, c->d_next, tt, c->stream));
     }

@@ -17,6 +17,12 @@
 // recv = next and counts the newly informed.  Per round at N = 1e9: the
 // friends table is streamed once (a wave's 64 rows are contiguous), the
 // 125-MB recv bitset is gathered once per call (Infinity-Cache resident).
+// Word summaries (k_pp_summary, one bit per 64-node word, 2 MB each, L2
+// resident) skip that gather where its answer is known: a pull from a word
+// with no informed node fails, and a push into a word with no live
+// uninformed node changes nothing (without a failed mask).  The early rounds,
+// where almost every call is a pull from an uninformed word, then cost the
+// table stream only.
 #include <algorithm>
 
 #include "gs_internal.h"
@@ -50,8 +56,25 @@ __device__ __forceinline__ void block_add(uint64_t* sh, const uint64_t (&v)[3], 
   }
 }
 
+// sumA bit w = recv word w has an informed node; sumB bit w = it has a node
+// that is neither informed nor failed (bits past n count as such: the
+// summary only ever skips work whose outcome it proves).
+__global__ __launch_bounds__(kPPBlock) void k_pp_summary(const DevState s, unsigned long long* __restrict__ sumA,
+                                                         unsigned long long* __restrict__ sumB) {
+  const uint64_t Wr = (s.W + 63) & ~63ull;  // whole waves stay in the loop together
+  for (uint64_t w = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; w < Wr;
+       w += (uint64_t)gridDim.x * kPPBlock) {
+    unsigned long long r = 0, f = ~0ull;
+    if (w < s.W) { r = s.recv[w]; f = s.crash[w]; }
+    const unsigned long long a = __ballot(r != 0), b = __ballot(w < s.W && (r | f) != ~0ull);
+    if ((threadIdx.x & 63) == 0) { sumA[w >> 6] = a; sumB[w >> 6] = b; }
+  }
+}
+
 __global__ __launch_bounds__(kPPBlock) void k_pp_round(const DevState s,
                                                        unsigned long long* __restrict__ next,
+                                                       const unsigned long long* __restrict__ sumA,
+                                                       const unsigned long long* __restrict__ sumB,
                                                        uint32_t t) {
   __shared__ uint64_t sh[3 * (kPPBlock / 64)];
   const uint32_t lane = threadIdx.x & 63;
@@ -71,17 +94,22 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_round(const DevState s,
       const bool kept = (int32_t)uniform(r.y, 100u) >= s.kd;
       const unsigned long long ubit = 1ull << (u & 63);
       ++fired;
+      const uint32_t sb = (u >> 6) & 63;  // u's word's bit in the summaries
       if ((Iw >> lane) & 1) {  // push
         if (kept) {
           ++sent;
-          // the failed-mask gather only when a mask was set (gs_set_failed)
-          const unsigned long long Iu = s.recv[u >> 6];
-          if (!s.check_crashed || !(s.crash[u >> 6] & ubit)) {
-            ++msgs;
-            if (!(Iu & ubit)) atomicOr(&next[u >> 6], ubit);
+          if (!s.check_crashed && !((sumB[u >> 12] >> sb) & 1)) {
+            ++msgs;  // u is informed: delivered, nothing to set
+          } else {
+            // the failed-mask gather only when a mask was set (gs_set_failed)
+            const unsigned long long Iu = s.recv[u >> 6];
+            if (!s.check_crashed || !(s.crash[u >> 6] & ubit)) {
+              ++msgs;
+              if (!(Iu & ubit)) atomicOr(&next[u >> 6], ubit);
+            }
           }
         }
-      } else if (s.recv[u >> 6] & ubit) {  // pull (u informed => u live)
+      } else if (((sumA[u >> 12] >> sb) & 1) && (s.recv[u >> 6] & ubit)) {  // pull (u informed => u live)
         if (kept) {
           ++sent;
           ++msgs;
@@ -127,10 +155,15 @@ __global__ void k_pp_seed(const DevState s, unsigned long long* next, uint32_t n
 
 }  // namespace
 
-hipError_t pp_round(const DevState& s, unsigned long long* next, uint32_t t, hipStream_t st) {
+hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long long* sum, uint32_t t,
+                    hipStream_t st) {
+  unsigned long long* sumA = sum;
+  unsigned long long* sumB = sum + pp_summary_words(s.W);
+  const uint32_t sblocks = (uint32_t)std::min<uint64_t>((s.W + kPPBlock - 1) / kPPBlock, 4096);
+  hipLaunchKernelGGL(k_pp_summary, dim3(sblocks), dim3(kPPBlock), 0, st, s, sumA, sumB);
   const uint64_t waves = (s.n + 63) / 64;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((waves + 3) / 4, 8192);
-  hipLaunchKernelGGL(k_pp_round, dim3(blocks), dim3(kPPBlock), 0, st, s, next, t);
+  hipLaunchKernelGGL(k_pp_round, dim3(blocks), dim3(kPPBlock), 0, st, s, next, sumA, sumB, t);
   return hipGetLastError();
 }
 

@@ -6,7 +6,7 @@ set -u
 out=${1:-gpurun_out/pmc}; shift || true
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-args="--steps 1 --warmup 0 --no-roofline --cpu-n 0 $*"
+args="--steps 1 --warmup 0 --no-roofline --no-extensions --cpu-n 0 $*"  # no extensions: the C3 host threads crash the profiler
 i=0
 for grp in \
   "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_BUSY_CYCLES" \
