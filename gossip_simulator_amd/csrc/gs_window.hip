@@ -144,6 +144,12 @@ __device__ __forceinline__ void block_scan256(uint32_t* cnt, uint32_t* off) {
   }
 }
 
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
+#pragma unroll
+  for (uint32_t o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 // Friends row of v into registers; slots past the list hold kEmptyMsg (rows
 // are sealed by k_seal_rows, so the length byte is not read).
 template <uint32_t MAXS>
@@ -187,6 +193,11 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
   // (one bucket's fire lists share friends-row lines in that XCD's L2)
   const uint32_t B = gridDim.x;
   const uint32_t lb = (B & 7) == 0 ? (blockIdx.x & 7) * (B >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  // per-tick fired | sent << 16 of this thread's nodes (<= 1024 nodes per
+  // thread per launch): registers, not same-address LDS atomics per node
+  uint32_t accp[kBitTicks];
+#pragma unroll
+  for (uint32_t kx = 0; kx < kBitTicks; ++kx) accp[kx] = 0;
   for (unsigned long long rd = lb; rd < rounds; rd += B) {
     sm.cnt[tid] = 0;
     __syncthreads();
@@ -237,8 +248,9 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
           }
         }
       }
-      atomicAdd(&sm.acc[k][0], 1ull);
-      if (sent) atomicAdd(&sm.acc[k][1], (unsigned long long)sent);
+#pragma unroll
+      for (uint32_t kx = 0; kx < kBitTicks; ++kx)
+        if (kx == k) accp[kx] += 1u | (sent << 16);
     }
     __syncthreads();
     if (!WRITE) {
@@ -274,6 +286,15 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
     }
   }
   if (!WRITE || !add_stats) return;  // an exact redo must not count the window twice
+#pragma unroll
+  for (uint32_t kx = 0; kx < kBitTicks; ++kx) {
+    if (kx >= L) continue;
+    const uint32_t fired = wave_sum32(accp[kx] & 0xFFFFu), sent = wave_sum32(accp[kx] >> 16);
+    if ((tid & 63) == 0) {
+      if (fired) atomicAdd(&sm.acc[kx][0], (unsigned long long)fired);
+      if (sent) atomicAdd(&sm.acc[kx][1], (unsigned long long)sent);
+    }
+  }
   __syncthreads();
   if (tid < L * 2) {
     const uint32_t k = tid >> 1, fld = tid & 1;
