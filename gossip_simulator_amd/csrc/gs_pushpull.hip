@@ -71,6 +71,13 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_summary(const DevState s, unsig
   }
 }
 
+// Each wave owns kPPU consecutive bitset words per pass and issues the loads
+// of all of them phase by phase (state words + deg, then the friend id, then
+// the peer word's summary, then the peer-word gathers), so kPPU independent
+// dependency chains are in flight per wave: one word per pass left the launch
+// bound by the chain's latency (8.8 ms per round with no gathers at all).
+constexpr uint32_t kPPU = 4;
+
 __global__ __launch_bounds__(kPPBlock) void k_pp_round(const DevState s,
                                                        unsigned long long* __restrict__ next,
                                                        const unsigned long long* __restrict__ sumA,
@@ -79,46 +86,72 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_round(const DevState s,
   __shared__ uint64_t sh[3 * (kPPBlock / 64)];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t c3 = ctr3(K_PUSHPULL, s.key.trial);
+  const bool cc = s.check_crashed;
   uint64_t fired = 0, sent = 0, msgs = 0;
-  const uint64_t step = (uint64_t)gridDim.x * kPPBlock;
-  for (uint64_t base = (uint64_t)blockIdx.x * kPPBlock + (threadIdx.x & ~63u); base < s.n; base += step) {
-    const uint64_t word = base >> 6;  // this wave's word (wave-uniform)
-    const uint64_t v = base + lane;
-    const unsigned long long Iw = s.recv[word], Fw = s.crash[word];
-    const bool live = v < s.n && !((Fw >> lane) & 1);
-    const uint32_t d = live ? s.deg[v] : 0u;
-    bool pulled = false;
-    if (d > 0) {
-      const u32x4 r = philox((uint32_t)v, t, 0, c3, s.key.k0, s.key.k1);
-      const uint32_t u = s.ids[v * s.stride + uniform(r.x, d)];
-      const bool kept = (int32_t)uniform(r.y, 100u) >= s.kd;
-      const unsigned long long ubit = 1ull << (u & 63);
-      ++fired;
-      const uint32_t sb = (u >> 6) & 63;  // u's word's bit in the summaries
-      if ((Iw >> lane) & 1) {  // push
-        if (kept) {
+  const uint64_t W = (s.n + 63) >> 6;
+  const uint64_t wid = (uint64_t)blockIdx.x * (kPPBlock / 64) + (threadIdx.x >> 6);
+  const uint64_t step = (uint64_t)gridDim.x * (kPPBlock / 64) * kPPU;
+  for (uint64_t w0 = wid * kPPU; w0 < W; w0 += step) {  // wave-uniform
+    unsigned long long Iw[kPPU], Fw[kPPU];
+    uint32_t d[kPPU], u[kPPU];
+    bool push[kPPU], kept[kPPU], sbit[kPPU];
+#pragma unroll
+    for (uint32_t i = 0; i < kPPU; ++i) {
+      const uint64_t word = w0 + i, v = (word << 6) + lane;
+      const bool inb = word < W;
+      Iw[i] = inb ? s.recv[word] : 0ull;
+      Fw[i] = inb ? s.crash[word] : ~0ull;
+      d[i] = v < s.n ? s.deg[v] : 0u;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kPPU; ++i) {
+      const uint64_t v = ((w0 + i) << 6) + lane;
+      if ((Fw[i] >> lane) & 1) d[i] = 0;  // failed (or past the table): never calls
+      push[i] = (Iw[i] >> lane) & 1;
+      u[i] = 0;
+      kept[i] = false;
+      if (d[i] > 0) {
+        const u32x4 r = philox((uint32_t)v, t, 0, c3, s.key.k0, s.key.k1);
+        u[i] = s.ids[v * s.stride + uniform(r.x, d[i])];
+        kept[i] = (int32_t)uniform(r.y, 100u) >= s.kd;
+      }
+    }
+    // summaries (L2 resident): push -> u's word has a live uninformed node;
+    // pull -> u's word has an informed node.  A dropped call needs neither.
+#pragma unroll
+    for (uint32_t i = 0; i < kPPU; ++i) {
+      sbit[i] = false;
+      if (kept[i]) sbit[i] = ((push[i] ? sumB : sumA)[u[i] >> 12] >> ((u[i] >> 6) & 63)) & 1;
+    }
+    unsigned long long Iu[kPPU], Cu[kPPU];
+#pragma unroll
+    for (uint32_t i = 0; i < kPPU; ++i) {
+      Iu[i] = sbit[i] ? s.recv[u[i] >> 6] : 0ull;
+      // the failed-mask gather only when a mask was set (gs_set_failed)
+      Cu[i] = (cc && kept[i] && push[i]) ? s.crash[u[i] >> 6] : 0ull;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kPPU; ++i) {
+      const unsigned long long ubit = 1ull << (u[i] & 63);
+      bool pulled = false;
+      if (d[i] > 0) ++fired;
+      if (kept[i]) {
+        if (push[i]) {
           ++sent;
-          if (!s.check_crashed && !((sumB[u >> 12] >> sb) & 1)) {
-            ++msgs;  // u is informed: delivered, nothing to set
-          } else {
-            // the failed-mask gather only when a mask was set (gs_set_failed)
-            const unsigned long long Iu = s.recv[u >> 6];
-            if (!s.check_crashed || !(s.crash[u >> 6] & ubit)) {
-              ++msgs;
-              if (!(Iu & ubit)) atomicOr(&next[u >> 6], ubit);
-            }
+          if (!(Cu[i] & ubit)) {  // u live: delivered
+            ++msgs;
+            // sbit clear: every live node of u's word is informed already
+            if (sbit[i] && !(Iu[i] & ubit)) atomicOr(&next[u[i] >> 6], ubit);
           }
-        }
-      } else if (((sumA[u >> 12] >> sb) & 1) && (s.recv[u >> 6] & ubit)) {  // pull (u informed => u live)
-        if (kept) {
+        } else if (Iu[i] & ubit) {  // pull from an informed u (u informed => u live)
           ++sent;
           ++msgs;
           pulled = true;
         }
       }
+      const unsigned long long bal = __ballot(pulled);
+      if (lane == 0 && bal) atomicOr(&next[w0 + i], bal);
     }
-    const unsigned long long bal = __ballot(pulled);
-    if (lane == 0 && bal) atomicOr(&next[word], bal);
   }
   const uint64_t v3[3] = {fired, sent, msgs};
   const uint32_t f3[3] = {ST_FIRED, ST_SENT, ST_MSGS};
@@ -161,8 +194,8 @@ hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long l
   unsigned long long* sumB = sum + pp_summary_words(s.W);
   const uint32_t sblocks = (uint32_t)std::min<uint64_t>((s.W + kPPBlock - 1) / kPPBlock, 4096);
   hipLaunchKernelGGL(k_pp_summary, dim3(sblocks), dim3(kPPBlock), 0, st, s, sumA, sumB);
-  const uint64_t waves = (s.n + 63) / 64;
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((waves + 3) / 4, 8192);
+  const uint64_t groups = (s.W + kPPU - 1) / kPPU;  // one wave per kPPU words
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((groups + 3) / 4, 8192);
   hipLaunchKernelGGL(k_pp_round, dim3(blocks), dim3(kPPBlock), 0, st, s, next, sumA, sumB, t);
   return hipGetLastError();
 }
