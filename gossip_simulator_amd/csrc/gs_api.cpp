@@ -349,7 +349,7 @@ int gs_create(const gs_params* params, gs_ctx** out) {
   // `stats` is per-broadcast state that gs_reset clears.
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const bool tick = !c->win && !c->pp;
-  const size_t b_next = c->pp ? al(s.W * 8) + al(2 * pp_summary_words(s.W) * 8) : 0;
+  const size_t b_next = c->pp ? al(s.W * 8) + al(pp_summary_total_words(s.W) * 8) : 0;
   const size_t b_bits = al(s.W * 8), b_ring = tick ? al((size_t)s.R * s.W * 8) : 0,
                b_cflag = tick ? al((size_t)s.R * s.C * 4) : 0,
                b_clist = tick ? al((size_t)s.R * kShards * s.CS * 4) : 0,

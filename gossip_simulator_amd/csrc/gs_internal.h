@@ -141,8 +141,12 @@ hipError_t win_schedule_one(const WinState& w, uint32_t node, uint32_t tick, hip
 
 // Push-pull extension (gs_pushpull.hip): one round per tick; `next` is the
 // informed set being built (equal to recv at the start of every round).
-// sum = 2 * pp_summary_words(W) words: the round's word summaries (rebuilt by pp_round).
+// sum = pp_summary_total_words(W) words: the round's word summaries, one bit
+// per 64-node word (A: any informed, B: any live uninformed) and a second
+// level with one bit per summary word (rebuilt by pp_round).
 inline uint64_t pp_summary_words(uint64_t W) { return (W + 63) / 64; }
+inline uint64_t pp_summary2_words(uint64_t W) { return (pp_summary_words(W) + 63) / 64; }
+inline uint64_t pp_summary_total_words(uint64_t W) { return 2 * pp_summary_words(W) + 2 * pp_summary2_words(W); }
 hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long long* sum, uint32_t t,
                     hipStream_t st);
 hipError_t pp_commit(const DevState& s, const unsigned long long* next, uint32_t t, hipStream_t st);

@@ -39,19 +39,20 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 }
 
 // Per-block sums of up to 3 counters into stats[slot][f0..], one atomic each.
+template <uint32_t B = kPPBlock>
 __device__ __forceinline__ void block_add(uint64_t* sh, const uint64_t (&v)[3], uint32_t nf,
                                           unsigned long long* row, const uint32_t (&fld)[3]) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid < 3 * (kPPBlock / 64)) sh[tid] = 0;
+  if (tid < 3 * (B / 64)) sh[tid] = 0;
   __syncthreads();
   for (uint32_t i = 0; i < nf; ++i) {
     const uint64_t s = wave_sum64(v[i]);
-    if (lane == 0) sh[i * (kPPBlock / 64) + wv] = s;
+    if (lane == 0) sh[i * (B / 64) + wv] = s;
   }
   __syncthreads();
   if (tid < nf) {
     uint64_t s = 0;
-    for (uint32_t k = 0; k < kPPBlock / 64; ++k) s += sh[tid * (kPPBlock / 64) + k];
+    for (uint32_t k = 0; k < B / 64; ++k) s += sh[tid * (B / 64) + k];
     if (s) atomicAdd(&row[fld[tid]], (unsigned long long)s);
   }
 }
@@ -78,19 +79,41 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_summary(const DevState s, unsig
 // bound by the chain's latency (8.8 ms per round with no gathers at all).
 constexpr uint32_t kPPU = 4;
 
-__global__ __launch_bounds__(kPPBlock) void k_pp_round(const DevState s,
-                                                       unsigned long long* __restrict__ next,
-                                                       const unsigned long long* __restrict__ sumA,
-                                                       const unsigned long long* __restrict__ sumB,
-                                                       uint32_t t) {
-  __shared__ uint64_t sh[3 * (kPPBlock / 64)];
+// Second level: bit j of sumA2/sumB2 = summary word j of sumA/sumB is non-zero.
+__global__ __launch_bounds__(kPPBlock) void k_pp_summary2(const unsigned long long* __restrict__ sum1, uint64_t S1,
+                                                          unsigned long long* __restrict__ sum2, uint64_t S2) {
+  const uint64_t Sr = (S1 + 63) & ~63ull;
+  for (uint64_t j = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; j < Sr; j += (uint64_t)gridDim.x * kPPBlock) {
+    const bool in = j < S1;
+    const unsigned long long a = __ballot(in && sum1[j] != 0), b = __ballot(in && sum1[S1 + j] != 0);
+    if ((threadIdx.x & 63) == 0) { sum2[j >> 6] = a; sum2[S2 + (j >> 6)] = b; }
+  }
+}
+
+// The second-level summaries (2 x S2 words, 61 KB at N = 1e9) are staged in
+// LDS when they fit (S2 > 0): a call whose peer's 4096-node block has no
+// informed node (pull) or no live uninformed node (push) then skips the L2
+// summary load too.  Persistent 1024-thread blocks, two per CU.
+constexpr uint32_t kPPRoundBlock = 1024;
+constexpr uint64_t kPPMaxS2 = 4000;  // 2 x 31.25 KB of dynamic LDS (under the 64 KB default)
+
+__global__ __launch_bounds__(kPPRoundBlock) void k_pp_round(const DevState s,
+                                                            unsigned long long* __restrict__ next,
+                                                            const unsigned long long* __restrict__ sumA,
+                                                            const unsigned long long* __restrict__ sumB,
+                                                            const unsigned long long* __restrict__ sum2,
+                                                            uint32_t S2, uint32_t t) {
+  __shared__ uint64_t sh[3 * (kPPRoundBlock / 64)];
+  extern __shared__ unsigned long long l2sum[];  // [0,S2) A2, [S2,2*S2) B2
+  for (uint32_t j = threadIdx.x; j < 2 * S2; j += kPPRoundBlock) l2sum[j] = sum2[j];
+  __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t c3 = ctr3(K_PUSHPULL, s.key.trial);
   const bool cc = s.check_crashed;
   uint64_t fired = 0, sent = 0, msgs = 0;
   const uint64_t W = (s.n + 63) >> 6;
-  const uint64_t wid = (uint64_t)blockIdx.x * (kPPBlock / 64) + (threadIdx.x >> 6);
-  const uint64_t step = (uint64_t)gridDim.x * (kPPBlock / 64) * kPPU;
+  const uint64_t wid = (uint64_t)blockIdx.x * (kPPRoundBlock / 64) + (threadIdx.x >> 6);
+  const uint64_t step = (uint64_t)gridDim.x * (kPPRoundBlock / 64) * kPPU;
   for (uint64_t w0 = wid * kPPU; w0 < W; w0 += step) {  // wave-uniform
     unsigned long long Iw[kPPU], Fw[kPPU];
     uint32_t d[kPPU], u[kPPU];
@@ -121,7 +144,10 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_round(const DevState s,
 #pragma unroll
     for (uint32_t i = 0; i < kPPU; ++i) {
       sbit[i] = false;
-      if (kept[i]) sbit[i] = ((push[i] ? sumB : sumA)[u[i] >> 12] >> ((u[i] >> 6) & 63)) & 1;
+      if (kept[i]) {
+        const bool top = S2 == 0 || ((l2sum[(push[i] ? S2 : 0u) + (u[i] >> 18)] >> ((u[i] >> 12) & 63)) & 1);
+        if (top) sbit[i] = ((push[i] ? sumB : sumA)[u[i] >> 12] >> ((u[i] >> 6) & 63)) & 1;
+      }
     }
     unsigned long long Iu[kPPU], Cu[kPPU];
 #pragma unroll
@@ -155,7 +181,7 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_round(const DevState s,
   }
   const uint64_t v3[3] = {fired, sent, msgs};
   const uint32_t f3[3] = {ST_FIRED, ST_SENT, ST_MSGS};
-  block_add(sh, v3, 3, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
+  block_add<kPPRoundBlock>(sh, v3, 3, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
 }
 
 __global__ __launch_bounds__(kPPBlock) void k_pp_commit(const DevState s,
@@ -194,9 +220,16 @@ hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long l
   unsigned long long* sumB = sum + pp_summary_words(s.W);
   const uint32_t sblocks = (uint32_t)std::min<uint64_t>((s.W + kPPBlock - 1) / kPPBlock, 4096);
   hipLaunchKernelGGL(k_pp_summary, dim3(sblocks), dim3(kPPBlock), 0, st, s, sumA, sumB);
+  const uint64_t S1 = pp_summary_words(s.W), S2 = pp_summary2_words(s.W);
+  unsigned long long* sum2 = sum + 2 * S1;
+  const uint32_t s2blocks = (uint32_t)std::min<uint64_t>((S1 + kPPBlock - 1) / kPPBlock, 1024);
+  hipLaunchKernelGGL(k_pp_summary2, dim3(s2blocks), dim3(kPPBlock), 0, st, sum, S1, sum2, S2);
+  const uint32_t S2l = S2 <= kPPMaxS2 ? (uint32_t)S2 : 0u;  // 0: no LDS stage, every call checks L2
   const uint64_t groups = (s.W + kPPU - 1) / kPPU;  // one wave per kPPU words
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((groups + 3) / 4, 8192);
-  hipLaunchKernelGGL(k_pp_round, dim3(blocks), dim3(kPPBlock), 0, st, s, next, sumA, sumB, t);
+  const uint32_t blocks =
+      (uint32_t)std::min<uint64_t>((groups + kPPRoundBlock / 64 - 1) / (kPPRoundBlock / 64), 512);
+  hipLaunchKernelGGL(k_pp_round, dim3(blocks), dim3(kPPRoundBlock), (size_t)2 * S2l * 8, st, s, next, sumA,
+                     sumB, sum2, S2l, t);
   return hipGetLastError();
 }
 
