@@ -77,7 +77,7 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_summary(const DevState s, unsig
 // the peer word's summary, then the peer-word gathers), so kPPU independent
 // dependency chains are in flight per wave: one word per pass left the launch
 // bound by the chain's latency (8.8 ms per round with no gathers at all).
-constexpr uint32_t kPPU = 4;
+constexpr uint32_t kPPU = 8;
 
 // Second level: bit j of sumA2/sumB2 = summary word j of sumA/sumB is non-zero.
 __global__ __launch_bounds__(kPPBlock) void k_pp_summary2(const unsigned long long* __restrict__ sum1, uint64_t S1,
