@@ -20,9 +20,10 @@
 // Word summaries (k_pp_summary, one bit per 64-node word, 2 MB each, L2
 // resident) skip that gather where its answer is known: a pull from a word
 // with no informed node fails, and a push into a word with no live
-// uninformed node changes nothing (without a failed mask).  The early rounds,
-// where almost every call is a pull from an uninformed word, then cost the
-// table stream only.
+// uninformed node changes nothing (without a failed mask).  A second level
+// (k_pp_summary2, one bit per 4096-node block, 61 KB at N = 1e9) sits in LDS
+// in front of them, so the early and late rounds, where almost every call is
+// decided by the summaries, cost the table stream only.
 #include <algorithm>
 
 #include "gs_internal.h"
