@@ -25,6 +25,7 @@
 // in front of them, so the early and late rounds, where almost every call is
 // decided by the summaries, cost the table stream only.
 #include <algorithm>
+#include <cstdlib>
 
 #include "gs_internal.h"
 
@@ -225,7 +226,10 @@ hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long l
   unsigned long long* sum2 = sum + 2 * S1;
   const uint32_t s2blocks = (uint32_t)std::min<uint64_t>((S1 + kPPBlock - 1) / kPPBlock, 1024);
   hipLaunchKernelGGL(k_pp_summary2, dim3(s2blocks), dim3(kPPBlock), 0, st, sum, S1, sum2, S2);
-  const uint32_t S2l = S2 <= kPPMaxS2 ? (uint32_t)S2 : 0u;  // 0: no LDS stage, every call checks L2
+  // 0: no LDS stage, every call checks L2 (N > ~1.02e9; GS_PP_L2_ONLY=1 forces
+  // it so the parity tests cover that path at small N)
+  const bool l2_only = S2 > kPPMaxS2 || getenv("GS_PP_L2_ONLY") != nullptr;
+  const uint32_t S2l = l2_only ? 0u : (uint32_t)S2;
   const uint64_t groups = (s.W + kPPU - 1) / kPPU;  // one wave per kPPU words
   const uint32_t blocks =
       (uint32_t)std::min<uint64_t>((groups + kPPRoundBlock / 64 - 1) / (kPPRoundBlock / 64), 512);

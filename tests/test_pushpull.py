@@ -159,6 +159,15 @@ def test_gpu_pushpull_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac):
 
 
 @pytest.mark.gpu
+def test_gpu_pushpull_bit_exact_l2_only(oracle, monkeypatch):
+    """The round kernel without its LDS summary level (the N > ~1.02e9 path),
+    forced by GS_PP_L2_ONLY: bit-exact to the oracle like the default path."""
+    monkeypatch.setenv("GS_PP_L2_ONLY", "1")
+    test_gpu_pushpull_bit_exact(oracle, dict(PP, n=65536 + 77, drop_rate=0.29, trial=5), 19, 18, 19, 0.03)
+    test_gpu_pushpull_bit_exact(oracle, dict(PP, n=20000), 6, 5, 6, 0.0)
+
+
+@pytest.mark.gpu
 def test_gpu_pushpull_c5_shape_1e6(oracle):
     """N = 1e6 over the GPU-built overlay (fanout 5, fanin 6), 0.5 % failed nodes:
     bit-exact to the oracle at every round until 99 % coverage."""
