@@ -16,7 +16,9 @@ GS_OK, GS_EINVAL, GS_ELIVELOCK, GS_EREJECT, GS_ENOMEM, GS_EDEVICE, GS_EOVERFLOW 
     0, -1, -2, -3, -4, -5, -6)
 GS_FLAG_TIMING = 1
 GS_FLAG_TICK_ENGINE = 2
-GS_RUN_COVERED, GS_RUN_QUIESCENT, GS_RUN_MAX_TICKS = 0, 1, 2
+GS_FLAG_PP_L2_ONLY = 4
+GS_RUN_COVERED, GS_RUN_QUIESCENT, GS_RUN_MAX_TICKS, GS_RUN_RUNNING = 0, 1, 2, -1
+GS_COMM_ID_BYTES = 128
 
 # Every symbol include/gossip.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -25,7 +27,8 @@ EXPORTS = (
     "gs_set_failed", "gs_broadcast_begin", "gs_step", "gs_run", "gs_totals",
     "gs_read_received", "gs_read_crashed", "gs_timing_get", "gs_format_float32",
     "gs_format_float64", "gs_format_duration", "gs_threshold", "gs_philox",
-    "gs_set_flags", "gs_reset", "gs_set_stream", "gs_frontier_export", "gs_frontier_import",
+    "gs_set_flags", "gs_reset", "gs_set_stream", "gs_create_multi", "gs_comm_unique_id",
+    "gs_create_rank", "gs_shard_info", "gs_trial_results",
 )
 
 
@@ -49,15 +52,21 @@ class Params(C.Structure):
         ("device", C.c_int32),
         ("flags", C.c_uint32),
         ("model", C.c_uint32),  # GS_MODEL_FLOOD = 0 (reference), GS_MODEL_PUSHPULL = 1
-        ("node_lo", C.c_uint64),
-        ("node_hi", C.c_uint64),
-        ("reserved_", C.c_uint64 * 4),
+        ("trials", C.c_uint32),  # batched independent trials (config C3); 0/1 = one
+        ("reserved0_", C.c_uint32),
+        ("reserved_", C.c_uint64 * 5),
     ]
 
 
 class TickStats(C.Structure):
     _fields_ = [(f, C.c_uint64) for f in
                 ("tick", "fired", "sent", "messages", "received", "crashed", "pending")]
+
+
+class TrialStats(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in
+                ("trial", "tick_99", "tick", "fired", "sent", "messages", "received", "crashed")] + \
+        [("status", C.c_int32), ("reserved_", C.c_int32)]
 
 
 class Window(C.Structure):
@@ -110,8 +119,11 @@ def load():
         "gs_set_flags": ([ctx, C.c_uint32], C.c_int),
         "gs_reset": ([ctx], C.c_int),
         "gs_set_stream": ([ctx, vp], C.c_int),
-        "gs_frontier_export": ([ctx, C.c_uint64, vp, C.c_uint64, C.c_uint64], C.c_int),
-        "gs_frontier_import": ([ctx, C.c_uint64, vp], C.c_int),
+        "gs_create_multi": ([P(Params), P(C.c_int), C.c_int, P(vp)], C.c_int),
+        "gs_comm_unique_id": ([C.c_char_p], C.c_int),
+        "gs_create_rank": ([P(Params), C.c_int, C.c_int, C.c_int, C.c_char_p, P(vp)], C.c_int),
+        "gs_shard_info": ([ctx, C.c_uint32, P(C.c_uint32), P(C.c_uint64), P(C.c_uint64)], C.c_int),
+        "gs_trial_results": ([ctx, P(TrialStats), sz, P(sz)], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -187,6 +187,8 @@ int main(int argc, char** argv) {
       {"seed", "uint", "Philox key for every random decision", "1", false, "1"},
       {"trial", "uint", "Philox trial index", "0", false, "0"},
       {"device", "int", "HIP device ordinal", "0", false, "0"},
+      {"gpus", "int", "node-range shards over devices device .. device+gpus-1 (one process)", "1", false,
+       "1"},
       {"peers", "string", "injected peer-table file (skips overlay construction)", "", false, ""},
       {"model", "string", "dissemination model: flood (the reference) or pushpull (extension)",
        "flood", false, "flood"},
@@ -230,7 +232,15 @@ int main(int argc, char** argv) {
     return 2;
   }
   gs_ctx* c = nullptr;
-  int rc = gs_create(&p, &c);
+  int rc;
+  const int64_t gpus = ival("gpus");
+  if (gpus > 1) {
+    std::vector<int> devs;
+    for (int64_t i = 0; i < gpus; ++i) devs.push_back((int)(p.device + i));
+    rc = gs_create_multi(&p, devs.data(), (int)gpus, &c);
+  } else {
+    rc = gs_create(&p, &c);
+  }
   if (rc) return die(nullptr, rc, "gs_create");
 
   printf("\n=== Constructing Overlay ===\n");                   // :219
@@ -262,20 +272,21 @@ int main(int argc, char** argv) {
   const auto b0 = std::chrono::steady_clock::now();
   rc = gs_broadcast_begin(c, -1);                               // :239-241
   if (rc) return die(c, rc, "gs_broadcast_begin");
-  gs_tick_stats tot{};
-  int status = GS_RUN_MAX_TICKS;
-  for (;;) {                                                    // :243-251
-    rc = gs_step(c, 10, nullptr);
-    if (rc) return die(c, rc, "gs_step");
-    gs_totals(c, &tot);
-    const float percent = (float)tot.received / (float)p.n;
+  // gs_run is the poll loop (:243-251) with the engine's stop rule: one row
+  // per 10-ms poll, printed in the reference's format
+  std::vector<gs_tick_stats> polls((size_t)std::min<uint64_t>(max_ticks / 10 + 2, 1u << 20));
+  size_t npoll = 0;
+  int32_t status = GS_RUN_MAX_TICKS;
+  rc = gs_run(c, 10, max_ticks, polls.data(), polls.size(), &npoll, &status);
+  if (rc) return die(c, rc, "gs_run");
+  for (size_t i = 0; i < npoll && i < polls.size(); ++i) {
+    const float percent = (float)polls[i].received / (float)p.n;
     char pb[64];
     gs_format_float32(percent * 100.0f, pb, sizeof(pb));
-    printf("%s%% covered, took %s\n", pb, dur_ms(tot.tick).c_str());
-    if (percent >= 0.99f) { status = GS_RUN_COVERED; break; }
-    if (tot.pending == 0) { status = GS_RUN_QUIESCENT; break; }
-    if (tot.tick >= max_ticks) break;
+    printf("%s%% covered, took %s\n", pb, dur_ms(polls[i].tick).c_str());
   }
+  gs_tick_stats tot{};
+  gs_totals(c, &tot);
   const double bc_wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - b0).count();
   if (status != GS_RUN_COVERED) {
     fflush(stdout);

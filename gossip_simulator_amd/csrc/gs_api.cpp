@@ -1,8 +1,14 @@
 // gs_api.cpp -- the C ABI of libgossip_hip.so (include/gossip.h).
 //
-// Owns one HIP device + stream per context and the HBM-resident state of
-// gs_internal.h.  Replaces the reference's main() body (simulator.go:207-253):
-// allocation (:208-212), overlay (:214-235), broadcast and polling (:237-253).
+// Replaces the reference's main() body (simulator.go:207-253): allocation
+// (:208-212), overlay (:214-235), broadcast and polling (:237-253).  Four
+// kinds of context sit behind the same calls:
+//   plain    one device, one stream, one trial (window / tick / push-pull engine)
+//   batched  one device, `trials` independent trials laid out at trial << tlog
+//            and run by the window engine at once (config C3)
+//   shard    one node range [lo, hi) of one broadcast (config C4): a member of a
+//            group, or one rank of a multi-process run (RCCL inside)
+//   group    gs_create_multi: shards or trial batches over several devices
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -11,12 +17,30 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gossip.h"
+#include "gs_comm.h"
 #include "gs_internal.h"
 
 using namespace gs;
+
+namespace {
+
+struct Buf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+// One trial's running counters and its stopping snapshot (gs_run's rule).
+struct TrialAcc {
+  uint64_t fired = 0, sent = 0, msgs = 0, recv = 0, crash = 0, sched = 0, tick99 = 0;
+  int32_t status = GS_RUN_RUNNING;
+  gs_trial_stats snap{};
+};
+
+}  // namespace
 
 struct gs_ctx {
   gs_params p{};
@@ -38,7 +62,7 @@ struct gs_ctx {
   std::vector<hipEvent_t> ev;
   gs_timing timing{};
   // push-pull extension (gs_pushpull.hip)
-  bool pp = false;
+  bool pp = false, pp_l2_only = false;
   unsigned long long* d_next = nullptr;  // informed set being built (state block)
   unsigned long long* d_ppsum = nullptr;  // push-pull word summaries (state block)
   uint32_t* d_flag = nullptr;
@@ -48,9 +72,31 @@ struct gs_ctx {
   void* d_win = nullptr;      // fcount + small per-window buffers
   void* d_flist = nullptr;    // [R][nfine][16384] u16
   size_t fcount_bytes = 0;
-  struct Buf { void* p = nullptr; size_t bytes = 0; } gmap, cmsg, fmsg, tmp;
+  Buf gmap, cmsg, fmsg, tmp;
   unsigned long long* h_cap = nullptr;  // pinned [257] coarse region plan
   unsigned long long* h_misc = nullptr; // pinned scratch (counts, flags)
+  // trials: `trials` per context (batched when > 1), ids trial << tlog | node
+  uint32_t trials = 1, tlog = 32;
+  uint64_t ntot = 0;                    // nodes in this context's id space
+  uint32_t* d_tstat = nullptr;          // [trials][kMaxWindow][kTStatFields]
+  uint32_t* h_tstat = nullptr;          // pinned copy
+  std::vector<TrialAcc> tacc;
+  // node-range shard (config C4)
+  bool shard = false;
+  uint32_t G = 1, rank = 0;
+  uint64_t lo = 0, hi = 0, seg_per = 0;
+  uint32_t* d_prow = nullptr;           // [n + 1] partitioned row starts
+  uint32_t* d_pent = nullptr;           // owned slots: (target - lo) << 5 | j
+  Buf gfire;                            // multi-process: this rank's all-gather buffer
+  unsigned long long* d_gcounts = nullptr;  // multi-process: [G][16] gathered fires per tick
+  ncclComm_t comm = nullptr;
+  // group (gs_create_multi)
+  bool group = false, gtrials = false;
+  std::vector<gs_ctx*> mem;
+  std::vector<int> gdevs;               // distinct devices, first-use order
+  std::vector<int> gdev_of;             // member -> index into gdevs
+  std::vector<Buf> gbuf;                // one all-gather buffer per distinct device
+  std::vector<hipEvent_t> gev_c, gev_x; // per member: compaction done; per device: copies done
 };
 
 namespace {
@@ -60,7 +106,7 @@ int fail(gs_ctx* c, int code, const std::string& msg) {
   return code;
 }
 
-bool grow(gs_ctx::Buf& b, size_t bytes) {
+bool grow(Buf& b, size_t bytes) {
   if (b.bytes >= bytes) return true;
   const size_t nb = std::max(bytes, b.bytes + b.bytes / 4);
   if (b.p) (void)hipFree(b.p);
@@ -70,6 +116,26 @@ bool grow(gs_ctx::Buf& b, size_t bytes) {
   b.bytes = nb;
   return true;
 }
+
+#define CK(c, expr)                                                                   \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      return fail((c), GS_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define NCK(c, expr)                                                                  \
+  do {                                                                                \
+    ncclResult_t r_ = (expr);                                                         \
+    if (r_ != ncclSuccess)                                                            \
+      return fail((c), GS_EDEVICE, std::string(#expr) + ": " + rccl_error((int)r_));  \
+  } while (0)
+
+#define RC(expr)              \
+  do {                        \
+    int rc_ = (expr);         \
+    if (rc_) return rc_;      \
+  } while (0)
 
 // Window-engine buffers.  Sizes at n = 1e9, R = 20: flist 40 GB (two bytes
 // per node per ring slot), fcount 4.9 MB; message buffers grow on demand.
@@ -86,6 +152,12 @@ int alloc_window(gs_ctx* c) {
   w.kd = s.kd;
   w.kc = s.kc;
   w.key = s.key;
+  w.base = (uint32_t)c->lo;
+  w.tlog = c->tlog;
+  w.tmask = c->tlog >= 32 ? ~0u : (1u << c->tlog) - 1;
+  w.G = c->G;
+  w.rank = c->rank;
+  w.seg_per = (uint32_t)c->seg_per;
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t units = (size_t)kMaxWindow * w.nfine + 1;
   const size_t b_fc = al((size_t)w.R * w.nfine * 4), b_units = al(units * 8),
@@ -121,13 +193,20 @@ int alloc_window(gs_ctx* c) {
   if (hipMemsetAsync(c->d_win, 0, total, c->stream) != hipSuccess)
     return fail(c, GS_EDEVICE, "memset of window buffers failed");
   if (hipHostMalloc((void**)&c->h_cap, 257 * 8) != hipSuccess ||
-      hipHostMalloc((void**)&c->h_misc, 512 * 8) != hipSuccess)
+      hipHostMalloc((void**)&c->h_misc, 1024 * 8) != hipSuccess)
     return fail(c, GS_ENOMEM, "cannot allocate pinned window buffers");
+  if (c->trials > 1) {
+    const size_t tb = (size_t)c->trials * kMaxWindow * kTStatFields * 4;
+    if (hipMalloc((void**)&c->d_tstat, tb) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_tstat, tb) != hipSuccess)
+      return fail(c, GS_ENOMEM, "cannot allocate per-trial counters");
+    w.tstat = c->d_tstat;
+  }
   return GS_OK;
 }
 
-// Coarse region plan: bucket c gets its node share of the window's T friend
-// slots (a kept send is at most one slot) plus 4096, or exactly `exact[c]`.
+// Coarse region plan: bucket c gets its node share of the window's T message
+// bound plus 4096, or exactly `exact[c]`.
 void plan_coarse(gs_ctx* c, uint64_t T, const unsigned long long* exact) {
   const WinState& w = c->ws;
   unsigned long long a = 0;
@@ -152,16 +231,17 @@ void refresh_window(gs_ctx* c) {
   w.err = c->d_err;
   w.stride = c->st.stride;
   w.stride_magic = c->st.stride_magic;
+  w.prow = c->d_prow;
+  w.pent = c->d_pent;
 }
 
-#define CK(c, expr)                                                                   \
-  do {                                                                                \
-    hipError_t e_ = (expr);                                                           \
-    if (e_ != hipSuccess)                                                             \
-      return fail((c), GS_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
-  } while (0)
-
 uint32_t ring_slots(const gs_params& p) { return p.delay_high > 2 ? (uint32_t)p.delay_high : 2u; }
+
+uint32_t ceil_log2(uint64_t x) {
+  uint32_t b = 0;
+  while ((1ull << b) < x) ++b;
+  return b;
+}
 
 int check_params(const gs_params* p, std::string& why) {
   if (!p) { why = "params is NULL"; return GS_EINVAL; }
@@ -177,8 +257,8 @@ int check_params(const gs_params* p, std::string& why) {
   }
   if (ring_slots(*p) > 4096) { why = "delayhigh must be <= 4096"; return GS_EINVAL; }
   if (p->model > GS_MODEL_PUSHPULL) { why = "model must be GS_MODEL_FLOOD or GS_MODEL_PUSHPULL"; return GS_EINVAL; }
-  if (p->model == GS_MODEL_PUSHPULL && !(p->node_lo == 0 && (p->node_hi == 0 || p->node_hi == p->n))) {
-    why = "push-pull runs are not node-range sharded (shard trials instead)";
+  if (p->trials > 1 && p->model != GS_MODEL_FLOOD) {
+    why = "batched trials run the flood model (the reference's)";
     return GS_EINVAL;
   }
   return GS_OK;
@@ -201,36 +281,47 @@ int set_stride(gs_ctx* c, uint32_t stride) {
   return GS_OK;
 }
 
+// Nodes of the table this context loads: a shard loads the whole (replicated)
+// table and keeps its partition.
+uint64_t table_n(const gs_ctx* c) { return c->shard ? c->p.n : c->ntot; }
+
 int alloc_table(gs_ctx* c, uint32_t stride) {
   if (c->d_deg) (void)hipFree(c->d_deg);
   if (c->d_ids) (void)hipFree(c->d_ids);
   c->d_deg = nullptr;
   c->d_ids = nullptr;
-  const uint64_t n = c->p.n;
+  const uint64_t n = table_n(c);
   if (hipMalloc(&c->d_deg, n) != hipSuccess || hipMalloc(&c->d_ids, n * stride * 4ull) != hipSuccess)
     return fail(c, GS_ENOMEM, "cannot allocate the peer table on the device");
-  int rc = set_stride(c, stride);
-  if (rc) return rc;
+  RC(set_stride(c, stride));
   refresh_state(c);
   return GS_OK;
 }
 
-__global__ void k_validate_peers(const uint8_t* deg, const uint32_t* ids, uint64_t n,
+void free_table(gs_ctx* c) {
+  if (c->d_deg) (void)hipFree(c->d_deg);
+  if (c->d_ids) (void)hipFree(c->d_ids);
+  c->d_deg = nullptr;
+  c->d_ids = nullptr;
+  refresh_state(c);
+}
+
+__global__ void k_validate_peers(const uint8_t* deg, const uint32_t* ids, uint64_t n, uint64_t bound,
                                  uint32_t stride, uint32_t* err) {
   for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
        v += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t d = deg[v];
     if (d > stride) { atomicOr(err, 1u); continue; }
     for (uint32_t j = 0; j < d; ++j)
-      if (ids[v * stride + j] >= n) atomicOr(err, 2u);
+      if (ids[v * stride + j] >= bound) atomicOr(err, 2u);
   }
 }
 
-int validate_table(gs_ctx* c) {
+int validate_table(gs_ctx* c, const uint8_t* deg, const uint32_t* ids, uint64_t n, uint64_t bound) {
   CK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
-  const uint64_t blocks = std::min<uint64_t>((c->p.n + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_validate_peers, dim3((uint32_t)blocks), dim3(256), 0, c->stream, c->d_deg,
-                     c->d_ids, c->p.n, c->st.stride, c->d_err);
+  const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_validate_peers, dim3((uint32_t)blocks), dim3(256), 0, c->stream, deg, ids, n, bound,
+                     c->st.stride, c->d_err);
   CK(c, hipGetLastError());
   uint32_t e = 0;
   CK(c, hipMemcpyAsync(&e, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
@@ -242,11 +333,55 @@ int validate_table(gs_ctx* c) {
 
 // The window engine reads friend rows without the length byte: slots past a
 // node's list are set to kEmptyMsg on the device copy.
-int seal_rows(gs_ctx* c) {
+int seal_rows(gs_ctx* c, const uint8_t* deg, uint32_t* ids, uint64_t n) {
   if (!c->win) return GS_OK;
-  CK(c, win_seal_rows(c->d_deg, c->d_ids, c->p.n, c->st.stride, c->stream));
+  CK(c, win_seal_rows(deg, ids, n, c->st.stride, c->stream));
   CK(c, hipStreamSynchronize(c->stream));
   return GS_OK;
+}
+
+// Shard c's partition of the sealed global table (ids, on c's device).
+int partition(gs_ctx* c, const uint32_t* ids) {
+  const uint64_t n = c->p.n;
+  if (c->d_prow) (void)hipFree(c->d_prow);
+  if (c->d_pent) (void)hipFree(c->d_pent);
+  c->d_prow = nullptr;
+  c->d_pent = nullptr;
+  uint32_t* cnt = nullptr;
+  unsigned long long* off = nullptr;
+  void* tmp = nullptr;
+  size_t tb = 0;
+  int rc = GS_OK;
+  unsigned long long total = 0;
+  uint32_t e = 0;
+  auto bail = [&](int code, const std::string& m) { rc = fail(c, code, m); };
+  if (hipMalloc(&cnt, (n + 1) * 4) != hipSuccess || hipMalloc(&off, (n + 1) * 8) != hipSuccess ||
+      hipMalloc(&c->d_prow, (n + 1) * 4) != hipSuccess) {
+    bail(GS_ENOMEM, "cannot allocate the shard's row index");
+  } else if (hipMemsetAsync(cnt + n, 0, 4, c->stream) != hipSuccess ||
+             part_count(ids, n, c->st.stride, (uint32_t)c->lo, (uint32_t)c->hi, cnt, c->stream) != hipSuccess ||
+             part_scan(cnt, n, off, nullptr, tb, c->stream) != hipSuccess || hipMalloc(&tmp, tb) != hipSuccess ||
+             part_scan(cnt, n, off, tmp, tb, c->stream) != hipSuccess ||
+             hipMemsetAsync(c->d_err, 0, 4, c->stream) != hipSuccess ||
+             part_narrow(off, n, c->d_prow, c->d_err, c->stream) != hipSuccess ||
+             hipMemcpyAsync(&total, off + n, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+             hipMemcpyAsync(&e, c->d_err, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+             hipStreamSynchronize(c->stream) != hipSuccess) {
+    bail(GS_EDEVICE, "building the shard's row index failed");
+  } else if (e) {
+    bail(GS_EINVAL, "a shard holds 2^32 or more friend slots: use more shards");
+  } else if (hipMalloc(&c->d_pent, std::max<unsigned long long>(total, 1) * 4) != hipSuccess) {
+    bail(GS_ENOMEM, "cannot allocate " + std::to_string(total) + " partitioned friend slots");
+  } else if (part_fill(ids, n, c->st.stride, (uint32_t)c->lo, (uint32_t)c->hi, c->d_prow, c->d_pent,
+                       c->stream) != hipSuccess ||
+             hipStreamSynchronize(c->stream) != hipSuccess) {
+    bail(GS_EDEVICE, "filling the shard's partition failed");
+  }
+  if (cnt) (void)hipFree(cnt);
+  if (off) (void)hipFree(off);
+  if (tmp) (void)hipFree(tmp);
+  refresh_window(c);
+  return rc;
 }
 
 bool covered(uint64_t recv, uint64_t n) {
@@ -254,6 +389,215 @@ bool covered(uint64_t recv, uint64_t n) {
   volatile float a = (float)recv, b = (float)n;
   volatile float pct = a / b;
   return pct >= 0.99f;
+}
+
+int ctx_setup(gs_ctx* c, const gs_params* params, int device, bool shard, uint32_t G, uint32_t rank,
+              std::string& why) {
+  c->p = *params;
+  c->p.device = device;
+  c->dev = device;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    why = "no HIP device visible (libgossip_hip needs an MI355X)";
+    return GS_EDEVICE;
+  }
+  if (c->dev < 0 || c->dev >= ndev) {
+    why = "device " + std::to_string(c->dev) + " out of range (" + std::to_string(ndev) + " visible)";
+    return GS_EDEVICE;
+  }
+  hipDeviceProp_t prop;
+  if (hipSetDevice(c->dev) != hipSuccess || hipGetDeviceProperties(&prop, c->dev) != hipSuccess ||
+      strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    why = "device " + std::to_string(c->dev) + " is not gfx950";
+    return GS_EDEVICE;
+  }
+  if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+    why = "cannot create a stream";
+    return GS_EDEVICE;
+  }
+  c->stream = c->own;
+  DevState& s = c->st;
+  const uint32_t stride0 = (uint32_t)std::max(c->p.fanout, c->p.fanin);
+  c->pp = c->p.model == GS_MODEL_PUSHPULL;
+  c->pp_l2_only = (c->p.flags & GS_FLAG_PP_L2_ONLY) != 0;
+  c->trials = std::max<uint32_t>(1, c->p.trials);
+  c->ntot = c->p.n;
+  if (c->trials > 1) {
+    c->tlog = std::max<uint32_t>(kFineLog, ceil_log2(c->p.n));
+    c->ntot = (uint64_t)c->trials << c->tlog;
+    if (c->ntot > 0x7FFFFFFFull) {
+      why = "trials x 2^ceil(log2 n) must be < 2^31 (batch fewer trials per context)";
+      return GS_EINVAL;
+    }
+  }
+  c->shard = shard;
+  c->G = G;
+  c->rank = rank;
+  if (shard) {
+    if (c->pp) { why = "push-pull runs are not node-range sharded (shard trials instead)"; return GS_EINVAL; }
+    c->seg_per = (((c->p.n + G - 1) / G) + kFineNodes - 1) & ~(uint64_t)(kFineNodes - 1);
+    if ((uint64_t)(G - 1) * c->seg_per >= c->p.n) {
+      why = "n = " + std::to_string(c->p.n) + " is too small for " + std::to_string(G) +
+            " shards of whole 16384-node buckets";
+      return GS_EINVAL;
+    }
+    if (c->seg_per > (1ull << 27)) { why = "a shard may own at most 2^27 nodes: use more shards"; return GS_EINVAL; }
+    c->lo = rank * c->seg_per;
+    c->hi = std::min<uint64_t>(c->lo + c->seg_per, c->p.n);
+    c->ntot = c->hi - c->lo;
+  }
+  s.lo = 0;
+  s.hi = (uint32_t)c->ntot;
+  s.n = c->ntot;
+  s.W = (s.n + 63) / 64;
+  s.C = (uint32_t)((s.n + (1ull << kChunkNodesLog) - 1) >> kChunkNodesLog);
+  s.CS = (s.C + kShards - 1) / kShards;
+  s.chunk_lo = 0;
+  s.chunk_hi = s.C;
+  s.sharded = 0;
+  s.R = ring_slots(c->p);
+  s.delay_low = c->p.delay_low;
+  s.delay_span = (uint32_t)(c->p.delay_high - c->p.delay_low);
+  s.kd = gs_threshold(c->p.drop_rate);
+  s.kc = gs_threshold(c->p.crash_rate);
+  s.key = Key{(uint32_t)c->p.seed, (uint32_t)(c->p.seed >> 32), c->p.trial};
+  // Engine: the window engine unless the ring is too long for LDS, rows are
+  // wider than 32 or the tick engine is forced; push-pull has its own kernels.
+  c->win = !c->pp && s.R <= kWinMaxRing && !(c->p.flags & GS_FLAG_TICK_ENGINE) && stride0 <= kWinMaxStride;
+  if ((c->trials > 1 || shard) && !c->win) {
+    why = "batched trials and node-range shards run on the window engine (delayhigh <= 256, "
+          "fanout/fanin <= 32, no GS_FLAG_TICK_ENGINE)";
+    return GS_EINVAL;
+  }
+  // One state allocation, 256-B aligned sub-buffers; everything before
+  // `stats` is per-broadcast state that gs_reset clears.
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const bool tick = !c->win && !c->pp;
+  const size_t b_next = c->pp ? al(s.W * 8) + al(pp_summary_total_words(s.W) * 8) : 0;
+  const size_t b_bits = al(s.W * 8), b_ring = tick ? al((size_t)s.R * s.W * 8) : 0,
+               b_cflag = tick ? al((size_t)s.R * s.C * 4) : 0,
+               b_clist = tick ? al((size_t)s.R * kShards * s.CS * 4) : 0,
+               b_ccount = tick ? al((size_t)s.R * kShards * kCounterStride * 4) : 0,
+               b_stats = al((size_t)kStatSlots * kStatFields * 8);
+  const size_t total = 2 * b_bits + b_next + b_ring + b_cflag + b_clist + b_ccount + b_stats + 256;
+  c->state_bytes = total;
+  if (hipMalloc(&c->d_state, total) != hipSuccess) {
+    why = "cannot allocate " + std::to_string(total) + " bytes of device state";
+    return GS_ENOMEM;
+  }
+  char* q = (char*)c->d_state;
+  s.recv = (unsigned long long*)q; q += b_bits;
+  s.crash = (unsigned long long*)q; q += b_bits;
+  c->d_next = b_next ? (unsigned long long*)q : nullptr;
+  c->d_ppsum = b_next ? (unsigned long long*)(q + al(s.W * 8)) : nullptr;
+  q += b_next;
+  s.ring = (unsigned long long*)q; q += b_ring;
+  s.cflag = (uint32_t*)q; q += b_cflag;
+  s.clist = (uint32_t*)q; q += b_clist;
+  s.ccount = (uint32_t*)q; q += b_ccount;
+  s.stats = (unsigned long long*)q; q += b_stats;
+  c->d_err = (uint32_t*)q;
+  c->d_flag = c->d_err + 1;
+  if (tick && s.kc > 0 && hipMalloc(&c->d_cnt, s.n * 4) != hipSuccess) {
+    why = "cannot allocate arrival counters";
+    return GS_ENOMEM;
+  }
+  s.cnt = c->d_cnt;
+  if (c->win) {
+    int rc = alloc_window(c);
+    if (rc) { why = c->err; return rc; }
+  }
+  c->tacc.assign(c->trials, TrialAcc{});
+  if (hipMemsetAsync(c->d_state, 0, total, c->stream) != hipSuccess ||
+      (c->d_cnt && hipMemsetAsync(c->d_cnt, 0, s.n * 4, c->stream) != hipSuccess) ||
+      hipHostMalloc((void**)&c->h_stats, (size_t)kStatSlots * kStatFields * 8) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess) {
+    why = "device initialisation failed";
+    return GS_EDEVICE;
+  }
+  return GS_OK;
+}
+
+void destroy_one(gs_ctx* c) {
+  if (!c) return;
+  for (gs_ctx* m : c->mem) destroy_one(m);
+  if (c->group) {
+    for (size_t i = 0; i < c->gdevs.size() && i < c->gbuf.size(); ++i)
+      if (c->gbuf[i].p) {
+        (void)hipSetDevice(c->gdevs[i]);
+        (void)hipFree(c->gbuf[i].p);
+      }
+    for (hipEvent_t e : c->gev_c) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->gev_x) (void)hipEventDestroy(e);
+    delete c;
+    return;
+  }
+  (void)hipSetDevice(c->dev);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm && rccl().ok) (void)rccl().comm_destroy(c->comm);
+  if (c->ws.dbg) {
+    unsigned long long h[2 * kStampPhases];
+    if (hipMemcpy(h, c->ws.dbg, sizeof h, hipMemcpyDeviceToHost) == hipSuccess)
+      for (int cls = 0; cls < 2; ++cls) {  // k_resolve phases (GS_STAMPS=1), thread 0 of every workgroup
+        const unsigned long long* d = h + cls * kStampPhases;
+        if (!d[0]) continue;
+        fprintf(stderr, "[stamps] k_resolve %s: %llu buckets, mean kcycles per bucket per phase:",
+                cls ? "M>=1024" : "M<1024", d[0]);
+        for (uint32_t i = 1; i < kStampPhases; ++i) fprintf(stderr, " %.2f", d[i] * 1e-3 / d[0]);
+        fprintf(stderr, "\n");
+      }
+    (void)hipFree(c->ws.dbg);
+  }
+  for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+  for (void* ptr : {(void*)c->d_deg, (void*)c->d_ids, c->d_state, (void*)c->d_cnt, (void*)c->d_failed, c->d_win,
+                    c->d_flist, (void*)c->d_tstat, (void*)c->d_prow, (void*)c->d_pent, (void*)c->d_gcounts})
+    if (ptr) (void)hipFree(ptr);
+  for (Buf* b : {&c->gmap, &c->cmsg, &c->fmsg, &c->tmp, &c->gfire})
+    if (b->p) (void)hipFree(b->p);
+  for (void* ptr : {(void*)c->h_cap, (void*)c->h_misc, (void*)c->h_stats, (void*)c->h_tstat})
+    if (ptr) (void)hipHostFree(ptr);
+  if (c->own) (void)hipStreamDestroy(c->own);
+  delete c;
+}
+
+int create_one(const gs_params* params, int device, bool shard, uint32_t G, uint32_t rank, gs_ctx** out) {
+  std::string why;
+  int rc = check_params(params, why);
+  if (!rc) {
+    gs_ctx* c = new gs_ctx();
+    rc = ctx_setup(c, params, device, shard, G, rank, why);
+    if (!rc) {
+      *out = c;
+      return GS_OK;
+    }
+    destroy_one(c);
+  }
+  fprintf(stderr, "gs_create: %s\n", why.c_str());
+  return rc;
+}
+
+// Runs f(member) for every member, one host thread each (members on several
+// devices, or several trial batches on one, overlap); first error wins.
+template <class F>
+int par_members(gs_ctx* g, F f) {
+  std::vector<int> rcs(g->mem.size(), 0);
+  std::vector<std::thread> th;
+  for (size_t i = 0; i < g->mem.size(); ++i)
+    th.emplace_back([&, i] {
+      (void)hipSetDevice(g->mem[i]->dev);
+      rcs[i] = f(g->mem[i]);
+    });
+  for (auto& t : th) t.join();
+  for (size_t i = 0; i < rcs.size(); ++i)
+    if (rcs[i]) return fail(g, rcs[i], "member " + std::to_string(i) + ": " + g->mem[i]->err);
+  return GS_OK;
+}
+
+// Host copies of the broadcast counters a gs_ctx keeps: for a group, the
+// group's own fields; members and ranks keep theirs.
+void reset_counters(gs_ctx* c) {
+  c->t = c->fired = c->sent = c->msgs = c->recv = c->crashed = c->pending = 0;
+  for (TrialAcc& a : c->tacc) a = TrialAcc{};
 }
 
 }  // namespace
@@ -280,169 +624,178 @@ const char* gs_last_error(const gs_ctx* c) { return c ? c->err.c_str() : "NULL c
 int gs_create(const gs_params* params, gs_ctx** out) {
   if (!out) return GS_EINVAL;
   *out = nullptr;
-  std::string why;
-  int rc = check_params(params, why);
-  if (rc) {
-    fprintf(stderr, "gs_create: %s\n", why.c_str());
-    return rc;
-  }
-  gs_ctx* c = new gs_ctx();
-  c->p = *params;
-  c->dev = params->device;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
-    fprintf(stderr, "gs_create: no HIP device visible (libgossip_hip needs an MI355X)\n");
-    delete c;
-    return GS_EDEVICE;
-  }
-  if (c->dev < 0 || c->dev >= ndev) {
-    fprintf(stderr, "gs_create: device %d out of range (%d visible)\n", c->dev, ndev);
-    delete c;
-    return GS_EDEVICE;
-  }
-  hipDeviceProp_t prop;
-  if (hipSetDevice(c->dev) != hipSuccess || hipGetDeviceProperties(&prop, c->dev) != hipSuccess ||
-      strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-    fprintf(stderr, "gs_create: device %d is not gfx950 (%s)\n", c->dev, prop.gcnArchName);
-    delete c;
-    return GS_EDEVICE;
-  }
-  if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
-    delete c;
-    return GS_EDEVICE;
-  }
-  c->stream = c->own;
-  DevState& s = c->st;
-  {
-    uint64_t lo = c->p.node_lo, hi = c->p.node_hi;
-    if (lo == 0 && hi == 0) hi = c->p.n;
-    if (lo > hi || hi > c->p.n || ((lo & 4095) && lo != c->p.n) ||
-        ((hi & 4095) && hi != c->p.n)) {
-      fprintf(stderr, "gs_create: node range [%llu, %llu) must be 4096-aligned within [0, n]\n",
-              (unsigned long long)lo, (unsigned long long)hi);
-      gs_destroy(c);
-      return GS_EINVAL;
+  return create_one(params, params ? params->device : 0, false, 1, 0, out);
+}
+
+int gs_create_multi(const gs_params* params, const int* devices, int ndev, gs_ctx** out) {
+  if (!out || !params || !devices || ndev < 1) return GS_EINVAL;
+  *out = nullptr;
+  gs_ctx* g = new gs_ctx();
+  g->group = true;
+  g->p = *params;
+  g->dev = devices[0];
+  g->trials = std::max<uint32_t>(1, params->trials);
+  g->gtrials = g->trials > 1;
+  if (g->gtrials && (uint32_t)ndev > g->trials) ndev = (int)g->trials;
+  for (int i = 0; i < ndev; ++i) {
+    gs_params mp = *params;
+    gs_ctx* m = nullptr;
+    int rc;
+    if (g->gtrials) {  // trials [t0, t1) on member i
+      const uint32_t t0 = (uint32_t)((uint64_t)g->trials * i / ndev), t1 = (uint32_t)((uint64_t)g->trials * (i + 1) / ndev);
+      mp.trial = params->trial + t0;
+      mp.trials = t1 - t0;
+      rc = create_one(&mp, devices[i], false, 1, 0, &m);
+    } else {
+      rc = create_one(&mp, devices[i], true, (uint32_t)ndev, (uint32_t)i, &m);
     }
-    s.lo = (uint32_t)lo;
-    s.hi = (uint32_t)hi;
-    s.chunk_lo = (uint32_t)(lo >> kChunkNodesLog);
-    s.chunk_hi = (uint32_t)((hi + (1ull << kChunkNodesLog) - 1) >> kChunkNodesLog);
-    s.sharded = !(lo == 0 && hi == c->p.n);
-  }
-  s.n = c->p.n;
-  s.W = (s.n + 63) / 64;
-  s.C = (uint32_t)((s.n + (1ull << kChunkNodesLog) - 1) >> kChunkNodesLog);
-  s.CS = (s.C + kShards - 1) / kShards;
-  s.R = ring_slots(c->p);
-  s.delay_low = c->p.delay_low;
-  s.delay_span = (uint32_t)(c->p.delay_high - c->p.delay_low);
-  s.kd = gs_threshold(c->p.drop_rate);
-  s.kc = gs_threshold(c->p.crash_rate);
-  s.key = Key{(uint32_t)c->p.seed, (uint32_t)(c->p.seed >> 32), c->p.trial};
-  // Engine: the window engine (gs_window.hip) unless the run is node-range
-  // sharded (per-tick frontier exchange) or its ring is too long for LDS.
-  // Push-pull has its own round kernels (gs_pushpull.hip).
-  c->pp = c->p.model == GS_MODEL_PUSHPULL;
-  c->win = !c->pp && !s.sharded && s.R <= kWinMaxRing && !(c->p.flags & GS_FLAG_TICK_ENGINE) &&
-           (uint32_t)std::max(c->p.fanout, c->p.fanin) <= kWinMaxStride;
-  // One state allocation, 256-B aligned sub-buffers; everything before
-  // `stats` is per-broadcast state that gs_reset clears.
-  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  const bool tick = !c->win && !c->pp;
-  const size_t b_next = c->pp ? al(s.W * 8) + al(pp_summary_total_words(s.W) * 8) : 0;
-  const size_t b_bits = al(s.W * 8), b_ring = tick ? al((size_t)s.R * s.W * 8) : 0,
-               b_cflag = tick ? al((size_t)s.R * s.C * 4) : 0,
-               b_clist = tick ? al((size_t)s.R * kShards * s.CS * 4) : 0,
-               b_ccount = tick ? al((size_t)s.R * kShards * kCounterStride * 4) : 0,
-               b_stats = al((size_t)kStatSlots * kStatFields * 8);
-  const size_t total = 2 * b_bits + b_next + b_ring + b_cflag + b_clist + b_ccount + b_stats + 256;
-  c->state_bytes = total;
-  if (hipMalloc(&c->d_state, total) != hipSuccess) {
-    fprintf(stderr, "gs_create: cannot allocate %zu bytes of device state\n", total);
-    gs_destroy(c);
-    return GS_ENOMEM;
-  }
-  char* q = (char*)c->d_state;
-  s.recv = (unsigned long long*)q; q += b_bits;
-  s.crash = (unsigned long long*)q; q += b_bits;
-  c->d_next = b_next ? (unsigned long long*)q : nullptr;
-  c->d_ppsum = b_next ? (unsigned long long*)(q + al(s.W * 8)) : nullptr;
-  q += b_next;
-  s.ring = (unsigned long long*)q; q += b_ring;
-  s.cflag = (uint32_t*)q; q += b_cflag;
-  s.clist = (uint32_t*)q; q += b_clist;
-  s.ccount = (uint32_t*)q; q += b_ccount;
-  s.stats = (unsigned long long*)q; q += b_stats;
-  c->d_err = (uint32_t*)q;
-  c->d_flag = c->d_err + 1;
-  if (tick && s.kc > 0) {
-    if (hipMalloc(&c->d_cnt, s.n * 4) != hipSuccess) {
-      fprintf(stderr, "gs_create: cannot allocate arrival counters\n");
-      gs_destroy(c);
-      return GS_ENOMEM;
-    }
-  }
-  s.cnt = c->d_cnt;
-  if (c->win) {
-    rc = alloc_window(c);
     if (rc) {
-      fprintf(stderr, "gs_create: %s\n", c->err.c_str());
-      gs_destroy(c);
+      destroy_one(g);
       return rc;
     }
+    g->mem.push_back(m);
+    auto it = std::find(g->gdevs.begin(), g->gdevs.end(), devices[i]);
+    if (it == g->gdevs.end()) {
+      g->gdevs.push_back(devices[i]);
+      g->gdev_of.push_back((int)g->gdevs.size() - 1);
+    } else {
+      g->gdev_of.push_back((int)(it - g->gdevs.begin()));
+    }
   }
-  if (hipMemsetAsync(c->d_state, 0, total, c->stream) != hipSuccess ||
-      (c->d_cnt && hipMemsetAsync(c->d_cnt, 0, s.n * 4, c->stream) != hipSuccess) ||
-      hipHostMalloc((void**)&c->h_stats, (size_t)kStatSlots * kStatFields * 8) != hipSuccess ||
-      hipStreamSynchronize(c->stream) != hipSuccess) {
-    gs_destroy(c);
+  g->gbuf.resize(g->gdevs.size());
+  for (size_t i = 0; i < g->mem.size(); ++i) {
+    hipEvent_t e;
+    (void)hipSetDevice(g->mem[i]->dev);
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      destroy_one(g);
+      return GS_EDEVICE;
+    }
+    g->gev_c.push_back(e);
+  }
+  for (size_t d = 0; d < g->gdevs.size(); ++d) {
+    hipEvent_t e;
+    (void)hipSetDevice(g->gdevs[d]);
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      destroy_one(g);
+      return GS_EDEVICE;
+    }
+    g->gev_x.push_back(e);
+  }
+  g->tacc.assign(g->gtrials ? 0 : 1, TrialAcc{});
+  *out = g;
+  return GS_OK;
+}
+
+int gs_comm_unique_id(uint8_t id[GS_COMM_ID_BYTES]) {
+  if (!id) return GS_EINVAL;
+  const Rccl& r = rccl();
+  if (!r.ok) {
+    fprintf(stderr, "gs_comm_unique_id: %s\n", r.why.c_str());
     return GS_EDEVICE;
+  }
+  ncclUniqueId u;
+  if (r.get_unique_id(&u) != ncclSuccess) return GS_EDEVICE;
+  static_assert(sizeof(ncclUniqueId) == GS_COMM_ID_BYTES, "RCCL unique id size");
+  memcpy(id, &u, GS_COMM_ID_BYTES);
+  return GS_OK;
+}
+
+int gs_create_rank(const gs_params* params, int device, int nranks, int rank, const uint8_t* id, gs_ctx** out) {
+  if (!out || !params || nranks < 1 || rank < 0 || rank >= nranks) return GS_EINVAL;
+  *out = nullptr;
+  const uint32_t T = std::max<uint32_t>(1, params->trials);
+  if (T > 1) {  // this rank's share of the trials, no communication
+    gs_params mp = *params;
+    const uint32_t t0 = (uint32_t)((uint64_t)T * rank / nranks), t1 = (uint32_t)((uint64_t)T * (rank + 1) / nranks);
+    if (t1 == t0) {
+      fprintf(stderr, "gs_create_rank: %u trials leave rank %d none\n", T, rank);
+      return GS_EINVAL;
+    }
+    mp.trial = params->trial + t0;
+    mp.trials = t1 - t0;
+    return create_one(&mp, device, false, 1, 0, out);
+  }
+  if (!id) return GS_EINVAL;
+  const Rccl& r = rccl();
+  if (!r.ok) {
+    fprintf(stderr, "gs_create_rank: %s\n", r.why.c_str());
+    return GS_EDEVICE;
+  }
+  gs_ctx* c = nullptr;
+  int rc = create_one(params, device, true, (uint32_t)nranks, (uint32_t)rank, &c);
+  if (rc) return rc;
+  ncclUniqueId u;
+  memcpy(&u, id, GS_COMM_ID_BYTES);
+  (void)hipSetDevice(device);
+  ncclResult_t nr = r.comm_init_rank(&c->comm, nranks, u, rank);
+  if (nr != ncclSuccess) {
+    fprintf(stderr, "gs_create_rank: ncclCommInitRank: %s\n", rccl_error((int)nr).c_str());
+    c->comm = nullptr;
+    destroy_one(c);
+    return GS_EDEVICE;
+  }
+  if (hipMalloc(&c->d_gcounts, (size_t)nranks * kMaxWindow * 8 + (size_t)kMaxWindow * 8) != hipSuccess) {
+    destroy_one(c);
+    return GS_ENOMEM;
   }
   *out = c;
   return GS_OK;
 }
 
-void gs_destroy(gs_ctx* c) {
-  if (!c) return;
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (c->ws.dbg) {
-    unsigned long long h[2 * kStampPhases];
-    if (hipMemcpy(h, c->ws.dbg, sizeof h, hipMemcpyDeviceToHost) == hipSuccess)
-      for (int cls = 0; cls < 2; ++cls) {  // k_resolve phases (GS_STAMPS=1), thread 0 of every workgroup
-        const unsigned long long* d = h + cls * kStampPhases;
-        if (!d[0]) continue;
-        fprintf(stderr, "[stamps] k_resolve %s: %llu buckets, mean kcycles per bucket per phase:",
-                cls ? "M>=1024" : "M<1024", d[0]);
-        for (uint32_t i = 1; i < kStampPhases; ++i) fprintf(stderr, " %.2f", d[i] * 1e-3 / d[0]);
-        fprintf(stderr, "\n");
-      }
-    (void)hipFree(c->ws.dbg);
+int gs_shard_info(const gs_ctx* c, uint32_t index, uint32_t* nshards, uint64_t* lo, uint64_t* hi) {
+  if (!c) return GS_EINVAL;
+  const bool sg = c->group && !c->gtrials;
+  const uint32_t ns = sg ? (uint32_t)c->mem.size() : c->shard ? c->G : 1u;
+  if (nshards) *nshards = ns;
+  if (index >= ns) return GS_EINVAL;
+  const gs_ctx* s = sg ? c->mem[0] : c;
+  uint64_t a = 0, b = c->p.n;
+  if (s->shard) {
+    a = std::min<uint64_t>(index * s->seg_per, c->p.n);
+    b = std::min<uint64_t>(a + s->seg_per, c->p.n);
   }
-  for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
-  if (c->d_deg) (void)hipFree(c->d_deg);
-  if (c->d_ids) (void)hipFree(c->d_ids);
-  if (c->d_state) (void)hipFree(c->d_state);
-  if (c->d_cnt) (void)hipFree(c->d_cnt);
-  if (c->d_failed) (void)hipFree(c->d_failed);
-  if (c->d_win) (void)hipFree(c->d_win);
-  if (c->d_flist) (void)hipFree(c->d_flist);
-  for (gs_ctx::Buf* b : {&c->gmap, &c->cmsg, &c->fmsg, &c->tmp})
-    if (b->p) (void)hipFree(b->p);
-  if (c->h_cap) (void)hipHostFree(c->h_cap);
-  if (c->h_misc) (void)hipHostFree(c->h_misc);
-  if (c->h_stats) (void)hipHostFree(c->h_stats);
-  if (c->own) (void)hipStreamDestroy(c->own);
-  delete c;
+  if (lo) *lo = a;
+  if (hi) *hi = b;
+  return GS_OK;
 }
 
-int gs_load_peers(gs_ctx* c, const uint8_t* deg, const uint32_t* ids, uint32_t stride) {
-  if (!c || !deg || !ids || stride == 0 || stride > 255) return fail(c, GS_EINVAL, "bad peer table");
-  if (c->begun) return fail(c, GS_EINVAL, "peers must be loaded before gs_broadcast_begin");
+void gs_destroy(gs_ctx* c) { destroy_one(c); }
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Peer tables
+// ---------------------------------------------------------------------------
+namespace {
+
+// Uploads a host table into `c`'s table buffers (c = a plain/batched context,
+// or the device leader of shards) and validates it.
+int upload_table(gs_ctx* c, const uint8_t* deg, const uint32_t* ids, uint32_t stride) {
   CK(c, hipSetDevice(c->dev));
   const uint32_t S = stride < 2 ? 2 : stride;
-  int rc = alloc_table(c, S);
-  if (rc) return rc;
-  const uint64_t n = c->p.n;
+  RC(alloc_table(c, S));
+  const uint64_t n = table_n(c);
+  if (c->trials > 1) {  // trial tables back to back -> the padded id space
+    const uint64_t np = c->p.n, per = 1ull << c->tlog;
+    std::vector<uint8_t> hd(n, 0);
+    std::vector<uint32_t> hi(n * S, 0);
+    for (uint32_t t = 0; t < c->trials; ++t)
+      for (uint64_t v = 0; v < np; ++v) {
+        const uint64_t src = t * np + v, dst = t * per + v;
+        const uint32_t d = deg[src];
+        if (d > stride) return fail(c, GS_EINVAL, "a friends-list length exceeds the row stride");
+        hd[dst] = (uint8_t)d;
+        for (uint32_t j = 0; j < d; ++j) {
+          const uint32_t x = ids[src * stride + j];
+          if (x >= np) return fail(c, GS_EINVAL, "a friend id is >= n");
+          hi[dst * S + j] = (uint32_t)(t * per) | x;
+        }
+      }
+    CK(c, hipMemcpyAsync(c->d_deg, hd.data(), n, hipMemcpyHostToDevice, c->stream));
+    CK(c, hipMemcpyAsync(c->d_ids, hi.data(), n * S * 4, hipMemcpyHostToDevice, c->stream));
+    CK(c, hipStreamSynchronize(c->stream));
+    return GS_OK;
+  }
   CK(c, hipMemcpyAsync(c->d_deg, deg, n, hipMemcpyHostToDevice, c->stream));
   if (S == stride) {
     CK(c, hipMemcpyAsync(c->d_ids, ids, n * S * 4, hipMemcpyHostToDevice, c->stream));
@@ -453,10 +806,62 @@ int gs_load_peers(gs_ctx* c, const uint8_t* deg, const uint32_t* ids, uint32_t s
     CK(c, hipMemcpyAsync(c->d_ids, tmp.data(), n * S * 4, hipMemcpyHostToDevice, c->stream));
     CK(c, hipStreamSynchronize(c->stream));
   }
-  rc = validate_table(c);
-  if (rc) return rc;
-  rc = seal_rows(c);
-  if (rc) return rc;
+  return validate_table(c, c->d_deg, c->d_ids, n, c->p.n);
+}
+
+// Shards: partition every member on the leader's device from the leader's
+// sealed table, then drop the replicated table.
+int partition_from(gs_ctx* leader, const std::vector<gs_ctx*>& ms) {
+  for (gs_ctx* m : ms) {
+    if (m != leader) {
+      RC(set_stride(m, leader->st.stride));
+      CK(m, hipStreamSynchronize(leader->stream));
+    }
+    RC(partition(m, leader->d_ids));
+    m->peers = true;
+  }
+  free_table(leader);
+  return GS_OK;
+}
+
+// Members sharing device d (group) or just c.
+std::vector<gs_ctx*> on_device(gs_ctx* g, size_t d) {
+  std::vector<gs_ctx*> v;
+  for (size_t i = 0; i < g->mem.size(); ++i)
+    if ((size_t)g->gdev_of[i] == d) v.push_back(g->mem[i]);
+  return v;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_load_peers(gs_ctx* c, const uint8_t* deg, const uint32_t* ids, uint32_t stride) {
+  if (!c || !deg || !ids || stride == 0 || stride > 255) return fail(c, GS_EINVAL, "bad peer table");
+  if (c->begun) return fail(c, GS_EINVAL, "peers must be loaded before gs_broadcast_begin");
+  if (c->group && c->gtrials) {
+    uint64_t off = 0;
+    for (gs_ctx* m : c->mem) {
+      RC(gs_load_peers(m, deg + off * c->p.n, ids + off * c->p.n * stride, stride) ? fail(c, GS_EINVAL, m->err) : 0);
+      off += m->trials;
+    }
+    c->peers = true;
+    return GS_OK;
+  }
+  if (c->group) {
+    for (size_t d = 0; d < c->gdevs.size(); ++d) {
+      std::vector<gs_ctx*> ms = on_device(c, d);
+      int rc = upload_table(ms[0], deg, ids, stride);
+      if (!rc) rc = seal_rows(ms[0], ms[0]->d_deg, ms[0]->d_ids, c->p.n);
+      if (!rc) rc = partition_from(ms[0], ms);
+      if (rc) return fail(c, rc, ms[0]->err);
+    }
+    c->peers = true;
+    return GS_OK;
+  }
+  RC(upload_table(c, deg, ids, stride));
+  RC(seal_rows(c, c->d_deg, c->d_ids, table_n(c)));
+  if (c->shard) RC(partition_from(c, {c}));
   c->peers = true;
   return GS_OK;
 }
@@ -465,29 +870,67 @@ int gs_load_peers_device(gs_ctx* c, const void* d_deg, const void* d_ids, uint32
   if (!c || !d_deg || !d_ids || stride < 2 || stride > 255)
     return fail(c, GS_EINVAL, "bad device peer table (stride must be in [2,255])");
   if (c->begun) return fail(c, GS_EINVAL, "peers must be loaded before gs_broadcast_begin");
+  if (c->group || c->trials > 1)
+    return fail(c, GS_EINVAL, "device tables load into one-device, one-trial contexts");
   CK(c, hipSetDevice(c->dev));
-  int rc = alloc_table(c, stride);
-  if (rc) return rc;
-  CK(c, hipMemcpyAsync(c->d_deg, d_deg, c->p.n, hipMemcpyDeviceToDevice, c->stream));
-  CK(c, hipMemcpyAsync(c->d_ids, d_ids, c->p.n * stride * 4ull, hipMemcpyDeviceToDevice, c->stream));
-  rc = validate_table(c);
-  if (rc) return rc;
-  rc = seal_rows(c);
-  if (rc) return rc;
+  RC(alloc_table(c, stride));
+  const uint64_t n = table_n(c);
+  CK(c, hipMemcpyAsync(c->d_deg, d_deg, n, hipMemcpyDeviceToDevice, c->stream));
+  CK(c, hipMemcpyAsync(c->d_ids, d_ids, n * stride * 4ull, hipMemcpyDeviceToDevice, c->stream));
+  RC(validate_table(c, c->d_deg, c->d_ids, n, c->p.n));
+  RC(seal_rows(c, c->d_deg, c->d_ids, n));
+  if (c->shard) RC(partition_from(c, {c}));
   c->peers = true;
   return GS_OK;
 }
 
 int gs_read_peers(gs_ctx* c, uint8_t* deg, uint32_t* ids, uint32_t* stride_out) {
   if (!c || !c->peers) return fail(c, GS_EINVAL, "no peer table");
+  if (c->group && c->gtrials) {
+    uint32_t s = 0;
+    uint64_t off = 0;
+    for (gs_ctx* m : c->mem) {
+      if (gs_read_peers(m, deg ? deg + off * c->p.n : nullptr, nullptr, &s)) return fail(c, GS_EINVAL, m->err);
+      if (ids && gs_read_peers(m, nullptr, ids + off * c->p.n * s, &s)) return fail(c, GS_EINVAL, m->err);
+      off += m->trials;
+    }
+    if (stride_out) *stride_out = s;
+    return GS_OK;
+  }
+  if (c->group || c->shard)
+    return fail(c, GS_EINVAL, "a sharded context keeps only its partition of the table");
   if (stride_out) *stride_out = c->st.stride;
   CK(c, hipSetDevice(c->dev));
+  const uint32_t S = c->st.stride;
+  if (c->trials > 1) {  // padded id space -> trial tables back to back, local ids
+    const uint64_t np = c->p.n, per = 1ull << c->tlog;
+    std::vector<uint8_t> hd(c->ntot);
+    std::vector<uint32_t> hi;
+    CK(c, hipMemcpyAsync(hd.data(), c->d_deg, c->ntot, hipMemcpyDeviceToHost, c->stream));
+    if (ids) {
+      hi.resize(c->ntot * S);
+      CK(c, hipMemcpyAsync(hi.data(), c->d_ids, c->ntot * S * 4ull, hipMemcpyDeviceToHost, c->stream));
+    }
+    CK(c, hipStreamSynchronize(c->stream));
+    for (uint32_t t = 0; t < c->trials; ++t)
+      for (uint64_t v = 0; v < np; ++v) {
+        const uint64_t src = t * per + v, dst = t * np + v;
+        if (deg) deg[dst] = hd[src];
+        if (ids)
+          for (uint32_t j = 0; j < S; ++j) {
+            const uint32_t x = hi[src * S + j];
+            ids[dst * S + j] = x == kEmptyMsg ? x : (x & ((uint32_t)per - 1));
+          }
+      }
+    return GS_OK;
+  }
   if (deg) CK(c, hipMemcpyAsync(deg, c->d_deg, c->p.n, hipMemcpyDeviceToHost, c->stream));
-  if (ids)
-    CK(c, hipMemcpyAsync(ids, c->d_ids, c->p.n * c->st.stride * 4ull, hipMemcpyDeviceToHost, c->stream));
+  if (ids) CK(c, hipMemcpyAsync(ids, c->d_ids, c->p.n * S * 4ull, hipMemcpyDeviceToHost, c->stream));
   CK(c, hipStreamSynchronize(c->stream));
   return GS_OK;
 }
+
+}  // extern "C"
 
 namespace {
 struct WinSink {
@@ -499,108 +942,213 @@ struct WinSink {
     ++w->n;
   }
 };
-}  // namespace
 
-int gs_build_overlay(gs_ctx* c, uint64_t max_ticks, gs_window* win, size_t cap, size_t* nwin,
-                     uint64_t* final_tick) {
-  if (!c) return GS_EINVAL;
-  if (c->begun) return fail(c, GS_EINVAL, "overlay must be built before gs_broadcast_begin");
+// The overlay of c's table_n(c) nodes (all trials of a batched context) into
+// c's table buffers.
+int overlay_into(gs_ctx* c, uint64_t max_ticks, gs_window* win, size_t cap, size_t* nwin, uint64_t* final_tick) {
   CK(c, hipSetDevice(c->dev));
   const uint32_t fo = (uint32_t)c->p.fanout, fi = (uint32_t)c->p.fanin;
   uint32_t stride = fo > fi ? fo : fi;
   if (stride < 2) stride = 2;
-  int rc = alloc_table(c, stride);
-  if (rc) return rc;
-  CK(c, hipMemsetAsync(c->d_ids, 0, c->p.n * stride * 4ull, c->stream));
-  CK(c, hipMemsetAsync(c->d_deg, 0, c->p.n, c->stream));
+  RC(alloc_table(c, stride));
+  const uint64_t n = table_n(c);
+  CK(c, hipMemsetAsync(c->d_ids, 0, n * stride * 4ull, c->stream));
+  CK(c, hipMemsetAsync(c->d_deg, 0, n, c->stream));
   WinSink ws{win, cap, 0};
   OverlayResult res;
   const auto t0 = std::chrono::steady_clock::now();
-  rc = overlay_build(c->p.n, c->p.fanout, c->p.fanin, c->p.delay_low, c->p.delay_high, c->st.key,
-                     c->d_deg, c->d_ids, stride, max_ticks, c->stream,
-                     OverlayWindowSink{&WinSink::push, &ws}, &res);
+  const int rc = overlay_build(c->p.n, c->trials, c->tlog, c->p.fanout, c->p.fanin, c->p.delay_low,
+                               c->p.delay_high, c->st.key, c->d_deg, c->d_ids, stride, max_ticks, c->stream,
+                               OverlayWindowSink{&WinSink::push, &ws}, &res);
   c->timing.overlay_ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (nwin) *nwin = ws.n;
   if (final_tick) *final_tick = res.final_tick;
   if (rc) return fail(c, rc, res.msg);
-  rc = seal_rows(c);
-  if (rc) return rc;
+  return seal_rows(c, c->d_deg, c->d_ids, n);
+}
+}  // namespace
+
+extern "C" {
+
+int gs_build_overlay(gs_ctx* c, uint64_t max_ticks, gs_window* win, size_t cap, size_t* nwin,
+                     uint64_t* final_tick) {
+  if (!c) return GS_EINVAL;
+  if (c->begun) return fail(c, GS_EINVAL, "overlay must be built before gs_broadcast_begin");
+  if (c->group && c->gtrials) {
+    std::vector<uint64_t> ft(c->mem.size(), 0);
+    std::vector<size_t> nw(c->mem.size(), 0);
+    std::vector<gs_ctx*>& ms = c->mem;
+    RC(par_members(c, [&](gs_ctx* m) {
+      const size_t i = (size_t)(std::find(ms.begin(), ms.end(), m) - ms.begin());
+      return gs_build_overlay(m, max_ticks, i == 0 ? win : nullptr, i == 0 ? cap : 0, &nw[i], &ft[i]);
+    }));
+    if (nwin) *nwin = nw[0];
+    if (final_tick) *final_tick = *std::max_element(ft.begin(), ft.end());
+    c->timing.overlay_ms = c->mem[0]->timing.overlay_ms;
+    c->peers = true;
+    return GS_OK;
+  }
+  if (c->group) {
+    for (size_t d = 0; d < c->gdevs.size(); ++d) {
+      std::vector<gs_ctx*> ms = on_device(c, d);
+      int rc = overlay_into(ms[0], max_ticks, d == 0 ? win : nullptr, d == 0 ? cap : 0,
+                            d == 0 ? nwin : nullptr, d == 0 ? final_tick : nullptr);
+      if (!rc) rc = partition_from(ms[0], ms);
+      if (rc) return fail(c, rc, ms[0]->err);
+    }
+    c->timing.overlay_ms = c->mem[0]->timing.overlay_ms;
+    c->peers = true;
+    return GS_OK;
+  }
+  RC(overlay_into(c, max_ticks, win, cap, nwin, final_tick));
+  if (c->shard) RC(partition_from(c, {c}));
   c->peers = true;
   return GS_OK;
 }
 
 int gs_set_failed(gs_ctx* c, const uint64_t* words, size_t nwords) {
-  if (!c || !words || nwords < c->st.W) return fail(c, GS_EINVAL, "mask needs ceil(n/64) words");
+  if (!c || !words || nwords < (c->p.n + 63) / 64) return fail(c, GS_EINVAL, "mask needs ceil(n/64) words");
   if (c->begun) return fail(c, GS_EINVAL, "failure mask must be set before gs_broadcast_begin");
+  if (c->trials > 1) return fail(c, GS_EINVAL, "failure masks are not supported for batched trials");
+  if (c->group) {
+    for (gs_ctx* m : c->mem)
+      if (gs_set_failed(m, words, nwords)) return fail(c, GS_EINVAL, m->err);
+    c->failed = true;
+    return GS_OK;
+  }
   CK(c, hipSetDevice(c->dev));
-  std::vector<uint64_t> w(words, words + c->st.W);
-  if (c->p.n & 63) w[c->st.W - 1] &= (1ull << (c->p.n & 63)) - 1;
-  if (!c->d_failed && hipMalloc(&c->d_failed, c->st.W * 8) != hipSuccess)
+  const uint64_t W = c->st.W, w0 = c->lo / 64;  // this context's words (a shard's own range)
+  std::vector<uint64_t> w(words + w0, words + w0 + W);
+  if (c->ntot & 63) w[W - 1] &= (1ull << (c->ntot & 63)) - 1;
+  if (!c->d_failed && hipMalloc(&c->d_failed, W * 8) != hipSuccess)
     return fail(c, GS_ENOMEM, "cannot allocate the failure mask");
-  CK(c, hipMemcpyAsync(c->d_failed, w.data(), c->st.W * 8, hipMemcpyHostToDevice, c->stream));
-  CK(c, hipMemcpyAsync(c->st.crash, c->d_failed, c->st.W * 8, hipMemcpyDeviceToDevice, c->stream));
+  CK(c, hipMemcpyAsync(c->d_failed, w.data(), W * 8, hipMemcpyHostToDevice, c->stream));
+  CK(c, hipMemcpyAsync(c->st.crash, c->d_failed, W * 8, hipMemcpyDeviceToDevice, c->stream));
   CK(c, hipStreamSynchronize(c->stream));
   c->failed = true;
   c->st.check_crashed = 1;
   return GS_OK;
 }
 
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Broadcast
+// ---------------------------------------------------------------------------
+namespace {
+
+// Is local node `u` of c crashed (a pre-failed mask)?
+int is_failed(gs_ctx* c, uint64_t u, bool* out) {
+  *out = false;
+  if (!c->failed) return GS_OK;
+  unsigned long long w = 0;
+  CK(c, hipMemcpyAsync(&w, c->st.crash + u / 64, 8, hipMemcpyDeviceToHost, c->stream));
+  CK(c, hipStreamSynchronize(c->stream));
+  *out = (w >> (u & 63)) & 1;
+  return GS_OK;
+}
+
+uint64_t keyed_sender(const gs_ctx* c) {
+  return uniform(draw0(c->st.key, K_SENDER, 0, 0, 0), (uint32_t)c->p.n);  // simulator.go:240
+}
+
+// Schedules the global sender s if c owns it (and it is live); *sched = 1 if so.
+int begin_one(gs_ctx* c, uint64_t s, uint32_t* sched) {
+  *sched = 0;
+  CK(c, hipSetDevice(c->dev));
+  if (c->trials > 1) {  // every trial's sender (:240 per trial when s == ~0)
+    CK(c, win_schedule(c->ws, (uint32_t)s, 0, c->trials, (uint32_t)c->p.n, c->stream));
+    CK(c, hipStreamSynchronize(c->stream));
+    *sched = c->trials;
+    return GS_OK;
+  }
+  if (s < c->lo || s >= (c->shard ? c->hi : c->p.n)) return GS_OK;  // another shard's node
+  const uint64_t u = s - c->lo;
+  bool dead = false;
+  RC(is_failed(c, u, &dead));
+  if (dead) return GS_OK;  // a failed sender never broadcasts
+  if (c->win) CK(c, win_schedule(c->ws, (uint32_t)u, 0, 1, (uint32_t)c->p.n, c->stream));
+  else CK(c, launch_schedule_one(c->st, (uint32_t)u, 0, c->stream));
+  CK(c, hipStreamSynchronize(c->stream));
+  *sched = 1;
+  return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int gs_broadcast_begin(gs_ctx* c, int64_t sender) {
   if (!c) return GS_EINVAL;
   if (!c->peers) return fail(c, GS_EINVAL, "load peers or build the overlay first");
   if (c->begun) return fail(c, GS_EINVAL, "broadcast already begun");
-  uint64_t s = sender < 0 ? uniform(draw0(c->st.key, K_SENDER, 0, 0, 0), (uint32_t)c->p.n)
-                          : (uint64_t)sender;
-  if (s >= c->p.n) return fail(c, GS_EINVAL, "sender out of range");
-  CK(c, hipSetDevice(c->dev));
+  if (sender >= 0 && (uint64_t)sender >= c->p.n) return fail(c, GS_EINVAL, "sender out of range");
+  reset_counters(c);
+  if (c->group && c->gtrials) {
+    for (gs_ctx* m : c->mem)
+      if (gs_broadcast_begin(m, sender)) return fail(c, GS_EINVAL, m->err);
+    c->pending = c->trials;
+    c->begun = true;
+    return GS_OK;
+  }
+  const bool batched = c->trials > 1;
+  const uint64_t s = sender >= 0 ? (uint64_t)sender : batched ? ~0ull : keyed_sender(c->group ? c->mem[0] : c);
   if (c->pp) {  // push-pull: the sender is informed (unless failed)
+    CK(c, hipSetDevice(c->dev));
     CK(c, pp_seed(c->st, c->d_next, (uint32_t)s, c->d_flag, c->stream));
     uint32_t ok = 0;
     CK(c, hipMemcpyAsync(&ok, c->d_flag, 4, hipMemcpyDeviceToHost, c->stream));
     CK(c, hipStreamSynchronize(c->stream));
-    c->t = 0;
     c->recv = c->pending = ok;
     c->begun = true;
     return GS_OK;
   }
-  const bool mine = s >= c->st.lo && s < c->st.hi;  // only the sender's owner schedules it
-  if (mine && c->win) CK(c, win_schedule_one(c->ws, (uint32_t)s, 0, c->stream));
-  else if (mine) CK(c, launch_schedule_one(c->st, (uint32_t)s, 0, c->stream));
-  CK(c, hipStreamSynchronize(c->stream));
-  c->t = 0;
-  c->pending = mine ? 1 : 0;
+  uint64_t scheduled = 0;
+  if (c->group) {
+    for (gs_ctx* m : c->mem) {
+      reset_counters(m);
+      uint32_t k = 0;
+      if (int rc = begin_one(m, s, &k)) return fail(c, rc, m->err);
+      scheduled += k;
+      m->begun = true;
+    }
+  } else {
+    uint32_t k = 0;
+    RC(begin_one(c, s, &k));
+    scheduled = k;
+    if (c->comm) {  // every rank learns whether the owner scheduled the sender
+      unsigned long long* d = c->d_gcounts;  // scratch
+      unsigned long long h = scheduled;
+      CK(c, hipMemcpyAsync(d, &h, 8, hipMemcpyHostToDevice, c->stream));
+      NCK(c, rccl().all_reduce(d, d, 1, ncclUint64, ncclSum, c->comm, c->stream));
+      CK(c, hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, c->stream));
+      CK(c, hipStreamSynchronize(c->stream));
+      scheduled = h;
+    }
+  }
+  c->pending = scheduled;
+  for (TrialAcc& a : c->tacc) a.sched = 0;
   c->begun = true;
   return GS_OK;
 }
 
 int gs_set_stream(gs_ctx* c, void* hip_stream) {
   if (!c) return GS_EINVAL;
+  if (c->group || c->comm) return fail(c, GS_EINVAL, "multi-device contexts keep their own streams");
+  CK(c, hipSetDevice(c->dev));
   CK(c, hipStreamSynchronize(c->stream));
   c->stream = hip_stream ? (hipStream_t)hip_stream : c->own;
   return GS_OK;
 }
 
-int gs_frontier_export(gs_ctx* c, uint64_t tick, void* dst, uint64_t word_lo, uint64_t nwords) {
-  if (!c || !dst || word_lo + nwords > c->st.W) return fail(c, GS_EINVAL, "bad frontier range");
-  if (!nwords) return GS_OK;
-  const size_t slot = (size_t)(tick % c->st.R);
-  CK(c, hipMemcpyAsync(dst, c->st.ring + slot * c->st.W + word_lo, nwords * 8,
-                       hipMemcpyDeviceToDevice, c->stream));
-  return GS_OK;
-}
+}  // extern "C"
 
-int gs_frontier_import(gs_ctx* c, uint64_t tick, const void* src) {
-  if (!c || !src) return fail(c, GS_EINVAL, "bad frontier source");
-  const size_t slot = (size_t)(tick % c->st.R);
-  CK(c, hipMemcpyAsync(c->st.ring + slot * c->st.W, src, c->st.W * 8, hipMemcpyDeviceToDevice,
-                       c->stream));
-  return GS_OK;
-}
+namespace {
 
-// Window engine: ticks [t0, t0 + n) as windows of <= min(max(delaylow,1),16)
+// Window engine: ticks [t0, t0 + n) as windows of <= min(max(delaylow,1),10)
 // ticks (gs_window.hip).  One host sync per window reads its task count.
-static int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing) {
+int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing, uint64_t tchunk) {
   WinState& w = c->ws;
   const uint32_t Lmax = std::min<uint32_t>(std::max<int32_t>(c->p.delay_low, 1), kBitTicks);
   uint32_t done = 0, widx = 0;
@@ -611,6 +1159,7 @@ static int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing) {
   while (done < n) {
     const uint32_t Lw = std::min(Lmax, n - done);
     const uint32_t t = (uint32_t)(t0 + done);
+    w.tofs = (uint32_t)(t - tchunk);
     auto units = [&](uint32_t Lu) -> int {
       CK(c, hipMemsetAsync(w.tfires, 0, kMaxWindow * 8, c->stream));
       CK(c, win_units(w, t, Lu, c->stream));
@@ -623,14 +1172,13 @@ static int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing) {
       CK(c, hipStreamSynchronize(c->stream));
       return GS_OK;
     };
-    if (int rc = units(Lw)) return rc;
+    RC(units(Lw));
     // fires per tick -> the window's length under the slot budget
     uint32_t L = 1;
     unsigned long long Tn = c->h_misc[0];  // broadcasts firing in the window
     while (L < Lw && (Tn + c->h_misc[L]) * w.stride <= slot_budget) Tn += c->h_misc[L++];
     // units are bucket-major: a cut window is laid out again for its L ticks
-    if (L < Lw)
-      if (int rc = units(L)) return rc;
+    if (L < Lw) RC(units(L));
     const unsigned long long T = Tn * w.stride;  // friend slots of the firing nodes
     plan_coarse(c, T, nullptr);
     const uint64_t fcap = T + T / 8 + (uint64_t)w.ncoarse * 256 * 513 + 16;
@@ -730,15 +1278,358 @@ static int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing) {
   return GS_OK;
 }
 
-int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
-  if (!c) return GS_EINVAL;
-  if (!c->begun) return fail(c, GS_EINVAL, "gs_broadcast_begin first");
-  CK(c, hipSetDevice(c->dev));
-  const bool timing = (c->p.flags & GS_FLAG_TIMING) != 0;
-  const bool flood = c->st.kc == 0;
+// ---- node-range shards ------------------------------------------------------
+// One window for shards `ms` (all shards of a group, or this rank's one shard
+// with an RCCL communicator), SURVEY.md section 8(e)2:
+//   1. each shard counts its fires per tick; the counts are gathered
+//      (host reads / RCCL all-gather) so every shard cuts the same window;
+//   2. each shard compacts its window fires; the lists are all-gathered
+//      (device copies / RCCL all-gather, in place);
+//   3. each shard expands EVERY firing node against its partition of the
+//      table and partitions / resolves its own buckets.
+int sync_all(const std::vector<gs_ctx*>& ms) {
+  for (gs_ctx* m : ms) {
+    CK(m, hipSetDevice(m->dev));
+    CK(m, hipStreamSynchronize(m->stream));
+  }
+  return GS_OK;
+}
+
+int shard_units(gs_ctx* m, uint32_t t, uint32_t Lu, bool gather) {
+  WinState& w = m->ws;
+  CK(m, hipSetDevice(m->dev));
+  CK(m, hipMemsetAsync(w.tfires, 0, kMaxWindow * 8, m->stream));
+  CK(m, win_units(w, t, Lu, m->stream));
+  size_t need = 0;
+  CK(m, win_scan_units(w, Lu, nullptr, need, m->stream));
+  if (!grow(m->tmp, need)) return fail(m, GS_ENOMEM, "cannot allocate scan scratch");
+  need = m->tmp.bytes;
+  CK(m, win_scan_units(w, Lu, m->tmp.p, need, m->stream));
+  if (!gather) return GS_OK;
+  if (m->comm) {
+    NCK(m, rccl().all_gather(w.tfires, m->d_gcounts, kMaxWindow, ncclUint64, m->comm, m->stream));
+    CK(m, hipMemcpyAsync(m->h_misc, m->d_gcounts, (size_t)m->G * kMaxWindow * 8, hipMemcpyDeviceToHost,
+                         m->stream));
+  } else {
+    CK(m, hipMemcpyAsync(m->h_misc, w.tfires, kMaxWindow * 8, hipMemcpyDeviceToHost, m->stream));
+  }
+  return GS_OK;
+}
+
+int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint32_t n, bool timing) {
+  gs_ctx* m0 = ms[0];
+  const uint32_t G = m0->G;
+  const uint64_t N = m0->p.n;
+  const uint32_t stride = m0->ws.stride;
+  const uint32_t Lmax = std::min<uint32_t>(std::max<int32_t>(m0->p.delay_low, 1), kBitTicks);
+  const uint64_t slot_budget = ((N + kFineNodes - 1) >> kFineLog) * (uint64_t)kWinSlotsPerBucket;
+  std::vector<unsigned long long> cnt((size_t)G * kMaxWindow);
+  uint32_t done = 0;
+  while (done < n) {
+    const uint32_t Lw = std::min(Lmax, n - done);
+    const uint32_t t = (uint32_t)(t0 + done);
+    for (gs_ctx* m : ms) RC(shard_units(m, t, Lw, true));
+    RC(sync_all(ms));
+    for (uint32_t r = 0; r < G; ++r)
+      for (uint32_t k = 0; k < kMaxWindow; ++k)
+        cnt[(size_t)r * kMaxWindow + k] = m0->comm ? m0->h_misc[(size_t)r * kMaxWindow + k]
+                                                   : (k < Lw ? ms[r]->h_misc[k] : 0ull);
+    auto F = [&](uint32_t k) {
+      unsigned long long s = 0;
+      for (uint32_t r = 0; r < G; ++r) s += cnt[(size_t)r * kMaxWindow + k];
+      return s;
+    };
+    // the same cut on every shard (global counts), as the unsharded engine would
+    uint32_t L = 1;
+    unsigned long long Tn = F(0);
+    while (L < Lw && (Tn + F(L)) * stride <= slot_budget) Tn += F(L++);
+    if (L < Lw)
+      for (gs_ctx* m : ms) RC(shard_units(m, t, L, false));
+    unsigned long long seg = 0;
+    std::vector<unsigned long long> own(G, 0);
+    for (uint32_t r = 0; r < G; ++r) {
+      for (uint32_t k = 0; k < L; ++k) own[r] += cnt[(size_t)r * kMaxWindow + k];
+      seg = std::max(seg, own[r]);
+    }
+    if (seg) {
+      // 2. compaction into segment `rank` of the device's all-gather buffer
+      for (size_t i = 0; i < ms.size(); ++i) {
+        gs_ctx* m = ms[i];
+        WinState& w = m->ws;
+        CK(m, hipSetDevice(m->dev));
+        Buf* b = &m->gfire;
+        if (acc->group) b = &acc->gbuf[acc->gdev_of[i]];
+        if (!grow(*b, (size_t)G * seg * 4)) return fail(m, GS_ENOMEM, "cannot allocate the window fire lists");
+        if (!grow(m->gmap, ((own[m->rank] + 63) / 64 + 1) * 4))
+          return fail(m, GS_ENOMEM, "cannot allocate the group map");
+        w.gmap = (uint32_t*)m->gmap.p;
+        w.gfire = (const uint32_t*)b->p;
+        w.gseg = seg;
+        CK(m, win_groupmap(w, L, m->stream));
+        CK(m, win_fire_compact(w, t, L, own[m->rank], (uint32_t*)b->p + (size_t)m->rank * seg, seg, m->stream));
+        if (acc->group) CK(m, hipEventRecord(acc->gev_c[i], m->stream));
+      }
+      // ... all-gathered
+      if (m0->comm) {
+        uint32_t* buf = (uint32_t*)m0->gfire.p;
+        NCK(m0, rccl().all_gather(buf + (size_t)m0->rank * seg, buf, seg, ncclUint32, m0->comm, m0->stream));
+      } else {
+        // each device's leader copies the other devices' segments in; every
+        // member waits for the compactions it reads
+        std::vector<int> done_dev(acc->gdevs.size(), 0);
+        for (size_t i = 0; i < ms.size(); ++i) {
+          gs_ctx* m = ms[i];
+          const int d = acc->gdev_of[i];
+          CK(m, hipSetDevice(m->dev));
+          if (done_dev[d]) {
+            CK(m, hipStreamWaitEvent(m->stream, acc->gev_x[d], 0));
+            continue;
+          }
+          done_dev[d] = 1;
+          for (size_t j = 0; j < ms.size(); ++j) {
+            if (j == i) continue;
+            CK(m, hipStreamWaitEvent(m->stream, acc->gev_c[j], 0));
+            const int dj = acc->gdev_of[j];
+            if (dj != d)
+              CK(m, hipMemcpyPeerAsync((uint32_t*)acc->gbuf[d].p + (size_t)ms[j]->rank * seg, m->dev,
+                                       (uint32_t*)acc->gbuf[dj].p + (size_t)ms[j]->rank * seg, ms[j]->dev,
+                                       seg * 4, m->stream));
+          }
+          CK(m, hipEventRecord(acc->gev_x[d], m->stream));
+        }
+      }
+      // 3. expand + partition
+      unsigned long long Ftot = 0;
+      for (uint32_t k = 0; k < L; ++k) Ftot += F(k);
+      for (gs_ctx* m : ms) {
+        WinState& w = m->ws;
+        CK(m, hipSetDevice(m->dev));
+        const unsigned long long Tub = Ftot * stride;  // bound on this shard's messages
+        const unsigned long long Test = (unsigned long long)((long double)Tub * (long double)m->ntot / (long double)N);
+        plan_coarse(m, Test, nullptr);
+        const uint64_t fcap = Tub + Tub / 8 + (uint64_t)w.ncoarse * 256 * 513 + 16;
+        if (!grow(m->cmsg, (m->h_cap[256] + 16) * 4) || !grow(m->fmsg, fcap * 4))
+          return fail(m, GS_ENOMEM, "cannot allocate " + std::to_string(Tub) + " window messages");
+        w.cmsg = (uint32_t*)m->cmsg.p;
+        w.fmsg = (uint32_t*)m->fmsg.p;
+        w.tofs = 0;
+        if (timing)
+          while (m->ev.size() < 5) {
+            hipEvent_t ev;
+            CK(m, hipEventCreate(&ev));
+            m->ev.push_back(ev);
+          }
+        hipEvent_t* e = timing ? &m->ev[0] : nullptr;
+        CK(m, hipMemcpyAsync(w.ccap, m->h_cap, 257 * 8, hipMemcpyHostToDevice, m->stream));
+        if (e) CK(m, hipEventRecord(e[0], m->stream));
+        CK(m, win_expand_sh(w, t, L, 1, m->stream));
+        if (e) CK(m, hipEventRecord(e[1], m->stream));
+        CK(m, win_plan(w, false, m->stream));
+        CK(m, win_part2(w, Tub, true, m->stream));
+        if (e) CK(m, hipEventRecord(e[2], m->stream));
+        CK(m, hipMemcpyAsync(m->h_misc + 1020, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
+      }
+      RC(sync_all(ms));
+      for (gs_ctx* m : ms) {  // regions sized from estimates: redo exactly on overflow
+        WinState& w = m->ws;
+        uint32_t err = (uint32_t)m->h_misc[1020];
+        const unsigned long long Tub = Ftot * stride;
+        if (err & kErrCoarse) {
+          CK(m, hipMemsetAsync(w.chist, 0, 256 * 8, m->stream));
+          CK(m, win_expand_sh(w, t, L, 0, m->stream));
+          CK(m, hipMemcpyAsync(m->h_misc, w.chist, 256 * 8, hipMemcpyDeviceToHost, m->stream));
+          CK(m, hipStreamSynchronize(m->stream));
+          plan_coarse(m, Tub, m->h_misc);
+          if (!grow(m->cmsg, (m->h_cap[256] + 16) * 4))
+            return fail(m, GS_ENOMEM, "cannot allocate the window messages");
+          w.cmsg = (uint32_t*)m->cmsg.p;
+          CK(m, hipMemcpyAsync(w.ccap, m->h_cap, 257 * 8, hipMemcpyHostToDevice, m->stream));
+          CK(m, hipMemsetAsync(w.cfill, 0, 256 * 8, m->stream));
+          CK(m, win_expand_sh(w, t, L, 2, m->stream));
+          CK(m, win_plan(w, false, m->stream));
+          err = kErrFine;
+        }
+        if (err & kErrFine) {
+          CK(m, hipMemsetAsync(w.fhist, 0, ((size_t)w.ncoarse * 256 + 1) * 8, m->stream));
+          CK(m, win_plan(w, true, m->stream));
+          CK(m, win_part2(w, Tub, false, m->stream));
+          size_t need2 = 0;
+          CK(m, win_scan_fine(w, nullptr, need2, m->stream));
+          if (!grow(m->tmp, need2)) return fail(m, GS_ENOMEM, "cannot allocate scan scratch");
+          need2 = m->tmp.bytes;
+          CK(m, win_scan_fine(w, m->tmp.p, need2, m->stream));
+          CK(m, hipMemsetAsync(w.ffill, 0, (size_t)w.nfine * 8, m->stream));
+          CK(m, win_part2(w, Tub, true, m->stream));
+          ++m->timing.exact_redos;
+        }
+      }
+    }
+    for (gs_ctx* m : ms) {  // consume the window's fire lists, resolve own buckets
+      WinState& w = m->ws;
+      CK(m, hipSetDevice(m->dev));
+      const uint32_t s0 = t % w.R;
+      const uint32_t first = std::min(L, w.R - s0);
+      CK(m, hipMemsetAsync(w.fcount + (size_t)s0 * w.nfine, 0, (size_t)first * w.nfine * 4, m->stream));
+      if (first < L) CK(m, hipMemsetAsync(w.fcount, 0, (size_t)(L - first) * w.nfine * 4, m->stream));
+      if (!seg) continue;
+      hipEvent_t* e = timing ? &m->ev[0] : nullptr;
+      if (e) CK(m, hipEventRecord(e[3], m->stream));
+      CK(m, win_resolve(w, t, L, m->stream));
+      CK(m, win_stats_reduce(w, t, L, m->stream));
+      if (e) {
+        CK(m, hipEventRecord(e[4], m->stream));
+        CK(m, hipStreamSynchronize(m->stream));
+        float ms1 = 0, ms2 = 0, ms3 = 0;
+        CK(m, hipEventElapsedTime(&ms1, e[0], e[1]));
+        CK(m, hipEventElapsedTime(&ms2, e[1], e[2]));
+        CK(m, hipEventElapsedTime(&ms3, e[3], e[4]));
+        m->timing.expand_ms += ms1;
+        m->timing.part_ms += ms2;
+        m->timing.deliver_ms += ms1 + ms2;
+        m->timing.resolve_ms += ms3;
+        m->timing.deliver_launches += 1;
+        m->timing.resolve_launches += 1;
+        m->timing.windows += 1;
+      }
+    }
+    done += L;
+  }
+  for (gs_ctx* m : ms) {
+    CK(m, hipSetDevice(m->dev));
+    CK(m, hipMemcpyAsync(m->h_misc + 1020, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
+  }
+  RC(sync_all(ms));
+  for (gs_ctx* m : ms)
+    if (m->h_misc[1020] & 4) return fail(m, GS_EOVERFLOW, "too many arrivals at one node in one tick");
+  return GS_OK;
+}
+
+// Per-tick host bookkeeping shared by every flood/push-pull context: c's
+// cumulative counters and (one trial) its TrialAcc.
+void account_tick(gs_ctx* c, uint64_t tick, const unsigned long long* s, gs_tick_stats* o) {
+  c->t = tick;
+  c->fired += s[ST_FIRED];
+  c->sent += s[ST_SENT];
+  c->msgs += s[ST_MSGS];
+  c->recv += s[ST_RECV];
+  c->crashed += s[ST_CRASH];
+  // push-pull: every informed node keeps calling
+  c->pending = c->pp ? c->recv : c->pending + s[ST_SCHED] - s[ST_FIRED];
+  if (c->tacc.size() == 1 && c->trials == 1) {
+    TrialAcc& a = c->tacc[0];
+    a.fired = c->fired; a.sent = c->sent; a.msgs = c->msgs; a.recv = c->recv; a.crash = c->crashed;
+    if (!a.tick99 && covered(a.recv, c->p.n)) a.tick99 = tick;
+  }
+  if (o) *o = gs_tick_stats{c->t, s[ST_FIRED], s[ST_SENT], s[ST_MSGS], c->recv, c->crashed, c->pending};
+}
+
+// Sharded step: `acc` keeps the global counters (the group, or the rank).
+int shard_step(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint32_t ticks, gs_tick_stats* out) {
+  const bool timing = (acc->p.flags & GS_FLAG_TIMING) != 0;
+  std::vector<unsigned long long> sum(kStatFields);
   uint32_t done = 0;
   while (done < ticks) {
     const uint32_t batch = std::min<uint32_t>(ticks - done, kStatSlots);
+    const uint64_t t0 = acc->t + 1;
+    const uint32_t i0 = (uint32_t)(t0 % kStatSlots);
+    const uint32_t first = std::min<uint32_t>(batch, kStatSlots - i0);
+    for (gs_ctx* m : ms) {
+      CK(m, hipSetDevice(m->dev));
+      CK(m, hipMemsetAsync(m->st.stats + (size_t)i0 * kStatFields, 0, (size_t)first * kStatFields * 8, m->stream));
+      if (first < batch)
+        CK(m, hipMemsetAsync(m->st.stats, 0, (size_t)(batch - first) * kStatFields * 8, m->stream));
+    }
+    RC(shard_windows(acc, ms, t0, batch, timing));
+    for (gs_ctx* m : ms) {
+      CK(m, hipSetDevice(m->dev));
+      unsigned long long* a = m->st.stats + (size_t)i0 * kStatFields;
+      if (m->comm) {  // the global per-tick counters on every rank
+        NCK(m, rccl().all_reduce(a, a, (size_t)first * kStatFields, ncclUint64, ncclSum, m->comm, m->stream));
+        if (first < batch)
+          NCK(m, rccl().all_reduce(m->st.stats, m->st.stats, (size_t)(batch - first) * kStatFields, ncclUint64,
+                                   ncclSum, m->comm, m->stream));
+      }
+      CK(m, hipMemcpyAsync(m->h_stats + (size_t)i0 * kStatFields, a, (size_t)first * kStatFields * 8,
+                           hipMemcpyDeviceToHost, m->stream));
+      if (first < batch)
+        CK(m, hipMemcpyAsync(m->h_stats, m->st.stats, (size_t)(batch - first) * kStatFields * 8,
+                             hipMemcpyDeviceToHost, m->stream));
+    }
+    RC(sync_all(ms));
+    for (uint32_t i = 0; i < batch; ++i) {
+      const size_t row = (size_t)((t0 + i) % kStatSlots) * kStatFields;
+      for (uint32_t f = 0; f < kStatFields; ++f) {
+        sum[f] = 0;
+        for (gs_ctx* m : ms) sum[f] += m->h_stats[row + f];
+      }
+      account_tick(acc, t0 + i, sum.data(), out ? &out[done + i] : nullptr);
+    }
+    done += batch;
+  }
+  return GS_OK;
+}
+
+// Batched trials: fold one chunk's per-trial counters (h_tstat, `nt` ticks
+// from tick t0) into the trials' running totals.
+void account_trials(gs_ctx* c, uint64_t t0, uint32_t nt) {
+  for (uint32_t tr = 0; tr < c->trials; ++tr) {
+    TrialAcc& a = c->tacc[tr];
+    for (uint32_t k = 0; k < nt; ++k) {
+      const uint32_t* r = c->h_tstat + ((size_t)tr * kMaxWindow + k) * kTStatFields;
+      a.fired += r[TS_FIRED];
+      a.sent += r[TS_SENT];
+      a.msgs += (uint64_t)r[TS_SENT] - r[TS_DEAD];
+      a.recv += r[TS_RECV];
+      a.sched += r[TS_RECV];  // every infection schedules one Broadcast
+      a.crash += r[TS_CRASH];
+      if (!a.tick99 && covered(a.recv, c->p.n)) a.tick99 = t0 + k;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
+  if (!c) return GS_EINVAL;
+  if (!c->begun) return fail(c, GS_EINVAL, "gs_broadcast_begin first");
+  if (c->group && c->gtrials) {
+    std::vector<std::vector<gs_tick_stats>> rows(c->mem.size(), std::vector<gs_tick_stats>(ticks));
+    std::vector<gs_ctx*>& ms = c->mem;
+    RC(par_members(c, [&](gs_ctx* m) {
+      const size_t i = (size_t)(std::find(ms.begin(), ms.end(), m) - ms.begin());
+      return gs_step(m, ticks, rows[i].data());
+    }));
+    std::vector<unsigned long long> s(kStatFields);
+    for (uint32_t k = 0; k < ticks; ++k) {
+      std::fill(s.begin(), s.end(), 0ull);
+      uint64_t pend = 0;
+      for (auto& r : rows) {
+        s[ST_FIRED] += r[k].fired;
+        s[ST_SENT] += r[k].sent;
+        s[ST_MSGS] += r[k].messages;
+        pend += r[k].pending;
+      }
+      uint64_t recv = 0, cr = 0;
+      for (auto& r : rows) { recv += r[k].received; cr += r[k].crashed; }
+      c->t = rows[0][k].tick;
+      c->fired += s[ST_FIRED]; c->sent += s[ST_SENT]; c->msgs += s[ST_MSGS];
+      c->recv = recv; c->crashed = cr; c->pending = pend;
+      if (out) out[k] = gs_tick_stats{c->t, s[ST_FIRED], s[ST_SENT], s[ST_MSGS], recv, cr, pend};
+    }
+    return GS_OK;
+  }
+  if (c->group) return shard_step(c, c->mem, ticks, out);
+  if (c->shard) return shard_step(c, {c}, ticks, out);
+  CK(c, hipSetDevice(c->dev));
+  const bool timing = (c->p.flags & GS_FLAG_TIMING) != 0;
+  const bool flood = c->st.kc == 0;
+  const bool batched = c->trials > 1;
+  uint32_t done = 0;
+  while (done < ticks) {
+    // batched trials: chunks of <= kMaxWindow ticks (the per-trial counter rows)
+    const uint32_t batch = std::min<uint32_t>(ticks - done, batched ? kMaxWindow : kStatSlots);
     const uint64_t t0 = c->t + 1;
     // zero this batch's stats entries (ring-indexed)
     const uint32_t i0 = (uint32_t)(t0 % kStatSlots);
@@ -747,21 +1638,20 @@ int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
                          c->stream));
     if (first < batch)
       CK(c, hipMemsetAsync(c->st.stats, 0, (size_t)(batch - first) * kStatFields * 8, c->stream));
+    if (batched)
+      CK(c, hipMemsetAsync(c->d_tstat, 0, (size_t)c->trials * kMaxWindow * kTStatFields * 4, c->stream));
     const uint32_t nev = timing && !c->win ? batch * (flood || c->pp ? 2 : 4) : 0;
     while (c->ev.size() < nev) {
       hipEvent_t e;
       CK(c, hipEventCreate(&e));
       c->ev.push_back(e);
     }
-    if (c->win) {
-      int rc = run_windows(c, t0, batch, timing);
-      if (rc) return rc;
-    }
+    if (c->win) RC(run_windows(c, t0, batch, timing, t0));
     for (uint32_t i = 0; i < batch && c->pp; ++i) {  // push-pull rounds
       const uint32_t tt = (uint32_t)(t0 + i);
       hipEvent_t* e = timing ? &c->ev[(size_t)i * 2] : nullptr;
       if (e) CK(c, hipEventRecord(e[0], c->stream));
-      CK(c, pp_round(c->st, c->d_next, c->d_ppsum, tt, c->stream));
+      CK(c, pp_round(c->st, c->d_next, c->d_ppsum, tt, c->pp_l2_only, c->stream));
       if (e) CK(c, hipEventRecord(e[1], c->stream));
       CK(c, pp_commit(c->st, c->d_next, tt, c->stream));
     }
@@ -783,6 +1673,9 @@ int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
     if (first < batch)
       CK(c, hipMemcpyAsync(c->h_stats, c->st.stats, (size_t)(batch - first) * kStatFields * 8,
                            hipMemcpyDeviceToHost, c->stream));
+    if (batched)
+      CK(c, hipMemcpyAsync(c->h_tstat, c->d_tstat, (size_t)c->trials * kMaxWindow * kTStatFields * 4,
+                           hipMemcpyDeviceToHost, c->stream));
     CK(c, hipStreamSynchronize(c->stream));
     if (timing && !c->win) {
       for (uint32_t i = 0; i < batch; ++i) {
@@ -800,51 +1693,128 @@ int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
     }
     for (uint32_t i = 0; i < batch; ++i) {
       const unsigned long long* s = c->h_stats + (size_t)((t0 + i) % kStatSlots) * kStatFields;
-      c->t = t0 + i;
-      c->fired += s[ST_FIRED];
-      c->sent += s[ST_SENT];
-      c->msgs += s[ST_MSGS];
-      c->recv += s[ST_RECV];
-      c->crashed += s[ST_CRASH];
-      // push-pull: every informed node keeps calling
-      c->pending = c->pp ? c->recv : c->pending + s[ST_SCHED] - s[ST_FIRED];
-      if (out) {
-        gs_tick_stats& o = out[done + i];
-        o.tick = c->t;
-        o.fired = s[ST_FIRED];
-        o.sent = s[ST_SENT];
-        o.messages = s[ST_MSGS];
-        o.received = c->recv;
-        o.crashed = c->crashed;
-        o.pending = c->pending;
-      }
+      account_tick(c, t0 + i, s, out ? &out[done + i] : nullptr);
     }
+    if (batched) account_trials(c, t0, batch);
     done += batch;
   }
   return GS_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+void snap_trial(const gs_ctx* c, uint32_t tr, int32_t status) {
+  TrialAcc& a = const_cast<gs_ctx*>(c)->tacc[tr];
+  a.status = status;
+  a.snap = gs_trial_stats{(uint64_t)c->p.trial + tr, a.tick99, c->t, a.fired, a.sent, a.msgs, a.recv,
+                          a.crash, status, 0};
+}
+
+// Push-pull's exact stop: can any call still change the informed set?
+int pp_stalled(gs_ctx* c, bool* stalled) {
+  *stalled = true;
+  if (c->st.kd >= 100) return GS_OK;  // every call is lost (simulator.go:172 quantisation)
+  unsigned long long live = 0;
+  CK(c, pp_live_edges(c->st, c->d_err + 2, c->stream));
+  uint32_t h = 0;
+  CK(c, hipMemcpyAsync(&h, c->d_err + 2, 4, hipMemcpyDeviceToHost, c->stream));
+  CK(c, hipStreamSynchronize(c->stream));
+  live = h;
+  *stalled = live == 0;
+  return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int gs_run(gs_ctx* c, uint32_t poll, uint64_t max_ticks, gs_tick_stats* out, size_t cap,
            size_t* nout, int32_t* status) {
   if (!c || poll == 0) return fail(c, GS_EINVAL, "poll must be >= 1");
+  if (c->group && c->gtrials) {  // every batch runs its own trials to their stops
+    std::vector<int32_t> sts(c->mem.size(), 0);
+    std::vector<gs_ctx*>& ms = c->mem;
+    RC(par_members(c, [&](gs_ctx* m) {
+      const size_t i = (size_t)(std::find(ms.begin(), ms.end(), m) - ms.begin());
+      return gs_run(m, poll, max_ticks, nullptr, 0, nullptr, &sts[i]);
+    }));
+    gs_tick_stats tot{};
+    uint64_t recv = 0, cr = 0, t = 0, pend = 0;
+    c->fired = c->sent = c->msgs = 0;
+    for (gs_ctx* m : ms) {
+      c->fired += m->fired; c->sent += m->sent; c->msgs += m->msgs;
+      recv += m->recv; cr += m->crashed; pend += m->pending; t = std::max(t, m->t);
+    }
+    c->t = t; c->recv = recv; c->crashed = cr; c->pending = pend;
+    tot = gs_tick_stats{t, c->fired, c->sent, c->msgs, recv, cr, pend};
+    if (out && cap) out[0] = tot;
+    if (nout) *nout = 1;
+    if (status) *status = *std::max_element(sts.begin(), sts.end());
+    return GS_OK;
+  }
   size_t k = 0;
   int32_t st = GS_RUN_MAX_TICKS;
+  const bool trials = c->trials > 1 && !c->group;
+  const bool flood = !c->pp;
   for (;;) {
     const uint64_t f0 = c->fired, s0 = c->sent, m0 = c->msgs, r0 = c->recv;
-    int rc = gs_step(c, poll, nullptr);
-    if (rc) return rc;
+    RC(gs_step(c, poll, nullptr));
     if (out && k < cap)
-      out[k] = gs_tick_stats{c->t, c->fired - f0, c->sent - s0, c->msgs - m0, c->recv, c->crashed,
-                             c->pending};
+      out[k] = gs_tick_stats{c->t, c->fired - f0, c->sent - s0, c->msgs - m0, c->recv, c->crashed, c->pending};
     ++k;
+    if (trials) {  // each trial stops at its own poll (simulator.go:243-251 per process)
+      uint32_t running = 0;
+      for (uint32_t tr = 0; tr < c->trials; ++tr) {
+        TrialAcc& a = c->tacc[tr];
+        if (a.status != GS_RUN_RUNNING) continue;
+        const uint64_t pend = 1 + a.sched - a.fired;
+        if (covered(a.recv, c->p.n)) snap_trial(c, tr, GS_RUN_COVERED);
+        else if (pend == 0) snap_trial(c, tr, GS_RUN_QUIESCENT);
+        else if (c->t >= max_ticks) snap_trial(c, tr, GS_RUN_MAX_TICKS);
+        else ++running;
+      }
+      if (running == 0) {
+        st = GS_RUN_COVERED;
+        for (const TrialAcc& a : c->tacc) st = std::max(st, a.status);
+        break;
+      }
+      continue;
+    }
     if (covered(c->recv, c->p.n)) { st = GS_RUN_COVERED; break; }
-    // push-pull: informed nodes call forever, so a poll window that informs
-    // nobody new (or an empty informed set) ends the run instead
-    if (c->pending == 0 || (c->pp && c->recv == r0)) { st = GS_RUN_QUIESCENT; break; }
+    if (flood && c->pending == 0) { st = GS_RUN_QUIESCENT; break; }
+    if (!flood && c->recv == r0) {  // push-pull: a window that informed nobody new
+      bool stalled = false;
+      RC(pp_stalled(c, &stalled));
+      if (stalled) { st = GS_RUN_QUIESCENT; break; }
+    }
     if (c->t >= max_ticks) { st = GS_RUN_MAX_TICKS; break; }
   }
+  if (!trials && c->tacc.size() == 1) snap_trial(c, 0, st);
   if (nout) *nout = k;
   if (status) *status = st;
+  return GS_OK;
+}
+
+int gs_trial_results(gs_ctx* c, gs_trial_stats* out, size_t cap, size_t* nout) {
+  if (!c) return GS_EINVAL;
+  size_t k = 0;
+  auto one = [&](const gs_ctx* x) {
+    for (size_t i = 0; i < x->tacc.size(); ++i, ++k) {
+      if (!out || k >= cap) continue;
+      const TrialAcc& a = x->tacc[i];
+      if (a.status != GS_RUN_RUNNING) {
+        out[k] = a.snap;
+      } else {
+        out[k] = gs_trial_stats{(uint64_t)x->p.trial + i, a.tick99, x->t, a.fired, a.sent, a.msgs, a.recv,
+                                a.crash, GS_RUN_RUNNING, 0};
+      }
+    }
+  };
+  if (c->group && c->gtrials) for (gs_ctx* m : c->mem) one(m);
+  else one(c);
+  if (nout) *nout = k;
   return GS_OK;
 }
 
@@ -854,45 +1824,89 @@ int gs_totals(gs_ctx* c, gs_tick_stats* out) {
   return GS_OK;
 }
 
-int gs_read_received(gs_ctx* c, uint64_t* words, size_t nwords) {
-  if (!c || !words || nwords < c->st.W) return fail(c, GS_EINVAL, "need ceil(n/64) words");
+}  // extern "C"
+
+namespace {
+
+// Bitset `which` (0 = received, 1 = crashed) of context c into words: a
+// shard's own words at their global positions, batched trials trial-major.
+int read_bits(gs_ctx* c, int which, uint64_t* words, size_t nwords) {
+  const uint64_t Wn = (c->p.n + 63) / 64;
+  if (c->group && c->gtrials) {
+    uint64_t off = 0;
+    for (gs_ctx* m : c->mem) {
+      if (read_bits(m, which, words + off * Wn, (size_t)m->trials * Wn)) return fail(c, GS_EINVAL, m->err);
+      off += m->trials;
+    }
+    return GS_OK;
+  }
+  if (c->group) {
+    std::fill(words, words + Wn, 0ull);
+    std::vector<uint64_t> tmp(Wn);
+    for (gs_ctx* m : c->mem) {
+      if (read_bits(m, which, tmp.data(), Wn)) return fail(c, GS_EINVAL, m->err);
+      for (uint64_t i = 0; i < Wn; ++i) words[i] |= tmp[i];
+    }
+    return GS_OK;
+  }
+  if (nwords < Wn * c->trials) return fail(c, GS_EINVAL, "need ceil(n/64) words per trial");
   CK(c, hipSetDevice(c->dev));
-  CK(c, hipMemcpyAsync(words, c->st.recv, c->st.W * 8, hipMemcpyDeviceToHost, c->stream));
+  const unsigned long long* src = which ? c->st.crash : c->st.recv;
+  if (c->trials > 1) {
+    CK(c, hipMemcpy2DAsync(words, Wn * 8, src, ((size_t)1 << c->tlog) / 8, Wn * 8, c->trials,
+                           hipMemcpyDeviceToHost, c->stream));
+  } else if (c->shard) {
+    std::fill(words, words + Wn, 0ull);
+    CK(c, hipMemcpyAsync(words + c->lo / 64, src, c->st.W * 8, hipMemcpyDeviceToHost, c->stream));
+  } else {
+    CK(c, hipMemcpyAsync(words, src, c->st.W * 8, hipMemcpyDeviceToHost, c->stream));
+  }
   CK(c, hipStreamSynchronize(c->stream));
   return GS_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int gs_read_received(gs_ctx* c, uint64_t* words, size_t nwords) {
+  if (!c || !words || nwords < (c->p.n + 63) / 64) return fail(c, GS_EINVAL, "need ceil(n/64) words");
+  return read_bits(c, 0, words, nwords);
+}
+
 int gs_read_crashed(gs_ctx* c, uint64_t* words, size_t nwords) {
-  if (!c || !words || nwords < c->st.W) return fail(c, GS_EINVAL, "need ceil(n/64) words");
-  CK(c, hipSetDevice(c->dev));
-  CK(c, hipMemcpyAsync(words, c->st.crash, c->st.W * 8, hipMemcpyDeviceToHost, c->stream));
-  CK(c, hipStreamSynchronize(c->stream));
-  return GS_OK;
+  if (!c || !words || nwords < (c->p.n + 63) / 64) return fail(c, GS_EINVAL, "need ceil(n/64) words");
+  return read_bits(c, 1, words, nwords);
 }
 
 int gs_timing_get(gs_ctx* c, gs_timing* out) {
   if (!c || !out) return GS_EINVAL;
-  *out = c->timing;
+  *out = c->group ? c->mem[0]->timing : c->timing;  // a group: its first member's kernels
+  if (c->group) out->overlay_ms = c->timing.overlay_ms;
   return GS_OK;
 }
 
 int gs_set_flags(gs_ctx* c, uint32_t flags) {
   if (!c) return GS_EINVAL;
   c->p.flags = flags;
+  for (gs_ctx* m : c->mem) m->p.flags = flags;
   return GS_OK;
 }
 
 int gs_reset(gs_ctx* c) {
   if (!c) return GS_EINVAL;
-  CK(c, hipSetDevice(c->dev));
-  // everything in the state block except the stats ring and error word
-  CK(c, hipMemsetAsync(c->d_state, 0, (char*)c->st.stats - (char*)c->d_state, c->stream));
-  if (c->d_cnt) CK(c, hipMemsetAsync(c->d_cnt, 0, c->p.n * 4, c->stream));
-  if (c->win) CK(c, hipMemsetAsync(c->ws.fcount, 0, c->fcount_bytes, c->stream));
-  if (c->failed)
-    CK(c, hipMemcpyAsync(c->st.crash, c->d_failed, c->st.W * 8, hipMemcpyDeviceToDevice, c->stream));
-  CK(c, hipStreamSynchronize(c->stream));
-  c->t = c->fired = c->sent = c->msgs = c->recv = c->crashed = c->pending = 0;
+  for (gs_ctx* m : c->mem) RC(gs_reset(m) ? fail(c, GS_EDEVICE, m->err) : 0);
+  if (!c->group) {
+    CK(c, hipSetDevice(c->dev));
+    // everything in the state block except the stats ring and error word
+    CK(c, hipMemsetAsync(c->d_state, 0, (char*)c->st.stats - (char*)c->d_state, c->stream));
+    if (c->d_cnt) CK(c, hipMemsetAsync(c->d_cnt, 0, c->st.n * 4, c->stream));
+    if (c->win) CK(c, hipMemsetAsync(c->ws.fcount, 0, c->fcount_bytes, c->stream));
+    if (c->failed)
+      CK(c, hipMemcpyAsync(c->st.crash, c->d_failed, c->st.W * 8, hipMemcpyDeviceToDevice, c->stream));
+    CK(c, hipStreamSynchronize(c->stream));
+  }
+  reset_counters(c);
   c->begun = false;
   return GS_OK;
 }

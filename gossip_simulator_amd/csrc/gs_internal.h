@@ -111,15 +111,43 @@ struct WinState {
   unsigned long long* ffill;     // [nfine] fine region fill
   unsigned long long* sstats;    // [kStatShards][kMaxWindow][kStatFields] per-window partial counters
   unsigned long long* dbg;       // diagnostic phase stamps (GS_STAMPS=1), else null
+  // batched trials: [trials][kMaxWindow][kTStatFields] per-window counters of every
+  // trial (null for a single-trial context)
+  uint32_t* tstat;
+  uint32_t tofs;                 // tstat row of the window's first tick (ticks since the rows were zeroed)
+  // node-range shard: partitioned friend rows (prow[v]..prow[v+1] of pent, entry =
+  // (target - base) << 5 | slot j) and the all-gathered window fire list
+  const uint32_t* prow;
+  const uint32_t* pent;
+  const uint32_t* gfire;         // [G][gseg] entries local_id << 4 | k, ~0u = padding
+  uint64_t gseg;                 // entries per shard segment of gfire
+  uint32_t G, rank;              // shards, this shard's index
+  uint32_t seg_per;              // nodes per shard (shard r owns [r*seg_per, ...))
   uint64_t n, W;
   uint32_t nfine, ncoarse, R, stride, stride_magic;
   int32_t delay_low;
   uint32_t delay_span;
   int32_t kd, kc;
+  // Philox node keys: a node's global id is g = base + local id; batched trials lay
+  // trial i's nodes out at i << tlog, so the key node is g & tmask and the key
+  // trial is key.trial + (g >> tlog) (tlog = 32: one trial)
+  uint32_t base;
+  uint32_t tlog, tmask;
   Key key;
 };
 constexpr uint32_t kStatShards = 256;
 constexpr uint32_t kStampPhases = 9;
+// per-trial window counters (batched trials)
+enum TStat : uint32_t { TS_FIRED = 0, TS_SENT = 1, TS_DEAD = 2, TS_RECV = 3, TS_CRASH = 4 };
+constexpr uint32_t kTStatFields = 8;
+
+// Key (node, counter word 3) of global id g for a draw of `kind`.
+__host__ __device__ __forceinline__ void node_key(uint32_t tlog, uint32_t tmask, const Key& key,
+                                                  uint64_t g, uint32_t kind, uint32_t& node,
+                                                  uint32_t& c3) {
+  node = (uint32_t)(g & tmask);
+  c3 = ctr3(kind, key.trial + (uint32_t)(g >> tlog));
+}
 
 constexpr uint32_t kErrArrivals = 4;  // > 65535 arrivals at one node in one tick
 constexpr uint32_t kErrCoarse = 8;    // a coarse region overflowed its estimate
@@ -137,7 +165,20 @@ hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s
 hipError_t win_seal_rows(const uint8_t* deg, uint32_t* ids, uint64_t n, uint32_t stride,
                          hipStream_t s);
 hipError_t win_stats_reduce(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
-hipError_t win_schedule_one(const WinState& w, uint32_t node, uint32_t tick, hipStream_t s);
+// node-range shards
+hipError_t part_count(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
+                      uint32_t* cnt, hipStream_t s);
+hipError_t part_scan(const uint32_t* cnt, uint64_t n, unsigned long long* off, void* tmp, size_t& tmp_bytes,
+                     hipStream_t s);
+hipError_t part_narrow(const unsigned long long* off, uint64_t n, uint32_t* prow, uint32_t* err, hipStream_t s);
+hipError_t part_fill(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
+                     const uint32_t* prow, uint32_t* pent, hipStream_t s);
+hipError_t win_fire_compact(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, uint32_t* out,
+                            uint64_t seg, hipStream_t s);
+hipError_t win_expand_sh(const WinState& w, uint32_t t0, uint32_t L, int mode, hipStream_t s);
+// Schedule local node `node` (batched: in every trial; ~0u: each trial's keyed sender) at `tick`.
+hipError_t win_schedule(const WinState& w, uint32_t node, uint32_t tick, uint32_t trials, uint32_t n,
+                        hipStream_t s);
 
 // Push-pull extension (gs_pushpull.hip): one round per tick; `next` is the
 // informed set being built (equal to recv at the start of every round).
@@ -148,7 +189,8 @@ inline uint64_t pp_summary_words(uint64_t W) { return (W + 63) / 64; }
 inline uint64_t pp_summary2_words(uint64_t W) { return (pp_summary_words(W) + 63) / 64; }
 inline uint64_t pp_summary_total_words(uint64_t W) { return 2 * pp_summary_words(W) + 2 * pp_summary2_words(W); }
 hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long long* sum, uint32_t t,
-                    hipStream_t st);
+                    bool l2_only, hipStream_t st);
+hipError_t pp_live_edges(const DevState& s, uint32_t* out, hipStream_t st);
 hipError_t pp_commit(const DevState& s, const unsigned long long* next, uint32_t t, hipStream_t st);
 hipError_t pp_seed(const DevState& s, unsigned long long* next, uint32_t node, uint32_t* flag,
                    hipStream_t st);
@@ -169,9 +211,11 @@ struct OverlayWindowSink {
   void (*push)(void* self, uint64_t tick, uint64_t makeups, uint64_t breakups);
   void* self;
 };
-int overlay_build(uint64_t n, int32_t fanout, int32_t fanin, int32_t delay_low,
-                  int32_t delay_high, Key key, uint8_t* d_deg, uint32_t* d_ids,
-                  uint32_t stride, uint64_t max_ticks, hipStream_t stream,
-                  OverlayWindowSink sink, OverlayResult* res);
+// n = nodes per trial; trials > 1 builds every trial's overlay at once in the
+// id space trial << tlog | node (tlog = 32 for one trial).
+int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, int32_t fanin,
+                  int32_t delay_low, int32_t delay_high, Key key, uint8_t* d_deg, uint32_t* d_ids,
+                  uint32_t stride, uint64_t max_ticks, hipStream_t stream, OverlayWindowSink sink,
+                  OverlayResult* res);
 
 }  // namespace gs

@@ -34,33 +34,47 @@ constexpr uint32_t kScatterBlock = 256;
 constexpr uint32_t kScatterIPT = 8;
 
 struct OvParams {
-  uint64_t n;
+  uint64_t n;                 // nodes per trial
   uint32_t fanout, fanin, stride, R, B;
   int32_t delay_low;
   uint32_t delay_span;
   Key key;
+  // batched trials: trial i's node v has id i << tlog | v (tlog = 32: one trial)
+  uint32_t tlog, tmask;
 };
+
+// Key node and counter word 3 of global id g (per-trial keys, gs_internal.h).
+__device__ __forceinline__ uint32_t ov_draw(const OvParams& p, uint32_t kind, uint32_t g, uint32_t b,
+                                            uint32_t c) {
+  uint32_t node, c3;
+  node_key(p.tlog, p.tmask, p.key, g, kind, node, c3);
+  return philox(node, b, c, c3, p.key.k0, p.key.k1).x;
+}
 
 __device__ __forceinline__ uint64_t ev_key(uint32_t dst, uint32_t src, uint32_t kind, uint32_t B) {
   return ((uint64_t)dst << (B + 1)) | ((uint64_t)src << 1) | kind;
 }
 
 // Item sources for the bucket scatter -------------------------------------
-struct PickSource {  // tick 0: item i = (v = i / fanout, j = i % fanout)
+struct PickSource {  // tick 0: item i = (trial i / (n*fanout), v, j = i % fanout)
   OvParams p;
   uint8_t* deg;
   uint32_t* ids;
   bool write_rows;
   __device__ __forceinline__ void get(uint64_t i, uint64_t& key, uint32_t& slot) const {
-    const uint32_t v = (uint32_t)(i / p.fanout), j = (uint32_t)(i % p.fanout);
-    uint32_t f = uniform(draw0(p.key, K_PICK, v, 0, j), (uint32_t)p.n);     // :97
+    const uint64_t per = p.n * p.fanout;
+    const uint32_t tr = (uint32_t)(i / per);
+    const uint64_t rem = i - (uint64_t)tr * per;
+    const uint32_t v = (uint32_t)(rem / p.fanout), j = (uint32_t)(rem % p.fanout);
+    const uint32_t tb = (uint32_t)((uint64_t)tr << p.tlog), gv = tb | v;
+    uint32_t f = uniform(ov_draw(p, K_PICK, gv, 0, j), (uint32_t)p.n);       // :97
     if (f == v) f = (uint32_t)((f + 1) % p.n);                              // :98-100
     if (write_rows) {
-      ids[(size_t)v * p.stride + j] = f;                                    // :101
-      if (j == 0) deg[v] = (uint8_t)p.fanout;
+      ids[(size_t)gv * p.stride + j] = tb | f;                              // :101
+      if (j == 0) deg[gv] = (uint8_t)p.fanout;
     }
-    key = ev_key(f, v, 0u, p.B);                                            // :102 Makeup
-    slot = fire_offset(p.delay_low, p.delay_span, draw0(p.key, K_OVDELAY, v, 0, j)) % p.R;
+    key = ev_key(tb | f, gv, 0u, p.B);                                      // :102 Makeup
+    slot = fire_offset(p.delay_low, p.delay_span, ov_draw(p, K_OVDELAY, gv, 0, j)) % p.R;
   }
 };
 
@@ -132,6 +146,7 @@ __global__ __launch_bounds__(256) void k_process(const OvParams p, uint32_t t, c
     const uint64_t start = (uint64_t)heads[h];
     const uint64_t end = (h + 1 < H) ? (uint64_t)heads[h + 1] : m;
     const uint32_t u = (uint32_t)(keys[start] >> (p.B + 1));
+    const uint32_t ul = u & p.tmask, tb = u & ~p.tmask;  // node within its trial, trial base
     const uint64_t smask = (1ull << p.B) - 1;
     uint32_t* row = ids + (size_t)u * p.stride;
     uint32_t d = deg[u];
@@ -146,7 +161,7 @@ __global__ __launch_bounds__(256) void k_process(const OvParams p, uint32_t t, c
         if (d < p.fanin) {
           row[d++] = src;
         } else {
-          const uint32_t pos = uniform(draw0(p.key, K_VICTIM, u, t, k), d);
+          const uint32_t pos = uniform(ov_draw(p, K_VICTIM, u, t, k), d);
           const uint32_t victim = row[pos];
           emitted = ev_key(victim, u, 1u, p.B);               // Breakup (:73)
           row[pos] = src;
@@ -160,13 +175,14 @@ __global__ __launch_bounds__(256) void k_process(const OvParams p, uint32_t t, c
             for (uint32_t q = idx; q + 1 < d; ++q) row[q] = row[q + 1];
             --d;
           } else {                                            // replace (:86-91)
-            uint32_t nf = 0, a = 0;
+            uint32_t nf = 0, a = 0, kn, c3;
+            node_key(p.tlog, p.tmask, p.key, u, K_REPLACE, kn, c3);
             for (; a < 256; ++a) {
-              const u32x4 r = philox(u, t, (k << 6) | (a >> 2), ctr3(K_REPLACE, p.key.trial),
-                                     p.key.k0, p.key.k1);
+              const u32x4 r = philox(kn, t, (k << 6) | (a >> 2), c3, p.key.k0, p.key.k1);
               nf = uniform(lane_of(r, a & 3), (uint32_t)p.n);
-              if (nf != src && nf != u) break;
+              if (nf != (src & p.tmask) && nf != ul) break;
             }
+            nf |= tb;
             if (a == 256) {
               err |= 1;
             } else {
@@ -179,7 +195,7 @@ __global__ __launch_bounds__(256) void k_process(const OvParams p, uint32_t t, c
       out[i] = emitted;
       if (emitted != kEmpty)
         oslot[i] = (uint16_t)((t + fire_offset(p.delay_low, p.delay_span,
-                                               draw0(p.key, K_OVDELAY, u, t, k))) % p.R);
+                                               ov_draw(p, K_OVDELAY, u, t, k))) % p.R);
     }
     deg[u] = (uint8_t)d;
   }
@@ -232,9 +248,9 @@ static uint32_t node_bits(uint64_t n) {
 
 }  // namespace
 
-int overlay_build(uint64_t n, int32_t fanout, int32_t fanin, int32_t delay_low,
-                  int32_t delay_high, Key key, uint8_t* d_deg, uint32_t* d_ids, uint32_t stride,
-                  uint64_t max_ticks, hipStream_t stream, OverlayWindowSink sink,
+int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, int32_t fanin,
+                  int32_t delay_low, int32_t delay_high, Key key, uint8_t* d_deg, uint32_t* d_ids,
+                  uint32_t stride, uint64_t max_ticks, hipStream_t stream, OverlayWindowSink sink,
                   OverlayResult* res) {
   res->rc = GS_OK;
   res->final_tick = 0;
@@ -245,7 +261,10 @@ int overlay_build(uint64_t n, int32_t fanout, int32_t fanin, int32_t delay_low,
   p.fanin = (uint32_t)fanin;
   p.stride = stride;
   p.R = delay_high > 2 ? (uint32_t)delay_high : 2u;
-  p.B = node_bits(n);
+  p.tlog = tlog;
+  p.tmask = tlog >= 32 ? ~0u : (1u << tlog) - 1;
+  const uint64_t ntot = trials > 1 ? (uint64_t)trials << tlog : n;  // id space
+  p.B = node_bits(ntot);
   p.delay_low = delay_low;
   p.delay_span = (uint32_t)(delay_high - delay_low);
   p.key = key;
@@ -280,7 +299,7 @@ int overlay_build(uint64_t n, int32_t fanout, int32_t fanin, int32_t delay_low,
 
   {
     // ---- tick 0: picks (count, size buckets, write) --------------------
-    const uint64_t items = n * (uint64_t)p.fanout;
+    const uint64_t items = n * (uint64_t)p.fanout * (trials > 1 ? trials : 1);
     if (items) {
       PickSource src{p, d_deg, d_ids, false};
       const uint64_t per = (uint64_t)kScatterBlock * kScatterIPT;
@@ -301,8 +320,8 @@ int overlay_build(uint64_t n, int32_t fanout, int32_t fanin, int32_t delay_low,
       OVCHK(hipGetLastError());
       for (uint32_t s = 0; s < R; ++s) { fill[s] += h_counts[s]; pending += h_counts[s]; }
       OVCHK(hipMemsetAsync(d_counts, 0, R * 8, stream));
-    } else if (n) {
-      OVCHK(hipMemsetAsync(d_deg, 0, n, stream));
+    } else if (ntot) {
+      OVCHK(hipMemsetAsync(d_deg, 0, ntot, stream));
     }
   }
 

@@ -25,7 +25,6 @@
 // in front of them, so the early and late rounds, where almost every call is
 // decided by the summaries, cost the table stream only.
 #include <algorithm>
-#include <cstdlib>
 
 #include "gs_internal.h"
 
@@ -202,6 +201,29 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_commit(const DevState s,
   block_add(sh, v3, 1, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
 }
 
+// Exact stop test (gs_run): out += edges (v, friends[v][j]) over which a call
+// could still change the informed set -- v live and informed with a live
+// uninformed friend (push), or v live and uninformed with an informed friend
+// (pull).  Zero means no later round can inform anyone.  Run only when a poll
+// window informed nobody new.
+__global__ __launch_bounds__(kPPBlock) void k_pp_live_edges(const DevState s, uint32_t* out) {
+  uint32_t cnt = 0;
+  for (uint64_t v = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; v < s.n; v += (uint64_t)gridDim.x * kPPBlock) {
+    const unsigned long long bit = 1ull << (v & 63);
+    if (s.crash[v >> 6] & bit) continue;
+    const bool iv = (s.recv[v >> 6] & bit) != 0;
+    const uint32_t d = s.deg[v];
+    for (uint32_t j = 0; j < d; ++j) {
+      const uint32_t u = s.ids[v * s.stride + j];
+      const unsigned long long ub = 1ull << (u & 63);
+      const bool iu = (s.recv[u >> 6] & ub) != 0, fu = (s.crash[u >> 6] & ub) != 0;
+      if (iv ? (!iu && !fu) : iu) { ++cnt; break; }
+    }
+  }
+  const uint32_t w = wave_sum64(cnt);
+  if ((threadIdx.x & 63) == 0 && w) atomicAdd(out, w);
+}
+
 // Sender (simulator.go:239-241 for the flood model): informed at begin unless
 // failed; flag[0] = 1 if it was informed.
 __global__ void k_pp_seed(const DevState s, unsigned long long* next, uint32_t node, uint32_t* flag) {
@@ -217,7 +239,7 @@ __global__ void k_pp_seed(const DevState s, unsigned long long* next, uint32_t n
 }  // namespace
 
 hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long long* sum, uint32_t t,
-                    hipStream_t st) {
+                    bool l2_only_flag, hipStream_t st) {
   unsigned long long* sumA = sum;
   unsigned long long* sumB = sum + pp_summary_words(s.W);
   const uint32_t sblocks = (uint32_t)std::min<uint64_t>((s.W + kPPBlock - 1) / kPPBlock, 4096);
@@ -226,9 +248,9 @@ hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long l
   unsigned long long* sum2 = sum + 2 * S1;
   const uint32_t s2blocks = (uint32_t)std::min<uint64_t>((S1 + kPPBlock - 1) / kPPBlock, 1024);
   hipLaunchKernelGGL(k_pp_summary2, dim3(s2blocks), dim3(kPPBlock), 0, st, sum, S1, sum2, S2);
-  // 0: no LDS stage, every call checks L2 (N > ~1.02e9; GS_PP_L2_ONLY=1 forces
-  // it so the parity tests cover that path at small N)
-  const bool l2_only = S2 > kPPMaxS2 || getenv("GS_PP_L2_ONLY") != nullptr;
+  // 0: no LDS stage, every call checks L2 (N > ~1.02e9; GS_FLAG_PP_L2_ONLY
+  // forces it so the parity tests cover that path at small N)
+  const bool l2_only = S2 > kPPMaxS2 || l2_only_flag;
   const uint32_t S2l = l2_only ? 0u : (uint32_t)S2;
   const uint64_t groups = (s.W + kPPU - 1) / kPPU;  // one wave per kPPU words
   const uint32_t blocks =
@@ -241,6 +263,14 @@ hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long l
 hipError_t pp_commit(const DevState& s, const unsigned long long* next, uint32_t t, hipStream_t st) {
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.W + kPPBlock - 1) / kPPBlock, 2048);
   hipLaunchKernelGGL(k_pp_commit, dim3(blocks), dim3(kPPBlock), 0, st, s, next, t);
+  return hipGetLastError();
+}
+
+hipError_t pp_live_edges(const DevState& s, uint32_t* out, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(out, 0, 4, st);
+  if (e != hipSuccess) return e;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.n + kPPBlock - 1) / kPPBlock, 8192);
+  hipLaunchKernelGGL(k_pp_live_edges, dim3(blocks), dim3(kPPBlock), 0, st, s, out);
   return hipGetLastError();
 }
 

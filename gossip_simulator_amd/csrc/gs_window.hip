@@ -150,6 +150,26 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
   return v;
 }
 
+// Batched trials: add (a, b) to fields (fa, fb) of row `key` of tstat
+// (key = trial * kMaxWindow + tick, ~0u = nothing), one atomic pair per
+// distinct key in the wave.  The wave's lanes usually share one key (firing
+// indices are bucket-major, and a bucket belongs to one trial).
+__device__ __forceinline__ void tstat_add(uint32_t* tstat, uint32_t key, uint32_t fa, uint32_t a,
+                                          uint32_t fb, uint32_t b) {
+  bool pend = key != ~0u;
+  for (unsigned long long bal = __ballot(pend); bal; bal = __ballot(pend)) {
+    const uint32_t lead = (uint32_t)__builtin_ctzll(bal);
+    const uint32_t k0 = __shfl(key, lead, 64);
+    const bool mine = pend && key == k0;
+    const uint32_t sa = wave_sum32(mine ? a : 0u), sb = wave_sum32(mine ? b : 0u);
+    if ((threadIdx.x & 63) == lead) {
+      if (sa) atomicAdd(&tstat[(size_t)k0 * kTStatFields + fa], sa);
+      if (sb) atomicAdd(&tstat[(size_t)k0 * kTStatFields + fb], sb);
+    }
+    pend = pend && !mine;
+  }
+}
+
 // Friends row of v into registers; slots past the list hold kEmptyMsg (rows
 // are sealed by k_seal_rows, so the length byte is not read).
 template <uint32_t MAXS>
@@ -182,7 +202,6 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
   const uint32_t tid = threadIdx.x;
   const uint32_t units = L * w.nfine;
   constexpr uint32_t per_round = kExpandBlock * NPT;
-  const uint32_t c3drop = ctr3(K_DROP, w.key.trial), c3crash = ctr3(K_CRASH, w.key.trial);
   if (tid < kMaxWindow * 2) (&sm.acc[0][0])[tid] = 0;
   static_assert(kExpandBlock == 256, "thread b owns coarse bin b");
   const unsigned long long cbase = w.ccap[tid], cend = w.ccap[tid + 1];  // bin tid's region
@@ -223,15 +242,19 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
       for (uint32_t j = 0; j < MAXS; ++j) { mm[q][j] = kEmptyMsg; mt[q][j] = ~0u; }
       if (vv[q] != ~0u) load_row<MAXS>(w, vv[q], mm[q]);  // all rows in flight
     }
+    uint32_t sentq[NPT];
 #pragma unroll
     for (uint32_t q = 0; q < NPT; ++q) {
+      sentq[q] = 0;
       if (vv[q] == ~0u) continue;
       const uint32_t v = vv[q], k = kk[q], t = t0 + k;
+      uint32_t vn, c3drop;
+      node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + v, K_DROP, vn, c3drop);
       uint32_t sent = 0;
 #pragma unroll
       for (uint32_t jg = 0; jg < (MAXS + 3) / 4; ++jg) {
         if (mm[q][jg * 4] == kEmptyMsg) break;
-        const u32x4 r = philox(v, t, jg, c3drop, w.key.k0, w.key.k1);   // :144, :172
+        const u32x4 r = philox(vn, t, jg, c3drop, w.key.k0, w.key.k1);   // :144, :172
 #pragma unroll
         for (uint32_t jj = 0; jj < 4; ++jj) {
           const uint32_t j = jg * 4 + jj;
@@ -240,17 +263,28 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
             const uint32_t tgt = mm[q][j], bin = tgt >> kCoarseShift;
             // the receiver's crash roll for ordinal 0 (:112, key (u, t, 0)) rides along
             uint32_t roll0 = 0;
-            if (w.kc > 0)
-              roll0 = (int32_t)uniform(philox(tgt, t, 0, c3crash, w.key.k0, w.key.k1).x, 100u) < w.kc;
+            if (w.kc > 0) {
+              uint32_t un, c3crash;
+              node_key(w.tlog, w.tmask, w.key, tgt, K_CRASH, un, c3crash);
+              roll0 = (int32_t)uniform(philox(un, t, 0, c3crash, w.key.k0, w.key.k1).x, 100u) < w.kc;
+            }
             mt[q][j] = bin | (atomicAdd(&sm.cnt[bin], 1u) << 8);
             mm[q][j] = (tgt & ((1u << kCoarseShift) - 1)) | (k << kCoarseShift) | (roll0 << kRoll0Coarse);
             ++sent;
           }
         }
       }
+      sentq[q] = sent;
 #pragma unroll
       for (uint32_t kx = 0; kx < kBitTicks; ++kx)
         if (kx == k) accp[kx] += 1u | (sent << 16);
+    }
+    if (WRITE && add_stats && w.tstat) {  // batched trials: fired/sent per (trial, tick)
+#pragma unroll
+      for (uint32_t q = 0; q < NPT; ++q) {
+        const uint32_t key = vv[q] == ~0u ? ~0u : (uint32_t)((uint64_t)vv[q] >> w.tlog) * kMaxWindow + w.tofs + kk[q];
+        tstat_add(w.tstat, key, TS_FIRED, 1u, TS_SENT, sentq[q]);
+      }
     }
     __syncthreads();
     if (!WRITE) {
@@ -499,9 +533,12 @@ __device__ __forceinline__ uint32_t msg_tick(uint32_t m) { return (m >> kFineLog
 // bucket with kk arrivals at tick t: ordinals 0..kk-1, keyed crash rolls.
 // (Large-bucket path.)
 __device__ __forceinline__ void resolve_node(const WinState& w, ResolveLds& sm, uint32_t f,
-                                             uint32_t loc, uint32_t kk, uint32_t t, uint32_t c3crash,
+                                             uint32_t loc, uint32_t kk, uint32_t t,
                                              uint32_t& cm, uint32_t& cr, uint32_t& cc, uint32_t& cs) {
-  const uint32_t u = (f << kFineLog) + loc, bit = 1u << (loc & 31), wi = loc >> 5;
+  const uint32_t bit = 1u << (loc & 31), wi = loc >> 5;
+  const uint64_t g = (uint64_t)w.base + (f << kFineLog) + loc;
+  uint32_t u, c3crash;
+  node_key(w.tlog, w.tmask, w.key, g, K_CRASH, u, c3crash);
   bool crashed = (sm.crash[wi] & bit) != 0;
   bool received = (sm.recv[wi] & bit) != 0;
   u32x4 r{0, 0, 0, 0};
@@ -522,7 +559,10 @@ __device__ __forceinline__ void resolve_node(const WinState& w, ResolveLds& sm, 
     received = true;
     ++cr;                                                        // :121
     // Broadcast() (:122, :141-142): fire at t + off
-    const uint32_t off = fire_offset(w.delay_low, w.delay_span, draw0(w.key, K_DELAY, u, t, 0));
+    uint32_t c3delay;
+    node_key(w.tlog, w.tmask, w.key, g, K_DELAY, u, c3delay);
+    const uint32_t off = fire_offset(w.delay_low, w.delay_span,
+                                     philox(u, t, 0, c3delay, w.key.k0, w.key.k1).x);
     const uint32_t s = (t + off) % w.R;
     const uint32_t pos = atomicAdd(&sm.fc[s], 1u);
     w.flist[((size_t)s * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
@@ -536,7 +576,7 @@ __device__ __forceinline__ void resolve_node(const WinState& w, ResolveLds& sm, 
 template <class Src>
 __device__ __forceinline__ void resolve_tick(const WinState& w, ResolveLds& sm, uint32_t f,
                                              const Src& src, uint32_t lo, uint32_t hi, uint32_t k,
-                                             uint32_t t, uint32_t c3crash) {
+                                             uint32_t t) {
   const uint32_t tid = threadIdx.x;
   for (uint32_t p = lo + tid; p < hi; p += kResolveBlock) {
     const uint32_t m = src[p];
@@ -553,7 +593,7 @@ __device__ __forceinline__ void resolve_tick(const WinState& w, ResolveLds& sm, 
     const uint32_t loc = msg_loc(m), sh = (loc & 1) * 16;
     const uint32_t kk = (atomicAnd(&sm.cnt[loc >> 1], ~(0xFFFFu << sh)) >> sh) & 0xFFFFu;
     arr += kk;
-    if (kk) resolve_node(w, sm, f, loc, kk, t, c3crash, cm, cr, cc, cs);
+    if (kk) resolve_node(w, sm, f, loc, kk, t, cm, cr, cc, cs);
   }
   if (arr != cm) atomicAdd(&sm.st[k][0], arr - cm);
   if (cr) atomicAdd(&sm.st[k][1], cr);
@@ -624,6 +664,42 @@ __device__ __forceinline__ void replay_node(const WinState& w, uint32_t u, uint3
   }
 }
 
+// Adds the lanes' per-tick counters (infected | crashed << 16, and receipts not
+// counted) plus sm.st to the per-tick totals and, for a batched trial, to
+// tstat[trial]; leaves them zeroed.  Block-uniform call.
+__device__ __forceinline__ void flush_counts(const WinState& w, ResolveLds& sm, uint32_t (&acc_rc)[kBitTicks],
+                                             uint32_t (&acc_d)[kBitTicks], uint32_t L, uint32_t trial) {
+#pragma unroll
+  for (uint32_t k = 0; k < kBitTicks; ++k) {
+    if (k >= L) continue;
+    const uint32_t rc = acc_rc[k];
+    const uint32_t sd = wave_sum(acc_d[k]), sr = wave_sum(rc & 0xFFFFu), sc = wave_sum(rc >> 16);
+    const uint32_t lane = lane_id();
+    const uint32_t v = lane == 0 ? sd : lane == 1 ? sr : sc;
+    if (lane < 3 && v) atomicAdd(&sm.st[k][lane], v);
+    acc_rc[k] = 0;
+    acc_d[k] = 0;
+  }
+  __syncthreads();
+  const uint32_t tid = threadIdx.x;
+  if (tid < L * 3) {
+    const uint32_t k = tid / 3, fld = tid - k * 3;
+    const uint32_t v = sm.st[k][fld];
+    // field 0 counts receipts that were NOT counted (:108, after a crash):
+    // the expand added every delivered send to ST_MSGS
+    unsigned long long* row = shard_row(w, k);
+    if (v && fld == 0) atomicAdd(&row[ST_MSGS], 0ull - (unsigned long long)v);
+    if (v && fld == 1) {
+      atomicAdd(&row[ST_RECV], (unsigned long long)v);
+      atomicAdd(&row[ST_SCHED], (unsigned long long)v);  // every infection schedules one Broadcast
+    }
+    if (v && fld == 2) atomicAdd(&row[ST_CRASH], (unsigned long long)v);
+    if (v && trial != ~0u) atomicAdd(&w.tstat[((size_t)trial * kMaxWindow + w.tofs + k) * kTStatFields + TS_DEAD + fld], v);
+    sm.st[k][fld] = 0;
+  }
+  __syncthreads();
+}
+
 // Persistent: workgroup g owns buckets g, g + G, g + 2G, ... (G = gridDim.x),
 // resolves its non-empty ones in turn, and adds its per-tick counters once at
 // the end.  Per bucket:
@@ -641,7 +717,6 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
   const uint32_t tid = threadIdx.x, G = gridDim.x;
   static_assert(kBitWords == kResolveBlock, "one bit word per thread");
   static_assert(kWinMaxRing <= kResolveBlock, "one ring slot per thread");
-  const uint32_t c3crash = ctr3(K_CRASH, w.key.trial), c3delay = ctr3(K_DELAY, w.key.trial);
   if (tid < kMaxWindow * 4) (&sm.st[0][0])[tid] = 0;
   if (tid == 0) { sm.nb = 0; sm.cls = 0; }
   if (tid < 2 * kStampPhases) (&sm.stamp[0][0])[tid] = 0;
@@ -670,6 +745,11 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
     const unsigned long long mb = mbB;
     const uint32_t node0 = f << kFineLog;
     const uint64_t wi = ((uint64_t)node0 >> 5) + tid;
+    // Philox keys of the bucket's nodes: key node knode0 + local offset (a
+    // bucket lies inside one trial), counter words c3crash / c3delay
+    uint32_t knode0, c3crash;
+    node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + node0, K_CRASH, knode0, c3crash);
+    const uint32_t c3delay = (c3crash & 0xFFFFFFu) | (K_DELAY << 24);
     const bool in = wi < w.W * 2;
     const uint32_t recv0 = in ? rwg[wi] : 0u, crash0 = in ? cwg[wi] : 0u;
     const uint32_t fcv = tid < w.R ? w.fcount[(size_t)tid * w.nfine + f] : 0u;
@@ -723,7 +803,7 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
     stamp(w, sm, 2);
     uint32_t rw = recv0, cw = crash0;
     if (sm.err != 3) {
-      const uint32_t ubase = node0 + tid * 32;
+      const uint32_t ubase = knode0 + tid * 32;
       // crash rolls of ordinals 1..3 for every (node, tick) with >= 2 receipts,
       // one lane per entry (in the tick loop they would serialise the wave);
       // this word's entries are contiguous from rcur, in tick loop order
@@ -754,7 +834,7 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
         const uint32_t r1 = sm.nroll < kDupCap ? sm.nroll : kDupCap;
         for (uint32_t q = r0 + tid; q < r1; q += kResolveBlock) {
           const uint32_t e = sm.dlist[q];
-          const uint32_t u = node0 + (e >> 9) * 32 + (e & 31), t = t0 + ((e >> 5) & 15);
+          const uint32_t u = knode0 + (e >> 9) * 32 + (e & 31), t = t0 + ((e >> 5) & 15);
           const u32x4 r = philox(u, t, 0, c3crash, w.key.k0, w.key.k1);  // :180, ordinals 0..3
           const uint32_t b1 = (int32_t)uniform(r.y, 100u) < w.kc, b2 = (int32_t)uniform(r.z, 100u) < w.kc,
                          b3 = (int32_t)uniform(r.w, 100u) < w.kc;
@@ -824,7 +904,7 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
       for (uint32_t q = tid; q < ni_all; q += kResolveBlock) {
         const uint32_t x = inf[q], loc = msg_loc(x), t = t0 + msg_tick(x);
         const uint32_t off = fire_offset(w.delay_low, w.delay_span,
-                                         philox(node0 + loc, t, 0, c3delay, w.key.k0, w.key.k1).x);
+                                         philox(knode0 + loc, t, 0, c3delay, w.key.k0, w.key.k1).x);
         const uint32_t slot = (t + off) % w.R;
         const uint32_t pos = atomicAdd(&sm.fc[slot], 1u);
         w.flist[((size_t)slot * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
@@ -839,7 +919,7 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
       sm.nrecv[tid] = 0;
       sm.ncrash[tid] = 0;
       __syncthreads();
-      for (uint32_t k = 0; k < L; ++k) resolve_tick(w, sm, f, gm, 0, M, k, t0 + k, c3crash);
+      for (uint32_t k = 0; k < L; ++k) resolve_tick(w, sm, f, gm, 0, M, k, t0 + k);
       rw = sm.recv[tid] | sm.nrecv[tid];
       cw = sm.crash[tid] | sm.ncrash[tid];
       if (tid == 0 && sm.err == 1) atomicOr(w.err, kErrArrivals);
@@ -853,31 +933,12 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
     if (tid < w.R) w.fcount[(size_t)tid * w.nfine + f] = sm.fc[tid];
     stamp(w, sm, 8);
     if (w.dbg && tid == 0) sm.stamp[sm.cls][0] += 1;
+    // batched trials: the bucket's counters go to its trial's rows (a bucket
+    // lies inside one trial) as well as to the per-tick totals
+    if (w.tstat) flush_counts(w, sm, acc_rc, acc_d, L, (uint32_t)(((uint64_t)w.base + node0) >> w.tlog));
   }
   if (w.dbg && tid < 2 * kStampPhases) atomicAdd(&w.dbg[tid], (&sm.stamp[0][0])[tid]);
-#pragma unroll
-  for (uint32_t k = 0; k < kBitTicks; ++k) {
-    if (k >= L) continue;
-    const uint32_t rc = acc_rc[k];
-    const uint32_t sd = wave_sum(acc_d[k]), sr = wave_sum(rc & 0xFFFFu), sc = wave_sum(rc >> 16);
-    const uint32_t lane = lane_id();
-    const uint32_t v = lane == 0 ? sd : lane == 1 ? sr : sc;
-    if (lane < 3 && v) atomicAdd(&sm.st[k][lane], v);
-  }
-  __syncthreads();
-  if (tid < L * 3) {
-    const uint32_t k = tid / 3, fld = tid - k * 3;
-    const uint32_t v = sm.st[k][fld];
-    // field 0 counts receipts that were NOT counted (:108, after a crash):
-    // the expand added every delivered send to ST_MSGS
-    unsigned long long* row = shard_row(w, k);
-    if (v && fld == 0) atomicAdd(&row[ST_MSGS], 0ull - (unsigned long long)v);
-    if (v && fld == 1) {
-      atomicAdd(&row[ST_RECV], (unsigned long long)v);
-      atomicAdd(&row[ST_SCHED], (unsigned long long)v);  // every infection schedules one Broadcast
-    }
-    if (v && fld == 2) atomicAdd(&row[ST_CRASH], (unsigned long long)v);
-  }
+  if (!w.tstat) flush_counts(w, sm, acc_rc, acc_d, L, ~0u);
 }
 
 // Small buckets (1..kSmallMax receipts in the window): one wave per bucket.
@@ -895,15 +956,18 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
 template <uint32_t E>
 __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w, uint32_t t0, uint32_t L) {
   constexpr uint32_t N = 64 * E, kWaves = kSmallBlock / 64;
-  __shared__ uint32_t st[kMaxWindow][4];  // dead (not counted), recv, crash per tick
-  __shared__ uint32_t sk[kWaves][N];      // each wave's sorted keys
+  __shared__ uint32_t st[kWaves][kMaxWindow][4];  // per wave: dead (not counted), recv, crash per tick
+  __shared__ uint32_t sk[kWaves][N];               // each wave's sorted keys
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid < kMaxWindow * 4) (&st[0][0])[tid] = 0;
+  static_assert(kWaves * kMaxWindow * 4 == kSmallBlock, "one counter per thread");
+  (&st[0][0][0])[tid] = 0;
   __syncthreads();
   const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
   const unsigned long long M = f < w.nfine ? w.ffill[f] : 0ull;
   if (M > (E == 1 ? 0ull : 64ull * (E / 4)) && M <= N) {
-    const uint32_t c3crash = ctr3(K_CRASH, w.key.trial), c3delay = ctr3(K_DELAY, w.key.trial);
+    uint32_t knode0, c3crash;  // keys of the bucket's nodes (one trial per bucket)
+    node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + (f << kFineLog), K_CRASH, knode0, c3crash);
+    const uint32_t c3delay = (c3crash & 0xFFFFFFu) | (K_DELAY << 24);
     const uint32_t* gm = w.fmsg + w.fstart[f];
     uint32_t key[E];  // loc << 5 | k << 1 | roll0; ~0u sorts last
 #pragma unroll
@@ -951,7 +1015,7 @@ __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w,
       const uint32_t i = r * 64 + lane;
       const uint32_t loc = key[r] >> 5;
       if (key[r] == ~0u || (i > 0 && (sk[wv][i - 1] >> 5) == loc)) continue;  // not a run head
-      const uint32_t u = (f << kFineLog) + loc, wi = u >> 5, bit = 1u << (u & 31);
+      const uint32_t wi = ((f << kFineLog) + loc) >> 5, bit = 1u << (loc & 31), u = knode0 + loc;
       const uint32_t cw = cwg[wi];
       bool rv = (rwg[wi] & bit) != 0, cr = (cw & bit) != 0, inf = false;
       uint32_t ktick = ~0u, ord = 0, tinf = 0;
@@ -961,7 +1025,7 @@ __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w,
         const uint32_t k = (e >> 1) & (kMaxWindow - 1), t = t0 + k;
         if (k != ktick) { ktick = k; ord = 0; } else { ++ord; }
         if (cr) {                                                   // :108 not counted
-          atomicAdd(&st[k][0], 1u);
+          atomicAdd(&st[wv][k][0], 1u);
           continue;
         }
         bool roll = e & 1u;                                         // :111-112, ordinal 0 rode along
@@ -973,11 +1037,11 @@ __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w,
         }
         if (roll) {                                                 // :113-115
           cr = true;
-          atomicAdd(&st[k][2], 1u);
+          atomicAdd(&st[wv][k][2], 1u);
         } else if (!rv) {                                           // :117-121
           rv = inf = true;
           tinf = t;
-          atomicAdd(&st[k][1], 1u);
+          atomicAdd(&st[wv][k][1], 1u);
         }
       }
       if (cr && !(cw & bit)) atomicOr(&cwg[wi], bit);
@@ -990,11 +1054,23 @@ __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w,
         w.flist[((size_t)slot * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
       }
     }
+    if (w.tstat) {  // batched trials: this bucket's counters go to its trial's rows
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lane < L * 3) {
+        const uint32_t k = lane / 3, fld = lane - k * 3;
+        const uint32_t v = st[wv][k][fld];
+        const uint32_t trial = (uint32_t)(((uint64_t)w.base + (f << kFineLog)) >> w.tlog);
+        if (v) atomicAdd(&w.tstat[((size_t)trial * kMaxWindow + w.tofs + k) * kTStatFields + TS_DEAD + fld], v);
+      }
+    }
   }
   __syncthreads();
   if (tid < L * 3) {
     const uint32_t k = tid / 3, fld = tid - k * 3;
-    const uint32_t v = st[k][fld];
+    uint32_t v = 0;
+    for (uint32_t q = 0; q < kWaves; ++q) v += st[q][k][fld];
     unsigned long long* row = shard_row(w, k);
     if (v && fld == 0) atomicAdd(&row[ST_MSGS], 0ull - (unsigned long long)v);
     if (v && fld == 1) {
@@ -1005,12 +1081,224 @@ __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w,
   }
 }
 
-__global__ void k_schedule_one_win(const WinState w, uint32_t node, uint32_t t) {
-  const uint32_t off = fire_offset(w.delay_low, w.delay_span, draw0(w.key, K_DELAY, node, t, 0));
+// Schedules the Broadcast() of local node `node` called at tick t (the sender,
+// simulator.go:240-241, fires after one delay).  Batched trials: one lane per
+// trial, sender `node` of every trial, or the keyed draw of :240 if node == ~0u.
+__global__ void k_schedule_win(const WinState w, uint32_t node, uint32_t t, uint32_t trials, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= trials) return;
+  uint32_t local = node;
+  if (trials > 1 || node == ~0u) {
+    uint32_t v = node;
+    if (node == ~0u) v = uniform(philox(0, 0, 0, ctr3(K_SENDER, w.key.trial + i), w.key.k0, w.key.k1).x, n);
+    local = (i << w.tlog) | v;  // batched contexts have base 0
+  }
+  uint32_t kn, c3;
+  node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + local, K_DELAY, kn, c3);
+  const uint32_t off = fire_offset(w.delay_low, w.delay_span, philox(kn, t, 0, c3, w.key.k0, w.key.k1).x);
   const uint32_t s = (t + off) % w.R;
-  const uint32_t f = node >> kFineLog;
+  const uint32_t f = local >> kFineLog;
   const uint32_t pos = atomicAdd(&w.fcount[(size_t)s * w.nfine + f], 1u);
-  w.flist[((size_t)s * w.nfine + f) * kFineNodes + pos] = (uint16_t)(node & (kFineNodes - 1));
+  w.flist[((size_t)s * w.nfine + f) * kFineNodes + pos] = (uint16_t)(local & (kFineNodes - 1));
+}
+
+// ---- node-range shards (config C4) -----------------
+// Shard r of G owns nodes [r * seg_per, min((r+1) * seg_per, N)).  It keeps,
+// for EVERY node v, only the friend slots whose target it owns (prow/pent,
+// built once from the replicated table), so per-window row reads and drop
+// draws shrink with G.  Every window the shards all-gather their firing lists
+// (gfire); each shard expands every firing node against its own partition and
+// resolves its own buckets with the kernels above (keys are global ids, so
+// the union over shards equals the unsharded run bit for bit).
+
+// cnt[v] = friend slots of v whose target lies in [lo, hi) (sealed rows: slots
+// past the list hold kEmptyMsg, which is never in range).
+__global__ void k_part_count(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
+                             uint32_t* cnt) {
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
+       v += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t c = 0;
+    for (uint32_t j = 0; j < stride; ++j) {
+      const uint32_t x = ids[v * stride + j];
+      c += (x >= lo && x < hi) ? 1u : 0u;
+    }
+    cnt[v] = c;
+  }
+}
+
+// prow[v] = (uint32) off[v]; flags err if the total does not fit 32 bits.
+__global__ void k_part_narrow(const unsigned long long* off, uint64_t n, uint32_t* prow, uint32_t* err) {
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v <= n;
+       v += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long x = off[v];
+    if (x >> 32) atomicOr(err, 1u);
+    prow[v] = (uint32_t)x;
+  }
+}
+
+// pent[prow[v] ..] = (target - lo) << 5 | j for the owned slots of v, in slot order.
+__global__ void k_part_fill(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
+                            const uint32_t* prow, uint32_t* pent) {
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
+       v += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t pos = prow[v];
+    for (uint32_t j = 0; j < stride; ++j) {
+      const uint32_t x = ids[v * stride + j];
+      if (x >= lo && x < hi) pent[pos++] = ((x - lo) << 5) | j;
+    }
+  }
+}
+
+// This shard's fires of the window as entries local_id << 4 | k at out[0, Tn),
+// out[Tn, seg) = ~0u (the all-gather moves seg entries per shard).
+__global__ void k_fire_compact(const WinState w, uint32_t t0, uint32_t L, unsigned long long Tn,
+                               uint32_t* out, unsigned long long seg) {
+  const uint32_t units = L * w.nfine;
+  for (unsigned long long g = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; g < seg;
+       g += (unsigned long long)gridDim.x * blockDim.x) {
+    uint32_t e = ~0u;
+    if (g < Tn) {
+      const uint32_t u = unit_of(w, g, Tn, units);
+      const uint32_t f = u / L, k = u - f * L;
+      const uint32_t s = (t0 + k) % w.R;
+      const uint32_t i = (uint32_t)(g - w.unit_off[u]);
+      e = (((f << kFineLog) + w.flist[((size_t)s * w.nfine + f) * kFineNodes + i]) << 4) | k;
+    }
+    out[g] = e;
+  }
+}
+
+// Expand of a shard (Node.Broadcast, simulator.go:141-147): one thread per
+// all-gathered firing entry; its partitioned row (<= MAXS owned slots, slot
+// order) is read, RandomDrop (:144, :172) is drawn once per group of 4
+// ORIGINAL slots that holds an owned slot (same keys as the unsharded
+// expand), and kept targets leave through the coarse LDS partition of
+// k_expand.  Fired is counted by the firing node's owner only.
+template <bool WRITE, uint32_t MAXS>
+__global__ __launch_bounds__(kExpandBlock) void k_expand_sh(const WinState w, uint32_t t0, uint32_t L,
+                                                            int add_stats) {
+  __shared__ ExpandLds<kExpandBlock * MAXS> sm;
+  const uint32_t tid = threadIdx.x;
+  if (tid < kMaxWindow * 2) (&sm.acc[0][0])[tid] = 0;
+  const unsigned long long cbase = w.ccap[tid], cend = w.ccap[tid + 1];
+  sm.cend[tid] = cend;
+  const unsigned long long total = (unsigned long long)w.G * w.gseg;
+  const unsigned long long rounds = (total + kExpandBlock - 1) / kExpandBlock;
+  const uint32_t B = gridDim.x;
+  const uint32_t lb = (B & 7) == 0 ? (blockIdx.x & 7) * (B >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  uint32_t accp[kBitTicks];
+#pragma unroll
+  for (uint32_t kx = 0; kx < kBitTicks; ++kx) accp[kx] = 0;
+  for (unsigned long long rd = lb; rd < rounds; rd += B) {
+    sm.cnt[tid] = 0;
+    __syncthreads();
+    uint32_t mm[MAXS], mt[MAXS];
+#pragma unroll
+    for (uint32_t j = 0; j < MAXS; ++j) { mm[j] = 0; mt[j] = ~0u; }
+    const unsigned long long idx = rd * kExpandBlock + tid;
+    uint32_t v = ~0u, k = 0, c = 0, own = 0;
+    if (idx < total) {
+      const uint32_t e = w.gfire[idx];
+      if (e != ~0u) {
+        const uint32_t r = (uint32_t)(idx / w.gseg);
+        v = r * w.seg_per + (e >> 4);
+        k = e & 15;
+        own = r == w.rank;
+        const uint32_t a = w.prow[v];
+        c = w.prow[v + 1] - a;
+#pragma unroll
+        for (uint32_t j = 0; j < MAXS; ++j)
+          if (j < c) mm[j] = w.pent[a + j];
+      }
+    }
+    uint32_t sent = 0;
+    if (c) {
+      const uint32_t t = t0 + k;
+      uint32_t gm = 0;  // groups of 4 original slots holding an owned slot
+#pragma unroll
+      for (uint32_t j = 0; j < MAXS; ++j)
+        if (j < c) gm |= 1u << ((mm[j] & 31) >> 2);
+      uint32_t vn, c3drop;
+      node_key(w.tlog, w.tmask, w.key, v, K_DROP, vn, c3drop);
+      uint32_t keep = 0;
+#pragma unroll
+      for (uint32_t g = 0; g < (kWinMaxStride + 3) / 4; ++g)
+        if ((gm >> g) & 1) {
+          const u32x4 r = philox(vn, t, g, c3drop, w.key.k0, w.key.k1);   // :144, :172
+          keep |= (((int32_t)uniform(r.x, 100u) >= w.kd ? 1u : 0u) |
+                   ((int32_t)uniform(r.y, 100u) >= w.kd ? 2u : 0u) |
+                   ((int32_t)uniform(r.z, 100u) >= w.kd ? 4u : 0u) |
+                   ((int32_t)uniform(r.w, 100u) >= w.kd ? 8u : 0u)) << (4 * g);
+        }
+#pragma unroll
+      for (uint32_t j = 0; j < MAXS; ++j) {
+        const uint32_t ent = mm[j];
+        if (j < c && ((keep >> (ent & 31)) & 1)) {                       // kept: :145
+          const uint32_t tl = ent >> 5, bin = tl >> kCoarseShift;
+          uint32_t roll0 = 0;
+          if (w.kc > 0) {
+            uint32_t un, c3crash;
+            node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + tl, K_CRASH, un, c3crash);
+            roll0 = (int32_t)uniform(philox(un, t, 0, c3crash, w.key.k0, w.key.k1).x, 100u) < w.kc;
+          }
+          mt[j] = bin | (atomicAdd(&sm.cnt[bin], 1u) << 8);
+          mm[j] = (tl & ((1u << kCoarseShift) - 1)) | (k << kCoarseShift) | (roll0 << kRoll0Coarse);
+          ++sent;
+        }
+      }
+    }
+    if (v != ~0u) {
+#pragma unroll
+      for (uint32_t kx = 0; kx < kBitTicks; ++kx)
+        if (kx == k) accp[kx] += own | (sent << 16);
+    }
+    __syncthreads();
+    if (!WRITE) {
+      if (sm.cnt[tid]) atomicAdd(&w.chist[tid], (unsigned long long)sm.cnt[tid]);
+      continue;
+    }
+    block_scan256(sm.cnt, sm.off);
+    const uint32_t mycnt = sm.cnt[tid];
+    unsigned long long at = 0;
+    if (mycnt) at = atomicAdd(&w.cfill[tid], (unsigned long long)mycnt);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < MAXS; ++j)
+      if (mt[j] != ~0u) {
+        const uint32_t bin = mt[j] & 255, p = sm.off[bin] + (mt[j] >> 8);
+        sm.sorted[p] = mm[j];
+        sm.sbin[p] = (uint8_t)bin;
+      }
+    if (mycnt) {
+      if (at + mycnt > cend - cbase) atomicOr(w.err, kErrCoarse);
+      sm.gbase[tid] = cbase + at;
+    }
+    __syncthreads();
+    const uint32_t tot = sm.off[256];
+    for (uint32_t p = tid; p < tot; p += kExpandBlock) {
+      const uint32_t b = sm.sbin[p];
+      const unsigned long long pos = sm.gbase[b] + (p - sm.off[b]);
+      if (pos < sm.cend[b]) w.cmsg[pos] = sm.sorted[p];
+    }
+  }
+  if (!WRITE || !add_stats) return;
+#pragma unroll
+  for (uint32_t kx = 0; kx < kBitTicks; ++kx) {
+    if (kx >= L) continue;
+    const uint32_t fired = wave_sum32(accp[kx] & 0xFFFFu), sent = wave_sum32(accp[kx] >> 16);
+    if ((tid & 63) == 0) {
+      if (fired) atomicAdd(&sm.acc[kx][0], (unsigned long long)fired);
+      if (sent) atomicAdd(&sm.acc[kx][1], (unsigned long long)sent);
+    }
+  }
+  __syncthreads();
+  if (tid < L * 2) {
+    const uint32_t k = tid >> 1, fld = tid & 1;
+    const unsigned long long v = sm.acc[k][fld];
+    unsigned long long* row = shard_row(w, k);
+    if (v) atomicAdd(&row[fld ? ST_SENT : ST_FIRED], v);
+    if (v && fld) atomicAdd(&row[ST_MSGS], v);
+  }
 }
 
 }  // namespace
@@ -1109,8 +1397,59 @@ hipError_t win_stats_reduce(const WinState& w, uint32_t t0, uint32_t L, hipStrea
   return hipGetLastError();
 }
 
-hipError_t win_schedule_one(const WinState& w, uint32_t node, uint32_t tick, hipStream_t s) {
-  hipLaunchKernelGGL(k_schedule_one_win, dim3(1), dim3(1), 0, s, w, node, tick);
+hipError_t win_schedule(const WinState& w, uint32_t node, uint32_t tick, uint32_t trials, uint32_t n,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(k_schedule_win, dim3((trials + 255) / 256), dim3(256), 0, s, w, node, tick, trials, n);
+  return hipGetLastError();
+}
+
+hipError_t part_count(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
+                      uint32_t* cnt, hipStream_t s) {
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_part_count, dim3(blocks ? blocks : 1), dim3(256), 0, s, ids, n, stride, lo, hi, cnt);
+  return hipGetLastError();
+}
+
+hipError_t part_scan(const uint32_t* cnt, uint64_t n, unsigned long long* off, void* tmp, size_t& tmp_bytes,
+                     hipStream_t s) {
+  // off[0..n] = exclusive prefix of cnt (cnt[n] must be 0)
+  return hipcub::DeviceScan::ExclusiveScan(tmp, tmp_bytes, cnt, off, hipcub::Sum(), 0ull, (int)(n + 1), s);
+}
+
+hipError_t part_narrow(const unsigned long long* off, uint64_t n, uint32_t* prow, uint32_t* err, hipStream_t s) {
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 256) / 256, 8192);
+  hipLaunchKernelGGL(k_part_narrow, dim3(blocks), dim3(256), 0, s, off, n, prow, err);
+  return hipGetLastError();
+}
+
+hipError_t part_fill(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
+                     const uint32_t* prow, uint32_t* pent, hipStream_t s) {
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_part_fill, dim3(blocks ? blocks : 1), dim3(256), 0, s, ids, n, stride, lo, hi, prow, pent);
+  return hipGetLastError();
+}
+
+hipError_t win_fire_compact(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, uint32_t* out,
+                            uint64_t seg, hipStream_t s) {
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((seg + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_fire_compact, dim3(blocks ? blocks : 1), dim3(256), 0, s, w, t0, L,
+                     (unsigned long long)Tn, out, (unsigned long long)seg);
+  return hipGetLastError();
+}
+
+// mode 0: count coarse buckets only; 1: write + per-tick stats; 2: write only
+hipError_t win_expand_sh(const WinState& w, uint32_t t0, uint32_t L, int mode, hipStream_t s) {
+  const uint64_t total = (uint64_t)w.G * w.gseg;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((total + kExpandBlock - 1) / kExpandBlock, 8192);
+  const dim3 grid(blocks ? blocks : 1), blk(kExpandBlock);
+  const int st = mode == 1 ? 1 : 0;
+  if (w.stride <= 8) {
+    if (mode) hipLaunchKernelGGL((k_expand_sh<true, 8>), grid, blk, 0, s, w, t0, L, st);
+    else hipLaunchKernelGGL((k_expand_sh<false, 8>), grid, blk, 0, s, w, t0, L, 0);
+  } else {
+    if (mode) hipLaunchKernelGGL((k_expand_sh<true, kWinMaxStride>), grid, blk, 0, s, w, t0, L, st);
+    else hipLaunchKernelGGL((k_expand_sh<false, kWinMaxStride>), grid, blk, 0, s, w, t0, L, 0);
+  }
   return hipGetLastError();
 }
 

@@ -13,9 +13,11 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib
-from ._lib import GossipError, Params, TickStats, Timing, Window
+from ._lib import GossipError, Params, TickStats, Timing, TrialStats, Window
 
 STAT_FIELDS = ("tick", "fired", "sent", "messages", "received", "crashed", "pending")
+TRIAL_FIELDS = ("trial", "tick_99", "tick", "fired", "sent", "messages", "received", "crashed",
+                "status")
 
 
 @dataclass
@@ -34,6 +36,8 @@ class Config:
     timing: bool = False
     engine: str = "window"  # "window" (default) or "tick" (per-tick atomic engine)
     model: str = "flood"    # "flood" (the reference) or "pushpull" (extension)
+    trials: int = 1         # batched independent trials trial .. trial+trials-1 (config C3)
+    pp_l2_only: bool = False  # push-pull: force the no-LDS summary path (tests)
 
     def to_params(self) -> Params:
         p = Params()
@@ -45,7 +49,9 @@ class Config:
             raise ValueError(f"model must be 'flood' or 'pushpull', not {self.model!r}")
         p.model = 1 if self.model == "pushpull" else 0
         p.flags = (_lib.GS_FLAG_TIMING if self.timing else 0) | \
-            (_lib.GS_FLAG_TICK_ENGINE if self.engine == "tick" else 0)
+            (_lib.GS_FLAG_TICK_ENGINE if self.engine == "tick" else 0) | \
+            (_lib.GS_FLAG_PP_L2_ONLY if self.pp_l2_only else 0)
+        p.trials = max(1, int(self.trials))
         return p
 
 
@@ -55,21 +61,46 @@ def _stats_array(buf, k: int) -> np.ndarray:
 
 
 class Simulator:
-    """One broadcast on one GPU (a gs_ctx)."""
+    """One broadcast (or one batch of trials) behind a gs_ctx.
 
-    def __init__(self, cfg: Config, node_range=None):
+    devices=None: one GPU (cfg.device), gs_create.  devices=[d0, d1, ...]:
+    gs_create_multi -- a node-range-sharded broadcast over those devices
+    (entries may repeat), or the trials split over them when cfg.trials > 1.
+    Simulator.rank(...): one rank of a multi-process run (gs_create_rank)."""
+
+    def __init__(self, cfg: Config, devices=None, _rank=None):
         self.cfg = cfg
         self.L = _lib.load()
         self._p = cfg.to_params()
-        if node_range is not None:
-            self._p.node_lo, self._p.node_hi = int(node_range[0]), int(node_range[1])
         h = C.c_void_p()
-        rc = self.L.gs_create(C.byref(self._p), C.byref(h))
+        if _rank is not None:
+            nranks, rank, cid = _rank
+            rc = self.L.gs_create_rank(C.byref(self._p), cfg.device, nranks, rank, cid, C.byref(h))
+            what = "gs_create_rank"
+        elif devices is not None:
+            devs = (C.c_int * len(devices))(*[int(d) for d in devices])
+            rc = self.L.gs_create_multi(C.byref(self._p), devs, len(devices), C.byref(h))
+            what = "gs_create_multi"
+        else:
+            rc = self.L.gs_create(C.byref(self._p), C.byref(h))
+            what = "gs_create"
         if rc != 0:
-            raise GossipError(rc, f"gs_create failed: {self.L.gs_strerror(rc).decode()}")
+            raise GossipError(rc, f"{what} failed: {self.L.gs_strerror(rc).decode()}")
         self.h = h
         self.n = cfg.n
+        self.trials = max(1, int(cfg.trials))
         self.words = (cfg.n + 63) // 64
+
+    @classmethod
+    def rank(cls, cfg: Config, nranks: int, rank: int, comm_id: bytes | None):
+        """Rank `rank` of `nranks` processes (gs_create_rank); comm_id from
+        comm_unique_id() on rank 0, shipped to every rank by the caller.  With
+        cfg.trials > 1 the rank gets its share of the trials (no comm_id)."""
+        sim = cls(cfg, _rank=(nranks, rank, comm_id))
+        if cfg.trials > 1:  # this rank's trials
+            t0 = cfg.trials * rank // nranks
+            sim.trials = cfg.trials * (rank + 1) // nranks - t0
+        return sim
 
     # -- plumbing --------------------------------------------------------
     def _check(self, rc: int, what: str):
@@ -93,10 +124,13 @@ class Simulator:
 
     # -- overlay (simulator.go:62-106, 127-164, 214-235) -------------------
     def load_peers(self, deg: np.ndarray, ids: np.ndarray):
+        """deg [n], ids [n, stride]; batched trials: the trials' tables back to
+        back (deg [trials*n], ids [trials*n, stride], ids local to the trial)."""
         deg = np.ascontiguousarray(deg, dtype=np.uint8)
         ids = np.ascontiguousarray(ids, dtype=np.uint32)
-        if deg.shape != (self.n,) or ids.ndim != 2 or ids.shape[0] != self.n:
-            raise ValueError("deg must be [n], ids [n, stride]")
+        m = self.n * self.trials
+        if deg.shape != (m,) or ids.ndim != 2 or ids.shape[0] != m:
+            raise ValueError("deg must be [trials*n], ids [trials*n, stride]")
         self._check(self.L.gs_load_peers(self.h, deg.ctypes.data, ids.ctypes.data, ids.shape[1]),
                     "gs_load_peers")
 
@@ -117,8 +151,8 @@ class Simulator:
     def read_peers(self):
         stride = C.c_uint32(0)
         self._check(self.L.gs_read_peers(self.h, None, None, C.byref(stride)), "gs_read_peers")
-        deg = np.zeros(self.n, dtype=np.uint8)
-        ids = np.zeros((self.n, stride.value), dtype=np.uint32)
+        deg = np.zeros(self.n * self.trials, dtype=np.uint8)
+        ids = np.zeros((self.n * self.trials, stride.value), dtype=np.uint32)
         self._check(self.L.gs_read_peers(self.h, deg.ctypes.data, ids.ctypes.data, C.byref(stride)),
                     "gs_read_peers")
         return deg, ids
@@ -150,38 +184,62 @@ class Simulator:
         return {f: int(getattr(t, f)) for f in STAT_FIELDS}
 
     def received(self) -> np.ndarray:
-        w = np.zeros(self.words, dtype=np.uint64)
+        """ceil(n/64) words (batched trials: [trials, ceil(n/64)])."""
+        w = np.zeros(self.words * self.trials, dtype=np.uint64)
         self._check(self.L.gs_read_received(self.h, w.ctypes.data, w.size), "gs_read_received")
-        return w
+        return w if self.trials == 1 else w.reshape(self.trials, self.words)
 
     def crashed(self) -> np.ndarray:
-        w = np.zeros(self.words, dtype=np.uint64)
+        w = np.zeros(self.words * self.trials, dtype=np.uint64)
         self._check(self.L.gs_read_crashed(self.h, w.ctypes.data, w.size), "gs_read_crashed")
-        return w
+        return w if self.trials == 1 else w.reshape(self.trials, self.words)
+
+    def trial_results(self) -> np.ndarray:
+        """[trials, len(TRIAL_FIELDS)] int64: per trial its number, first
+        covered tick, stopping poll's tick and counters there, and status."""
+        buf = (TrialStats * self.trials)()
+        k = C.c_size_t(0)
+        self._check(self.L.gs_trial_results(self.h, buf, self.trials, C.byref(k)), "gs_trial_results")
+        return np.array([[int(getattr(buf[i], f)) for f in TRIAL_FIELDS] for i in range(k.value)],
+                        dtype=np.int64).reshape(k.value, len(TRIAL_FIELDS))
+
+    def shard_info(self):
+        """[(lo, hi)] node range of every shard."""
+        ns = C.c_uint32(0)
+        lo, hi = C.c_uint64(0), C.c_uint64(0)
+        self._check(self.L.gs_shard_info(self.h, 0, C.byref(ns), C.byref(lo), C.byref(hi)), "gs_shard_info")
+        out = []
+        for i in range(ns.value):
+            self._check(self.L.gs_shard_info(self.h, i, None, C.byref(lo), C.byref(hi)), "gs_shard_info")
+            out.append((int(lo.value), int(hi.value)))
+        return out
 
     def set_flags(self, timing: bool):
         flags = (_lib.GS_FLAG_TIMING if timing else 0) | \
-            (_lib.GS_FLAG_TICK_ENGINE if self.cfg.engine == "tick" else 0)
+            (_lib.GS_FLAG_TICK_ENGINE if self.cfg.engine == "tick" else 0) | \
+            (_lib.GS_FLAG_PP_L2_ONLY if self.cfg.pp_l2_only else 0)
         self._check(self.L.gs_set_flags(self.h, flags), "gs_set_flags")
 
     def reset(self):
         self._check(self.L.gs_reset(self.h), "gs_reset")
 
-    # -- node-range sharding hooks ---------------------------------------
     def set_stream(self, hip_stream: int | None):
         self._check(self.L.gs_set_stream(self.h, hip_stream), "gs_set_stream")
-
-    def frontier_export(self, tick: int, dst_ptr: int, word_lo: int, nwords: int):
-        self._check(self.L.gs_frontier_export(self.h, tick, dst_ptr, word_lo, nwords),
-                    "gs_frontier_export")
-
-    def frontier_import(self, tick: int, src_ptr: int):
-        self._check(self.L.gs_frontier_import(self.h, tick, src_ptr), "gs_frontier_import")
 
     def timing(self) -> dict:
         t = Timing()
         self._check(self.L.gs_timing_get(self.h, C.byref(t)), "gs_timing_get")
         return {f: getattr(t, f) for f, _ in Timing._fields_}
+
+
+def comm_unique_id() -> bytes:
+    """RCCL unique id for gs_create_rank (rank 0 makes it, every rank uses it)."""
+    L = _lib.load()
+    b = C.create_string_buffer(_lib.GS_COMM_ID_BYTES)
+    rc = L.gs_comm_unique_id(b)
+    if rc != 0:
+        raise GossipError(rc, "gs_comm_unique_id failed")
+    return b.raw
 
 
 def covered(recv: int, n: int) -> bool:

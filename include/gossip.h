@@ -11,7 +11,10 @@
  *  - return 0 on success, <0 on error (GS_E*); message via gs_last_error().
  *  - all caller buffers are caller-owned and copied during the call; nothing
  *    is retained across calls (cgo pointer rules).
- *  - one gs_ctx is single-threaded; it owns one HIP device, one stream.
+ *  - one gs_ctx is single-threaded.  gs_create gives one HIP device and one
+ *    stream; gs_create_multi spreads one context over several devices (or
+ *    several shards of one device) and gs_create_rank makes one shard of a
+ *    multi-process (RCCL) run -- every other call is the same for all three.
  *  - node ids are uint32 (n <= 2^31-1); friend rows are uint32[stride] with a
  *    uint8 length per node (a friends list is at most 255 long).
  *  - every random decision is drawn from Philox4x32-10 keyed by
@@ -26,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 2
+#define GS_ABI_VERSION 3
 
 enum {
   GS_OK = 0,
@@ -41,6 +44,8 @@ enum {
 /* Flags (gs_params.flags). */
 #define GS_FLAG_TIMING 1u /* time every tick kernel with HIP events (gs_timing) */
 #define GS_FLAG_TICK_ENGINE 2u /* force the per-tick atomic engine (default: window engine) */
+#define GS_FLAG_PP_L2_ONLY 4u  /* push-pull: skip the LDS-staged second-level summaries (the path
+                                * N > ~1.02e9 takes); read at gs_create, for tests */
 
 /* Dissemination model (gs_params.model). */
 #define GS_MODEL_FLOOD 0u    /* the reference: every receipt re-broadcasts to all friends (simulator.go:107-149) */
@@ -64,10 +69,13 @@ typedef struct gs_params {
   int32_t device;      /* HIP device ordinal                                  */
   uint32_t flags;      /* GS_FLAG_*                                           */
   uint32_t model;      /* GS_MODEL_* (0 = the reference's push flooding)      */
-  /* Node-range sharding (config C4): this context owns nodes [node_lo,
-   * node_hi); both multiples of 4096 except node_hi == n.  0,0 = all nodes. */
-  uint64_t node_lo, node_hi;
-  uint64_t reserved_[4];
+  /* Batched independent trials (config C3): trials trial .. trial+trials-1 of n
+   * nodes each, run at once (one overlay, one broadcast per trial, keyed by
+   * its trial number exactly as a one-trial context).  0 or 1 = one trial.
+   * The reference runs one trial per process (simulator.go:207-253). */
+  uint32_t trials;
+  uint32_t reserved0_;
+  uint64_t reserved_[5];
 } gs_params;
 
 /* One tick (1 ms) of the broadcast phase; the reference exposes these as the
@@ -106,7 +114,19 @@ typedef struct gs_timing {
 } gs_timing;
 
 /* gs_run status */
-enum { GS_RUN_COVERED = 0, GS_RUN_QUIESCENT = 1, GS_RUN_MAX_TICKS = 2 };
+enum { GS_RUN_COVERED = 0, GS_RUN_QUIESCENT = 1, GS_RUN_MAX_TICKS = 2, GS_RUN_RUNNING = -1 };
+
+/* One trial's outcome (batched trials, or the one trial of any flood context):
+ * the counters at the poll that stopped it under gs_run's rule -- what the
+ * reference prints at :252-253 -- plus the first tick it was covered. */
+typedef struct gs_trial_stats {
+  uint64_t trial;     /* trial number (Philox counter word 3)                 */
+  uint64_t tick_99;   /* first tick with float32(recv)/float32(n) >= 0.99, else 0 */
+  uint64_t tick;      /* tick of the stopping poll (or the last tick run)     */
+  uint64_t fired, sent, messages, received, crashed;  /* cumulative at `tick` */
+  int32_t status;     /* GS_RUN_* (GS_RUN_RUNNING: not stopped yet)          */
+  int32_t reserved_;
+} gs_trial_stats;
 
 typedef struct gs_ctx gs_ctx;
 
@@ -115,14 +135,39 @@ const char* gs_strerror(int code);
 
 /* Replaces simulator.go:186-212 (flag globals, GlobalView/NewNode allocation).
  * Validates params exactly as the reference would fail: n == 0 (:240 panics),
- * delay_high <= delay_low (:167 panics). */
+ * delay_high <= delay_low (:167 panics).  One device (params.device). */
 int gs_create(const gs_params* params, gs_ctx** out);
+
+/* ---- multi-GPU (no reference counterpart: the reference runs every node as
+ * a goroutine of one process, simulator.go:214-217) ----
+ * One context over ndev devices (entries may repeat: several shards or trial
+ * batches on one GPU).  params.trials > 1: the trials are split over the
+ * devices and run with no communication.  Otherwise ONE broadcast whose node
+ * range is split into ndev shards (config C4): every window the shards
+ * all-gather their firing lists (device-to-device copies) and sum their
+ * counters; results are bit-identical to gs_create's. */
+int gs_create_multi(const gs_params* params, const int* devices, int ndev, gs_ctx** out);
+/* Multi-process (one process per GPU): rank 0 calls gs_comm_unique_id and
+ * ships the GS_COMM_ID_BYTES bytes to every rank; each rank calls
+ * gs_create_rank.  A flood run is then node-range sharded over the ranks with
+ * an RCCL all-gather per window and an RCCL sum per gs_step (every rank's
+ * gs_step/gs_run/gs_totals return the global counters); params.trials > 1
+ * gives each rank its share of the trials (no communication, id may be NULL). */
+#define GS_COMM_ID_BYTES 128
+int gs_comm_unique_id(uint8_t id[GS_COMM_ID_BYTES]);
+int gs_create_rank(const gs_params* params, int device, int nranks, int rank,
+                   const uint8_t* id, gs_ctx** out);
+/* Nodes [lo, hi) owned by shard `index` of a context (index < *nshards);
+ * an unsharded context is one shard [0, n). */
+int gs_shard_info(const gs_ctx* ctx, uint32_t index, uint32_t* nshards, uint64_t* lo, uint64_t* hi);
 void gs_destroy(gs_ctx* ctx);
 const char* gs_last_error(const gs_ctx* ctx);
 
 /* Injects a peer table in place of the overlay (the `friends` slices,
  * simulator.go:45,58).  deg[n] uint8, ids[n*stride] uint32 row-major.
- * Host buffers; copied. */
+ * Host buffers; copied.  Batched trials: trials tables back to back
+ * (deg[trials*n], ids[trials*n*stride], ids local to their trial).  A sharded
+ * context keeps only each shard's partition (gs_read_peers then fails). */
 int gs_load_peers(gs_ctx* ctx, const uint8_t* deg, const uint32_t* ids, uint32_t stride);
 /* Same, from device-resident buffers (copied device-to-device). */
 int gs_load_peers_device(gs_ctx* ctx, const void* d_deg, const void* d_ids, uint32_t stride);
@@ -137,11 +182,13 @@ int gs_build_overlay(gs_ctx* ctx, uint64_t max_ticks, gs_window* win, size_t cap
                      size_t* nwin, uint64_t* final_tick);
 
 /* Pre-failed node mask (extension, config C5): words[ceil(n/64)], set bits
- * are crash-stopped before the broadcast (they never count nor forward). */
+ * are crash-stopped before the broadcast: they never count nor forward, and
+ * a failed sender does not broadcast (both models).  Not for batched trials. */
 int gs_set_failed(gs_ctx* ctx, const uint64_t* words, size_t nwords);
 
 /* Replaces simulator.go:239-241.  sender < 0 draws it from the keyed stream
- * like rand.Intn(len(GlobalView)).  The sender is NOT marked received. */
+ * like rand.Intn(len(GlobalView)) (per trial when batched).  The sender is NOT
+ * marked received. */
 int gs_broadcast_begin(gs_ctx* ctx, int64_t sender);
 /* Advances `ticks` ticks of the receive/broadcast actors (simulator.go:107-123,
  * 140-149, 166-184); out[i] (may be NULL) gets each tick's stats. */
@@ -149,13 +196,22 @@ int gs_step(gs_ctx* ctx, uint32_t ticks, gs_tick_stats* out);
 /* Replaces the poll loop simulator.go:243-251: steps `poll` ticks at a time
  * until float32(received)/float32(n) >= 0.99 at a poll (GS_RUN_COVERED), no
  * broadcast is pending (GS_RUN_QUIESCENT; the reference would spin forever;
- * push-pull: a poll window informed nobody new), or max_ticks.  out (may be NULL) receives one gs_tick_stats per poll. */
+ * push-pull: no call can change the informed set any more -- no live
+ * informed node has a live uninformed friend and no live uninformed node has
+ * an informed friend, or every call is dropped), or max_ticks.  out (may be
+ * NULL) receives one gs_tick_stats per poll.  Batched trials: each trial
+ * stops at its own poll (gs_trial_results); the run ends when all have. */
 int gs_run(gs_ctx* ctx, uint32_t poll, uint64_t max_ticks, gs_tick_stats* out,
            size_t cap, size_t* nout, int32_t* status);
 /* Cumulative totals so far (tick, fired/sent/messages summed). */
 int gs_totals(gs_ctx* ctx, gs_tick_stats* out);
 
-/* Bitset dumps for per-round parity: words[ceil(n/64)], bit v of word v/64. */
+/* Per-trial outcomes, trials in order (cap entries; *nout gets the count). */
+int gs_trial_results(gs_ctx* ctx, gs_trial_stats* out, size_t cap, size_t* nout);
+
+/* Bitset dumps for per-round parity: words[ceil(n/64)], bit v of word v/64
+ * (batched trials: trials x ceil(n/64) words, trial-major).  A rank of a
+ * multi-process run fills only the words of the nodes it owns (others 0). */
 int gs_read_received(gs_ctx* ctx, uint64_t* words, size_t nwords);
 int gs_read_crashed(gs_ctx* ctx, uint64_t* words, size_t nwords);
 
@@ -167,18 +223,9 @@ int gs_set_flags(gs_ctx* ctx, uint32_t flags);
  * (a fresh process in the reference, simulator.go:207). */
 int gs_reset(gs_ctx* ctx);
 
-/* ---- node-range sharding hooks (no reference counterpart: the reference
- * runs every node as a goroutine of one process, simulator.go:214-217) ---- */
-/* Run all later device work on `hip_stream` (a hipStream_t, e.g. the stream
- * RCCL collectives are issued on); NULL restores the context's own stream. */
+/* Run all later device work of a one-device context on `hip_stream` (a
+ * hipStream_t owned by the caller); NULL restores the context's own stream. */
 int gs_set_stream(gs_ctx* ctx, void* hip_stream);
-/* Enqueue a copy of words [word_lo, word_lo+nwords) of the fire slot that
- * tick `tick` will process into the device buffer dst (no host sync). */
-int gs_frontier_export(gs_ctx* ctx, uint64_t tick, void* dst, uint64_t word_lo,
-                       uint64_t nwords);
-/* Enqueue an overwrite of that fire slot with ceil(n/64) words from the
- * device buffer src (the all-gathered global firing set; no host sync). */
-int gs_frontier_import(gs_ctx* ctx, uint64_t tick, const void* src);
 
 /* ---- host-only helpers for the reference's stdout contract ------------- */
 /* Go fmt %v of a float32 (strconv 'g', -1, 32), e.g. 99.61 or 9.9999994e-08

@@ -346,8 +346,9 @@ int or_engine_begin(or_engine* e, int64_t sender) {
     e->begun = 1;
     return 0;
   }
-  if (s >= e->lo && s < e->hi)   /* only the owner of the sender schedules it */
-    schedule(e, (uint32_t)s, 0); /* simulator.go:241; sender NOT marked received */
+  /* only the owner of the sender schedules it (simulator.go:241; the sender
+   * is NOT marked received); a pre-failed sender (extension) never broadcasts */
+  if (s >= e->lo && s < e->hi && !BIT(e->crashed, s)) schedule(e, (uint32_t)s, 0);
   e->begun = 1;
   return 0;
 }

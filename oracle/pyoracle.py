@@ -230,10 +230,35 @@ def run_to_coverage(p: Params, deg, ids, sender=-1, poll=10, max_ticks=100000,
         last = s[-1]
         if covered(int(last[4]), p.n) or int(last[6]) == 0 or int(last[0]) >= max_ticks:
             break
-        if p.model == MODEL_PUSHPULL and int(last[4]) == r0:  # gs_run's push-pull quiescence
+        # gs_run's push-pull stop: a poll informed nobody new and no call can
+        # change the informed set any more
+        if p.model == MODEL_PUSHPULL and int(last[4]) == r0 and \
+                pp_stalled(p, deg, ids, e.received(), e.crashed()):
             break
         r0 = int(last[4])
     return np.concatenate(rows), e
+
+
+def _bits(words, idx):
+    return ((words[idx >> 6] >> (idx & 63).astype(np.uint64)) & np.uint64(1)).astype(bool)
+
+
+def pp_stalled(p: Params, deg, ids, recv, failed) -> bool:
+    """Push-pull quiescence: no live informed node has a live uninformed friend
+    and no live uninformed node has an informed friend (or every call is lost)."""
+    if threshold(p.drop_rate) >= 100:
+        return True
+    n = int(p.n)
+    v = np.arange(n, dtype=np.int64)
+    deg = np.asarray(deg, dtype=np.int64)
+    ids = np.asarray(ids, dtype=np.int64)
+    live = ~_bits(failed, v)
+    iv = _bits(recv, v)
+    slot = np.arange(ids.shape[1])[None, :] < deg[:, None]
+    iu = _bits(recv, ids)
+    fu = _bits(failed, ids)
+    useful = np.where(iv[:, None], ~iu & ~fu, iu) & slot & live[:, None]
+    return not useful.any()
 
 
 def refsim(p: Params, rng_seed: int, max_ms: int = 10_000_000) -> RefsimResult:

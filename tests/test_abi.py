@@ -31,7 +31,7 @@ def test_exports_every_declared_symbol(L):
     for s in syms:
         assert hasattr(lib, s), f"{s} declared in include/gossip.h but not exported"
     assert sorted(L.EXPORTS) == syms
-    assert lib.gs_version() == 2
+    assert lib.gs_version() == 3
 
 
 def test_struct_sizes_match_header(L):
@@ -39,6 +39,7 @@ def test_struct_sizes_match_header(L):
     assert C.sizeof(L.Params) == 8 + 4 * 4 + 8 + 8 + 8 + 4 + 4 + 4 + 4 + 8 + 8 + 4 * 8
     assert C.sizeof(L.TickStats) == 7 * 8
     assert C.sizeof(L.Window) == 3 * 8
+    assert C.sizeof(L.TrialStats) == 8 * 8 + 2 * 4
 
 
 @pytest.mark.parametrize("x,s", [

@@ -237,14 +237,3 @@ def test_run_polls_like_reference(gs, oracle):
         assert int(polls[-1][0]) == int(rows[-1][0])
         assert int(polls[-1][4]) == int(rows[-1][4])
         assert int(polls[:, 3].sum()) == int(rows[:, 3].sum())
-
-
-def test_concurrent_trials_match_serial(gs):
-    """Config C3 path: trials run concurrently (one context and stream per
-    host thread) give the same per-trial table as one at a time."""
-    from gossip_simulator_amd import dist as gd
-    cfg = gs.Config(n=20000, crashrate=0.01, seed=5, engine=gs.engine)
-    serial = gd.run_trials(gs.Simulator, cfg, total=6)
-    threaded = gd.run_trials(gs.Simulator, cfg, total=6, concurrency=4)
-    assert np.array_equal(serial, threaded)
-    assert list(serial[:, 0]) == list(range(6))

@@ -131,7 +131,7 @@ def test_oracle_known_answers(oracle):
     (dict(PP, n=20000, drop_rate=1.0), 6, 5, 6, 0.0),       # every call lost
     (dict(PP, n=65536 + 77, drop_rate=0.29, trial=5), 19, 18, 19, 0.03),  # wide rows
 ])
-def test_gpu_pushpull_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac):
+def test_gpu_pushpull_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac, l2_only=False):
     import gossip_simulator_amd as gs
     gs.load()
     n = kw["n"]
@@ -144,7 +144,8 @@ def test_gpu_pushpull_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac):
     e.begin(-1)
     cfg = gs.Config(n=n, fanout=kw["fanout"], fanin=kw["fanin"], delaylow=kw["delay_low"],
                     delayhigh=kw["delay_high"], droprate=kw["drop_rate"], crashrate=kw["crash_rate"],
-                    seed=kw["seed"], trial=kw["trial"], model="pushpull")
+                    seed=kw["seed"], trial=kw["trial"], model="pushpull", pp_l2_only=l2_only,
+                    timing=l2_only)
     with gs.Simulator(cfg) as sim:
         sim.load_peers(deg, ids)
         if failed is not None:
@@ -159,12 +160,12 @@ def test_gpu_pushpull_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac):
 
 
 @pytest.mark.gpu
-def test_gpu_pushpull_bit_exact_l2_only(oracle, monkeypatch):
+def test_gpu_pushpull_bit_exact_l2_only(oracle):
     """The round kernel without its LDS summary level (the N > ~1.02e9 path),
-    forced by GS_PP_L2_ONLY: bit-exact to the oracle like the default path."""
-    monkeypatch.setenv("GS_PP_L2_ONLY", "1")
-    test_gpu_pushpull_bit_exact(oracle, dict(PP, n=65536 + 77, drop_rate=0.29, trial=5), 19, 18, 19, 0.03)
-    test_gpu_pushpull_bit_exact(oracle, dict(PP, n=20000), 6, 5, 6, 0.0)
+    forced by GS_FLAG_PP_L2_ONLY: bit-exact to the oracle like the default path."""
+    test_gpu_pushpull_bit_exact(oracle, dict(PP, n=65536 + 77, drop_rate=0.29, trial=5), 19, 18, 19, 0.03,
+                                l2_only=True)
+    test_gpu_pushpull_bit_exact(oracle, dict(PP, n=20000), 6, 5, 6, 0.0, l2_only=True)
 
 
 @pytest.mark.gpu
