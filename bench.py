@@ -13,7 +13,15 @@ in HBM before the timed region; the overlay build is timed separately.
 Multi-GPU: one process per GPU; each rank runs an independent trial (its own
 overlay, trial = rank) -- batched Monte Carlo trials with no data-path
 collective, so "scaling" is weak and value = all ranks' delivered sends / the
-slowest rank's time.
+slowest rank's time.  `value` counts delivered sends (friend slots not
+dropped, simulator.go:144-145); the reference's TotalMessage (:111) also leaves
+out receipts at crashed nodes and is reported as config.messages_per_step.
+
+Extensions in the same line: config C3 (10,000 trials of N = 1e5, batched
+contexts, split over the ranks), config C4 (N = 1e8, fanout 18, fanin 19,
+one broadcast node-range sharded over the ranks: RCCL all-gather of each
+window's firing lists inside libgossip_hip.so; one shard at --gpus 1), and
+config C5's push-pull and failure-mask runs.
 
 Roofline: HBM-bound; 12 algorithmic bytes per delivered send (4-B friend id +
 4-B read and 4-B write of the target's state word), divided by
@@ -51,8 +59,10 @@ def parse():
     ap.add_argument("--cpu-n", type=int, default=10_000_000,
                     help="nodes in the bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--no-c3", action="store_true",
-                    help="skip the C3 concurrent-trials sample (its host threads crash rocprofv3's tracer)")
+    ap.add_argument("--no-c3", action="store_true", help="skip the C3 batched-trials run")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 node-range-sharded run")
+    ap.add_argument("--c3-trials", type=int, default=10_000)
+    ap.add_argument("--c3-batch", type=int, default=2500, help="trials per batched context")
     ap.add_argument("--no-extensions", action="store_true",
                     help="skip the C5 extension runs (1%% failed mask, push-pull)")
     return ap.parse_args()
@@ -159,7 +169,9 @@ def main():
     if not a.no_extensions:
         ext.update(pushpull_runs(a, gs, rank, local))
         if not a.no_c3:
-            ext["c3_trials"] = c3_trials(a, gs, rank, local)
+            ext["c3_trials"] = c3_trials(a, gs, rank, world, local, dist)
+        if not a.no_c4:
+            ext["c4_sharded"] = c4_sharded(a, gs, rank, world, local, dist)
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_n > 0:
@@ -180,6 +192,7 @@ def main():
             "dtype": "u32",
             "data": "synthetic (GPU-built overlay, keyed Philox)",
             "config": {"workload": "C5-reference-model: single push-flood broadcast per GPU",
+                       "value_counts": "delivered sends (simulator.go:144-145), not TotalMessage (:111)",
                        "n": a.n, "fanout": a.fanout, "fanin": a.fanin,
                        "delaylow": a.delaylow, "delayhigh": a.delayhigh,
                        "droprate": a.droprate, "crashrate": a.crashrate,
@@ -286,23 +299,112 @@ def pushpull_runs(a, gs, rank, local):
     return out
 
 
-def c3_trials(a, gs, rank, local, total=96, conc=16):
-    """Config C3 sample: independent trials at N = 1e5 (defaults otherwise:
-    crashrate 0.001), each its own GPU-built overlay + broadcast to 99 %,
-    `conc` at a time on this GPU (dist.run_trials, one context and stream per
-    host thread).  The full C3 (10,000 trials) is this rate x 10,000 / N GPUs."""
+def c3_trials(a, gs, rank, world, local, dist):
+    """Config C3: a.c3_trials trials at N = 1e5 (reference defaults), each its
+    own GPU-built overlay and broadcast to its 99 % poll, split over the ranks
+    and run as batched contexts of a.c3_batch trials (all of a batch's
+    overlays, then all its broadcasts, at once).  Timed end to end: context
+    creation, overlay, broadcast, results."""
     import numpy as np
+    import torch
+    from dataclasses import replace
     from gossip_simulator_amd import dist as gd
+    t0, t1 = gd.trial_range(a.c3_trials, rank, world)
     cfg = gs.Config(n=100_000, seed=a.seed, device=local)
-    gd.run_trials(gs.Simulator, cfg, total=conc, concurrency=conc)  # warmup
-    t0 = time.perf_counter()
-    res = gd.run_trials(gs.Simulator, cfg, total=total, concurrency=conc)
-    dt = time.perf_counter() - t0
-    log(f"C3 sample: {total} trials in {dt:.2f} s ({conc} concurrent)")
-    return {"trials_per_s": round(total / dt, 2), "n": 100_000, "trials": total, "concurrent": conc,
-            "delivered_per_s": round(float(res[:, 3].sum()) / dt, 1),
-            "median_tick_99": int(np.median(res[:, 1])),
-            "s_for_10000_trials_1gpu": round(10_000 * dt / total, 1)}
+
+    def batch(lo, hi):
+        with gs.Simulator(replace(cfg, trial=lo, trials=hi - lo)) as sim:
+            sim.build_overlay()
+            sim.broadcast_begin(-1)
+            sim.run(poll=10)
+            return sim.trial_results()
+
+    batch(t0, min(t1, t0 + 64))  # warmup (code objects, allocator)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    start = time.perf_counter()
+    rows = [batch(b, min(b + a.c3_batch, t1)) for b in range(t0, t1, a.c3_batch)]
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - start
+    res = np.concatenate(rows) if rows else np.zeros((0, 9), np.int64)
+    tot = torch.tensor([float(dt), float(res[:, 4].sum()), float(res[:, 5].sum()), float(len(res)),
+                        float((res[:, 8] == 0).sum())], dtype=torch.float64, device="cuda")
+    if dist is not None:
+        mx = tot[:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        tot[0] = mx[0]
+    dt, sent, msgs, ntr, ncov = [float(x) for x in tot.cpu()]
+    cov = res[res[:, 8] == 0]
+    log(f"C3: {int(ntr)} trials in {dt:.2f} s ({int(ncov)} covered)")
+    return {"trials": int(ntr), "n": 100_000, "batch": a.c3_batch, "s_total": round(dt, 3),
+            "trials_per_s": round(ntr / dt, 1), "delivered_per_s": round(sent / dt, 1),
+            "messages_per_s": round(msgs / dt, 1), "covered": int(ncov),
+            "median_tick_99_rank0": int(np.median(cov[:, 1])) if len(cov) else None,
+            "mean_messages_per_trial": round(msgs / max(ntr, 1), 1),
+            "note": "measured: every trial's overlay + broadcast to its stopping poll, whole job"}
+
+
+def c4_sharded(a, gs, rank, world, local, dist):
+    """Config C4: N = 1e8, fanout 18 (floor(ln 1e8)), fanin 19, reference
+    defaults otherwise; ONE broadcast with the node range sharded over the
+    ranks (gs_create_rank: per-window RCCL all-gather of the firing lists, per-
+    step RCCL sum of the counters) -- one shard through the same window driver
+    at --gpus 1.  value = delivered sends / wall time of the broadcast."""
+    import torch
+    from gossip_simulator_amd import dist as gd
+    cfg = gs.Config(n=100_000_000, fanout=18, fanin=19, seed=a.seed, device=local)
+    sim = gd.open_shard(cfg, rank, world) if world > 1 else gs.Simulator(cfg, devices=[local])
+    try:
+        t0 = time.perf_counter()
+        sim.build_overlay()
+        ov = time.perf_counter() - t0
+        steps = max(a.steps // 4, 2)
+        for _ in range(2):
+            sim.reset()
+            sim.broadcast_begin(-1)
+            sim.run(poll=10)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(steps):
+            sim.reset()
+            sim.broadcast_begin(-1)
+            _, status = sim.run(poll=10)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t1
+        tot = sim.totals()  # global counters on every rank
+        if dist is not None:
+            t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        sim.set_flags(True)
+        sim.reset()
+        sim.broadcast_begin(-1)
+        sim.run(poll=10)
+        tm = sim.timing()
+        sim.set_flags(False)
+        kern = tm["deliver_ms"] + tm["resolve_ms"]
+        launches = max(int(tm["resolve_launches"]), 1)
+        shard_sent = tot["sent"] / world  # a shard's share of the deliveries (balanced ranges)
+        ach = BYTES_PER_SEND * shard_sent / (kern * 1e-3) / 1e9 if kern > 0 else 0.0
+        log(f"C4 sharded x{world}: {dt * 1e3 / steps:.1f} ms per broadcast, {tot['sent'] / (dt / steps):.3e} msgs/s")
+        return {"value": round(tot["sent"] * steps / dt, 1), "unit": "msgs/s", "shards": world,
+                "ms_per_step": round(dt * 1e3 / steps, 3), "steps": steps, "n": cfg.n, "fanout": 18, "fanin": 19,
+                "ticks": tot["tick"], "status": STATUS[status], "coverage": round(tot["received"] / cfg.n, 6),
+                "delivered_per_step": tot["sent"], "messages_per_step": tot["messages"],
+                "overlay_s": round(ov, 3),
+                "roofline": {"bound": "hbm", "kernel": "shard window pipeline k_expand_sh -> k_plan/k_part2 -> "
+                             "k_resolve (rank 0)", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
+                             "avg_launch_us": round(kern * 1e3 / launches, 2), "launches": launches,
+                             "kernels_total_ms": {"k_expand_sh": round(tm["expand_ms"], 3),
+                                                  "k_plan+k_part2": round(tm["part_ms"], 3),
+                                                  "k_resolve": round(tm["resolve_ms"], 3)}}}
+    finally:
+        sim.close()
 
 
 def pmc_traffic():
