@@ -75,6 +75,12 @@ struct gs_ctx {
   Buf gmap, cmsg, fmsg, tmp;
   unsigned long long* h_cap = nullptr;  // pinned [257] coarse region plan
   unsigned long long* h_misc = nullptr; // pinned scratch (counts, flags)
+  // device-driven windows (run_async)
+  WinCtl* d_ctl = nullptr;
+  unsigned long long* d_stage = nullptr;  // [kSlots][kStageWords]
+  unsigned long long* h_stage = nullptr;  // pinned copy
+  std::vector<hipEvent_t> wev;            // one per staging slot
+  bool async_off = false;                 // GS_SYNC_WINDOWS=1: host-driven windows only (A/B tests)
   // trials: `trials` per context (batched when > 1), ids trial << tlog | node
   uint32_t trials = 1, tlog = 32;
   uint64_t ntot = 0;                    // nodes in this context's id space
@@ -508,6 +514,7 @@ int ctx_setup(gs_ctx* c, const gs_params* params, int device, bool shard, uint32
     if (rc) { why = c->err; return rc; }
   }
   c->tacc.assign(c->trials, TrialAcc{});
+  c->async_off = getenv("GS_SYNC_WINDOWS") != nullptr;
   if (hipMemsetAsync(c->d_state, 0, total, c->stream) != hipSuccess ||
       (c->d_cnt && hipMemsetAsync(c->d_cnt, 0, s.n * 4, c->stream) != hipSuccess) ||
       hipHostMalloc((void**)&c->h_stats, (size_t)kStatSlots * kStatFields * 8) != hipSuccess ||
@@ -554,8 +561,11 @@ void destroy_one(gs_ctx* c) {
     if (ptr) (void)hipFree(ptr);
   for (Buf* b : {&c->gmap, &c->cmsg, &c->fmsg, &c->tmp, &c->gfire})
     if (b->p) (void)hipFree(b->p);
-  for (void* ptr : {(void*)c->h_cap, (void*)c->h_misc, (void*)c->h_stats, (void*)c->h_tstat})
+  for (void* ptr : {(void*)c->h_cap, (void*)c->h_misc, (void*)c->h_stats, (void*)c->h_tstat, (void*)c->h_stage})
     if (ptr) (void)hipHostFree(ptr);
+  for (void* ptr : {(void*)c->d_ctl, (void*)c->d_stage})
+    if (ptr) (void)hipFree(ptr);
+  for (hipEvent_t e : c->wev) (void)hipEventDestroy(e);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
 }
@@ -1278,6 +1288,144 @@ int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing, uint64_t tchunk
   return GS_OK;
 }
 
+// ---- device-driven windows ----------------------------------------------------
+// The unsharded one-trial window engine runs gs_step / gs_run without a host
+// round trip per window: k_cut makes the window cut and coarse plan on the
+// device, k_close applies gs_run's poll rule there, every kernel reads the
+// window from ctl, and the host enqueues window i before it reads window
+// i-1's results (staging slot + event), so the GPU never waits on it.  A
+// partition overflow (skewed targets, or a message buffer too small) makes
+// every later kernel a no-op; the host then finishes with run_windows, which
+// redoes that window exactly and grows the buffers.
+constexpr uint32_t kSlots = 4;
+
+bool async_ok(const gs_ctx* c) {
+  return c->win && !c->pp && !c->shard && !c->group && c->trials == 1 && !c->async_off &&
+         !(c->p.flags & GS_FLAG_TIMING);
+}
+
+uint64_t cover_threshold(uint64_t n) {  // smallest r with covered(r, n)
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) / 2;
+    if (covered(mid, n)) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
+
+int async_setup(gs_ctx* c) {
+  if (!c->d_ctl) {
+    CK(c, hipMalloc(&c->d_ctl, sizeof(WinCtl)));
+    CK(c, hipMalloc(&c->d_stage, (size_t)kSlots * kStageWords * 8));
+    CK(c, hipHostMalloc((void**)&c->h_stage, (size_t)kSlots * kStageWords * 8));
+    for (uint32_t i = 0; i < kSlots; ++i) {
+      hipEvent_t e;
+      CK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      c->wev.push_back(e);
+    }
+  }
+  // the message buffers keep the size the windows so far needed: a window
+  // that needs more is flagged and redone host-driven, which grows them
+  if (!grow(c->gmap, ((c->ntot + 1 + 63) / 64 + 1) * 4) || !grow(c->cmsg, 64) || !grow(c->fmsg, 64))
+    return fail(c, GS_ENOMEM, "cannot allocate the window message buffers");
+  return GS_OK;
+}
+
+// Ticks c->t+1 .. tend-1, or (poll > 0) until gs_run's rule stops the run at a
+// poll.  on_tick(tick, row) sees every tick's counters in order.  *stop gets
+// 1 + GS_RUN_* if a poll stopped the run; *fallback = true if a window
+// overflowed (the caller continues host-driven from c->t).
+template <class OnTick>
+int run_async(gs_ctx* c, uint64_t tend, uint32_t poll, uint64_t max_ticks, OnTick on_tick, uint32_t* stop,
+              bool* fallback) {
+  *stop = 0;
+  *fallback = false;
+  RC(async_setup(c));
+  WinState w = c->ws;
+  w.ctl = c->d_ctl;
+  w.stage = c->d_stage;
+  w.lstride = std::min<uint32_t>(std::max<int32_t>(c->p.delay_low, 1), kBitTicks);
+  w.gmap = (uint32_t*)c->gmap.p;
+  w.cmsg = (uint32_t*)c->cmsg.p;
+  w.fmsg = (uint32_t*)c->fmsg.p;
+  WinCtl h{};
+  h.tnext = (uint32_t)(c->t + 1);
+  h.tend = (uint32_t)std::min<uint64_t>(tend, 0xFFFFFFFFull);
+  h.poll = poll;
+  h.pbase = (uint32_t)c->t;
+  h.lmax = w.lstride;
+  h.recv = c->recv;
+  h.crashed = c->crashed;
+  h.pending = c->pending;
+  h.cover = cover_threshold(c->p.n);
+  h.max_ticks = max_ticks;
+  h.cmsg_cap = c->cmsg.bytes / 4 > 16 ? c->cmsg.bytes / 4 - 16 : 0;
+  h.fmsg_cap = c->fmsg.bytes / 4 > 16 ? c->fmsg.bytes / 4 - 16 : 0;
+  CK(c, hipMemcpyAsync(c->d_ctl, &h, sizeof h, hipMemcpyHostToDevice, c->stream));
+  CK(c, hipMemsetAsync(w.tfires, 0, kMaxWindow * 8, c->stream));
+  const uint64_t budget = (uint64_t)w.nfine * kWinSlotsPerBucket;
+  // launch sizes: grid-stride kernels, sized for the dense windows
+  const uint64_t Tn_bound = std::min<uint64_t>(c->ntot + 1, 4096ull * 1024),
+                 T_bound = std::min<uint64_t>((c->ntot + 1) * w.stride, 2048ull * 16384);
+  size_t need = 0;
+  CK(c, win_scan_units_masked(w, nullptr, need, c->stream));
+  if (!grow(c->tmp, need)) return fail(c, GS_ENOMEM, "cannot allocate scan scratch");
+  auto enqueue = [&](uint32_t slot) -> int {
+    CK(c, win_units(w, 0, w.lstride, c->stream));
+    CK(c, win_cut(w, budget, c->stream));
+    size_t nb = c->tmp.bytes;
+    CK(c, win_scan_units_masked(w, c->tmp.p, nb, c->stream));
+    CK(c, win_groupmap(w, w.lstride, c->stream));
+    CK(c, win_expand(w, 0, w.lstride, Tn_bound, 1, c->stream));
+    CK(c, win_plan(w, false, c->stream));
+    CK(c, win_part2(w, T_bound, true, c->stream));
+    CK(c, win_consume(w, c->stream));
+    CK(c, win_resolve(w, 0, w.lstride, c->stream));
+    CK(c, win_close(w, slot, c->stream));
+    CK(c, hipMemcpyAsync(c->h_stage + (size_t)slot * kStageWords, c->d_stage + (size_t)slot * kStageWords,
+                         kStageWords * 8, hipMemcpyDeviceToHost, c->stream));
+    CK(c, hipEventRecord(c->wev[slot], c->stream));
+    return GS_OK;
+  };
+  // window i-1's results: 0 = go on, 1 = finished (the enqueued window i is a no-op)
+  auto absorb = [&](uint32_t slot, int* what) -> int {
+    CK(c, hipEventSynchronize(c->wev[slot]));
+    const unsigned long long* st = c->h_stage + (size_t)slot * kStageWords;
+    const uint32_t t0 = (uint32_t)st[0], L = (uint32_t)st[1];
+    *what = 0;
+    if (st[3] & (kErrCoarse | kErrFine)) {  // overflow: later windows did nothing
+      *fallback = true;
+      *what = 1;
+      return GS_OK;
+    }
+    for (uint32_t k = 0; k < L; ++k) on_tick((uint64_t)t0 + k, st + 8 + (size_t)k * kStatFields);
+    if (st[2]) *stop = (uint32_t)st[2];
+    if (st[2] || L == 0 || (uint64_t)t0 + L >= tend) *what = 1;
+    return GS_OK;
+  };
+  RC(enqueue(0));
+  for (uint32_t i = 1;; ++i) {
+    RC(enqueue(i % kSlots));
+    int what = 0;
+    RC(absorb((i - 1) % kSlots, &what));
+    if (what) break;
+  }
+  CK(c, hipStreamSynchronize(c->stream));
+  if (*fallback) {  // undo what the failed window left: its partial counters and flags
+    uint32_t e = 0;
+    CK(c, hipMemcpy(&e, c->d_err, 4, hipMemcpyDeviceToHost));
+    e &= ~(kErrCoarse | kErrFine);
+    CK(c, hipMemcpy(c->d_err, &e, 4, hipMemcpyHostToDevice));
+    CK(c, hipMemsetAsync(c->ws.sstats, 0, (size_t)kStatShards * kMaxWindow * kStatFields * 8, c->stream));
+    CK(c, hipMemsetAsync(c->ws.tfires, 0, kMaxWindow * 8, c->stream));
+    CK(c, hipStreamSynchronize(c->stream));
+  }
+  uint32_t err = 0;
+  CK(c, hipMemcpy(&err, c->d_err, 4, hipMemcpyDeviceToHost));
+  if (err & kErrArrivals) return fail(c, GS_EOVERFLOW, "too many arrivals at one node in one tick");
+  return GS_OK;
+}
+
 // ---- node-range shards ------------------------------------------------------
 // One window for shards `ms` (all shards of a group, or this rank's one shard
 // with an RCCL communicator), SURVEY.md section 8(e)2:
@@ -1623,6 +1771,19 @@ int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
   if (c->group) return shard_step(c, c->mem, ticks, out);
   if (c->shard) return shard_step(c, {c}, ticks, out);
   CK(c, hipSetDevice(c->dev));
+  if (async_ok(c) && ticks > 0) {  // device-driven windows
+    uint32_t stop = 0, k = 0;
+    bool fallback = false;
+    RC(run_async(c, c->t + ticks + 1, 0, ~0ull,
+                 [&](uint64_t tick, const unsigned long long* row) {
+                   account_tick(c, tick, row, out ? &out[k] : nullptr);
+                   ++k;
+                 },
+                 &stop, &fallback));
+    if (!fallback) return GS_OK;
+    ticks -= k;  // a window overflowed: the rest host-driven (it redoes that window exactly)
+    if (out) out += k;
+  }
   const bool timing = (c->p.flags & GS_FLAG_TIMING) != 0;
   const bool flood = c->st.kc == 0;
   const bool batched = c->trials > 1;
@@ -1758,12 +1919,38 @@ int gs_run(gs_ctx* c, uint32_t poll, uint64_t max_ticks, gs_tick_stats* out, siz
   int32_t st = GS_RUN_MAX_TICKS;
   const bool trials = c->trials > 1 && !c->group;
   const bool flood = !c->pp;
+  const uint64_t pbase = c->t;
+  uint64_t f0 = c->fired, s0 = c->sent, m0 = c->msgs;
+  if (async_ok(c)) {  // device-driven windows: the poll rule runs on the device (k_close)
+    uint32_t stop = 0;
+    bool fallback = false;
+    RC(run_async(c, ~0ull, poll, max_ticks,
+                 [&](uint64_t tick, const unsigned long long* row) {
+                   account_tick(c, tick, row, nullptr);
+                   if ((tick - pbase) % poll) return;
+                   if (out && k < cap)
+                     out[k] = gs_tick_stats{c->t, c->fired - f0, c->sent - s0, c->msgs - m0, c->recv,
+                                            c->crashed, c->pending};
+                   ++k;
+                   f0 = c->fired; s0 = c->sent; m0 = c->msgs;
+                 },
+                 &stop, &fallback));
+    if (!fallback) {
+      st = stop ? (int32_t)stop - 1 : GS_RUN_MAX_TICKS;
+      snap_trial(c, 0, st);
+      if (nout) *nout = k;
+      if (status) *status = st;
+      return GS_OK;
+    }
+  }
   for (;;) {
-    const uint64_t f0 = c->fired, s0 = c->sent, m0 = c->msgs, r0 = c->recv;
-    RC(gs_step(c, poll, nullptr));
+    const uint64_t r0 = c->recv;
+    // one poll (the first may finish a poll the device-driven windows began)
+    RC(gs_step(c, (uint32_t)(poll - (c->t - pbase) % poll), nullptr));
     if (out && k < cap)
       out[k] = gs_tick_stats{c->t, c->fired - f0, c->sent - s0, c->msgs - m0, c->recv, c->crashed, c->pending};
     ++k;
+    f0 = c->fired; s0 = c->sent; m0 = c->msgs;
     if (trials) {  // each trial stops at its own poll (simulator.go:243-251 per process)
       uint32_t running = 0;
       for (uint32_t tr = 0; tr < c->trials; ++tr) {

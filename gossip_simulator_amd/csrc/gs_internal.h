@@ -87,6 +87,18 @@ constexpr uint32_t kBitTicks = 10;              // window length k_resolve's per
 constexpr uint32_t kWinSlotsPerBucket = 1u << 16;  // window cut: friend slots per fine bucket
                                                 // (bounds the message buffers, not LDS)
 
+// Device-driven window loop (gs_run / gs_step of an unsharded one-trial
+// context): the window's start, length and the poll rule's counters live on
+// the device, so the host enqueues windows without waiting for any of them.
+struct WinCtl {
+  uint32_t t, L, tnext, tend;        // window start, length; next start; first tick not run
+  uint32_t poll, pbase, stop, lmax;  // polls at pbase + k*poll (0: none); 1 + GS_RUN_* once stopped
+  unsigned long long Tn, T;          // broadcasts firing in the window, their friend slots
+  unsigned long long recv, crashed, pending, cover, max_ticks;  // poll rule state
+  unsigned long long cmsg_cap, fmsg_cap;  // message buffer capacities (elements)
+};
+constexpr uint32_t kStageWords = 8 + 16 * 8;  // per-window staging: snapshot + per-tick rows
+
 struct WinState {
   const uint8_t* deg;
   const uint32_t* ids;
@@ -115,6 +127,9 @@ struct WinState {
   // trial (null for a single-trial context)
   uint32_t* tstat;
   uint32_t tofs;                 // tstat row of the window's first tick (ticks since the rows were zeroed)
+  WinCtl* ctl;                   // device-driven windows (null: the host passes t0 / L)
+  unsigned long long* stage;     // [slots][kStageWords] per-window results for the host (device-driven)
+  uint32_t lstride;              // unit layout stride: units u = f * lstride + k
   // node-range shard: partitioned friend rows (prow[v]..prow[v+1] of pent, entry =
   // (target - base) << 5 | slot j) and the all-gathered window fire list
   const uint32_t* prow;
@@ -154,6 +169,11 @@ constexpr uint32_t kErrCoarse = 8;    // a coarse region overflowed its estimate
 constexpr uint32_t kErrFine = 16;     // a fine region overflowed its estimate
 
 hipError_t win_units(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
+// device-driven windows (w.ctl set, w.lstride = ctl->lmax)
+hipError_t win_cut(const WinState& w, unsigned long long budget, hipStream_t s);
+hipError_t win_scan_units_masked(const WinState& w, void* tmp, size_t& tmp_bytes, hipStream_t s);
+hipError_t win_consume(const WinState& w, hipStream_t s);
+hipError_t win_close(const WinState& w, uint32_t slot, hipStream_t s);
 hipError_t win_scan_units(const WinState& w, uint32_t L, void* tmp, size_t& tmp_bytes, hipStream_t s);
 hipError_t win_groupmap(const WinState& w, uint32_t L, hipStream_t s);
 hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, int mode,

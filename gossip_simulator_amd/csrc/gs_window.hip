@@ -30,6 +30,7 @@
 // Fire lists: fcount[R][nfine] + flist[R][nfine][16384] (u16 local ids).
 #include <hipcub/hipcub.hpp>
 
+#include "gossip.h"
 #include "gs_internal.h"
 
 namespace gs {
@@ -43,22 +44,56 @@ constexpr uint32_t kResolveBlock = 512;
 constexpr uint32_t kRoll0Coarse = kCoarseShift + 4;
 constexpr uint32_t kRoll0Fine = kFineLog + 4;
 
-// Units = (fine bucket f, tick k), bucket-major (u = f*L + k): the L fire lists
-// of one bucket are expanded back to back, so friends-row lines that several
-// ticks of the window share are fetched once into the XCD's L2.  usize = fires;
-// tfires[k] = fires per tick (the host's window cut).  Also zeroes the window's
+// Device-driven windows (w.ctl set): the window being opened starts at
+// ctl->tnext and may hold up to Lw ticks (none once the run has stopped, a
+// partition overflowed -- the host then redoes that window -- or tend is
+// reached; never past the next poll).  0 = nothing to do.
+__device__ __forceinline__ bool win_abort(const WinState& w) {
+  return (*w.err & (kErrCoarse | kErrFine)) != 0;
+}
+__device__ __forceinline__ uint32_t win_open(const WinState& w, uint32_t& t) {
+  const WinCtl* c = w.ctl;
+  if (win_abort(w) || c->stop) return 0;
+  t = c->tnext;
+  if (t >= c->tend) return 0;
+  uint32_t Lw = min(c->lmax, c->tend - t);
+  if (c->poll) {
+    const uint32_t P = c->pbase + c->poll * ((t - c->pbase + c->poll - 1) / c->poll);  // next poll tick
+    Lw = min(Lw, P - t + 1);
+  }
+  return Lw;
+}
+// A kernel of an opened window: its start and length (0: skip the window).
+__device__ __forceinline__ uint32_t win_live(const WinState& w, uint32_t& t0, uint32_t L) {
+  if (!w.ctl) return L;
+  if (win_abort(w)) return 0;
+  t0 = w.ctl->t;
+  return w.ctl->L;
+}
+
+// Units = (fine bucket f, tick k), bucket-major (u = f*Ls + k, Ls = the layout
+// stride: L, or lmax for device-driven windows): the L fire lists of one
+// bucket are expanded back to back, so friends-row lines that several ticks of
+// the window share are fetched once into the XCD's L2.  usize = fires;
+// tfires[k] = fires per tick (the window cut).  Also zeroes the window's
 // counters (one launch instead of several memsets).
 __global__ void k_units(const WinState w, uint32_t t0, uint32_t L) {
   __shared__ uint32_t s_t[kMaxWindow];
-  const uint32_t units = L * w.nfine;
+  uint32_t Ls = L;
+  if (w.ctl) {
+    L = win_open(w, t0);
+    if (!L) return;
+    Ls = w.lstride;
+  }
+  const uint32_t units = Ls * w.nfine;
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
   if (threadIdx.x < kMaxWindow) s_t[threadIdx.x] = 0;
   __syncthreads();
   for (uint32_t u = tid; u <= units; u += nth) {
     if (u == units) { w.usize[u] = 0; continue; }
-    const uint32_t f = u / L, k = u - f * L;
-    const uint32_t s = (t0 + k) % w.R;
-    const uint32_t c = w.fcount[(size_t)s * w.nfine + f];
+    const uint32_t f = u / Ls, k = u - f * Ls;
+    uint32_t c = 0;
+    if (k < L) c = w.fcount[(size_t)((t0 + k) % w.R) * w.nfine + f];
     w.usize[u] = c;
     if (c) atomicAdd(&s_t[k], c);
   }
@@ -66,11 +101,81 @@ __global__ void k_units(const WinState w, uint32_t t0, uint32_t L) {
   if (threadIdx.x < L && s_t[threadIdx.x]) atomicAdd(&w.tfires[threadIdx.x], (unsigned long long)s_t[threadIdx.x]);
   for (uint32_t i = tid; i < 256; i += nth) { w.chist[i] = 0; w.cfill[i] = 0; }
   for (uint32_t i = tid; i < w.nfine; i += nth) w.ffill[i] = 0;
-  if (tid == 0) *w.err &= ~(kErrCoarse | kErrFine);
+  if (tid == 0 && !w.ctl) *w.err &= ~(kErrCoarse | kErrFine);  // device-driven: sticky until the host redoes
+}
+
+// Device-driven windows: the cut (as the host-driven engine makes it: a
+// window holds whole ticks while its friend slots fit `budget`), the coarse
+// region plan of the window's T friend slots, and the window's place in ctl.
+// One block.
+__global__ void k_cut(const WinState w, unsigned long long budget) {
+  __shared__ unsigned long long s_sz[256];
+  __shared__ unsigned long long s_T;
+  __shared__ uint32_t s_go;
+  WinCtl* c = w.ctl;
+  const uint32_t b = threadIdx.x;  // 256 threads: thread b plans coarse bin b
+  if (win_abort(w)) return;  // keep ctl: the host redoes the failed window
+  uint32_t t = 0;
+  const uint32_t Lw = win_open(w, t);
+  __syncthreads();
+  if (b == 0) {
+    s_go = Lw != 0;
+    if (!Lw) {  // stopped or past tend: the rest of this window does nothing
+      c->L = 0;
+      c->Tn = 0;
+    } else {
+      uint32_t L = 1;
+      unsigned long long Tn = w.tfires[0];
+      while (L < Lw && (Tn + w.tfires[L]) * w.stride <= budget) Tn += w.tfires[L++];
+      for (uint32_t k = 0; k < kMaxWindow; ++k) w.tfires[k] = 0;
+      c->t = t;
+      c->L = L;
+      c->tnext = t + L;
+      c->Tn = Tn;
+      c->T = Tn * w.stride;
+      s_T = Tn * w.stride;
+    }
+  }
+  __syncthreads();
+  if (!s_go) return;
+  // coarse regions: node share of T + 4096 each (plan_coarse on the host)
+  const unsigned long long lo = (unsigned long long)b << kCoarseShift;
+  const unsigned long long hi = min((unsigned long long)w.n, lo + (1ull << kCoarseShift));
+  s_sz[b] = b < w.ncoarse ? (unsigned long long)((double)s_T * (double)(hi - lo) / (double)w.n) + 4096 : 0ull;
+  __syncthreads();
+  for (uint32_t o = 1; o < 256; o <<= 1) {  // inclusive scan
+    const unsigned long long x = b >= o ? s_sz[b - o] : 0ull;
+    __syncthreads();
+    s_sz[b] += x;
+    __syncthreads();
+  }
+  const unsigned long long total = s_sz[255];
+  if (total > c->cmsg_cap) {  // the buffer is too small: no region at all, the host grows and redoes
+    w.ccap[b] = 0;
+    if (b == 0) { w.ccap[256] = 0; atomicOr(w.err, kErrCoarse); }
+    return;
+  }
+  w.ccap[b] = b ? s_sz[b - 1] : 0ull;
+  if (b == 255) w.ccap[256] = total;
+}
+
+// Device-driven windows: the window's fire lists are consumed.
+__global__ void k_consume(const WinState w) {
+  uint32_t t0 = 0;
+  const uint32_t L = win_live(w, t0, 0);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < L * w.nfine; i += gridDim.x * blockDim.x) {
+    const uint32_t k = i / w.nfine, f = i - k * w.nfine;
+    w.fcount[(size_t)((t0 + k) % w.R) * w.nfine + f] = 0;
+  }
 }
 
 // gmap[q] = unit holding firing index 64*q.
 __global__ void k_groupmap(const WinState w, uint32_t L) {
+  if (w.ctl) {
+    uint32_t t0;
+    if (!win_live(w, t0, 0)) return;
+    L = w.lstride;
+  }
   const uint32_t units = L * w.nfine;
   for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
     const unsigned long long a = w.unit_off[u], b = w.unit_off[u + 1];
@@ -110,6 +215,53 @@ __global__ void k_stats_reduce(const WinState w, uint32_t t0, uint32_t L) {
     *x = 0;
   }
   if (sum) w.stats[(size_t)((t0 + k) % kStatSlots) * kStatFields + fld] += sum;
+}
+
+// Device-driven windows: the window's per-tick counters (stats ring, and
+// staging slot `slot` for the host with the window's snapshot), the poll
+// rule's running state and, at a poll tick, gs_run's stop rule
+// (simulator.go:243-248: covered at float32 99 %; the engine also stops when
+// nothing is pending or max_ticks has passed).  One block of 128 threads.
+__global__ void k_close(const WinState w, uint32_t slot) {
+  __shared__ unsigned long long rows[kMaxWindow][kStatFields];
+  WinCtl* c = w.ctl;
+  unsigned long long* st = w.stage + (size_t)slot * kStageWords;
+  uint32_t t0 = 0;
+  const uint32_t L = win_live(w, t0, 0);
+  const uint32_t tid = threadIdx.x, k = tid / kStatFields, fld = tid % kStatFields;
+  if (k < L) {
+    unsigned long long sum = 0;
+    for (uint32_t sh = 0; sh < kStatShards; ++sh) {
+      unsigned long long* x = &w.sstats[((size_t)sh * kMaxWindow + k) * kStatFields + fld];
+      sum += *x;
+      *x = 0;
+    }
+    rows[k][fld] = sum;
+    w.stats[(size_t)((t0 + k) % kStatSlots) * kStatFields + fld] = sum;
+    st[8 + k * kStatFields + fld] = sum;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  uint32_t stop = c->stop;
+  if (L) {
+    for (uint32_t j = 0; j < L; ++j) {
+      c->recv += rows[j][ST_RECV];
+      c->crashed += rows[j][ST_CRASH];
+      c->pending += rows[j][ST_SCHED] - rows[j][ST_FIRED];
+    }
+    const uint32_t tl = t0 + L - 1;  // windows never cross a poll tick
+    if (c->poll && (tl - c->pbase) % c->poll == 0 && !stop) {
+      if (c->recv >= c->cover) stop = 1 + GS_RUN_COVERED;
+      else if (c->pending == 0) stop = 1 + GS_RUN_QUIESCENT;
+      else if (tl >= c->max_ticks) stop = 1 + GS_RUN_MAX_TICKS;
+      c->stop = stop;
+    }
+  }
+  st[0] = t0;
+  st[1] = L;
+  st[2] = stop;
+  st[3] = *w.err;
+  st[4] = L ? c->Tn : 0;
 }
 
 template <uint32_t SLOTS>  // LDS message slots per round: block * nodes per thread * row length
@@ -200,7 +352,14 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
                                                          unsigned long long Tn, int add_stats) {
   __shared__ ExpandLds<kExpandBlock * NPT * MAXS> sm;
   const uint32_t tid = threadIdx.x;
-  const uint32_t units = L * w.nfine;
+  uint32_t Ls = L;  // unit layout stride
+  if (w.ctl) {
+    L = win_live(w, t0, 0);
+    if (!L) return;
+    Tn = w.ctl->Tn;
+    Ls = w.lstride;
+  }
+  const uint32_t units = Ls * w.nfine;
   constexpr uint32_t per_round = kExpandBlock * NPT;
   if (tid < kMaxWindow * 2) (&sm.acc[0][0])[tid] = 0;
   static_assert(kExpandBlock == 256, "thread b owns coarse bin b");
@@ -229,7 +388,7 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
       kk[q] = 0;
       if (g < Tn) {
         const uint32_t u = unit_of(w, g, Tn, units);
-        const uint32_t f = u / L, k = u - f * L;
+        const uint32_t f = u / Ls, k = u - f * Ls;
         const uint32_t s = (t0 + k) % w.R;
         const uint32_t i = (uint32_t)(g - w.unit_off[u]);
         vv[q] = (f << kFineLog) + w.flist[((size_t)s * w.nfine + f) * kFineNodes + i];
@@ -357,6 +516,10 @@ __global__ void k_plan(const WinState w, bool exact) {
   __shared__ unsigned long long s_cap[256];
   __shared__ uint32_t s_tp[257];
   const uint32_t tid = threadIdx.x;  // 256 threads per block
+  if (w.ctl) {
+    uint32_t t0;
+    if (!win_live(w, t0, 0)) return;
+  }
   const unsigned long long cnt = w.cfill[tid] < w.ccap[tid + 1] - w.ccap[tid]
                                      ? w.cfill[tid] : w.ccap[tid + 1] - w.ccap[tid];
   const bool live = tid < w.ncoarse;
@@ -375,9 +538,14 @@ __global__ void k_plan(const WinState w, bool exact) {
     if (tid == 0) w.tprefix[256] = s_tp[256];
   }
   if (exact) return;  // fstart comes from the exact count + scan instead
+  // device-driven windows: regions past the buffer are empty, and the window
+  // is flagged for the host to grow the buffer and redo it
+  const unsigned long long cap = w.ctl ? w.ctl->fmsg_cap : ~0ull;
+  if (w.ctl && blockIdx.x == 0 && tid == 0 && s_base[w.ncoarse] > cap) atomicOr(w.err, kErrFine);
   for (uint32_t f = blockIdx.x * blockDim.x + tid; f <= w.nfine; f += gridDim.x * blockDim.x) {
     const uint32_t c = f >> 8, d = f & 255;
-    w.fstart[f] = f == w.nfine ? s_base[w.ncoarse] : s_base[c] + d * s_cap[c];
+    const unsigned long long x = f == w.nfine ? s_base[w.ncoarse] : s_base[c] + d * s_cap[c];
+    w.fstart[f] = x < cap ? x : cap;
   }
 }
 
@@ -402,6 +570,10 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   __shared__ TileSort ts;
   __shared__ uint32_t s_tp[257];
   const uint32_t tid = threadIdx.x;
+  if (w.ctl) {
+    uint32_t t0;
+    if (!win_live(w, t0, 0)) return;
+  }
   if (tid <= 256) s_tp[tid] = w.tprefix[tid];
   __syncthreads();
   const uint32_t ntiles = s_tp[256];
@@ -715,6 +887,8 @@ __device__ __forceinline__ void flush_counts(const WinState& w, ResolveLds& sm, 
 __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
   __shared__ ResolveLds sm;
   const uint32_t tid = threadIdx.x, G = gridDim.x;
+  L = win_live(w, t0, L);
+  if (!L) return;
   static_assert(kBitWords == kResolveBlock, "one bit word per thread");
   static_assert(kWinMaxRing <= kResolveBlock, "one ring slot per thread");
   if (tid < kMaxWindow * 4) (&sm.st[0][0])[tid] = 0;
@@ -959,6 +1133,8 @@ __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w,
   __shared__ uint32_t st[kWaves][kMaxWindow][4];  // per wave: dead (not counted), recv, crash per tick
   __shared__ uint32_t sk[kWaves][N];               // each wave's sorted keys
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  L = win_live(w, t0, L);
+  if (!L) return;
   static_assert(kWaves * kMaxWindow * 4 == kSmallBlock, "one counter per thread");
   (&st[0][0][0])[tid] = 0;
   __syncthreads();
@@ -1307,6 +1483,39 @@ hipError_t win_units(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s) 
   const uint32_t units = std::max<uint32_t>(L * w.nfine + 1, w.nfine);
   const uint32_t blocks = std::min<uint32_t>((units + 255) / 256, 4096);
   hipLaunchKernelGGL(k_units, dim3(blocks), dim3(256), 0, s, w, t0, L);
+  return hipGetLastError();
+}
+
+hipError_t win_cut(const WinState& w, unsigned long long budget, hipStream_t s) {
+  hipLaunchKernelGGL(k_cut, dim3(1), dim3(256), 0, s, w, budget);
+  return hipGetLastError();
+}
+
+// Device-driven windows: units of ticks >= ctl->L count as empty.
+struct MaskedUnits {
+  const unsigned long long* usize;
+  const WinCtl* ctl;
+  uint32_t lstride;
+  __device__ __forceinline__ unsigned long long operator()(const uint32_t& u) const {
+    return (u % lstride) < ctl->L ? usize[u] : 0ull;
+  }
+};
+
+hipError_t win_scan_units_masked(const WinState& w, void* tmp, size_t& tmp_bytes, hipStream_t s) {
+  hipcub::CountingInputIterator<uint32_t> it(0);
+  hipcub::TransformInputIterator<unsigned long long, MaskedUnits, hipcub::CountingInputIterator<uint32_t>> in(
+      it, MaskedUnits{w.usize, w.ctl, w.lstride});
+  return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, in, w.unit_off, (int)(w.lstride * w.nfine + 1), s);
+}
+
+hipError_t win_consume(const WinState& w, hipStream_t s) {
+  const uint32_t blocks = std::min<uint32_t>((w.lstride * w.nfine + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_consume, dim3(blocks), dim3(256), 0, s, w);
+  return hipGetLastError();
+}
+
+hipError_t win_close(const WinState& w, uint32_t slot, hipStream_t s) {
+  hipLaunchKernelGGL(k_close, dim3(1), dim3(kMaxWindow * kStatFields), 0, s, w, slot);
   return hipGetLastError();
 }
 
