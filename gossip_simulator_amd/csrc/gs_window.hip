@@ -196,6 +196,22 @@ __device__ __forceinline__ uint32_t unit_of(const WinState& w, unsigned long lon
   return lo;
 }
 
+// The same for a wave whose 64 lanes hold the 64 consecutive firing indices
+// of group g0 / 64 (g0 wave-uniform): the group's unit bounds are two scalar
+// loads, and only a group that spans several units searches per lane.
+__device__ __forceinline__ uint32_t unit_of_wave(const WinState& w, unsigned long long g0, unsigned long long g,
+                                                 unsigned long long Tn, uint32_t units) {
+  const unsigned long long q = g0 >> 6;
+  uint32_t lo = w.gmap[q];
+  uint32_t hi = ((q + 1) << 6) < Tn ? w.gmap[q + 1] : units - 1;
+  if (lo == hi) return lo;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (w.unit_off[mid] <= g) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
 // Per-tick counters are added into one of kStatShards copies (by workgroup)
 // and summed into the stats ring by k_stats_reduce: tens of thousands of
 // workgroups adding into the same few lines would serialise at the memory-side
@@ -383,16 +399,19 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
     uint32_t vv[NPT], kk[NPT];
 #pragma unroll
     for (uint32_t q = 0; q < NPT; ++q) {
-      const unsigned long long g = rd * per_round + q * kExpandBlock + tid;
+      const unsigned long long g0 = rd * per_round + q * kExpandBlock + __builtin_amdgcn_readfirstlane(tid & ~63u);
+      const unsigned long long g = g0 + (tid & 63);
       vv[q] = ~0u;
       kk[q] = 0;
-      if (g < Tn) {
-        const uint32_t u = unit_of(w, g, Tn, units);
+      if (g0 < Tn) {
+        const uint32_t u = unit_of_wave(w, g0, g < Tn ? g : Tn - 1, Tn, units);
+        if (g < Tn) {
         const uint32_t f = u / Ls, k = u - f * Ls;
         const uint32_t s = (t0 + k) % w.R;
         const uint32_t i = (uint32_t)(g - w.unit_off[u]);
         vv[q] = (f << kFineLog) + w.flist[((size_t)s * w.nfine + f) * kFineNodes + i];
         kk[q] = k;
+        }
       }
     }
 #pragma unroll
@@ -1128,11 +1147,17 @@ __global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, 
 // Instance E takes buckets with 64*(E/4) < M <= 64*E receipts (E = 1, 4);
 // k_resolve takes the rest.  The launches touch disjoint buckets.
 template <uint32_t E>
+__device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t t0, uint32_t L, uint32_t f,
+                                                     unsigned long long M, uint32_t (&st)[16][kMaxWindow][4],
+                                                     uint32_t* skw);
+
+// One launch for both sizes: each wave takes one bucket and the E = 1 or
+// E = 4 body by its receipt count (wave-uniform).
 __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w, uint32_t t0, uint32_t L) {
-  constexpr uint32_t N = 64 * E, kWaves = kSmallBlock / 64;
+  constexpr uint32_t kWaves = kSmallBlock / 64;
   __shared__ uint32_t st[kWaves][kMaxWindow][4];  // per wave: dead (not counted), recv, crash per tick
-  __shared__ uint32_t sk[kWaves][N];               // each wave's sorted keys
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  __shared__ uint32_t sk[kWaves][64 * 4];          // each wave's sorted keys
+  const uint32_t tid = threadIdx.x, wv = tid >> 6;
   L = win_live(w, t0, L);
   if (!L) return;
   static_assert(kWaves * kMaxWindow * 4 == kSmallBlock, "one counter per thread");
@@ -1140,7 +1165,30 @@ __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w,
   __syncthreads();
   const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
   const unsigned long long M = f < w.nfine ? w.ffill[f] : 0ull;
-  if (M > (E == 1 ? 0ull : 64ull * (E / 4)) && M <= N) {
+  if (M > 0 && M <= 64) resolve_small_bucket<1>(w, t0, L, f, M, st, sk[wv]);
+  else if (M > 64 && M <= 256) resolve_small_bucket<4>(w, t0, L, f, M, st, sk[wv]);
+  __syncthreads();
+  if (tid < L * 3) {
+    const uint32_t k = tid / 3, fld = tid - k * 3;
+    uint32_t v = 0;
+    for (uint32_t q = 0; q < kWaves; ++q) v += st[q][k][fld];
+    unsigned long long* row = shard_row(w, k);
+    if (v && fld == 0) atomicAdd(&row[ST_MSGS], 0ull - (unsigned long long)v);
+    if (v && fld == 1) {
+      atomicAdd(&row[ST_RECV], (unsigned long long)v);
+      atomicAdd(&row[ST_SCHED], (unsigned long long)v);  // every infection schedules one Broadcast
+    }
+    if (v && fld == 2) atomicAdd(&row[ST_CRASH], (unsigned long long)v);
+  }
+}
+
+template <uint32_t E>
+__device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t t0, uint32_t L, uint32_t f,
+                                                     unsigned long long M, uint32_t (&st)[16][kMaxWindow][4],
+                                                     uint32_t* skw) {
+  constexpr uint32_t N = 64 * E;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  {
     uint32_t knode0, c3crash;  // keys of the bucket's nodes (one trial per bucket)
     node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + (f << kFineLog), K_CRASH, knode0, c3crash);
     const uint32_t c3delay = (c3crash & 0xFFFFFFu) | (K_DELAY << 24);
@@ -1180,7 +1228,7 @@ __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w,
         }
       }
 #pragma unroll
-    for (uint32_t r = 0; r < E; ++r) sk[wv][r * 64 + lane] = key[r];
+    for (uint32_t r = 0; r < E; ++r) skw[r * 64 + lane] = key[r];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1190,13 +1238,13 @@ __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w,
     for (uint32_t r = 0; r < E; ++r) {
       const uint32_t i = r * 64 + lane;
       const uint32_t loc = key[r] >> 5;
-      if (key[r] == ~0u || (i > 0 && (sk[wv][i - 1] >> 5) == loc)) continue;  // not a run head
+      if (key[r] == ~0u || (i > 0 && (skw[i - 1] >> 5) == loc)) continue;  // not a run head
       const uint32_t wi = ((f << kFineLog) + loc) >> 5, bit = 1u << (loc & 31), u = knode0 + loc;
       const uint32_t cw = cwg[wi];
       bool rv = (rwg[wi] & bit) != 0, cr = (cw & bit) != 0, inf = false;
       uint32_t ktick = ~0u, ord = 0, tinf = 0;
       for (uint32_t q = i; q < N; ++q) {  // along the run (~0u never matches a loc)
-        const uint32_t e = sk[wv][q];
+        const uint32_t e = skw[q];
         if ((e >> 5) != loc) break;
         const uint32_t k = (e >> 1) & (kMaxWindow - 1), t = t0 + k;
         if (k != ktick) { ktick = k; ord = 0; } else { ++ord; }
@@ -1242,24 +1290,8 @@ __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w,
       }
     }
   }
-  __syncthreads();
-  if (tid < L * 3) {
-    const uint32_t k = tid / 3, fld = tid - k * 3;
-    uint32_t v = 0;
-    for (uint32_t q = 0; q < kWaves; ++q) v += st[q][k][fld];
-    unsigned long long* row = shard_row(w, k);
-    if (v && fld == 0) atomicAdd(&row[ST_MSGS], 0ull - (unsigned long long)v);
-    if (v && fld == 1) {
-      atomicAdd(&row[ST_RECV], (unsigned long long)v);
-      atomicAdd(&row[ST_SCHED], (unsigned long long)v);  // every infection schedules one Broadcast
-    }
-    if (v && fld == 2) atomicAdd(&row[ST_CRASH], (unsigned long long)v);
-  }
 }
 
-// Schedules the Broadcast() of local node `node` called at tick t (the sender,
-// simulator.go:240-241, fires after one delay).  Batched trials: one lane per
-// trial, sender `node` of every trial, or the keyed draw of :240 if node == ~0u.
 __global__ void k_schedule_win(const WinState w, uint32_t node, uint32_t t, uint32_t trials, uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= trials) return;
@@ -1594,9 +1626,8 @@ hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s
   uint32_t G = std::min<uint32_t>(w.nfine, 2 * cus);
   G = std::max<uint32_t>(G, (w.nfine + kResolveMaxBuckets - 1) / kResolveMaxBuckets);
   const uint32_t gs = (w.nfine + kSmallBlock / 64 - 1) / (kSmallBlock / 64);
-  hipLaunchKernelGGL(k_resolve_small<1>, dim3(gs), dim3(kSmallBlock), 0, s, w, t0, L);
-  hipLaunchKernelGGL(k_resolve_small<4>, dim3(gs), dim3(kSmallBlock), 0, s, w, t0, L);
-  static_assert(kSmallMax == 64 * 4, "the two instances cover 1..kSmallMax");
+  hipLaunchKernelGGL(k_resolve_small, dim3(gs), dim3(kSmallBlock), 0, s, w, t0, L);
+  static_assert(kSmallMax == 64 * 4, "the two bodies cover 1..kSmallMax");
   hipLaunchKernelGGL(k_resolve, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
   return hipGetLastError();
 }

@@ -15,6 +15,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "_build", "libgsoracle.so")
+_OMP_PATH = os.path.join(_HERE, "_build", "libgsomp.so")
 
 
 def build() -> str:
@@ -208,6 +209,77 @@ class Engine:
 
 
 STAT_FIELDS = ("tick", "fired", "sent", "messages", "received", "crashed", "pending")
+
+_omp = None
+
+
+def omp_lib():
+    """The all-core OpenMP port (gsomp.c): bench.py's cpu_baseline."""
+    global _omp
+    if _omp is None:
+        if not os.path.exists(_OMP_PATH):
+            build()
+        L = C.CDLL(_OMP_PATH)
+        P = C.POINTER
+        L.om_engine_new.argtypes = [P(Params), C.c_void_p, C.c_void_p, C.c_uint32, C.c_int]
+        L.om_engine_new.restype = C.c_void_p
+        L.om_engine_free.argtypes = [C.c_void_p]
+        L.om_engine_begin.argtypes = [C.c_void_p, C.c_int64]
+        L.om_engine_step.argtypes = [C.c_void_p, C.c_uint32, P(TickStats)]
+        L.om_engine_read_received.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.om_engine_read_crashed.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.om_engine_set_failed.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.om_threads.argtypes = [C.c_void_p]
+        L.om_threads.restype = C.c_int
+        _omp = L
+    return _omp
+
+
+class OmpEngine:
+    """The tick engine on every core (gsomp.c); same results as Engine."""
+
+    def __init__(self, p: Params, deg: np.ndarray, ids: np.ndarray, threads: int = 0):
+        self.p = p
+        self.n = int(p.n)
+        self.W = (self.n + 63) // 64
+        deg = np.ascontiguousarray(deg, dtype=np.uint8)
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        self.h = omp_lib().om_engine_new(C.byref(p), deg.ctypes.data, ids.ctypes.data, ids.shape[1], threads)
+        if not self.h:
+            raise ValueError("om_engine_new rejected the parameters/table")
+        self.threads = int(omp_lib().om_threads(self.h))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            omp_lib().om_engine_free(self.h)
+            self.h = None
+
+    def begin(self, sender: int = -1):
+        if omp_lib().om_engine_begin(self.h, sender) != 0:
+            raise ValueError("om_engine_begin failed")
+
+    def set_failed(self, words: np.ndarray):
+        words = np.ascontiguousarray(words, dtype=np.uint64)
+        if omp_lib().om_engine_set_failed(self.h, words.ctypes.data, words.size) != 0:
+            raise ValueError("om_engine_set_failed failed")
+
+    def step(self, ticks: int = 1) -> np.ndarray:
+        out = (TickStats * ticks)()
+        if omp_lib().om_engine_step(self.h, ticks, out) != 0:
+            raise RuntimeError("om_engine_step failed")
+        return np.array([[out[i].tick, out[i].fired, out[i].sent, out[i].messages,
+                          out[i].received, out[i].crashed, out[i].pending]
+                         for i in range(ticks)], dtype=np.uint64).reshape(ticks, 7)
+
+    def received(self) -> np.ndarray:
+        w = np.zeros(self.W, dtype=np.uint64)
+        omp_lib().om_engine_read_received(self.h, w.ctypes.data, self.W)
+        return w
+
+    def crashed(self) -> np.ndarray:
+        w = np.zeros(self.W, dtype=np.uint64)
+        omp_lib().om_engine_read_crashed(self.h, w.ctypes.data, self.W)
+        return w
 
 
 def covered(recv: int, n: int) -> bool:
