@@ -312,21 +312,34 @@ def c3_trials(a, gs, rank, world, local, dist):
     t0, t1 = gd.trial_range(a.c3_trials, rank, world)
     cfg = gs.Config(n=100_000, seed=a.seed, device=local)
 
-    def batch(lo, hi):
-        with gs.Simulator(replace(cfg, trial=lo, trials=hi - lo)) as sim:
-            sim.build_overlay()
-            sim.broadcast_begin(-1)
-            sim.run(poll=10)
-            return sim.trial_results()
-
-    batch(t0, min(t1, t0 + 64))  # warmup (code objects, allocator)
+    with gs.Simulator(replace(cfg, trial=t0, trials=min(64, t1 - t0))) as sim:  # warmup: code objects
+        sim.build_overlay()
+        sim.broadcast_begin(-1)
+        sim.run(poll=10)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     start = time.perf_counter()
-    rows = [batch(b, min(b + a.c3_batch, t1)) for b in range(t0, t1, a.c3_batch)]
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - start
+    rows = []
+    # one context per batch size, renumbered batch after batch (gs_set_trial)
+    sims = {}
+    try:
+        for b in range(t0, t1, a.c3_batch):
+            T = min(b + a.c3_batch, t1) - b
+            if T not in sims:
+                sims[T] = gs.Simulator(replace(cfg, trial=b, trials=T))
+            sim = sims[T]
+            sim.reset()
+            sim.set_trial(b)
+            sim.build_overlay()
+            sim.broadcast_begin(-1)
+            sim.run(poll=10)
+            rows.append(sim.trial_results())
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - start
+    finally:
+        for s_ in sims.values():
+            s_.close()
     res = np.concatenate(rows) if rows else np.zeros((0, 9), np.int64)
     tot = torch.tensor([float(dt), float(res[:, 4].sum()), float(res[:, 5].sum()), float(len(res)),
                         float((res[:, 8] == 0).sum())], dtype=torch.float64, device="cuda")

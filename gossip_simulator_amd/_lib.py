@@ -28,7 +28,7 @@ EXPORTS = (
     "gs_read_received", "gs_read_crashed", "gs_timing_get", "gs_format_float32",
     "gs_format_float64", "gs_format_duration", "gs_threshold", "gs_philox",
     "gs_set_flags", "gs_reset", "gs_set_stream", "gs_create_multi", "gs_comm_unique_id",
-    "gs_create_rank", "gs_shard_info", "gs_trial_results",
+    "gs_create_rank", "gs_shard_info", "gs_trial_results", "gs_set_trial",
 )
 
 
@@ -124,6 +124,7 @@ def load():
         "gs_create_rank": ([P(Params), C.c_int, C.c_int, C.c_int, C.c_char_p, P(vp)], C.c_int),
         "gs_shard_info": ([ctx, C.c_uint32, P(C.c_uint32), P(C.c_uint64), P(C.c_uint64)], C.c_int),
         "gs_trial_results": ([ctx, P(TrialStats), sz, P(sz)], C.c_int),
+        "gs_set_trial": ([ctx, C.c_uint32], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -51,6 +51,7 @@ struct gs_ctx {
   DevState st{};
   uint8_t* d_deg = nullptr;
   uint32_t* d_ids = nullptr;
+  uint32_t tab_stride = 0;  // row stride d_ids was allocated for
   void* d_state = nullptr;  // one allocation for recv/crash/ring/cflag/clist/ccount/stats
   uint32_t* d_cnt = nullptr;
   uint32_t* d_err = nullptr;
@@ -103,6 +104,7 @@ struct gs_ctx {
   std::vector<int> gdev_of;             // member -> index into gdevs
   std::vector<Buf> gbuf;                // one all-gather buffer per distinct device
   std::vector<hipEvent_t> gev_c, gev_x; // per member: compaction done; per device: copies done
+  OverlayWork ovw;                      // overlay builder buffers, kept between builds
 };
 
 namespace {
@@ -292,13 +294,17 @@ int set_stride(gs_ctx* c, uint32_t stride) {
 uint64_t table_n(const gs_ctx* c) { return c->shard ? c->p.n : c->ntot; }
 
 int alloc_table(gs_ctx* c, uint32_t stride) {
-  if (c->d_deg) (void)hipFree(c->d_deg);
-  if (c->d_ids) (void)hipFree(c->d_ids);
-  c->d_deg = nullptr;
-  c->d_ids = nullptr;
   const uint64_t n = table_n(c);
-  if (hipMalloc(&c->d_deg, n) != hipSuccess || hipMalloc(&c->d_ids, n * stride * 4ull) != hipSuccess)
-    return fail(c, GS_ENOMEM, "cannot allocate the peer table on the device");
+  if (!(c->d_deg && c->d_ids && c->tab_stride == stride)) {  // same shape: reuse (batch after batch)
+    if (c->d_deg) (void)hipFree(c->d_deg);
+    if (c->d_ids) (void)hipFree(c->d_ids);
+    c->d_deg = nullptr;
+    c->d_ids = nullptr;
+    c->tab_stride = 0;
+    if (hipMalloc(&c->d_deg, n) != hipSuccess || hipMalloc(&c->d_ids, n * stride * 4ull) != hipSuccess)
+      return fail(c, GS_ENOMEM, "cannot allocate the peer table on the device");
+    c->tab_stride = stride;
+  }
   RC(set_stride(c, stride));
   refresh_state(c);
   return GS_OK;
@@ -309,6 +315,7 @@ void free_table(gs_ctx* c) {
   if (c->d_ids) (void)hipFree(c->d_ids);
   c->d_deg = nullptr;
   c->d_ids = nullptr;
+  c->tab_stride = 0;
   refresh_state(c);
 }
 
@@ -556,6 +563,7 @@ void destroy_one(gs_ctx* c) {
     (void)hipFree(c->ws.dbg);
   }
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+  overlay_free(&c->ovw);
   for (void* ptr : {(void*)c->d_deg, (void*)c->d_ids, c->d_state, (void*)c->d_cnt, (void*)c->d_failed, c->d_win,
                     c->d_flist, (void*)c->d_tstat, (void*)c->d_prow, (void*)c->d_pent, (void*)c->d_gcounts})
     if (ptr) (void)hipFree(ptr);
@@ -969,11 +977,13 @@ int overlay_into(gs_ctx* c, uint64_t max_ticks, gs_window* win, size_t cap, size
   const auto t0 = std::chrono::steady_clock::now();
   const int rc = overlay_build(c->p.n, c->trials, c->tlog, c->p.fanout, c->p.fanin, c->p.delay_low,
                                c->p.delay_high, c->st.key, c->d_deg, c->d_ids, stride, max_ticks, c->stream,
-                               OverlayWindowSink{&WinSink::push, &ws}, &res);
+                               OverlayWindowSink{&WinSink::push, &ws}, &res, &c->ovw);
   c->timing.overlay_ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (nwin) *nwin = ws.n;
   if (final_tick) *final_tick = res.final_tick;
+  // batched contexts rebuild per batch (gs_set_trial): keep the workspace
+  if (c->trials <= 1) overlay_free(&c->ovw);
   if (rc) return fail(c, rc, res.msg);
   return seal_rows(c, c->d_deg, c->d_ids, n);
 }
@@ -2070,6 +2080,27 @@ int gs_timing_get(gs_ctx* c, gs_timing* out) {
   if (!c || !out) return GS_EINVAL;
   *out = c->group ? c->mem[0]->timing : c->timing;  // a group: its first member's kernels
   if (c->group) out->overlay_ms = c->timing.overlay_ms;
+  return GS_OK;
+}
+
+int gs_set_trial(gs_ctx* c, uint32_t trial) {
+  if (!c) return GS_EINVAL;
+  if (c->begun) return fail(c, GS_EINVAL, "gs_reset before gs_set_trial");
+  if (c->group) {
+    uint32_t t = trial;
+    for (gs_ctx* m : c->mem) {
+      RC(gs_set_trial(m, c->gtrials ? t : trial) ? fail(c, GS_EINVAL, m->err) : 0);
+      t += m->trials;
+    }
+    c->p.trial = trial;
+    c->peers = false;
+    return GS_OK;
+  }
+  c->p.trial = trial;
+  c->st.key.trial = trial;
+  c->ws.key.trial = trial;
+  c->peers = false;  // the overlay of the new trials is still to be built (or loaded)
+  reset_counters(c);
   return GS_OK;
 }
 

@@ -19,6 +19,8 @@
 #include <stdint.h>
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "gs_rng.h"
 
 namespace gs {
@@ -231,11 +233,18 @@ struct OverlayWindowSink {
   void (*push)(void* self, uint64_t tick, uint64_t makeups, uint64_t breakups);
   void* self;
 };
+// Device buffers the overlay builder keeps between builds (one per context).
+struct OverlayWork {
+  struct Buf { void* p = nullptr; size_t bytes = 0; };
+  std::vector<Buf> bucket;  // per arrival slot
+  Buf scratch, outb, oslotb, heads, cub_tmp, meta;
+};
+void overlay_free(OverlayWork* ws);
 // n = nodes per trial; trials > 1 builds every trial's overlay at once in the
 // id space trial << tlog | node (tlog = 32 for one trial).
 int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, int32_t fanin,
                   int32_t delay_low, int32_t delay_high, Key key, uint8_t* d_deg, uint32_t* d_ids,
                   uint32_t stride, uint64_t max_ticks, hipStream_t stream, OverlayWindowSink sink,
-                  OverlayResult* res);
+                  OverlayResult* res, OverlayWork* ws);
 
 }  // namespace gs

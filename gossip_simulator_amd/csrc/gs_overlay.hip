@@ -224,14 +224,11 @@ __global__ __launch_bounds__(256) void k_process(const OvParams p, uint32_t t, c
     }                                                                            \
   } while (0)
 
-struct DevBuf {
-  void* p = nullptr;
-  size_t bytes = 0;
-};
+using DevBuf = OverlayWork::Buf;
 
 static hipError_t grow(DevBuf& b, size_t bytes) {
   if (b.bytes >= bytes) return hipSuccess;
-  const size_t nb = std::max(bytes, b.bytes * 5 / 4);
+  const size_t nb = std::max(bytes, b.bytes * 3 / 2);
   if (b.p) (void)hipFree(b.p);
   b.p = nullptr;
   b.bytes = 0;
@@ -248,10 +245,22 @@ static uint32_t node_bits(uint64_t n) {
 
 }  // namespace
 
+void overlay_free(OverlayWork* ws) {
+  if (!ws) return;
+  for (auto& b : ws->bucket)
+    if (b.p) (void)hipFree(b.p);
+  ws->bucket.clear();
+  for (DevBuf* b : {&ws->scratch, &ws->outb, &ws->oslotb, &ws->heads, &ws->cub_tmp, &ws->meta}) {
+    if (b->p) (void)hipFree(b->p);
+    b->p = nullptr;
+    b->bytes = 0;
+  }
+}
+
 int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, int32_t fanin,
                   int32_t delay_low, int32_t delay_high, Key key, uint8_t* d_deg, uint32_t* d_ids,
                   uint32_t stride, uint64_t max_ticks, hipStream_t stream, OverlayWindowSink sink,
-                  OverlayResult* res) {
+                  OverlayResult* res, OverlayWork* ws) {
   res->rc = GS_OK;
   res->final_tick = 0;
   res->msg[0] = 0;
@@ -275,9 +284,13 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
     return res->rc;
   }
   const uint32_t R = p.R;
-  std::vector<DevBuf> bucket(R);
+  // buffers live in the caller's workspace across builds (batched C3 builds
+  // one overlay per batch; reallocating tens of GB per tick was the cost)
+  if (ws->bucket.size() < R) ws->bucket.resize(R);
+  std::vector<DevBuf>& bucket = ws->bucket;
   std::vector<uint64_t> fill(R, 0);
-  DevBuf scratch, outb, oslotb, heads, cub_tmp, meta;
+  DevBuf &scratch = ws->scratch, &outb = ws->outb, &oslotb = ws->oslotb, &heads = ws->heads,
+         &cub_tmp = ws->cub_tmp, &meta = ws->meta;
   // meta layout: counts[R] | fill[R] | ptrs[R] | nheads | TickCounters
   uint64_t pending = 0, wm = 0, wb = 0;
   std::vector<unsigned long long> h_counts(R), hfill(R);
@@ -391,7 +404,7 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
         if (!h_counts[q]) continue;
         if (bucket[q].bytes < (fill[q] + h_counts[q]) * 8) {
           DevBuf nb;
-          OVCHK(grow(nb, (fill[q] + h_counts[q]) * 8 * 5 / 4));
+          OVCHK(grow(nb, (fill[q] + h_counts[q]) * 8 * 3 / 2));
           if (fill[q])
             OVCHK(hipMemcpyAsync(nb.p, bucket[q].p, fill[q] * 8, hipMemcpyDeviceToDevice, stream));
           OVCHK(hipStreamSynchronize(stream));
@@ -432,9 +445,6 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
 
 cleanup:
   (void)hipStreamSynchronize(stream);
-  for (auto& b : bucket) if (b.p) (void)hipFree(b.p);
-  for (DevBuf* b : {&scratch, &outb, &oslotb, &heads, &cub_tmp, &meta})
-    if (b->p) (void)hipFree(b->p);
   return res->rc;
 }
 

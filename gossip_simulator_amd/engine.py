@@ -223,6 +223,11 @@ class Simulator:
     def reset(self):
         self._check(self.L.gs_reset(self.h), "gs_reset")
 
+    def set_trial(self, trial: int):
+        """Renumber the trial(s) (then build_overlay again), keeping the buffers."""
+        self._check(self.L.gs_set_trial(self.h, trial), "gs_set_trial")
+        self.cfg.trial = trial
+
     def set_stream(self, hip_stream: int | None):
         self._check(self.L.gs_set_stream(self.h, hip_stream), "gs_set_stream")
 

@@ -216,6 +216,11 @@ int gs_read_received(gs_ctx* ctx, uint64_t* words, size_t nwords);
 int gs_read_crashed(gs_ctx* ctx, uint64_t* words, size_t nwords);
 
 int gs_timing_get(gs_ctx* ctx, gs_timing* out);
+/* Renumber the context's trial(s) to trial .. trial+trials-1 (Philox
+ * counter word 3) between runs, keeping its device buffers: the overlay must
+ * be built or loaded again before gs_broadcast_begin (config C3 runs batch
+ * after batch in one context this way). */
+int gs_set_trial(gs_ctx* ctx, uint32_t trial);
 /* Replace gs_params.flags (e.g. toggle GS_FLAG_TIMING between runs). */
 int gs_set_flags(gs_ctx* ctx, uint32_t flags);
 /* Return to the state before gs_broadcast_begin: clears received/crashed,
