@@ -169,7 +169,7 @@ int alloc_window(gs_ctx* c) {
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t units = (size_t)kMaxWindow * w.nfine + 1;
   const size_t b_fc = al((size_t)w.R * w.nfine * 4), b_units = al(units * 8),
-               b_small = al(256 * 8) * 3 + al(257 * 4) + al(257 * 8) + al(kMaxWindow * 8),
+               b_small = al(kRegions * 8) * 2 + al((kRegions + 1) * 8) + al((kRegions + 1) * 4) + al(kMaxWindow * 8),
                b_fhist = al(((size_t)w.ncoarse * 256 + 1) * 8), b_fbase = al(((size_t)w.nfine + 1) * 8),
                b_ffill = al((size_t)w.nfine * 8),
                b_sst = al((size_t)kStatShards * kMaxWindow * kStatFields * 8);
@@ -183,10 +183,10 @@ int alloc_window(gs_ctx* c) {
   w.fcount = (uint32_t*)q; q += b_fc;
   w.usize = (unsigned long long*)q; q += b_units;
   w.unit_off = (unsigned long long*)q; q += b_units;
-  w.chist = (unsigned long long*)q; q += al(256 * 8);
-  w.cfill = (unsigned long long*)q; q += al(256 * 8);
-  w.ccap = (unsigned long long*)q; q += al(257 * 8);
-  w.tprefix = (uint32_t*)q; q += al(257 * 4);
+  w.chist = (unsigned long long*)q; q += al(kRegions * 8);
+  w.cfill = (unsigned long long*)q; q += al(kRegions * 8);
+  w.ccap = (unsigned long long*)q; q += al((kRegions + 1) * 8);
+  w.tprefix = (uint32_t*)q; q += al((kRegions + 1) * 4);
   w.tfires = (unsigned long long*)q;
   q = (char*)c->d_win + b_fc + 2 * b_units + b_small;
   w.fhist = (unsigned long long*)q; q += b_fhist;
@@ -200,8 +200,8 @@ int alloc_window(gs_ctx* c) {
   c->fcount_bytes = (size_t)w.R * w.nfine * 4;
   if (hipMemsetAsync(c->d_win, 0, total, c->stream) != hipSuccess)
     return fail(c, GS_EDEVICE, "memset of window buffers failed");
-  if (hipHostMalloc((void**)&c->h_cap, 257 * 8) != hipSuccess ||
-      hipHostMalloc((void**)&c->h_misc, 1024 * 8) != hipSuccess)
+  if (hipHostMalloc((void**)&c->h_cap, (kRegions + 1) * 8) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_misc, 4096 * 8) != hipSuccess)
     return fail(c, GS_ENOMEM, "cannot allocate pinned window buffers");
   if (c->trials > 1) {
     const size_t tb = (size_t)c->trials * kMaxWindow * kTStatFields * 4;
@@ -213,20 +213,25 @@ int alloc_window(gs_ctx* c) {
   return GS_OK;
 }
 
-// Coarse region plan: bucket c gets its node share of the window's T message
-// bound plus 4096, or exactly `exact[c]`.
+// Coarse region plan: each of bin b's 8 sub-regions gets 1/8 of the bin's
+// node share of the window's T message bound plus 512, or exactly
+// `exact[region]` (region = bin * 8 + sub).
 void plan_coarse(gs_ctx* c, uint64_t T, const unsigned long long* exact) {
   const WinState& w = c->ws;
   unsigned long long a = 0;
   for (uint32_t b = 0; b < 256; ++b) {
-    c->h_cap[b] = a;
-    if (b >= w.ncoarse) continue;
-    if (exact) { a += exact[b]; continue; }
     const uint64_t lo = (uint64_t)b << kCoarseShift;
     const uint64_t hi = std::min<uint64_t>(w.n, lo + (1ull << kCoarseShift));
-    a += (unsigned long long)((long double)T * (long double)(hi - lo) / (long double)w.n) + 4096;
+    const unsigned long long sub =
+        b < w.ncoarse ? (unsigned long long)((double)T * (double)(hi - lo) / (double)w.n / kCoarseSub) + 512 : 0ull;
+    for (uint32_t x = 0; x < kCoarseSub; ++x) {
+      const uint32_t r = b * kCoarseSub + x;
+      c->h_cap[r] = a;
+      if (b >= w.ncoarse) continue;
+      a += exact ? exact[r] : sub;
+    }
   }
-  c->h_cap[256] = a;
+  c->h_cap[kRegions] = a;
 }
 
 void refresh_window(gs_ctx* c) {
@@ -1202,7 +1207,7 @@ int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing, uint64_t tchunk
     const unsigned long long T = Tn * w.stride;  // friend slots of the firing nodes
     plan_coarse(c, T, nullptr);
     const uint64_t fcap = T + T / 8 + (uint64_t)w.ncoarse * 256 * 513 + 16;
-    if (!grow(c->gmap, ((Tn + 63) / 64 + 1) * 4) || !grow(c->cmsg, (c->h_cap[256] + 16) * 4) ||
+    if (!grow(c->gmap, ((Tn + 63) / 64 + 1) * 4) || !grow(c->cmsg, (c->h_cap[kRegions] + 16) * 4) ||
         !grow(c->fmsg, fcap * 4))
       return fail(c, GS_ENOMEM, "cannot allocate " + std::to_string(T) + " window messages");
     w.gmap = (uint32_t*)c->gmap.p;
@@ -1216,7 +1221,7 @@ int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing, uint64_t tchunk
       }
     hipEvent_t* e = timing ? &c->ev[(size_t)widx * 5] : nullptr;
     if (T) {
-      CK(c, hipMemcpyAsync(w.ccap, c->h_cap, 257 * 8, hipMemcpyHostToDevice, c->stream));
+      CK(c, hipMemcpyAsync(w.ccap, c->h_cap, (kRegions + 1) * 8, hipMemcpyHostToDevice, c->stream));
       CK(c, win_groupmap(w, L, c->stream));
       if (e) CK(c, hipEventRecord(e[0], c->stream));
       CK(c, win_expand(w, t, L, Tn, 1, c->stream));
@@ -1229,13 +1234,13 @@ int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing, uint64_t tchunk
       CK(c, hipStreamSynchronize(c->stream));
       uint32_t err = (uint32_t)c->h_misc[0];
       if (err & kErrCoarse) {
-        CK(c, hipMemsetAsync(w.chist, 0, 256 * 8, c->stream));
+        CK(c, hipMemsetAsync(w.chist, 0, kRegions * 8, c->stream));
         CK(c, win_expand(w, t, L, Tn, 0, c->stream));
-        CK(c, hipMemcpyAsync(c->h_misc, w.chist, 256 * 8, hipMemcpyDeviceToHost, c->stream));
+        CK(c, hipMemcpyAsync(c->h_misc, w.chist, kRegions * 8, hipMemcpyDeviceToHost, c->stream));
         CK(c, hipStreamSynchronize(c->stream));
         plan_coarse(c, T, c->h_misc);
-        CK(c, hipMemcpyAsync(w.ccap, c->h_cap, 257 * 8, hipMemcpyHostToDevice, c->stream));
-        CK(c, hipMemsetAsync(w.cfill, 0, 256 * 8, c->stream));
+        CK(c, hipMemcpyAsync(w.ccap, c->h_cap, (kRegions + 1) * 8, hipMemcpyHostToDevice, c->stream));
+        CK(c, hipMemsetAsync(w.cfill, 0, kRegions * 8, c->stream));
         CK(c, win_expand(w, t, L, Tn, 2, c->stream));
         CK(c, win_plan(w, false, c->stream));
         err = kErrFine;  // the fine regions must be redone as well
@@ -1566,7 +1571,7 @@ int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint
         const unsigned long long Test = (unsigned long long)((long double)Tub * (long double)m->ntot / (long double)N);
         plan_coarse(m, Test, nullptr);
         const uint64_t fcap = Tub + Tub / 8 + (uint64_t)w.ncoarse * 256 * 513 + 16;
-        if (!grow(m->cmsg, (m->h_cap[256] + 16) * 4) || !grow(m->fmsg, fcap * 4))
+        if (!grow(m->cmsg, (m->h_cap[kRegions] + 16) * 4) || !grow(m->fmsg, fcap * 4))
           return fail(m, GS_ENOMEM, "cannot allocate " + std::to_string(Tub) + " window messages");
         w.cmsg = (uint32_t*)m->cmsg.p;
         w.fmsg = (uint32_t*)m->fmsg.p;
@@ -1578,31 +1583,31 @@ int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint
             m->ev.push_back(ev);
           }
         hipEvent_t* e = timing ? &m->ev[0] : nullptr;
-        CK(m, hipMemcpyAsync(w.ccap, m->h_cap, 257 * 8, hipMemcpyHostToDevice, m->stream));
+        CK(m, hipMemcpyAsync(w.ccap, m->h_cap, (kRegions + 1) * 8, hipMemcpyHostToDevice, m->stream));
         if (e) CK(m, hipEventRecord(e[0], m->stream));
         CK(m, win_expand_sh(w, t, L, 1, m->stream));
         if (e) CK(m, hipEventRecord(e[1], m->stream));
         CK(m, win_plan(w, false, m->stream));
         CK(m, win_part2(w, Tub, true, m->stream));
         if (e) CK(m, hipEventRecord(e[2], m->stream));
-        CK(m, hipMemcpyAsync(m->h_misc + 1020, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
+        CK(m, hipMemcpyAsync(m->h_misc + 4090, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
       }
       RC(sync_all(ms));
       for (gs_ctx* m : ms) {  // regions sized from estimates: redo exactly on overflow
         WinState& w = m->ws;
-        uint32_t err = (uint32_t)m->h_misc[1020];
+        uint32_t err = (uint32_t)m->h_misc[4090];
         const unsigned long long Tub = Ftot * stride;
         if (err & kErrCoarse) {
-          CK(m, hipMemsetAsync(w.chist, 0, 256 * 8, m->stream));
+          CK(m, hipMemsetAsync(w.chist, 0, kRegions * 8, m->stream));
           CK(m, win_expand_sh(w, t, L, 0, m->stream));
-          CK(m, hipMemcpyAsync(m->h_misc, w.chist, 256 * 8, hipMemcpyDeviceToHost, m->stream));
+          CK(m, hipMemcpyAsync(m->h_misc, w.chist, kRegions * 8, hipMemcpyDeviceToHost, m->stream));
           CK(m, hipStreamSynchronize(m->stream));
           plan_coarse(m, Tub, m->h_misc);
-          if (!grow(m->cmsg, (m->h_cap[256] + 16) * 4))
+          if (!grow(m->cmsg, (m->h_cap[kRegions] + 16) * 4))
             return fail(m, GS_ENOMEM, "cannot allocate the window messages");
           w.cmsg = (uint32_t*)m->cmsg.p;
-          CK(m, hipMemcpyAsync(w.ccap, m->h_cap, 257 * 8, hipMemcpyHostToDevice, m->stream));
-          CK(m, hipMemsetAsync(w.cfill, 0, 256 * 8, m->stream));
+          CK(m, hipMemcpyAsync(w.ccap, m->h_cap, (kRegions + 1) * 8, hipMemcpyHostToDevice, m->stream));
+          CK(m, hipMemsetAsync(w.cfill, 0, kRegions * 8, m->stream));
           CK(m, win_expand_sh(w, t, L, 2, m->stream));
           CK(m, win_plan(w, false, m->stream));
           err = kErrFine;
@@ -1654,11 +1659,11 @@ int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint
   }
   for (gs_ctx* m : ms) {
     CK(m, hipSetDevice(m->dev));
-    CK(m, hipMemcpyAsync(m->h_misc + 1020, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
+    CK(m, hipMemcpyAsync(m->h_misc + 4090, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
   }
   RC(sync_all(ms));
   for (gs_ctx* m : ms)
-    if (m->h_misc[1020] & 4) return fail(m, GS_EOVERFLOW, "too many arrivals at one node in one tick");
+    if (m->h_misc[4090] & 4) return fail(m, GS_EOVERFLOW, "too many arrivals at one node in one tick");
   return GS_OK;
 }
 

@@ -81,6 +81,12 @@ constexpr uint32_t kFineLog = 14;               // 16384 nodes per fine bucket
 constexpr uint32_t kFineNodes = 1u << kFineLog;
 constexpr uint32_t kCoarseShift = kFineLog + 8; // 256 fine buckets per coarse bucket
 constexpr uint32_t kMaxWindow = 16;             // tick offset in 4 bits
+// Coarse regions: each of the 256 coarse bins has kCoarseSub sub-regions, one
+// per XCD (a block writes the sub-region of blockIdx % 8): the reservation
+// atomics of a bin spread over 8 addresses, and the runs written into one
+// sub-region meet in one XCD's L2.
+constexpr uint32_t kCoarseSub = 8;
+constexpr uint32_t kRegions = 256 * kCoarseSub;
 constexpr uint32_t kWinMaxRing = 256;
 constexpr uint32_t kWinMaxStride = 32;          // friends-row length the window engine takes
 constexpr uint32_t kEmptyMsg = 0xFFFFFFFFu;
@@ -116,10 +122,10 @@ struct WinState {
   uint32_t* gmap;                // [ceil(fires/64)] unit of every 64th firing index
   uint32_t* cmsg;                // coarse regions: u_in_coarse | k << 22
   uint32_t* fmsg;                // fine regions:   u_in_fine   | k << 14
-  unsigned long long* chist;     // [256] exact coarse counts (fallback)
-  unsigned long long* ccap;      // [257] coarse region starts (host-planned)
-  unsigned long long* cfill;     // [256] coarse region fill
-  uint32_t* tprefix;             // [257] part2 tiles per coarse bucket (prefix)
+  unsigned long long* chist;     // [kRegions] exact coarse region counts (fallback)
+  unsigned long long* ccap;      // [kRegions + 1] coarse region starts, region = bin * 8 + sub
+  unsigned long long* cfill;     // [kRegions] coarse region fill
+  uint32_t* tprefix;             // [kRegions + 1] part2 tiles per coarse region (prefix)
   unsigned long long* fhist;     // [ncoarse*256 + 1] exact fine counts (fallback)
   unsigned long long* fstart;    // [nfine + 1] fine region starts
   unsigned long long* ffill;     // [nfine] fine region fill

@@ -30,6 +30,8 @@
 // Fire lists: fcount[R][nfine] + flist[R][nfine][16384] (u16 local ids).
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+
 #include "gossip.h"
 #include "gs_internal.h"
 
@@ -39,6 +41,9 @@ namespace {
 constexpr uint32_t kExpandBlock = 256;
 constexpr uint32_t kExpandNpt = 4;        // firing nodes per thread per round (rows <= 8)
 constexpr uint32_t kResolveBlock = 512;
+#ifndef GS_RESOLVE_WAVES
+#define GS_RESOLVE_WAVES 4  // min waves per SIMD: two 512-thread workgroups per CU
+#endif
 // Messages: coarse = u_in_coarse | k << 22 | roll0 << 26; fine = loc | k << 14 |
 // roll0 << 18, where roll0 is the receiver's crash roll for ordinal 0.
 constexpr uint32_t kRoll0Coarse = kCoarseShift + 4;
@@ -99,7 +104,7 @@ __global__ void k_units(const WinState w, uint32_t t0, uint32_t L) {
   }
   __syncthreads();
   if (threadIdx.x < L && s_t[threadIdx.x]) atomicAdd(&w.tfires[threadIdx.x], (unsigned long long)s_t[threadIdx.x]);
-  for (uint32_t i = tid; i < 256; i += nth) { w.chist[i] = 0; w.cfill[i] = 0; }
+  for (uint32_t i = tid; i < kRegions; i += nth) { w.chist[i] = 0; w.cfill[i] = 0; }
   for (uint32_t i = tid; i < w.nfine; i += nth) w.ffill[i] = 0;
   if (tid == 0 && !w.ctl) *w.err &= ~(kErrCoarse | kErrFine);  // device-driven: sticky until the host redoes
 }
@@ -138,12 +143,15 @@ __global__ void k_cut(const WinState w, unsigned long long budget) {
   }
   __syncthreads();
   if (!s_go) return;
-  // coarse regions: node share of T + 4096 each (plan_coarse on the host)
+  // coarse regions: each sub-region gets 1/8 of its bin's node share of T,
+  // plus 512 (plan_coarse on the host)
   const unsigned long long lo = (unsigned long long)b << kCoarseShift;
   const unsigned long long hi = min((unsigned long long)w.n, lo + (1ull << kCoarseShift));
-  s_sz[b] = b < w.ncoarse ? (unsigned long long)((double)s_T * (double)(hi - lo) / (double)w.n) + 4096 : 0ull;
+  const unsigned long long sub =
+      b < w.ncoarse ? (unsigned long long)((double)s_T * (double)(hi - lo) / (double)w.n / kCoarseSub) + 512 : 0ull;
+  s_sz[b] = sub * kCoarseSub;
   __syncthreads();
-  for (uint32_t o = 1; o < 256; o <<= 1) {  // inclusive scan
+  for (uint32_t o = 1; o < 256; o <<= 1) {  // inclusive scan over bins
     const unsigned long long x = b >= o ? s_sz[b - o] : 0ull;
     __syncthreads();
     s_sz[b] += x;
@@ -151,12 +159,13 @@ __global__ void k_cut(const WinState w, unsigned long long budget) {
   }
   const unsigned long long total = s_sz[255];
   if (total > c->cmsg_cap) {  // the buffer is too small: no region at all, the host grows and redoes
-    w.ccap[b] = 0;
-    if (b == 0) { w.ccap[256] = 0; atomicOr(w.err, kErrCoarse); }
+    for (uint32_t x = 0; x < kCoarseSub; ++x) w.ccap[b * kCoarseSub + x] = 0;
+    if (b == 0) { w.ccap[kRegions] = 0; atomicOr(w.err, kErrCoarse); }
     return;
   }
-  w.ccap[b] = b ? s_sz[b - 1] : 0ull;
-  if (b == 255) w.ccap[256] = total;
+  const unsigned long long base = b ? s_sz[b - 1] : 0ull;
+  for (uint32_t x = 0; x < kCoarseSub; ++x) w.ccap[b * kCoarseSub + x] = base + x * sub;
+  if (b == 255) w.ccap[kRegions] = total;
 }
 
 // Device-driven windows: the window's fire lists are consumed.
@@ -363,6 +372,28 @@ __device__ __forceinline__ void load_row(const WinState& w, uint32_t v, uint32_t
 // any is used.  Kept targets are counting-sorted in LDS by coarse bucket and
 // leave as coalesced runs, one global reservation per (round, bucket).
 // WRITE=false only counts (exact fallback).
+// XCD-aware round split: workgroups are dealt to the 8 XCDs round-robin
+// (XCD = blockIdx & 7), so with a grid that is a multiple of 8 each XCD takes
+// one contiguous eighth of the rounds, shared among its B/8 workgroups --
+// fire lists of one bucket share friends-row lines in that XCD's L2, and the
+// coarse sub-region (bin, blockIdx & 7) a workgroup writes receives an equal
+// share of the window whatever the round count (a sparse window on a large
+// fixed grid must not pile onto XCD 0).  Other grids: plain grid stride.
+__device__ __forceinline__ void xcd_rounds(unsigned long long rounds, unsigned long long& beg,
+                                           unsigned long long& end, unsigned long long& step) {
+  const uint32_t B = gridDim.x;
+  if ((B & 7) == 0) {
+    const unsigned long long per = (rounds + 7) >> 3, x = blockIdx.x & 7;
+    beg = x * per + (blockIdx.x >> 3);
+    end = (x + 1) * per < rounds ? (x + 1) * per : rounds;
+    step = B >> 3;
+  } else {
+    beg = blockIdx.x;
+    end = rounds;
+    step = B;
+  }
+}
+
 template <bool WRITE, uint32_t MAXS, uint32_t NPT>
 __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint32_t t0, uint32_t L,
                                                          unsigned long long Tn, int add_stats) {
@@ -379,20 +410,18 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
   constexpr uint32_t per_round = kExpandBlock * NPT;
   if (tid < kMaxWindow * 2) (&sm.acc[0][0])[tid] = 0;
   static_assert(kExpandBlock == 256, "thread b owns coarse bin b");
-  const unsigned long long cbase = w.ccap[tid], cend = w.ccap[tid + 1];  // bin tid's region
+  const uint32_t reg = tid * kCoarseSub + (blockIdx.x & (kCoarseSub - 1));  // bin tid, this XCD's sub-region
+  const unsigned long long cbase = w.ccap[reg], cend = w.ccap[reg + 1];
   sm.cend[tid] = cend;
   const unsigned long long rounds = (Tn + per_round - 1) / per_round;
-  // XCD-aware: workgroups are dealt to the 8 XCDs round-robin, so logical
-  // workgroup ids are remapped to give each XCD a contiguous run of rounds
-  // (one bucket's fire lists share friends-row lines in that XCD's L2)
-  const uint32_t B = gridDim.x;
-  const uint32_t lb = (B & 7) == 0 ? (blockIdx.x & 7) * (B >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  unsigned long long rbeg, rend, rstep;
+  xcd_rounds(rounds, rbeg, rend, rstep);
   // per-tick fired | sent << 16 of this thread's nodes (<= 1024 nodes per
   // thread per launch): registers, not same-address LDS atomics per node
   uint32_t accp[kBitTicks];
 #pragma unroll
   for (uint32_t kx = 0; kx < kBitTicks; ++kx) accp[kx] = 0;
-  for (unsigned long long rd = lb; rd < rounds; rd += B) {
+  for (unsigned long long rd = rbeg; rd < rend; rd += rstep) {
     sm.cnt[tid] = 0;
     __syncthreads();
     uint32_t mm[NPT][MAXS], mt[NPT][MAXS];  // message, bin | rank << 8 (~0u = none)
@@ -466,7 +495,7 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
     }
     __syncthreads();
     if (!WRITE) {
-      if (sm.cnt[tid]) atomicAdd(&w.chist[tid], (unsigned long long)sm.cnt[tid]);
+      if (sm.cnt[tid]) atomicAdd(&w.chist[reg], (unsigned long long)sm.cnt[tid]);
       continue;  // the next round's first barrier orders the reuse of sm.cnt
     }
     block_scan256(sm.cnt, sm.off);
@@ -474,7 +503,7 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
     // LDS scatter below (which needs only off[] from the scan)
     const uint32_t mycnt = sm.cnt[tid];
     unsigned long long at = 0;
-    if (mycnt) at = atomicAdd(&w.cfill[tid], (unsigned long long)mycnt);
+    if (mycnt) at = atomicAdd(&w.cfill[reg], (unsigned long long)mycnt);
     __syncthreads();
 #pragma unroll
     for (uint32_t q = 0; q < NPT; ++q)
@@ -534,27 +563,43 @@ __global__ void k_plan(const WinState w, bool exact) {
   __shared__ unsigned long long s_base[257];
   __shared__ unsigned long long s_cap[256];
   __shared__ uint32_t s_tp[257];
-  const uint32_t tid = threadIdx.x;  // 256 threads per block
+  const uint32_t tid = threadIdx.x;  // 256 threads per block: thread c plans coarse bucket c
   if (w.ctl) {
     uint32_t t0;
     if (!win_live(w, t0, 0)) return;
   }
-  const unsigned long long cnt = w.cfill[tid] < w.ccap[tid + 1] - w.ccap[tid]
-                                     ? w.cfill[tid] : w.ccap[tid + 1] - w.ccap[tid];
+  // messages of bucket c = the fills of its sub-regions (capped at their size);
+  // part2 tiles never cross a sub-region
+  unsigned long long cnt = 0;
+  uint32_t tiles[kCoarseSub], ntile = 0;
+#pragma unroll
+  for (uint32_t x = 0; x < kCoarseSub; ++x) {
+    const uint32_t r = tid * kCoarseSub + x;
+    const unsigned long long room = w.ccap[r + 1] - w.ccap[r];
+    const unsigned long long f = w.cfill[r] < room ? w.cfill[r] : room;
+    cnt += f;
+    tiles[x] = (uint32_t)((f + kPartTile - 1) / kPartTile);
+    ntile += tiles[x];
+  }
   const bool live = tid < w.ncoarse;
   // the last coarse bucket may hold fewer than 256 fine buckets
   const uint32_t nf = live ? min(256u, w.nfine - tid * 256) : 1u;
   s_cap[tid] = live ? (cnt + cnt / 8 + nf - 1) / nf + 512 : 0;
   s_base[tid + 1] = s_cap[tid] * 256;
-  s_tp[tid + 1] = live ? (uint32_t)((cnt + kPartTile - 1) / kPartTile) : 0;
+  s_tp[tid + 1] = live ? ntile : 0;
   if (tid == 0) { s_base[0] = 0; s_tp[0] = 0; }
   __syncthreads();
   if (tid == 0)
     for (int i = 1; i <= 256; ++i) { s_base[i] += s_base[i - 1]; s_tp[i] += s_tp[i - 1]; }
   __syncthreads();
   if (blockIdx.x == 0) {
-    w.tprefix[tid] = s_tp[tid];
-    if (tid == 0) w.tprefix[256] = s_tp[256];
+    uint32_t a = s_tp[tid];
+#pragma unroll
+    for (uint32_t x = 0; x < kCoarseSub; ++x) {
+      w.tprefix[tid * kCoarseSub + x] = a;
+      a += live ? tiles[x] : 0u;
+    }
+    if (tid == 255) w.tprefix[kRegions] = s_tp[256];
   }
   if (exact) return;  // fstart comes from the exact count + scan instead
   // device-driven windows: regions past the buffer are empty, and the window
@@ -587,26 +632,26 @@ struct TileSort {
 template <bool SCATTER>
 __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_part2(const WinState w) {
   __shared__ TileSort ts;
-  __shared__ uint32_t s_tp[257];
+  __shared__ uint32_t s_tp[kRegions + 1];
   const uint32_t tid = threadIdx.x;
   if (w.ctl) {
     uint32_t t0;
     if (!win_live(w, t0, 0)) return;
   }
-  if (tid <= 256) s_tp[tid] = w.tprefix[tid];
+  for (uint32_t i = tid; i <= kRegions; i += kPartBlock) s_tp[i] = w.tprefix[i];
   __syncthreads();
-  const uint32_t ntiles = s_tp[256];
+  const uint32_t ntiles = s_tp[kRegions];
   for (uint32_t g = blockIdx.x; g < ntiles; g += gridDim.x) {
-    uint32_t lo = 0, hi = 255;  // coarse bucket c: s_tp[c] <= g < s_tp[c+1]
+    uint32_t lo = 0, hi = kRegions - 1;  // coarse region r: s_tp[r] <= g < s_tp[r+1]
     while (lo < hi) {
       const uint32_t mid = (lo + hi + 1) >> 1;
       if (s_tp[mid] <= g) lo = mid; else hi = mid - 1;
     }
-    const uint32_t c = lo;
-    const unsigned long long cb = w.ccap[c];
-    const unsigned long long fill = w.cfill[c] < w.ccap[c + 1] - cb ? w.cfill[c] : w.ccap[c + 1] - cb;
+    const uint32_t r = lo, c = r / kCoarseSub;
+    const unsigned long long cb = w.ccap[r];
+    const unsigned long long fill = w.cfill[r] < w.ccap[r + 1] - cb ? w.cfill[r] : w.ccap[r + 1] - cb;
     const unsigned long long ce = cb + fill;
-    const unsigned long long base = cb + (unsigned long long)(g - s_tp[c]) * kPartTile;
+    const unsigned long long base = cb + (unsigned long long)(g - s_tp[r]) * kPartTile;
     if (tid < 256) ts.cnt[tid] = 0;
     __syncthreads();
     constexpr uint32_t kPer = kPartTile / kPartBlock;
@@ -903,7 +948,7 @@ __device__ __forceinline__ void flush_counts(const WinState& w, ResolveLds& sm, 
 //            (single receipts), counting chain entries only for b2 nodes; the
 //            infections of the tick are Broadcast() in the lane (:122, :141)
 // A bucket with more repeats than kDupCap takes the per-tick large path.
-__global__ __launch_bounds__(kResolveBlock, 4) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
+__global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
   __shared__ ResolveLds sm;
   const uint32_t tid = threadIdx.x, G = gridDim.x;
   L = win_live(w, t0, L);
@@ -1388,16 +1433,17 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand_sh(const WinState w, ui
   __shared__ ExpandLds<kExpandBlock * MAXS> sm;
   const uint32_t tid = threadIdx.x;
   if (tid < kMaxWindow * 2) (&sm.acc[0][0])[tid] = 0;
-  const unsigned long long cbase = w.ccap[tid], cend = w.ccap[tid + 1];
+  const uint32_t reg = tid * kCoarseSub + (blockIdx.x & (kCoarseSub - 1));  // bin tid, this XCD's sub-region
+  const unsigned long long cbase = w.ccap[reg], cend = w.ccap[reg + 1];
   sm.cend[tid] = cend;
   const unsigned long long total = (unsigned long long)w.G * w.gseg;
   const unsigned long long rounds = (total + kExpandBlock - 1) / kExpandBlock;
-  const uint32_t B = gridDim.x;
-  const uint32_t lb = (B & 7) == 0 ? (blockIdx.x & 7) * (B >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  unsigned long long rbeg, rend, rstep;
+  xcd_rounds(rounds, rbeg, rend, rstep);
   uint32_t accp[kBitTicks];
 #pragma unroll
   for (uint32_t kx = 0; kx < kBitTicks; ++kx) accp[kx] = 0;
-  for (unsigned long long rd = lb; rd < rounds; rd += B) {
+  for (unsigned long long rd = rbeg; rd < rend; rd += rstep) {
     sm.cnt[tid] = 0;
     __syncthreads();
     uint32_t mm[MAXS], mt[MAXS];
@@ -1462,13 +1508,13 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand_sh(const WinState w, ui
     }
     __syncthreads();
     if (!WRITE) {
-      if (sm.cnt[tid]) atomicAdd(&w.chist[tid], (unsigned long long)sm.cnt[tid]);
+      if (sm.cnt[tid]) atomicAdd(&w.chist[reg], (unsigned long long)sm.cnt[tid]);
       continue;
     }
     block_scan256(sm.cnt, sm.off);
     const uint32_t mycnt = sm.cnt[tid];
     unsigned long long at = 0;
-    if (mycnt) at = atomicAdd(&w.cfill[tid], (unsigned long long)mycnt);
+    if (mycnt) at = atomicAdd(&w.cfill[reg], (unsigned long long)mycnt);
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < MAXS; ++j)
@@ -1568,13 +1614,18 @@ hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, i
                       hipStream_t s) {
   // rows of <= 6 (C5's fanin 6) and <= 8 slots: 4 nodes per thread; LDS holds
   // block * 4 * row slots, so 6-slot rows fit four workgroups per CU
-  const uint32_t per_round = w.stride <= 8 ? kExpandBlock * kExpandNpt : kExpandBlock;
+  // GS_XNPT=2: two firing nodes per thread (experiment: LDS and VGPRs for 8 workgroups per CU)
+  static const uint32_t npt = [] { const char* e = getenv("GS_XNPT"); return e && atoi(e) == 2 ? 2u : kExpandNpt; }();
+  const uint32_t per_round = w.stride <= 8 ? kExpandBlock * (w.stride <= 6 ? npt : kExpandNpt) : kExpandBlock;
   const uint64_t rounds = (Tn + per_round - 1) / per_round;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>(rounds, 8192);
   const dim3 grid(blocks ? blocks : 1), blk(kExpandBlock);
   const unsigned long long tn = Tn;
   const int st = mode == 1 ? 1 : 0;
-  if (w.stride <= 6) {
+  if (w.stride <= 6 && npt == 2) {
+    if (mode) hipLaunchKernelGGL((k_expand<true, 6, 2>), grid, blk, 0, s, w, t0, L, tn, st);
+    else hipLaunchKernelGGL((k_expand<false, 6, 2>), grid, blk, 0, s, w, t0, L, tn, 0);
+  } else if (w.stride <= 6) {
     if (mode) hipLaunchKernelGGL((k_expand<true, 6, kExpandNpt>), grid, blk, 0, s, w, t0, L, tn, st);
     else hipLaunchKernelGGL((k_expand<false, 6, kExpandNpt>), grid, blk, 0, s, w, t0, L, tn, 0);
   } else if (w.stride <= 8) {
