@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libgossip_hip.so")
+# GS_LIB_PATH: an experimental build of the same ABI (A/B timing only)
+LIB_PATH = os.environ.get("GS_LIB_PATH") or os.path.join(PKG_DIR, "libgossip_hip.so")
 CLI_PATH = os.path.join(PKG_DIR, "bin", "gossip_sim")
 
 GS_OK, GS_EINVAL, GS_ELIVELOCK, GS_EREJECT, GS_ENOMEM, GS_EDEVICE, GS_EOVERFLOW = (

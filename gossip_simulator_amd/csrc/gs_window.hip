@@ -461,7 +461,15 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
 #pragma unroll
       for (uint32_t jg = 0; jg < (MAXS + 3) / 4; ++jg) {
         if (mm[q][jg * 4] == kEmptyMsg) break;
+#ifdef GS_EXP_DROP2X  // timing experiment only: a second (unused in practice) drop draw
+        u32x4 r = philox(vn, t, jg, c3drop, w.key.k0, w.key.k1);
+        {
+          const u32x4 r2 = philox(vn, t + 7777u, jg, c3drop, w.key.k0, w.key.k1);
+          if (r2.x == 0x12345678u && r2.y == 0x9ABCDEF0u) r.x ^= 1u;
+        }
+#else
         const u32x4 r = philox(vn, t, jg, c3drop, w.key.k0, w.key.k1);   // :144, :172
+#endif
 #pragma unroll
         for (uint32_t jj = 0; jj < 4; ++jj) {
           const uint32_t j = jg * 4 + jj;
@@ -474,6 +482,12 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
               uint32_t un, c3crash;
               node_key(w.tlog, w.tmask, w.key, tgt, K_CRASH, un, c3crash);
               roll0 = (int32_t)uniform(philox(un, t, 0, c3crash, w.key.k0, w.key.k1).x, 100u) < w.kc;
+#ifdef GS_EXP_ROLL2X  // timing experiment only: a second (unused in practice) crash draw
+              {
+                const u32x4 r2 = philox(un, t + 7777u, 0, c3crash, w.key.k0, w.key.k1);
+                if (r2.x == 0x12345678u && r2.y == 0x9ABCDEF0u) roll0 ^= 1u;
+              }
+#endif
             }
             mt[q][j] = bin | (atomicAdd(&sm.cnt[bin], 1u) << 8);
             mm[q][j] = (tgt & ((1u << kCoarseShift) - 1)) | (k << kCoarseShift) | (roll0 << kRoll0Coarse);
