@@ -18,6 +18,8 @@ GS_OK, GS_EINVAL, GS_ELIVELOCK, GS_EREJECT, GS_ENOMEM, GS_EDEVICE, GS_EOVERFLOW 
 GS_FLAG_TIMING = 1
 GS_FLAG_TICK_ENGINE = 2
 GS_FLAG_PP_L2_ONLY = 4
+GS_FLAG_PP_DENSE = 8
+GS_FLAG_PP_EARLY = 16
 GS_RUN_COVERED, GS_RUN_QUIESCENT, GS_RUN_MAX_TICKS, GS_RUN_RUNNING = 0, 1, 2, -1
 GS_COMM_ID_BYTES = 128
 
@@ -78,7 +80,8 @@ class Timing(C.Structure):
     _fields_ = [("deliver_ms", C.c_double), ("resolve_ms", C.c_double),
                 ("deliver_launches", C.c_uint64), ("resolve_launches", C.c_uint64),
                 ("overlay_ms", C.c_double), ("expand_ms", C.c_double),
-                ("part_ms", C.c_double), ("windows", C.c_uint64), ("exact_redos", C.c_uint64)]
+                ("part_ms", C.c_double), ("windows", C.c_uint64), ("exact_redos", C.c_uint64),
+                ("prep_ms", C.c_double)]
 
 
 _lib = None

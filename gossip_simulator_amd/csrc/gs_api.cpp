@@ -67,6 +67,12 @@ struct gs_ctx {
   unsigned long long* d_next = nullptr;  // informed set being built (state block)
   unsigned long long* d_ppsum = nullptr;  // push-pull word summaries (state block)
   uint32_t* d_flag = nullptr;
+  // sparse early rounds (PPSparse): reverse table, informed list, failed-slot
+  // mask, round control; rebuilt when the table (table_ver) or the failure
+  // mask (fail_ver) changes
+  Buf pp_rend, pp_rsrc, pp_rslot, pp_ilist, pp_fmask, pp_scan, pp_ctlb;
+  uint64_t table_ver = 0, fail_ver = 0, rev_ver = ~0ull, fm_tver = ~0ull, fm_fver = ~0ull;
+  PPSparse sp{};
   // window engine (gs_window.hip)
   bool win = false;
   WinState ws{};
@@ -352,6 +358,7 @@ int validate_table(gs_ctx* c, const uint8_t* deg, const uint32_t* ids, uint64_t 
 // The window engine reads friend rows without the length byte: slots past a
 // node's list are set to kEmptyMsg on the device copy.
 int seal_rows(gs_ctx* c, const uint8_t* deg, uint32_t* ids, uint64_t n) {
+  ++c->table_ver;  // every table change ends here
   if (!c->win) return GS_OK;
   CK(c, win_seal_rows(deg, ids, n, c->st.stride, c->stream));
   CK(c, hipStreamSynchronize(c->stream));
@@ -572,7 +579,8 @@ void destroy_one(gs_ctx* c) {
   for (void* ptr : {(void*)c->d_deg, (void*)c->d_ids, c->d_state, (void*)c->d_cnt, (void*)c->d_failed, c->d_win,
                     c->d_flist, (void*)c->d_tstat, (void*)c->d_prow, (void*)c->d_pent, (void*)c->d_gcounts})
     if (ptr) (void)hipFree(ptr);
-  for (Buf* b : {&c->gmap, &c->cmsg, &c->fmsg, &c->tmp, &c->gfire})
+  for (Buf* b : {&c->gmap, &c->cmsg, &c->fmsg, &c->tmp, &c->gfire, &c->pp_rend, &c->pp_rsrc, &c->pp_rslot,
+                 &c->pp_ilist, &c->pp_fmask, &c->pp_scan, &c->pp_ctlb})
     if (b->p) (void)hipFree(b->p);
   for (void* ptr : {(void*)c->h_cap, (void*)c->h_misc, (void*)c->h_stats, (void*)c->h_tstat, (void*)c->h_stage})
     if (ptr) (void)hipHostFree(ptr);
@@ -1053,6 +1061,7 @@ int gs_set_failed(gs_ctx* c, const uint64_t* words, size_t nwords) {
   CK(c, hipStreamSynchronize(c->stream));
   c->failed = true;
   c->st.check_crashed = 1;
+  ++c->fail_ver;
   return GS_OK;
 }
 
@@ -1100,6 +1109,62 @@ int begin_one(gs_ctx* c, uint64_t s, uint32_t* sched) {
   return GS_OK;
 }
 
+// Push-pull sparse-round buffers: the reverse table
+// once per peer table, the failed-slot mask once per (table, failure mask),
+// the informed list and round control.  GS_FLAG_PP_DENSE, or buffers that do
+// not fit, leave the dense rounds only (same results).
+int pp_prepare(gs_ctx* c) {
+  c->sp = PPSparse{};
+  if (c->p.flags & GS_FLAG_PP_DENSE) return GS_OK;
+  const DevState& s = c->st;
+  const uint64_t n = s.n, E = n * s.stride;
+  const auto t0 = std::chrono::steady_clock::now();
+  bool built = false;
+  if (c->rev_ver != c->table_ver) {
+    const size_t scan = pp_rev_scan_bytes(n);
+    if (!grow(c->pp_rend, (n + 1) * 8) || !grow(c->pp_rsrc, E * 4) || !grow(c->pp_rslot, E) ||
+        !grow(c->pp_scan, scan + 256) || !grow(c->pp_ilist, n * 4) || !grow(c->pp_ctlb, sizeof(PPCtl))) {
+      (void)hipGetLastError();
+      return GS_OK;  // dense rounds only
+    }
+    CK(c, pp_rev_build(s, (unsigned long long*)c->pp_rend.p, (uint32_t*)c->pp_rsrc.p, (uint8_t*)c->pp_rslot.p,
+                       c->pp_scan.p, c->pp_scan.bytes, c->stream));
+    c->rev_ver = c->table_ver;
+    c->fm_tver = ~0ull;
+    built = true;
+  }
+  c->sp.ctl = (PPCtl*)c->pp_ctlb.p;
+  c->sp.ilist = (uint32_t*)c->pp_ilist.p;
+  c->sp.rend = (const unsigned long long*)c->pp_rend.p;
+  c->sp.rsrc = (const uint32_t*)c->pp_rsrc.p;
+  c->sp.rslot = (const uint8_t*)c->pp_rslot.p;
+  if (c->failed && s.stride <= 8) {  // the dense rounds read fmask instead of gathering failed words
+    if (c->fm_tver != c->table_ver || c->fm_fver != c->fail_ver) {
+      if (!grow(c->pp_fmask, (n + 3) & ~3ull)) {
+        (void)hipGetLastError();
+        return GS_OK;
+      }
+      CK(c, pp_fmask_build(s, c->sp.rend, c->sp.rsrc, c->sp.rslot, (uint8_t*)c->pp_fmask.p, c->stream));
+      c->fm_tver = c->table_ver;
+      c->fm_fver = c->fail_ver;
+      built = true;
+    }
+    c->sp.fmask = (const uint8_t*)c->pp_fmask.p;
+  }
+  if (built) {
+    CK(c, hipStreamSynchronize(c->stream));
+    c->timing.prep_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return GS_OK;
+}
+
+// Early rounds while |I| <= n >> shift (GS_PP_SHIFT, default 8, for tuning).
+uint32_t pp_shift() {
+  const char* e = getenv("GS_PP_SHIFT");
+  const int v = e ? atoi(e) : 8;
+  return (uint32_t)std::min(std::max(v, 0), 63);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1121,7 +1186,10 @@ int gs_broadcast_begin(gs_ctx* c, int64_t sender) {
   const uint64_t s = sender >= 0 ? (uint64_t)sender : batched ? ~0ull : keyed_sender(c->group ? c->mem[0] : c);
   if (c->pp) {  // push-pull: the sender is informed (unless failed)
     CK(c, hipSetDevice(c->dev));
-    CK(c, pp_seed(c->st, c->d_next, (uint32_t)s, c->d_flag, c->stream));
+    RC(pp_prepare(c));
+    const uint64_t n = c->st.n;
+    const unsigned long long thr = (c->p.flags & GS_FLAG_PP_EARLY) ? n : (n >> pp_shift());
+    CK(c, pp_seed(c->st, c->d_next, (uint32_t)s, c->d_flag, c->sp, thr, c->stream));
     uint32_t ok = 0;
     CK(c, hipMemcpyAsync(&ok, c->d_flag, 4, hipMemcpyDeviceToHost, c->stream));
     CK(c, hipStreamSynchronize(c->stream));
@@ -1827,9 +1895,9 @@ int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
       const uint32_t tt = (uint32_t)(t0 + i);
       hipEvent_t* e = timing ? &c->ev[(size_t)i * 2] : nullptr;
       if (e) CK(c, hipEventRecord(e[0], c->stream));
-      CK(c, pp_round(c->st, c->d_next, c->d_ppsum, tt, c->pp_l2_only, c->stream));
+      CK(c, pp_round(c->st, c->d_next, c->d_ppsum, tt, c->pp_l2_only, c->sp, c->stream));
+      CK(c, pp_commit(c->st, c->d_next, tt, c->sp, c->stream));
       if (e) CK(c, hipEventRecord(e[1], c->stream));
-      CK(c, pp_commit(c->st, c->d_next, tt, c->stream));
     }
     for (uint32_t i = 0; i < batch && !c->win && !c->pp; ++i) {
       const uint32_t tt = (uint32_t)(t0 + i);

@@ -216,12 +216,48 @@ hipError_t win_schedule(const WinState& w, uint32_t node, uint32_t tick, uint32_
 inline uint64_t pp_summary_words(uint64_t W) { return (W + 63) / 64; }
 inline uint64_t pp_summary2_words(uint64_t W) { return (pp_summary_words(W) + 63) / 64; }
 inline uint64_t pp_summary_total_words(uint64_t W) { return 2 * pp_summary_words(W) + 2 * pp_summary2_words(W); }
+//
+// Sparse early rounds: while |I| <= thr the round walks the informed list
+// instead of streaming the table -- each informed u makes its own call, and
+// the uninformed callers that pull from u are found among u's in-edges
+// (reverse table: in-edges (v, j) with ids[v*stride + j] = u, of node u at
+// [u ? rend[u-1] : 0, rend[u])).  The round's mode is decided on the device
+// (k_pp_mode) from PPCtl, so rounds stay queued without host syncs.
+enum PPMode : uint32_t { PP_DENSE = 0, PP_EARLY = 1 };
+struct PPCtl {
+  unsigned long long ninf;      // |I|: informed nodes (all modes)
+  unsigned long long nlist;     // informed-list entries (valid while early_ok)
+  unsigned long long nnew;      // entries appended by this round (early)
+  unsigned long long thr;       // early rounds while ninf <= thr
+  unsigned long long ncallers;  // live nodes with a non-empty row: calls per round
+  uint32_t mode;                // PPMode of the current round
+  uint32_t early_ok;            // the informed list is complete (never re-entered)
+};
+struct PPSparse {
+  PPCtl* ctl;                   // null: dense rounds only
+  uint32_t* ilist;              // [n] informed nodes in order of informing
+  const unsigned long long* rend;  // [n] end of node u's in-edges
+  const uint32_t* rsrc;         // [E] caller v of each in-edge
+  const uint8_t* rslot;         // [E] its slot j
+  const uint8_t* fmask;         // [n] bit j: friend j is failed (stride <= 8 and a mask set), else null
+};
 hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long long* sum, uint32_t t,
-                    bool l2_only, hipStream_t st);
+                    bool l2_only, const PPSparse& sp, hipStream_t st);
 hipError_t pp_live_edges(const DevState& s, uint32_t* out, hipStream_t st);
-hipError_t pp_commit(const DevState& s, const unsigned long long* next, uint32_t t, hipStream_t st);
+hipError_t pp_commit(const DevState& s, const unsigned long long* next, uint32_t t, const PPSparse& sp,
+                     hipStream_t st);
+// Sender informed unless failed; flag = 1 if informed.  Also initialises ctl
+// (counts live callers: a pass over deg and the failed mask).
 hipError_t pp_seed(const DevState& s, unsigned long long* next, uint32_t node, uint32_t* flag,
-                   hipStream_t st);
+                   const PPSparse& sp, unsigned long long thr, hipStream_t st);
+// Reverse table: rend must hold n + 1 words of scratch-free u64 space; tmp /
+// tmp_bytes the hipcub scan workspace (pp_rev_scan_bytes).
+size_t pp_rev_scan_bytes(uint64_t n);
+hipError_t pp_rev_build(const DevState& s, unsigned long long* rend, uint32_t* rsrc, uint8_t* rslot, void* tmp,
+                        size_t tmp_bytes, hipStream_t st);
+// fmask from the reverse table and the failed mask (stride <= 8).
+hipError_t pp_fmask_build(const DevState& s, const unsigned long long* rend, const uint32_t* rsrc,
+                          const uint8_t* rslot, uint8_t* fmask, hipStream_t st);
 
 // Launchers (gs_broadcast.hip).
 hipError_t launch_tick(const DevState& st, uint32_t tick, int mode, hipStream_t s);

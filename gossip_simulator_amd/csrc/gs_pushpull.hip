@@ -26,6 +26,8 @@
 // decided by the summaries, cost the table stream only.
 #include <algorithm>
 
+#include <hipcub/hipcub.hpp>
+
 #include "gs_internal.h"
 
 namespace gs {
@@ -62,7 +64,8 @@ __device__ __forceinline__ void block_add(uint64_t* sh, const uint64_t (&v)[3], 
 // that is neither informed nor failed (bits past n count as such: the
 // summary only ever skips work whose outcome it proves).
 __global__ __launch_bounds__(kPPBlock) void k_pp_summary(const DevState s, unsigned long long* __restrict__ sumA,
-                                                         unsigned long long* __restrict__ sumB) {
+                                                         unsigned long long* __restrict__ sumB, const PPCtl* ctl) {
+  if (ctl && ctl->mode != PP_DENSE) return;
   const uint64_t Wr = (s.W + 63) & ~63ull;  // whole waves stay in the loop together
   for (uint64_t w = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; w < Wr;
        w += (uint64_t)gridDim.x * kPPBlock) {
@@ -82,7 +85,9 @@ constexpr uint32_t kPPU = 8;
 
 // Second level: bit j of sumA2/sumB2 = summary word j of sumA/sumB is non-zero.
 __global__ __launch_bounds__(kPPBlock) void k_pp_summary2(const unsigned long long* __restrict__ sum1, uint64_t S1,
-                                                          unsigned long long* __restrict__ sum2, uint64_t S2) {
+                                                          unsigned long long* __restrict__ sum2, uint64_t S2,
+                                                          const PPCtl* ctl) {
+  if (ctl && ctl->mode != PP_DENSE) return;
   const uint64_t Sr = (S1 + 63) & ~63ull;
   for (uint64_t j = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; j < Sr; j += (uint64_t)gridDim.x * kPPBlock) {
     const bool in = j < S1;
@@ -103,9 +108,11 @@ __global__ __launch_bounds__(kPPRoundBlock) void k_pp_round(const DevState s,
                                                             const unsigned long long* __restrict__ sumA,
                                                             const unsigned long long* __restrict__ sumB,
                                                             const unsigned long long* __restrict__ sum2,
-                                                            uint32_t S2, uint32_t t) {
+                                                            uint32_t S2, uint32_t t, const PPCtl* ctl,
+                                                            const uint8_t* __restrict__ fmask) {
   __shared__ uint64_t sh[3 * (kPPRoundBlock / 64)];
   extern __shared__ unsigned long long l2sum[];  // [0,S2) A2, [S2,2*S2) B2
+  if (ctl && ctl->mode != PP_DENSE) return;
   for (uint32_t j = threadIdx.x; j < 2 * S2; j += kPPRoundBlock) l2sum[j] = sum2[j];
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
@@ -117,7 +124,7 @@ __global__ __launch_bounds__(kPPRoundBlock) void k_pp_round(const DevState s,
   const uint64_t step = (uint64_t)gridDim.x * (kPPRoundBlock / 64) * kPPU;
   for (uint64_t w0 = wid * kPPU; w0 < W; w0 += step) {  // wave-uniform
     unsigned long long Iw[kPPU], Fw[kPPU];
-    uint32_t d[kPPU], u[kPPU];
+    uint32_t d[kPPU], u[kPPU], fm[kPPU];
     bool push[kPPU], kept[kPPU], sbit[kPPU];
 #pragma unroll
     for (uint32_t i = 0; i < kPPU; ++i) {
@@ -126,6 +133,7 @@ __global__ __launch_bounds__(kPPRoundBlock) void k_pp_round(const DevState s,
       Iw[i] = inb ? s.recv[word] : 0ull;
       Fw[i] = inb ? s.crash[word] : ~0ull;
       d[i] = v < s.n ? s.deg[v] : 0u;
+      fm[i] = fmask && v < s.n ? fmask[v] : 0u;
     }
 #pragma unroll
     for (uint32_t i = 0; i < kPPU; ++i) {
@@ -136,7 +144,9 @@ __global__ __launch_bounds__(kPPRoundBlock) void k_pp_round(const DevState s,
       kept[i] = false;
       if (d[i] > 0) {
         const u32x4 r = philox((uint32_t)v, t, 0, c3, s.key.k0, s.key.k1);
-        u[i] = s.ids[v * s.stride + uniform(r.x, d[i])];
+        const uint32_t j = uniform(r.x, d[i]);
+        u[i] = s.ids[v * s.stride + j];
+        fm[i] = (fm[i] >> j) & 1;  // the picked friend is failed (fmask)
         kept[i] = (int32_t)uniform(r.y, 100u) >= s.kd;
       }
     }
@@ -154,8 +164,10 @@ __global__ __launch_bounds__(kPPRoundBlock) void k_pp_round(const DevState s,
 #pragma unroll
     for (uint32_t i = 0; i < kPPU; ++i) {
       Iu[i] = sbit[i] ? s.recv[u[i] >> 6] : 0ull;
-      // the failed-mask gather only when a mask was set (gs_set_failed)
-      Cu[i] = (cc && kept[i] && push[i]) ? s.crash[u[i] >> 6] : 0ull;
+      // the failed-mask gather only when a mask was set (gs_set_failed) and
+      // no per-node failed-slot mask replaces it
+      Cu[i] = (cc && !fmask && kept[i] && push[i]) ? s.crash[u[i] >> 6]
+              : (fm[i] ? (1ull << (u[i] & 63)) : 0ull);
     }
 #pragma unroll
     for (uint32_t i = 0; i < kPPU; ++i) {
@@ -187,8 +199,9 @@ __global__ __launch_bounds__(kPPRoundBlock) void k_pp_round(const DevState s,
 
 __global__ __launch_bounds__(kPPBlock) void k_pp_commit(const DevState s,
                                                         const unsigned long long* __restrict__ next,
-                                                        uint32_t t) {
-  __shared__ uint64_t sh[3 * (kPPBlock / 64)];
+                                                        uint32_t t, PPCtl* ctl) {
+  __shared__ uint64_t sh[kPPBlock / 64];
+  if (ctl && ctl->mode != PP_DENSE) return;
   uint64_t newly = 0;
   for (uint64_t w = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; w < s.W;
        w += (uint64_t)gridDim.x * kPPBlock) {
@@ -196,9 +209,166 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_commit(const DevState s,
     newly += (uint64_t)__popcll(nx & ~old);
     if (nx != old) s.recv[w] = nx;
   }
-  const uint64_t v3[3] = {newly, 0, 0};
-  const uint32_t f3[3] = {ST_RECV, 0, 0};
-  block_add(sh, v3, 1, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
+  const uint64_t ws = wave_sum64(newly);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = ws;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t b = 0;
+    for (uint32_t k = 0; k < kPPBlock / 64; ++k) b += sh[k];
+    if (b) {
+      atomicAdd(&s.stats[(size_t)(t % kStatSlots) * kStatFields + ST_RECV], (unsigned long long)b);
+      if (ctl) atomicAdd(&ctl->ninf, (unsigned long long)b);
+    }
+  }
+}
+
+// ---- sparse early rounds ------------------------------------------------------
+// Round mode and the previous early round's bookkeeping (one thread).
+__global__ void k_pp_mode(PPCtl* c) {
+  if (c->mode == PP_EARLY) {  // the last round appended nnew informed nodes
+    c->nlist += c->nnew;
+    c->ninf += c->nnew;
+  }
+  c->nnew = 0;
+  const bool early = c->early_ok && c->ninf <= c->thr;
+  c->mode = early ? PP_EARLY : PP_DENSE;
+  if (!early) c->early_ok = 0;  // |I| only grows: the list is never needed again
+}
+
+// Appends v to the informed list when this lane's atomicOr on `next` set its
+// bit first: one global atomic per wave (the lanes taking part may be any
+// subset of the wave).
+__device__ __forceinline__ void pp_append(PPCtl* c, uint32_t* ilist, bool take, uint32_t v) {
+  const unsigned long long bal = __ballot(take);
+  if (!bal) return;
+  const uint32_t lane = threadIdx.x & 63, lead = (uint32_t)__builtin_ctzll(bal);
+  unsigned long long base = 0;
+  if (lane == lead) base = atomicAdd(&c->nnew, (unsigned long long)__popcll(bal));
+  base = __shfl(base, lead, 64);
+  if (take) {
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+    ilist[c->nlist + base + rank] = v;
+  }
+}
+
+// One early round: lane per informed node u of the
+// list.  u's own call is a push (u informed => live); every in-edge (v, j)
+// of u whose caller v is live, uninformed, picks slot j and is not lost is a
+// successful pull.  Same draws and counters as k_pp_round.
+__global__ __launch_bounds__(kPPBlock) void k_ppe_round(const DevState s, unsigned long long* __restrict__ next,
+                                                        PPSparse sp, uint32_t t) {
+  __shared__ uint64_t sh[3 * (kPPBlock / 64)];
+  PPCtl* c = sp.ctl;
+  if (c->mode != PP_EARLY) return;
+  const unsigned long long nl = c->nlist;
+  const uint32_t c3 = ctr3(K_PUSHPULL, s.key.trial);
+  const bool cc = s.check_crashed;
+  uint64_t sent = 0, msgs = 0;
+  const uint64_t G = (uint64_t)gridDim.x * kPPBlock;
+  const uint64_t nlr = (nl + 63) & ~63ull;  // whole waves iterate together (pp_append)
+  for (uint64_t i = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; i < nlr; i += G) {
+    const bool live = i < nl;
+    const uint32_t u = live ? sp.ilist[i] : 0u;
+    // own call: push
+    bool take = false;
+    uint32_t w = 0;
+    const uint32_t d = live ? s.deg[u] : 0u;
+    if (d > 0) {
+      const u32x4 r = philox(u, t, 0, c3, s.key.k0, s.key.k1);
+      if ((int32_t)uniform(r.y, 100u) >= s.kd) {
+        w = s.ids[(uint64_t)u * s.stride + uniform(r.x, d)];
+        const unsigned long long wb = 1ull << (w & 63);
+        ++sent;
+        if (!(cc && (s.crash[w >> 6] & wb))) {  // w live: delivered
+          ++msgs;
+          if (!(s.recv[w >> 6] & wb)) take = !(atomicOr(&next[w >> 6], wb) & wb);
+        }
+      }
+    }
+    pp_append(c, sp.ilist, take, w);
+    // pulls from u: u's in-edges
+    unsigned long long q = live ? (u ? sp.rend[u - 1] : 0ull) : 0ull;
+    const unsigned long long e = live ? sp.rend[u] : 0ull;
+    while (__ballot(q < e)) {
+      bool tk = false;
+      uint32_t v = 0;
+      if (q < e) {
+        v = sp.rsrc[q];
+        const uint32_t j = sp.rslot[q];
+        ++q;
+        const unsigned long long vb = 1ull << (v & 63);
+        // v informed: its own list entry pushes; v failed: never calls
+        if (!(s.recv[v >> 6] & vb) && !(cc && (s.crash[v >> 6] & vb))) {
+          const u32x4 r = philox(v, t, 0, c3, s.key.k0, s.key.k1);
+          if (uniform(r.x, s.deg[v]) == j && (int32_t)uniform(r.y, 100u) >= s.kd) {
+            ++sent;
+            ++msgs;
+            tk = !(atomicOr(&next[v >> 6], vb) & vb);
+          }
+        }
+      }
+      pp_append(c, sp.ilist, tk, v);
+    }
+  }
+  const uint64_t v3[3] = {blockIdx.x == 0 && threadIdx.x == 0 ? c->ncallers : 0ull, sent, msgs};
+  const uint32_t f3[3] = {ST_FIRED, ST_SENT, ST_MSGS};
+  block_add(sh, v3, 3, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
+}
+
+// The early round's newly informed nodes join recv (next holds them already).
+__global__ __launch_bounds__(kPPBlock) void k_ppe_commit(const DevState s, PPSparse sp, uint32_t t) {
+  const PPCtl* c = sp.ctl;
+  if (c->mode != PP_EARLY) return;
+  const unsigned long long nl = c->nlist, nn = c->nnew;
+  for (uint64_t i = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; i < nn; i += (uint64_t)gridDim.x * kPPBlock) {
+    const uint32_t v = sp.ilist[nl + i];
+    atomicOr(&s.recv[v >> 6], 1ull << (v & 63));
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nn)
+    atomicAdd(&s.stats[(size_t)(t % kStatSlots) * kStatFields + ST_RECV], nn);
+}
+
+// Live nodes with a non-empty row (each calls once per round).
+__global__ __launch_bounds__(kPPBlock) void k_pp_callers(const DevState s, PPCtl* c) {
+  uint64_t k = 0;
+  for (uint64_t v = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; v < s.n; v += (uint64_t)gridDim.x * kPPBlock)
+    k += s.deg[v] > 0 && !((s.crash[v >> 6] >> (v & 63)) & 1);
+  k = wave_sum64(k);
+  if ((threadIdx.x & 63) == 0 && k) atomicAdd(&c->ncallers, (unsigned long long)k);
+}
+
+// ---- reverse table ------------------------------------------------------------
+__global__ __launch_bounds__(kPPBlock) void k_rev_count(const DevState s, unsigned long long* cnt) {
+  for (uint64_t v = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; v < s.n; v += (uint64_t)gridDim.x * kPPBlock) {
+    const uint32_t d = s.deg[v];
+    for (uint32_t j = 0; j < d; ++j) atomicAdd(&cnt[s.ids[v * s.stride + j]], 1ull);
+  }
+}
+
+// After the exclusive scan rend[u] = start of u's in-edges; each fill bumps
+// it, so it ends as the end of u's in-edges (= the start of u + 1's).
+__global__ __launch_bounds__(kPPBlock) void k_rev_fill(const DevState s, unsigned long long* rend, uint32_t* rsrc,
+                                                       uint8_t* rslot) {
+  for (uint64_t v = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; v < s.n; v += (uint64_t)gridDim.x * kPPBlock) {
+    const uint32_t d = s.deg[v];
+    for (uint32_t j = 0; j < d; ++j) {
+      const unsigned long long at = atomicAdd(&rend[s.ids[v * s.stride + j]], 1ull);
+      rsrc[at] = (uint32_t)v;
+      rslot[at] = (uint8_t)j;
+    }
+  }
+}
+
+// fmask[v] bit j = ids[v][j] is failed: each failed node marks its in-edges.
+__global__ __launch_bounds__(kPPBlock) void k_pp_fmask(const DevState s, const unsigned long long* rend,
+                                                       const uint32_t* rsrc, const uint8_t* rslot, uint32_t* fm4) {
+  for (uint64_t f = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; f < s.n; f += (uint64_t)gridDim.x * kPPBlock) {
+    if (!((s.crash[f >> 6] >> (f & 63)) & 1)) continue;
+    for (unsigned long long q = f ? rend[f - 1] : 0ull; q < rend[f]; ++q) {
+      const uint32_t v = rsrc[q];
+      atomicOr(&fm4[v >> 2], (1u << rslot[q]) << (8 * (v & 3)));
+    }
+  }
 }
 
 // Exact stop test (gs_run): out += edges (v, friends[v][j]) over which a call
@@ -225,8 +395,10 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_live_edges(const DevState s, ui
 }
 
 // Sender (simulator.go:239-241 for the flood model): informed at begin unless
-// failed; flag[0] = 1 if it was informed.
-__global__ void k_pp_seed(const DevState s, unsigned long long* next, uint32_t node, uint32_t* flag) {
+// failed; flag[0] = 1 if it was informed.  ctl (zeroed, ncallers counted):
+// the informed list starts as the sender.
+__global__ void k_pp_seed(const DevState s, unsigned long long* next, uint32_t node, uint32_t* flag, PPSparse sp,
+                          unsigned long long thr) {
   const unsigned long long bit = 1ull << (node & 63);
   const bool ok = !(s.crash[node >> 6] & bit);
   if (ok) {
@@ -234,20 +406,36 @@ __global__ void k_pp_seed(const DevState s, unsigned long long* next, uint32_t n
     next[node >> 6] |= bit;
   }
   *flag = ok ? 1u : 0u;
+  if (sp.ctl) {
+    PPCtl* c = sp.ctl;
+    c->ninf = ok ? 1 : 0;
+    c->nlist = ok ? 1 : 0;
+    c->nnew = 0;
+    c->thr = thr;
+    c->mode = PP_DENSE;
+    c->early_ok = 1;
+    if (ok) sp.ilist[0] = node;
+  }
 }
 
 }  // namespace
 
 hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long long* sum, uint32_t t,
-                    bool l2_only_flag, hipStream_t st) {
+                    bool l2_only_flag, const PPSparse& sp, hipStream_t st) {
+  if (sp.ctl) {
+    hipLaunchKernelGGL(k_pp_mode, dim3(1), dim3(1), 0, st, sp.ctl);
+    // early rounds: the list grows at most ~(1 + in-degree)-fold per round;
+    // a fixed grid, idle blocks leave at once
+    hipLaunchKernelGGL(k_ppe_round, dim3(2048), dim3(kPPBlock), 0, st, s, next, sp, t);
+  }
   unsigned long long* sumA = sum;
   unsigned long long* sumB = sum + pp_summary_words(s.W);
   const uint32_t sblocks = (uint32_t)std::min<uint64_t>((s.W + kPPBlock - 1) / kPPBlock, 4096);
-  hipLaunchKernelGGL(k_pp_summary, dim3(sblocks), dim3(kPPBlock), 0, st, s, sumA, sumB);
+  hipLaunchKernelGGL(k_pp_summary, dim3(sblocks), dim3(kPPBlock), 0, st, s, sumA, sumB, sp.ctl);
   const uint64_t S1 = pp_summary_words(s.W), S2 = pp_summary2_words(s.W);
   unsigned long long* sum2 = sum + 2 * S1;
   const uint32_t s2blocks = (uint32_t)std::min<uint64_t>((S1 + kPPBlock - 1) / kPPBlock, 1024);
-  hipLaunchKernelGGL(k_pp_summary2, dim3(s2blocks), dim3(kPPBlock), 0, st, sum, S1, sum2, S2);
+  hipLaunchKernelGGL(k_pp_summary2, dim3(s2blocks), dim3(kPPBlock), 0, st, sum, S1, sum2, S2, sp.ctl);
   // 0: no LDS stage, every call checks L2 (N > ~1.02e9; GS_FLAG_PP_L2_ONLY
   // forces it so the parity tests cover that path at small N)
   const bool l2_only = S2 > kPPMaxS2 || l2_only_flag;
@@ -256,13 +444,15 @@ hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long l
   const uint32_t blocks =
       (uint32_t)std::min<uint64_t>((groups + kPPRoundBlock / 64 - 1) / (kPPRoundBlock / 64), 512);
   hipLaunchKernelGGL(k_pp_round, dim3(blocks), dim3(kPPRoundBlock), (size_t)2 * S2l * 8, st, s, next, sumA,
-                     sumB, sum2, S2l, t);
+                     sumB, sum2, S2l, t, (const PPCtl*)sp.ctl, sp.fmask);
   return hipGetLastError();
 }
 
-hipError_t pp_commit(const DevState& s, const unsigned long long* next, uint32_t t, hipStream_t st) {
+hipError_t pp_commit(const DevState& s, const unsigned long long* next, uint32_t t, const PPSparse& sp,
+                     hipStream_t st) {
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.W + kPPBlock - 1) / kPPBlock, 2048);
-  hipLaunchKernelGGL(k_pp_commit, dim3(blocks), dim3(kPPBlock), 0, st, s, next, t);
+  hipLaunchKernelGGL(k_pp_commit, dim3(blocks), dim3(kPPBlock), 0, st, s, next, t, sp.ctl);
+  if (sp.ctl) hipLaunchKernelGGL(k_ppe_commit, dim3(1024), dim3(kPPBlock), 0, st, s, sp, t);
   return hipGetLastError();
 }
 
@@ -275,8 +465,42 @@ hipError_t pp_live_edges(const DevState& s, uint32_t* out, hipStream_t st) {
 }
 
 hipError_t pp_seed(const DevState& s, unsigned long long* next, uint32_t node, uint32_t* flag,
-                   hipStream_t st) {
-  hipLaunchKernelGGL(k_pp_seed, dim3(1), dim3(1), 0, st, s, next, node, flag);
+                   const PPSparse& sp, unsigned long long thr, hipStream_t st) {
+  if (sp.ctl) {
+    hipError_t e = hipMemsetAsync(sp.ctl, 0, sizeof(PPCtl), st);
+    if (e != hipSuccess) return e;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.n + kPPBlock - 1) / kPPBlock, 4096);
+    hipLaunchKernelGGL(k_pp_callers, dim3(blocks), dim3(kPPBlock), 0, st, s, sp.ctl);
+  }
+  hipLaunchKernelGGL(k_pp_seed, dim3(1), dim3(1), 0, st, s, next, node, flag, sp, thr);
+  return hipGetLastError();
+}
+
+size_t pp_rev_scan_bytes(uint64_t n) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (unsigned long long*)nullptr,
+                                         (unsigned long long*)nullptr, (int)(n + 1));
+  return bytes;
+}
+
+hipError_t pp_rev_build(const DevState& s, unsigned long long* rend, uint32_t* rsrc, uint8_t* rslot, void* tmp,
+                        size_t tmp_bytes, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(rend, 0, (s.n + 1) * 8, st);
+  if (e != hipSuccess) return e;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.n + kPPBlock - 1) / kPPBlock, 8192);
+  hipLaunchKernelGGL(k_rev_count, dim3(blocks), dim3(kPPBlock), 0, st, s, rend);
+  e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, rend, rend, (int)(s.n + 1), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_rev_fill, dim3(blocks), dim3(kPPBlock), 0, st, s, rend, rsrc, rslot);
+  return hipGetLastError();
+}
+
+hipError_t pp_fmask_build(const DevState& s, const unsigned long long* rend, const uint32_t* rsrc,
+                          const uint8_t* rslot, uint8_t* fmask, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(fmask, 0, (s.n + 3) & ~3ull, st);
+  if (e != hipSuccess) return e;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.n + kPPBlock - 1) / kPPBlock, 8192);
+  hipLaunchKernelGGL(k_pp_fmask, dim3(blocks), dim3(kPPBlock), 0, st, s, rend, rsrc, rslot, (uint32_t*)fmask);
   return hipGetLastError();
 }
 

@@ -38,6 +38,18 @@ class Config:
     model: str = "flood"    # "flood" (the reference) or "pushpull" (extension)
     trials: int = 1         # batched independent trials trial .. trial+trials-1 (config C3)
     pp_l2_only: bool = False  # push-pull: force the no-LDS summary path (tests)
+    pp_rounds: str = "auto"   # push-pull: "auto" (sparse early rounds while |I| <= n/256),
+                              # "dense" (every round streams the table), "early" (sparse at any |I|)
+
+    def flags(self, timing: bool | None = None) -> int:
+        if self.pp_rounds not in ("auto", "dense", "early"):
+            raise ValueError(f"pp_rounds must be 'auto', 'dense' or 'early', not {self.pp_rounds!r}")
+        t = self.timing if timing is None else timing
+        return (_lib.GS_FLAG_TIMING if t else 0) | \
+            (_lib.GS_FLAG_TICK_ENGINE if self.engine == "tick" else 0) | \
+            (_lib.GS_FLAG_PP_L2_ONLY if self.pp_l2_only else 0) | \
+            (_lib.GS_FLAG_PP_DENSE if self.pp_rounds == "dense" else 0) | \
+            (_lib.GS_FLAG_PP_EARLY if self.pp_rounds == "early" else 0)
 
     def to_params(self) -> Params:
         p = Params()
@@ -48,9 +60,7 @@ class Config:
         if self.model not in ("flood", "pushpull"):
             raise ValueError(f"model must be 'flood' or 'pushpull', not {self.model!r}")
         p.model = 1 if self.model == "pushpull" else 0
-        p.flags = (_lib.GS_FLAG_TIMING if self.timing else 0) | \
-            (_lib.GS_FLAG_TICK_ENGINE if self.engine == "tick" else 0) | \
-            (_lib.GS_FLAG_PP_L2_ONLY if self.pp_l2_only else 0)
+        p.flags = self.flags()
         p.trials = max(1, int(self.trials))
         return p
 
@@ -215,9 +225,7 @@ class Simulator:
         return out
 
     def set_flags(self, timing: bool):
-        flags = (_lib.GS_FLAG_TIMING if timing else 0) | \
-            (_lib.GS_FLAG_TICK_ENGINE if self.cfg.engine == "tick" else 0) | \
-            (_lib.GS_FLAG_PP_L2_ONLY if self.cfg.pp_l2_only else 0)
+        flags = self.cfg.flags(timing)
         self._check(self.L.gs_set_flags(self.h, flags), "gs_set_flags")
 
     def reset(self):

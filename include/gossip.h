@@ -46,6 +46,10 @@ enum {
 #define GS_FLAG_TICK_ENGINE 2u /* force the per-tick atomic engine (default: window engine) */
 #define GS_FLAG_PP_L2_ONLY 4u  /* push-pull: skip the LDS-staged second-level summaries (the path
                                 * N > ~1.02e9 takes); read at gs_create, for tests */
+#define GS_FLAG_PP_DENSE 8u    /* push-pull: every round streams the whole table (no reverse
+                                * table, no sparse early rounds); same results, for tests */
+#define GS_FLAG_PP_EARLY 16u   /* push-pull: sparse early rounds at any informed count (default:
+                                * while |I| <= n/256); same results, for tests */
 
 /* Dissemination model (gs_params.model). */
 #define GS_MODEL_FLOOD 0u    /* the reference: every receipt re-broadcasts to all friends (simulator.go:107-149) */
@@ -111,6 +115,8 @@ typedef struct gs_timing {
   double part_ms;          /* window engine: k_plan + k_part2 (fine partition)        */
   uint64_t windows;        /* window engine: windows processed                */
   uint64_t exact_redos;    /* window engine: windows re-partitioned exactly   */
+  double prep_ms;          /* push-pull: wall time of the last reverse-table / failed-slot-mask
+                            * build (at gs_broadcast_begin, once per table / failure mask) */
 } gs_timing;
 
 /* gs_run status */

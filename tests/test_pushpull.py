@@ -123,6 +123,7 @@ def test_oracle_known_answers(oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("rounds", ["auto", "early", "dense"])
 @pytest.mark.parametrize("kw,stride,dlo,dhi,fail_frac", [
     (dict(PP, n=1), 2, 1, 2, 0.0),
     (dict(PP, n=2, drop_rate=0.0), 3, 0, 3, 0.0),
@@ -131,7 +132,11 @@ def test_oracle_known_answers(oracle):
     (dict(PP, n=20000, drop_rate=1.0), 6, 5, 6, 0.0),       # every call lost
     (dict(PP, n=65536 + 77, drop_rate=0.29, trial=5), 19, 18, 19, 0.03),  # wide rows
 ])
-def test_gpu_pushpull_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac, l2_only=False):
+def test_gpu_pushpull_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac, rounds, l2_only=False):
+    """Per round bit-exact to the oracle: with the default round selection,
+    with sparse early rounds forced for the whole run (informed list +
+    reverse table) and with dense rounds only (no reverse table, and the
+    failed-word gather instead of the failed-slot mask)."""
     import gossip_simulator_amd as gs
     gs.load()
     n = kw["n"]
@@ -145,7 +150,7 @@ def test_gpu_pushpull_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac, l2_only
     cfg = gs.Config(n=n, fanout=kw["fanout"], fanin=kw["fanin"], delaylow=kw["delay_low"],
                     delayhigh=kw["delay_high"], droprate=kw["drop_rate"], crashrate=kw["crash_rate"],
                     seed=kw["seed"], trial=kw["trial"], model="pushpull", pp_l2_only=l2_only,
-                    timing=l2_only)
+                    timing=l2_only, pp_rounds=rounds)
     with gs.Simulator(cfg) as sim:
         sim.load_peers(deg, ids)
         if failed is not None:
@@ -164,8 +169,8 @@ def test_gpu_pushpull_bit_exact_l2_only(oracle):
     """The round kernel without its LDS summary level (the N > ~1.02e9 path),
     forced by GS_FLAG_PP_L2_ONLY: bit-exact to the oracle like the default path."""
     test_gpu_pushpull_bit_exact(oracle, dict(PP, n=65536 + 77, drop_rate=0.29, trial=5), 19, 18, 19, 0.03,
-                                l2_only=True)
-    test_gpu_pushpull_bit_exact(oracle, dict(PP, n=20000), 6, 5, 6, 0.0, l2_only=True)
+                                "dense", l2_only=True)
+    test_gpu_pushpull_bit_exact(oracle, dict(PP, n=20000), 6, 5, 6, 0.0, "auto", l2_only=True)
 
 
 @pytest.mark.gpu
@@ -197,8 +202,9 @@ def test_gpu_pushpull_c5_shape_1e6(oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("rounds", ["auto", "early"])
 @pytest.mark.parametrize("fail_frac", [0.0, 0.02])
-def test_gpu_pushpull_run_polls_like_oracle(oracle, fail_frac):
+def test_gpu_pushpull_run_polls_like_oracle(oracle, fail_frac, rounds):
     """gs_run: 10-round polls, stop at 99 % (float32 rule) or after a poll
     window that informed nobody new (2 % failed nodes cannot reach 99 %)."""
     import gossip_simulator_amd as gs
@@ -209,7 +215,8 @@ def test_gpu_pushpull_run_polls_like_oracle(oracle, fail_frac):
     p = oracle.make_params(**kw)
     failed = words_of(np.random.default_rng(3).random(n) < fail_frac) if fail_frac else None
     rows, e = oracle.run_to_coverage(p, deg, ids, failed=failed)
-    cfg = gs.Config(n=n, droprate=kw["drop_rate"], crashrate=0.0, seed=kw["seed"], model="pushpull")
+    cfg = gs.Config(n=n, droprate=kw["drop_rate"], crashrate=0.0, seed=kw["seed"], model="pushpull",
+                    pp_rounds=rounds)
     with gs.Simulator(cfg) as sim:
         sim.load_peers(deg, ids)
         if failed is not None:
