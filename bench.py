@@ -148,14 +148,16 @@ def main():
         per = {"k_expand": tm["expand_ms"], "k_plan+k_part2": tm["part_ms"],
                "k_resolve": tm["resolve_ms"]}
         traffic, tnote = pmc_traffic()
+        alg = int(BYTES_PER_SEND * tot_r["sent"] / max(launches, 1))
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                "traffic_note": tnote,
+                "traffic_ratio": round(traffic / alg, 3) if traffic and alg else None,
+                "traffic_note": tnote + "; traffic_ratio = PMC bytes / algorithmic bytes per launch",
                 "kernel": "window pipeline k_expand -> k_plan/k_part2 -> k_resolve "
                           "(one launch of each per window)",
                 "avg_launch_us": round(kern_ms * 1e3 / max(launches, 1), 2),
                 "launches": launches,
-                "bytes_per_launch": int(BYTES_PER_SEND * tot_r["sent"] / max(launches, 1)),
+                "bytes_per_launch": alg,
                 "kernels_avg_us": {k: round(v * 1e3 / max(launches, 1), 2) for k, v in per.items()},
                 "kernels_total_ms": {k: round(v, 3) for k, v in per.items()},
                 "exact_redos": int(tm["exact_redos"]),

@@ -1123,7 +1123,7 @@ int pp_prepare(gs_ctx* c) {
   if (c->rev_ver != c->table_ver) {
     const size_t scan = pp_rev_scan_bytes(n);
     if (!grow(c->pp_rend, (n + 1) * 8) || !grow(c->pp_rsrc, E * 4) || !grow(c->pp_rslot, E) ||
-        !grow(c->pp_scan, scan + 256) || !grow(c->pp_ilist, n * 4) || !grow(c->pp_ctlb, sizeof(PPCtl))) {
+        !grow(c->pp_scan, scan + 256) || !grow(c->pp_ilist, (n + kPPSegs) * 4) || !grow(c->pp_ctlb, sizeof(PPCtl))) {
       (void)hipGetLastError();
       return GS_OK;  // dense rounds only
     }

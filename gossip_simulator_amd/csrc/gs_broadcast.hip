@@ -54,30 +54,24 @@ struct Counters {
   uint32_t v[6];
 };
 
-// Receive case of Node.Start for node u with k arrivals this tick
-// (simulator.go:107-123), ordinals in order; draws keyed by (u, t, ordinal).
-__device__ __forceinline__ void resolve_node(const DevState& st, uint32_t u, uint32_t k,
+// Receive case of Node.Start for node u with k arrivals this tick, `ones` of
+// them carrying a crash roll (simulator.go:107-123, rule A6: first_crash).
+__device__ __forceinline__ void resolve_node(const DevState& st, uint32_t u, uint32_t k, uint32_t ones,
                                              uint32_t t, Counters& c) {
   const unsigned long long bit = 1ull << (u & 63);
-  bool crashed = (st.crash[u >> 6] & bit) != 0;
-  bool received = (st.recv[u >> 6] & bit) != 0;
-  u32x4 r{0, 0, 0, 0};
-  for (uint32_t i = 0; i < k; ++i) {
-    if (crashed) break;                                   // :108
-    c.v[ST_MSGS]++;                                       // :111
-    if ((i & 3) == 0) r = philox(u, t, i >> 2, ctr3(K_CRASH, st.key.trial), st.key.k0, st.key.k1);
-    if ((int32_t)uniform(lane_of(r, i & 3), 100u) < st.kc) {  // :112-115
-      atomicOr(&st.crash[u >> 6], bit);
-      c.v[ST_CRASH]++;
-      crashed = true;
-      break;
-    }
-    if (received) continue;                               // :117
+  if (st.crash[u >> 6] & bit) return;                     // :108 (not counted)
+  const uint32_t g = ones ? first_crash(u, t, k, ones, ctr3(K_ORDER, st.key.trial), st.key.k0, st.key.k1)
+                          : k + 1;
+  c.v[ST_MSGS] += g <= k ? g : k;                         // :111
+  if (g > 1 && !(st.recv[u >> 6] & bit)) {                // :117
     atomicOr(&st.recv[u >> 6], bit);                      // :120
-    received = true;
     c.v[ST_RECV]++;                                       // :121
     schedule(st, u, t);                                   // :122
     c.v[ST_SCHED]++;
+  }
+  if (g <= k) {                                           // :112-115
+    atomicOr(&st.crash[u >> 6], bit);
+    c.v[ST_CRASH]++;
   }
 }
 
@@ -137,10 +131,13 @@ __device__ __forceinline__ void process_chunk(const DevState& st, uint32_t t, ui
         }
       } else if (MODE == MODE_COUNT) {
         c.v[ST_SENT]++;
-        atomicAdd(&st.cnt[u], 1u);
+        // the message's crash roll (:180), keyed by its sender's slot
+        const uint32_t roll = (int32_t)uniform(lane_of(philox(v, t, j >> 2, ctr3(K_CRASH, st.key.trial),
+                                                             st.key.k0, st.key.k1), j & 3), 100u) < st.kc;
+        atomicAdd(&st.cnt[u], 1u + (roll << 16));  // receipts | crash rolls << 16
       } else {
         const uint32_t k = atomicExch(&st.cnt[u], 0u);
-        if (k) resolve_node(st, u, k, t, c);
+        if (k) resolve_node(st, u, k & 0xFFFFu, k >> 16, t, c);
       }
     }
     wave_sync();

@@ -224,18 +224,27 @@ inline uint64_t pp_summary_total_words(uint64_t W) { return 2 * pp_summary_words
 // [u ? rend[u-1] : 0, rend[u])).  The round's mode is decided on the device
 // (k_pp_mode) from PPCtl, so rounds stay queued without host syncs.
 enum PPMode : uint32_t { PP_DENSE = 0, PP_EARLY = 1 };
+// The informed list is kPPSegs segments of seg_cap entries; workgroup b
+// appends to segment b % nseg (one counter per segment: a single append
+// counter saturated at ~1e8 atomics/s).  A full segment sets ovf: the round
+// still commits exactly (from the bitsets) and later rounds are dense.
+constexpr uint32_t kPPSegs = 256;
 struct PPCtl {
   unsigned long long ninf;      // |I|: informed nodes (all modes)
-  unsigned long long nlist;     // informed-list entries (valid while early_ok)
-  unsigned long long nnew;      // entries appended by this round (early)
   unsigned long long thr;       // early rounds while ninf <= thr
   unsigned long long ncallers;  // live nodes with a non-empty row: calls per round
+  unsigned long long seg_cap;   // entries per segment
+  uint32_t nseg;                // segments in use (<= kPPSegs)
   uint32_t mode;                // PPMode of the current round
   uint32_t early_ok;            // the informed list is complete (never re-entered)
+  uint32_t ovf;                 // a segment overflowed this round
+  unsigned long long segcnt[kPPSegs];      // entries in segment s (incl. this round's appends)
+  unsigned long long seglen[kPPSegs];      // entries at the start of this round
+  unsigned long long segpre[kPPSegs + 1];  // prefix of seglen: list index -> segment
 };
 struct PPSparse {
   PPCtl* ctl;                   // null: dense rounds only
-  uint32_t* ilist;              // [n] informed nodes in order of informing
+  uint32_t* ilist;              // [nseg][seg_cap] informed nodes, per segment in order of informing
   const unsigned long long* rend;  // [n] end of node u's in-edges
   const uint32_t* rsrc;         // [E] caller v of each in-edge
   const uint8_t* rslot;         // [E] its slot j

@@ -163,7 +163,9 @@ __global__ __launch_bounds__(kPPRoundBlock) void k_pp_round(const DevState s,
     unsigned long long Iu[kPPU], Cu[kPPU];
 #pragma unroll
     for (uint32_t i = 0; i < kPPU; ++i) {
-      Iu[i] = sbit[i] ? s.recv[u[i] >> 6] : 0ull;
+      // pulls gather the peer's word; a push needs no gather (its atomicOr
+      // below is idempotent and returns nothing, so the wave does not wait)
+      Iu[i] = (sbit[i] && !push[i]) ? s.recv[u[i] >> 6] : 0ull;
       // the failed-mask gather only when a mask was set (gs_set_failed) and
       // no per-node failed-slot mask replaces it
       Cu[i] = (cc && !fmask && kept[i] && push[i]) ? s.crash[u[i] >> 6]
@@ -180,7 +182,7 @@ __global__ __launch_bounds__(kPPRoundBlock) void k_pp_round(const DevState s,
           if (!(Cu[i] & ubit)) {  // u live: delivered
             ++msgs;
             // sbit clear: every live node of u's word is informed already
-            if (sbit[i] && !(Iu[i] & ubit)) atomicOr(&next[u[i] >> 6], ubit);
+            if (sbit[i]) atomicOr(&next[u[i] >> 6], ubit);
           }
         } else if (Iu[i] & ubit) {  // pull from an informed u (u informed => u live)
           ++sent;
@@ -223,31 +225,50 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_commit(const DevState s,
 }
 
 // ---- sparse early rounds ------------------------------------------------------
-// Round mode and the previous early round's bookkeeping (one thread).
-__global__ void k_pp_mode(PPCtl* c) {
-  if (c->mode == PP_EARLY) {  // the last round appended nnew informed nodes
-    c->nlist += c->nnew;
-    c->ninf += c->nnew;
+// Round mode and the list bookkeeping (one block of kPPSegs threads): the
+// previous early round's appends join the list unless a segment overflowed.
+__global__ __launch_bounds__(kPPSegs) void k_pp_mode(PPCtl* c) {
+  __shared__ unsigned long long sc[kPPSegs];
+  const uint32_t tid = threadIdx.x;
+  const bool was_early = c->mode == PP_EARLY;
+  const bool ok = c->early_ok && !c->ovf;
+  unsigned long long len = 0;
+  if (tid < c->nseg) {
+    len = c->segcnt[tid];
+    c->seglen[tid] = len;
   }
-  c->nnew = 0;
-  const bool early = c->early_ok && c->ninf <= c->thr;
-  c->mode = early ? PP_EARLY : PP_DENSE;
-  if (!early) c->early_ok = 0;  // |I| only grows: the list is never needed again
+  sc[tid] = len;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long a = 0;
+    for (uint32_t k = 0; k < c->nseg; ++k) {
+      c->segpre[k] = a;
+      a += sc[k];
+    }
+    c->segpre[c->nseg] = a;
+    const bool early = ok && c->ninf <= c->thr;
+    c->mode = early ? PP_EARLY : PP_DENSE;
+    if (!early) c->early_ok = 0;  // |I| only grows: the list is never needed again
+    (void)was_early;
+  }
 }
 
 // Appends v to the informed list when this lane's atomicOr on `next` set its
-// bit first: one global atomic per wave (the lanes taking part may be any
-// subset of the wave).
-__device__ __forceinline__ void pp_append(PPCtl* c, uint32_t* ilist, bool take, uint32_t v) {
+// bit first: one atomic per wave on segment blockIdx % nseg's counter (the
+// lanes taking part may be any subset of the wave).
+__device__ __forceinline__ void pp_append(PPCtl* c, uint32_t* ilist, uint32_t seg, unsigned long long cap,
+                                          bool take, uint32_t v) {
   const unsigned long long bal = __ballot(take);
   if (!bal) return;
   const uint32_t lane = threadIdx.x & 63, lead = (uint32_t)__builtin_ctzll(bal);
   unsigned long long base = 0;
-  if (lane == lead) base = atomicAdd(&c->nnew, (unsigned long long)__popcll(bal));
+  if (lane == lead) base = atomicAdd(&c->segcnt[seg], (unsigned long long)__popcll(bal));
   base = __shfl(base, lead, 64);
   if (take) {
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-    ilist[c->nlist + base + rank] = v;
+    const unsigned long long at =
+        base + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+    if (at < cap) ilist[(size_t)seg * cap + at] = v;
+    else c->ovf = 1u;
   }
 }
 
@@ -258,9 +279,15 @@ __device__ __forceinline__ void pp_append(PPCtl* c, uint32_t* ilist, bool take, 
 __global__ __launch_bounds__(kPPBlock) void k_ppe_round(const DevState s, unsigned long long* __restrict__ next,
                                                         PPSparse sp, uint32_t t) {
   __shared__ uint64_t sh[3 * (kPPBlock / 64)];
+  __shared__ unsigned long long pre[kPPSegs + 1];
   PPCtl* c = sp.ctl;
   if (c->mode != PP_EARLY) return;
-  const unsigned long long nl = c->nlist;
+  const uint32_t nseg = c->nseg;
+  const unsigned long long cap = c->seg_cap;
+  for (uint32_t k = threadIdx.x; k <= nseg; k += kPPBlock) pre[k] = c->segpre[k];
+  __syncthreads();
+  const unsigned long long nl = pre[nseg];
+  const uint32_t myseg = blockIdx.x % nseg;
   const uint32_t c3 = ctr3(K_PUSHPULL, s.key.trial);
   const bool cc = s.check_crashed;
   uint64_t sent = 0, msgs = 0;
@@ -268,7 +295,15 @@ __global__ __launch_bounds__(kPPBlock) void k_ppe_round(const DevState s, unsign
   const uint64_t nlr = (nl + 63) & ~63ull;  // whole waves iterate together (pp_append)
   for (uint64_t i = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; i < nlr; i += G) {
     const bool live = i < nl;
-    const uint32_t u = live ? sp.ilist[i] : 0u;
+    uint32_t u = 0;
+    if (live) {  // list index -> (segment, entry)
+      uint32_t lo = 0, hi = nseg - 1;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= i) lo = mid; else hi = mid - 1;
+      }
+      u = sp.ilist[(size_t)lo * cap + (i - pre[lo])];
+    }
     // own call: push
     bool take = false;
     uint32_t w = 0;
@@ -285,7 +320,7 @@ __global__ __launch_bounds__(kPPBlock) void k_ppe_round(const DevState s, unsign
         }
       }
     }
-    pp_append(c, sp.ilist, take, w);
+    pp_append(c, sp.ilist, myseg, cap, take, w);
     // pulls from u: u's in-edges
     unsigned long long q = live ? (u ? sp.rend[u - 1] : 0ull) : 0ull;
     const unsigned long long e = live ? sp.rend[u] : 0ull;
@@ -307,7 +342,7 @@ __global__ __launch_bounds__(kPPBlock) void k_ppe_round(const DevState s, unsign
           }
         }
       }
-      pp_append(c, sp.ilist, tk, v);
+      pp_append(c, sp.ilist, myseg, cap, tk, v);
     }
   }
   const uint64_t v3[3] = {blockIdx.x == 0 && threadIdx.x == 0 ? c->ncallers : 0ull, sent, msgs};
@@ -315,17 +350,43 @@ __global__ __launch_bounds__(kPPBlock) void k_ppe_round(const DevState s, unsign
   block_add(sh, v3, 3, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
 }
 
-// The early round's newly informed nodes join recv (next holds them already).
-__global__ __launch_bounds__(kPPBlock) void k_ppe_commit(const DevState s, PPSparse sp, uint32_t t) {
-  const PPCtl* c = sp.ctl;
+// The early round's newly informed nodes join recv (next holds them already):
+// from the list, or -- if a segment overflowed -- from the bitsets.
+__global__ __launch_bounds__(kPPBlock) void k_ppe_commit(const DevState s, const unsigned long long* __restrict__ next,
+                                                         PPSparse sp, uint32_t t) {
+  __shared__ uint64_t sh[kPPBlock / 64];
+  PPCtl* c = sp.ctl;
   if (c->mode != PP_EARLY) return;
-  const unsigned long long nl = c->nlist, nn = c->nnew;
-  for (uint64_t i = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; i < nn; i += (uint64_t)gridDim.x * kPPBlock) {
-    const uint32_t v = sp.ilist[nl + i];
-    atomicOr(&s.recv[v >> 6], 1ull << (v & 63));
+  const uint64_t G = (uint64_t)gridDim.x * kPPBlock, gid = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x;
+  uint64_t newly = 0;
+  if (c->ovf) {
+    for (uint64_t w = gid; w < s.W; w += G) {
+      const unsigned long long nx = next[w], old = s.recv[w];
+      newly += (uint64_t)__popcll(nx & ~old);
+      if (nx != old) s.recv[w] = nx;
+    }
+  } else {
+    const unsigned long long cap = c->seg_cap;
+    for (uint32_t sg = 0; sg < c->nseg; ++sg) {
+      const unsigned long long b = c->seglen[sg], e = c->segcnt[sg];
+      for (uint64_t k = b + gid; k < e; k += G) {
+        const uint32_t v = sp.ilist[(size_t)sg * cap + k];
+        atomicOr(&s.recv[v >> 6], 1ull << (v & 63));
+        ++newly;
+      }
+    }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && nn)
-    atomicAdd(&s.stats[(size_t)(t % kStatSlots) * kStatFields + ST_RECV], nn);
+  const uint64_t ws = wave_sum64(newly);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = ws;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t b = 0;
+    for (uint32_t k = 0; k < kPPBlock / 64; ++k) b += sh[k];
+    if (b) {
+      atomicAdd(&s.stats[(size_t)(t % kStatSlots) * kStatFields + ST_RECV], (unsigned long long)b);
+      atomicAdd(&c->ninf, (unsigned long long)b);
+    }
+  }
 }
 
 // Live nodes with a non-empty row (each calls once per round).
@@ -406,14 +467,15 @@ __global__ void k_pp_seed(const DevState s, unsigned long long* next, uint32_t n
     next[node >> 6] |= bit;
   }
   *flag = ok ? 1u : 0u;
-  if (sp.ctl) {
+  if (sp.ctl) {  // ctl was zeroed: the list is segment 0 = {sender}
     PPCtl* c = sp.ctl;
     c->ninf = ok ? 1 : 0;
-    c->nlist = ok ? 1 : 0;
-    c->nnew = 0;
     c->thr = thr;
+    c->nseg = (uint32_t)(s.n >> 12 < kPPSegs ? (s.n >> 12 ? s.n >> 12 : 1) : kPPSegs);
+    c->seg_cap = (s.n + c->nseg - 1) / c->nseg;
     c->mode = PP_DENSE;
     c->early_ok = 1;
+    c->segcnt[0] = ok ? 1 : 0;
     if (ok) sp.ilist[0] = node;
   }
 }
@@ -423,7 +485,7 @@ __global__ void k_pp_seed(const DevState s, unsigned long long* next, uint32_t n
 hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long long* sum, uint32_t t,
                     bool l2_only_flag, const PPSparse& sp, hipStream_t st) {
   if (sp.ctl) {
-    hipLaunchKernelGGL(k_pp_mode, dim3(1), dim3(1), 0, st, sp.ctl);
+    hipLaunchKernelGGL(k_pp_mode, dim3(1), dim3(kPPSegs), 0, st, sp.ctl);
     // early rounds: the list grows at most ~(1 + in-degree)-fold per round;
     // a fixed grid, idle blocks leave at once
     hipLaunchKernelGGL(k_ppe_round, dim3(2048), dim3(kPPBlock), 0, st, s, next, sp, t);
@@ -452,7 +514,7 @@ hipError_t pp_commit(const DevState& s, const unsigned long long* next, uint32_t
                      hipStream_t st) {
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.W + kPPBlock - 1) / kPPBlock, 2048);
   hipLaunchKernelGGL(k_pp_commit, dim3(blocks), dim3(kPPBlock), 0, st, s, next, t, sp.ctl);
-  if (sp.ctl) hipLaunchKernelGGL(k_ppe_commit, dim3(1024), dim3(kPPBlock), 0, st, s, sp, t);
+  if (sp.ctl) hipLaunchKernelGGL(k_ppe_commit, dim3(1024), dim3(kPPBlock), 0, st, s, next, sp, t);
   return hipGetLastError();
 }
 

@@ -6,12 +6,15 @@
 //   kind SENDER  simulator.go:240   ctr {0, 0, 0, .}            out[0] -> U_n
 //   kind DELAY   simulator.go:167   ctr {v, t, 0, .}            out[0] -> U_(high-low)
 //   kind DROP    simulator.go:172   ctr {v, t, j/4, .}          out[j%4] -> U_100
-//   kind CRASH   simulator.go:180   ctr {u, t, i/4, .}          out[i%4] -> U_100
+//   kind CRASH   simulator.go:180   ctr {v, t, j/4, .}          out[j%4] -> U_100 (the crash roll
+//                                   a message from sender v, fire tick t, slot j carries)
 //   kind PICK    simulator.go:97    ctr {v, 0, j, .}            out[0] -> U_n
 //   kind OVDELAY simulator.go:153,160 ctr {u, t, k, .}          out[0] -> U_(high-low)
 //   kind VICTIM  simulator.go:71    ctr {u, t, k, .}            out[0] -> U_deg
 //   kind REPLACE simulator.go:86-88 ctr {u, t, k*64+a/4, .}     out[a%4] -> U_n
 //   kind PUSHPULL (extension)        ctr {v, t, 0, .}            out[0] -> U_deg, out[1] -> U_100
+//   kind ORDER   simulator.go:107-115 ctr {u, t, (g-1)/4, .}    out[(g-1)%4] -> U_(k-g+1): receipt
+//                                   order, first_crash() below
 // with counter word 3 = kind << 24 | trial.  U_m(r) = floor(r*m / 2^32).
 #pragma once
 #include <stdint.h>
@@ -22,7 +25,8 @@ namespace gs {
 enum Kind : uint32_t {
   K_SENDER = 1, K_DELAY = 2, K_DROP = 3, K_CRASH = 4,
   K_PICK = 5, K_OVDELAY = 6, K_VICTIM = 7, K_REPLACE = 8,
-  K_PUSHPULL = 9  // push-pull extension: peer pick + loss per (node, round)
+  K_PUSHPULL = 9,  // push-pull extension: peer pick + loss per (node, round)
+  K_ORDER = 10     // receipt order of a (node, tick): first-crash position
 };
 
 struct u32x4 { uint32_t x, y, z, w; };
@@ -91,6 +95,23 @@ __host__ __device__ __forceinline__ uint32_t draw0(const Key& k, uint32_t kind, 
 __host__ __device__ __forceinline__ uint32_t fire_offset(int32_t low, uint32_t span, uint32_t r) {
   const int64_t d = (int64_t)low + (int64_t)uniform(r, span);
   return d < 1 ? 1u : (uint32_t)d;
+}
+
+// Rule A6 (simulator.go:107-123): the k receipts of node u at tick t are
+// taken in a uniformly random order; each carries its own crash roll (kind
+// CRASH, keyed by its sender), and `ones` of them (1 <= ones <= k) crash the
+// node.  Returns the 1-based position of the first crashing receipt: draws
+// U_(k-g+1)(r_g) < ones, g = 1, 2, ..., with r_g = Philox{u, t, (g-1)/4,
+// c3order} lane (g-1)%4 (oracle/gsoracle.c or_first_crash).  k == 1 or
+// ones == k needs no draw.
+__host__ __device__ __forceinline__ uint32_t first_crash(uint32_t u, uint32_t t, uint32_t k, uint32_t ones,
+                                                         uint32_t c3order, uint32_t k0, uint32_t k1) {
+  if (k <= 1 || ones >= k) return 1;
+  u32x4 r{0, 0, 0, 0};
+  for (uint32_t g = 1;; ++g) {  // ends by g = k - ones + 1, where U_ones < ones
+    if (((g - 1) & 3) == 0) r = philox(u, t, (g - 1) >> 2, c3order, k0, k1);
+    if (uniform(lane_of(r, (g - 1) & 3), k - g + 1) < ones) return g;
+  }
 }
 
 }  // namespace gs

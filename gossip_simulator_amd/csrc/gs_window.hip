@@ -457,38 +457,21 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
       const uint32_t v = vv[q], k = kk[q], t = t0 + k;
       uint32_t vn, c3drop;
       node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + v, K_DROP, vn, c3drop);
+      const uint32_t c3crash = (c3drop & 0xFFFFFFu) | (K_CRASH << 24);
       uint32_t sent = 0;
 #pragma unroll
       for (uint32_t jg = 0; jg < (MAXS + 3) / 4; ++jg) {
         if (mm[q][jg * 4] == kEmptyMsg) break;
-#ifdef GS_EXP_DROP2X  // timing experiment only: a second (unused in practice) drop draw
-        u32x4 r = philox(vn, t, jg, c3drop, w.key.k0, w.key.k1);
-        {
-          const u32x4 r2 = philox(vn, t + 7777u, jg, c3drop, w.key.k0, w.key.k1);
-          if (r2.x == 0x12345678u && r2.y == 0x9ABCDEF0u) r.x ^= 1u;
-        }
-#else
         const u32x4 r = philox(vn, t, jg, c3drop, w.key.k0, w.key.k1);   // :144, :172
-#endif
+        // the messages' crash rolls (:180), keyed by this sender's slots like the drop
+        const u32x4 rc = w.kc > 0 ? philox(vn, t, jg, c3crash, w.key.k0, w.key.k1) : u32x4{~0u, ~0u, ~0u, ~0u};
 #pragma unroll
         for (uint32_t jj = 0; jj < 4; ++jj) {
           const uint32_t j = jg * 4 + jj;
           if (j >= MAXS) break;
           if (mm[q][j] != kEmptyMsg && (int32_t)uniform(lane_of(r, jj), 100u) >= w.kd) {  // kept: :145
             const uint32_t tgt = mm[q][j], bin = tgt >> kCoarseShift;
-            // the receiver's crash roll for ordinal 0 (:112, key (u, t, 0)) rides along
-            uint32_t roll0 = 0;
-            if (w.kc > 0) {
-              uint32_t un, c3crash;
-              node_key(w.tlog, w.tmask, w.key, tgt, K_CRASH, un, c3crash);
-              roll0 = (int32_t)uniform(philox(un, t, 0, c3crash, w.key.k0, w.key.k1).x, 100u) < w.kc;
-#ifdef GS_EXP_ROLL2X  // timing experiment only: a second (unused in practice) crash draw
-              {
-                const u32x4 r2 = philox(un, t + 7777u, 0, c3crash, w.key.k0, w.key.k1);
-                if (r2.x == 0x12345678u && r2.y == 0x9ABCDEF0u) roll0 ^= 1u;
-              }
-#endif
-            }
+            const uint32_t roll0 = (int32_t)uniform(lane_of(rc, jj), 100u) < w.kc;
             mt[q][j] = bin | (atomicAdd(&sm.cnt[bin], 1u) << 8);
             mm[q][j] = (tgt & ((1u << kCoarseShift) - 1)) | (k << kCoarseShift) | (roll0 << kRoll0Coarse);
             ++sent;
@@ -723,27 +706,27 @@ constexpr uint32_t kResolveMaxBuckets = 256;  // buckets one persistent workgrou
 constexpr uint32_t kSmallMax = 256;           // buckets with <= this many receipts: k_resolve_small
 constexpr uint32_t kSmallBlock = 1024;        // k_resolve_small: 16 waves, one bucket each
 
-// Bit-parallel resolve (k_resolve): per tick k of the window, b1 = nodes with
-// >= 1 receipt, b2 = nodes with >= 2, rl = nodes whose ordinal-0 crash roll
-// fired; receipts beyond the second of a (node, tick) are listed per 32-node
-// word (dlist, chained from dhead).  The large path (resolve_tick) reuses the
-// same LDS for per-node counters and bit words.
+// Bit-parallel resolve (k_resolve): per tick k of the window, over the
+// receipts WITHOUT a crash roll b1 = nodes with >= 1, b2 = nodes with >= 2;
+// rl = nodes with a receipt that carries a crash roll.  The third and later
+// roll-free receipts of a (node, tick) and every crash-roll receipt (rare:
+// 1 % at crashrate 0.01) are listed per 32-node word (dlist, chained from
+// dhead).  The large path (resolve_tick) reuses the same LDS for per-node
+// counters and bit words.
 constexpr uint32_t kBitWords = kFineNodes / 32;
-constexpr uint32_t kDupCap = 3840;     // third+ receipts per bucket (more: large path); the
-                                       // slots after them hold the batched crash rolls
+constexpr uint32_t kDupCap = 3840;     // listed receipts per bucket (more: large path)
 struct ResolveLds {
   union {
     struct {                            // b1 .. dlist, then the infection list
       uint32_t b1[kBitTicks][kBitWords];
       uint32_t b2[kBitTicks][kBitWords];
       uint32_t rl[kBitTicks][kBitWords];
-      uint32_t dlist[kDupCap];          // [0, ndup): loc | k << 14 | next << 18 (next = index + 1,
-                                        // 0 = end); then roll entries word << 9 | k << 5 | bit,
-                                        // with the ordinal 1..3 crash rolls in bits 18..20
+      uint32_t dlist[kDupCap];          // [0, ndup): loc | k << 14 | roll << 18 | next << 19
+                                        // (next = index + 1, 0 = end)
       uint32_t dhead[kBitWords];
     };
     struct {                            // large path
-      uint32_t cnt[kFineNodes / 2];     // u16 per node: arrivals at the current tick
+      uint32_t cnt[kFineNodes];         // per node at the current tick: arrivals | crash rolls << 16
       uint32_t recv[kBitWords];
       uint32_t crash[kBitWords];
       uint32_t nrecv[kBitWords];
@@ -754,7 +737,6 @@ struct ResolveLds {
   uint32_t st[kMaxWindow][4];       // dead (not counted), recv, crash per tick: whole launch
   uint32_t blist[kResolveMaxBuckets];  // this workgroup's non-empty buckets
   uint32_t ndup;
-  uint32_t nroll;
   uint32_t ninf;
   uint32_t err;
   uint32_t nb;
@@ -780,43 +762,34 @@ __device__ __forceinline__ uint32_t msg_loc(uint32_t m) { return m & (kFineNodes
 __device__ __forceinline__ uint32_t msg_tick(uint32_t m) { return (m >> kFineLog) & (kMaxWindow - 1); }
 
 // The receive case of Node.Start (simulator.go:107-123) for node `loc` of the
-// bucket with kk arrivals at tick t: ordinals 0..kk-1, keyed crash rolls.
-// (Large-bucket path.)
+// bucket with kk arrivals at tick t, `ones` of them carrying a crash roll
+// (rule A6, first_crash).  (Large-bucket path.)
 __device__ __forceinline__ void resolve_node(const WinState& w, ResolveLds& sm, uint32_t f,
-                                             uint32_t loc, uint32_t kk, uint32_t t,
+                                             uint32_t loc, uint32_t kk, uint32_t ones, uint32_t t,
                                              uint32_t& cm, uint32_t& cr, uint32_t& cc, uint32_t& cs) {
   const uint32_t bit = 1u << (loc & 31), wi = loc >> 5;
+  if (sm.crash[wi] & bit) return;                                  // :108 (not counted)
   const uint64_t g = (uint64_t)w.base + (f << kFineLog) + loc;
-  uint32_t u, c3crash;
-  node_key(w.tlog, w.tmask, w.key, g, K_CRASH, u, c3crash);
-  bool crashed = (sm.crash[wi] & bit) != 0;
-  bool received = (sm.recv[wi] & bit) != 0;
-  u32x4 r{0, 0, 0, 0};
-  for (uint32_t i = 0; i < kk; ++i) {
-    if (crashed) break;                                          // :108
-    ++cm;                                                        // :111
-    if (w.kc > 0) {
-      if ((i & 3) == 0) r = philox(u, t, i >> 2, c3crash, w.key.k0, w.key.k1);
-      if ((int32_t)uniform(lane_of(r, i & 3), 100u) < w.kc) {   // :112-115
-        atomicOr(&sm.crash[wi], bit);
-        ++cc;
-        crashed = true;
-        break;
-      }
-    }
-    if (received) continue;                                      // :117
-    atomicOr(&sm.recv[wi], bit);                                 // :120
-    received = true;
-    ++cr;                                                        // :121
+  uint32_t u, c3order;
+  node_key(w.tlog, w.tmask, w.key, g, K_ORDER, u, c3order);
+  const uint32_t pos = ones ? first_crash(u, t, kk, ones, c3order, w.key.k0, w.key.k1) : kk + 1;
+  cm += pos <= kk ? pos : kk;                                      // :111
+  if (pos > 1 && !(sm.recv[wi] & bit)) {                           // :117
+    atomicOr(&sm.recv[wi], bit);                                   // :120
+    ++cr;                                                          // :121
     // Broadcast() (:122, :141-142): fire at t + off
     uint32_t c3delay;
     node_key(w.tlog, w.tmask, w.key, g, K_DELAY, u, c3delay);
     const uint32_t off = fire_offset(w.delay_low, w.delay_span,
                                      philox(u, t, 0, c3delay, w.key.k0, w.key.k1).x);
     const uint32_t s = (t + off) % w.R;
-    const uint32_t pos = atomicAdd(&sm.fc[s], 1u);
-    w.flist[((size_t)s * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
+    const uint32_t at = atomicAdd(&sm.fc[s], 1u);
+    w.flist[((size_t)s * w.nfine + f) * kFineNodes + at] = (uint16_t)loc;
     ++cs;
+  }
+  if (pos <= kk) {                                                 // :112-115
+    atomicOr(&sm.crash[wi], bit);
+    ++cc;
   }
 }
 
@@ -831,19 +804,18 @@ __device__ __forceinline__ void resolve_tick(const WinState& w, ResolveLds& sm, 
   for (uint32_t p = lo + tid; p < hi; p += kResolveBlock) {
     const uint32_t m = src[p];
     if (msg_tick(m) != k) continue;
-    const uint32_t loc = msg_loc(m), sh = (loc & 1) * 16;
-    const uint32_t old = atomicAdd(&sm.cnt[loc >> 1], 1u << sh);
-    if (((old >> sh) & 0xFFFFu) == 0xFFFFu) sm.err = 1;
+    const uint32_t old = atomicAdd(&sm.cnt[msg_loc(m)], 1u + (((m >> kRoll0Fine) & 1u) << 16));
+    if ((old & 0xFFFFu) == 0xFFFFu) sm.err = 1;
   }
   __syncthreads();
   uint32_t arr = 0, cm = 0, cr = 0, cc = 0, cs = 0;
   for (uint32_t p = lo + tid; p < hi; p += kResolveBlock) {
     const uint32_t m = src[p];
     if (msg_tick(m) != k) continue;
-    const uint32_t loc = msg_loc(m), sh = (loc & 1) * 16;
-    const uint32_t kk = (atomicAnd(&sm.cnt[loc >> 1], ~(0xFFFFu << sh)) >> sh) & 0xFFFFu;
-    arr += kk;
-    if (kk) resolve_node(w, sm, f, loc, kk, t, cm, cr, cc, cs);
+    const uint32_t loc = msg_loc(m);
+    const uint32_t kk = atomicExch(&sm.cnt[loc], 0u);
+    arr += kk & 0xFFFFu;
+    if (kk) resolve_node(w, sm, f, loc, kk & 0xFFFFu, kk >> 16, t, cm, cr, cc, cs);
   }
   if (arr != cm) atomicAdd(&sm.st[k][0], arr - cm);
   if (cr) atomicAdd(&sm.st[k][1], cr);
@@ -874,43 +846,27 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
-// Receipt ordinals of one node with c >= 2 receipts at tick t (rule A6,
-// simulator.go:107-123): counted -> crash roll (ordinal 0 rode with the
-// message, later ordinals draw U_100(u, t, i)) -> first receipt infects.
-// roll123 = the rolls of ordinals 1..3 when `have` (batched), else drawn here.
+// One node with c >= 2 receipts at tick t, `ones` of them carrying a crash
+// roll (rule A6, simulator.go:107-123): counted up to and including the first
+// crash (first_crash), infected if a receipt came before it.
 __device__ __forceinline__ void replay_node(const WinState& w, uint32_t u, uint32_t t, uint32_t c,
-                                            uint32_t bit, bool roll0, bool have, uint32_t roll123,
-                                            uint32_t c3crash, uint32_t& cw, uint32_t& rw,
-                                            uint32_t& infS, uint32_t& nd, uint32_t& nc, uint32_t& ni) {
+                                            uint32_t ones, uint32_t bit, uint32_t c3order, uint32_t& cw,
+                                            uint32_t& rw, uint32_t& infS, uint32_t& nd, uint32_t& nc,
+                                            uint32_t& ni) {
   if (cw & bit) {  // crashed before this tick: nothing is counted (:108)
     nd += c;
     return;
   }
-  u32x4 r{0, 0, 0, 0};
-  for (uint32_t i = 0; i < c; ++i) {                              // :111 counted
-    bool roll = roll0;                                            // :112
-    if (i > 0) {
-      roll = false;
-      if (w.kc > 0) {
-        if (have && i <= 3) {
-          roll = (roll123 >> (i - 1)) & 1;
-        } else {
-          if ((!have && i == 1) || (i & 3) == 0) r = philox(u, t, i >> 2, c3crash, w.key.k0, w.key.k1);
-          roll = (int32_t)uniform(lane_of(r, i & 3), 100u) < w.kc;
-        }
-      }
-    }
-    if (roll) {                                                   // :113-115
-      cw |= bit;
-      ++nc;
-      nd += c - 1 - i;                                            // the rest of the tick
-      return;
-    }
-    if (!(rw & bit)) {                                            // :117-121
-      rw |= bit;
-      infS |= bit;
-      ++ni;
-    }
+  const uint32_t g = ones ? first_crash(u, t, c, ones, c3order, w.key.k0, w.key.k1) : c + 1;
+  if (g > 1 && !(rw & bit)) {                                     // :117-121
+    rw |= bit;
+    infS |= bit;
+    ++ni;
+  }
+  if (g <= c) {                                                   // :112-115
+    cw |= bit;
+    ++nc;
+    nd += c - g;                                                  // the rest of the tick
   }
 }
 
@@ -998,10 +954,10 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
     const uint32_t node0 = f << kFineLog;
     const uint64_t wi = ((uint64_t)node0 >> 5) + tid;
     // Philox keys of the bucket's nodes: key node knode0 + local offset (a
-    // bucket lies inside one trial), counter words c3crash / c3delay
-    uint32_t knode0, c3crash;
-    node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + node0, K_CRASH, knode0, c3crash);
-    const uint32_t c3delay = (c3crash & 0xFFFFFFu) | (K_DELAY << 24);
+    // bucket lies inside one trial), counter words c3order / c3delay
+    uint32_t knode0, c3order;
+    node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + node0, K_ORDER, knode0, c3order);
+    const uint32_t c3delay = (c3order & 0xFFFFFFu) | (K_DELAY << 24);
     const bool in = wi < w.W * 2;
     const uint32_t recv0 = in ? rwg[wi] : 0u, crash0 = in ? cwg[wi] : 0u;
     const uint32_t fcv = tid < w.R ? w.fcount[(size_t)tid * w.nfine + f] : 0u;
@@ -1028,23 +984,27 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) {
         bool dup = false;
-        uint32_t loc = 0, k = 0;
+        uint32_t loc = 0, k = 0, roll = 0;
         if (m[u] != ~0u) {
           loc = msg_loc(m[u]);
           k = msg_tick(m[u]);
           const uint32_t bit = 1u << (loc & 31);
-          if ((m[u] >> kRoll0Fine) & 1) atomicOr(&sm.rl[k][loc >> 5], bit);
-          // thermometer: b1 = >= 1 receipt, b2 = >= 2; the third and later
-          // receipts of a (node, tick) are chained under their word
-          if (atomicOr(&sm.b1[k][loc >> 5], bit) & bit)
+          roll = (m[u] >> kRoll0Fine) & 1;
+          if (roll) {  // a crash roll: flagged, and chained with its flag
+            atomicOr(&sm.rl[k][loc >> 5], bit);
+            dup = true;
+          } else if (atomicOr(&sm.b1[k][loc >> 5], bit) & bit) {
+            // thermometer: b1 = >= 1 receipt, b2 = >= 2; the third and later
+            // receipts of a (node, tick) are chained under their word
             dup = (atomicOr(&sm.b2[k][loc >> 5], bit) & bit) != 0;
+          }
         }
-        if (!__ballot(dup)) continue;  // no third receipt in this wave
+        if (!__ballot(dup)) continue;  // nothing to chain in this wave
         const uint32_t at = wave_append(&sm.ndup, dup);
         if (dup) {
           if (at < kDupCap) {
             const uint32_t prev = atomicExch(&sm.dhead[loc >> 5], at + 1);
-            sm.dlist[at] = loc | (k << kFineLog) | (prev << 18);
+            sm.dlist[at] = loc | (k << kFineLog) | (roll << 18) | (prev << 19);
           } else {
             sm.err = 3;
           }
@@ -1056,44 +1016,6 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
     uint32_t rw = recv0, cw = crash0;
     if (sm.err != 3) {
       const uint32_t ubase = knode0 + tid * 32;
-      // crash rolls of ordinals 1..3 for every (node, tick) with >= 2 receipts,
-      // one lane per entry (in the tick loop they would serialise the wave);
-      // this word's entries are contiguous from rcur, in tick loop order
-      uint32_t rcur = kDupCap;
-      if (w.kc > 0) {
-        uint32_t cnt = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < kBitTicks; ++k)
-          if (k < L) cnt += __popc(sm.b2[k][tid]);
-        uint32_t x = cnt;
-#pragma unroll
-        for (uint32_t o = 1; o < 64; o <<= 1) {
-          const uint32_t y = __shfl_up(x, o, 64);
-          if (lane_id() >= o) x += y;
-        }
-        if (tid == 0) sm.nroll = sm.ndup < kDupCap ? sm.ndup : kDupCap;
-        __syncthreads();
-        uint32_t base = 0;
-        if (lane_id() == 63 && x) base = atomicAdd(&sm.nroll, x);
-        rcur = __shfl(base, 63, 64) + x - cnt;
-        uint32_t j = rcur;
-#pragma unroll
-        for (uint32_t k = 0; k < kBitTicks; ++k)
-          for (uint32_t d = k < L ? sm.b2[k][tid] : 0u; d; d &= d - 1, ++j)
-            if (j < kDupCap) sm.dlist[j] = (tid << 9) | (k << 5) | __builtin_ctz(d);
-        __syncthreads();
-        const uint32_t r0 = sm.ndup < kDupCap ? sm.ndup : kDupCap;
-        const uint32_t r1 = sm.nroll < kDupCap ? sm.nroll : kDupCap;
-        for (uint32_t q = r0 + tid; q < r1; q += kResolveBlock) {
-          const uint32_t e = sm.dlist[q];
-          const uint32_t u = knode0 + (e >> 9) * 32 + (e & 31), t = t0 + ((e >> 5) & 15);
-          const u32x4 r = philox(u, t, 0, c3crash, w.key.k0, w.key.k1);  // :180, ordinals 0..3
-          const uint32_t b1 = (int32_t)uniform(r.y, 100u) < w.kc, b2 = (int32_t)uniform(r.z, 100u) < w.kc,
-                         b3 = (int32_t)uniform(r.w, 100u) < w.kc;
-          sm.dlist[q] = e | (b1 << 18) | (b2 << 19) | (b3 << 20);
-        }
-        __syncthreads();
-      }
       // ticks: thread tid resolves nodes 32*tid .. 32*tid+31, tick by tick
       uint32_t infk[kBitTicks], ninf = 0;  // infections per tick of this word
 #pragma unroll
@@ -1101,27 +1023,24 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
         infk[k] = 0;
         if (k >= L) continue;
         const uint32_t A = sm.b1[k][tid], D = sm.b2[k][tid], R = sm.rl[k][tid];
-        const uint32_t S = A & ~D;                       // one receipt at this tick
+        const uint32_t S = A & ~D & ~R;                  // one receipt at this tick, no crash roll
         const uint32_t deadS = S & cw;                   // :108 crashed: not counted
-        const uint32_t crS = S & ~cw & R;                // :112-115
-        uint32_t infS = S & ~cw & ~R & ~rw;              // :117-121
-        cw |= crS;
+        uint32_t infS = S & ~cw & ~rw;                   // :117-121
         rw |= infS;
-        uint32_t nd = __popc(deadS), nc = __popc(crS), ni = __popc(infS);
+        uint32_t nd = __popc(deadS), nc = 0, ni = __popc(infS);
         const uint32_t t = t0 + k;
-        for (uint32_t dm = D; dm; dm &= dm - 1) {        // nodes with repeats at this tick
+        for (uint32_t dm = D | R; dm; dm &= dm - 1) {    // repeats or crash rolls at this tick
           const uint32_t b = __builtin_ctz(dm), loc = tid * 32 + b;
-          uint32_t c = 2;
+          uint32_t c = ((A >> b) & 1) + ((D >> b) & 1), ones = 0;
           for (uint32_t q = sm.dhead[tid]; q;) {
             const uint32_t e = sm.dlist[q - 1];
-            c += (e & ((1u << 18) - 1)) == (loc | (k << kFineLog)) ? 1u : 0u;
-            q = e >> 18;
+            if ((e & ((1u << 18) - 1)) == (loc | (k << kFineLog))) {
+              ++c;
+              ones += (e >> 18) & 1;
+            }
+            q = e >> 19;
           }
-          const bool have = rcur < kDupCap;
-          const uint32_t r123 = have ? (sm.dlist[rcur] >> 18) & 7 : 0u;
-          ++rcur;
-          replay_node(w, ubase + b, t, c, 1u << b, (R >> b) & 1, have, r123, c3crash, cw, rw, infS, nd,
-                      nc, ni);
+          replay_node(w, ubase + b, t, c, ones, 1u << b, c3order, cw, rw, infS, nd, nc, ni);
         }
         // per-tick counters stay in the lane until the launch ends
         acc_rc[k] += ni | (nc << 16);
@@ -1165,7 +1084,7 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
       // large path: per-node counters, the messages streamed once per tick
       __syncthreads();
       uint4* c4 = reinterpret_cast<uint4*>(sm.cnt);
-      for (uint32_t q = tid; q < kFineNodes / 8; q += kResolveBlock) c4[q] = make_uint4(0, 0, 0, 0);
+      for (uint32_t q = tid; q < kFineNodes / 4; q += kResolveBlock) c4[q] = make_uint4(0, 0, 0, 0);
       sm.recv[tid] = recv0;
       sm.crash[tid] = crash0;
       sm.nrecv[tid] = 0;
@@ -1248,11 +1167,11 @@ __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t
   constexpr uint32_t N = 64 * E;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   {
-    uint32_t knode0, c3crash;  // keys of the bucket's nodes (one trial per bucket)
-    node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + (f << kFineLog), K_CRASH, knode0, c3crash);
-    const uint32_t c3delay = (c3crash & 0xFFFFFFu) | (K_DELAY << 24);
+    uint32_t knode0, c3order;  // keys of the bucket's nodes (one trial per bucket)
+    node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + (f << kFineLog), K_ORDER, knode0, c3order);
+    const uint32_t c3delay = (c3order & 0xFFFFFFu) | (K_DELAY << 24);
     const uint32_t* gm = w.fmsg + w.fstart[f];
-    uint32_t key[E];  // loc << 5 | k << 1 | roll0; ~0u sorts last
+    uint32_t key[E];  // loc << 5 | k << 1 | crash roll; ~0u sorts last
 #pragma unroll
     for (uint32_t r = 0; r < E; ++r) {
       const uint32_t i = r * 64 + lane;
@@ -1301,30 +1220,31 @@ __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t
       const uint32_t wi = ((f << kFineLog) + loc) >> 5, bit = 1u << (loc & 31), u = knode0 + loc;
       const uint32_t cw = cwg[wi];
       bool rv = (rwg[wi] & bit) != 0, cr = (cw & bit) != 0, inf = false;
-      uint32_t ktick = ~0u, ord = 0, tinf = 0;
-      for (uint32_t q = i; q < N; ++q) {  // along the run (~0u never matches a loc)
+      uint32_t tinf = 0;
+      for (uint32_t q = i; q < N;) {  // along the run, one (node, tick) group at a time
         const uint32_t e = skw[q];
-        if ((e >> 5) != loc) break;
+        if ((e >> 5) != loc) break;  // (~0u never matches a loc)
         const uint32_t k = (e >> 1) & (kMaxWindow - 1), t = t0 + k;
-        if (k != ktick) { ktick = k; ord = 0; } else { ++ord; }
+        uint32_t c = 0, ones = 0;  // receipts, crash rolls among them
+        for (; q < N && (skw[q] >> 1) == (e >> 1); ++q) {
+          ++c;
+          ones += skw[q] & 1u;
+        }
         if (cr) {                                                   // :108 not counted
-          atomicAdd(&st[wv][k][0], 1u);
+          atomicAdd(&st[wv][k][0], c);
           continue;
         }
-        bool roll = e & 1u;                                         // :111-112, ordinal 0 rode along
-        if (ord > 0) {
-          roll = false;
-          if (w.kc > 0)
-            roll = (int32_t)uniform(lane_of(philox(u, t, ord >> 2, c3crash, w.key.k0, w.key.k1), ord & 3),
-                                    100u) < w.kc;
-        }
-        if (roll) {                                                 // :113-115
-          cr = true;
-          atomicAdd(&st[wv][k][2], 1u);
-        } else if (!rv) {                                           // :117-121
+        // rule A6: counted up to the first crash, informed if a receipt came first
+        const uint32_t g = ones ? first_crash(u, t, c, ones, c3order, w.key.k0, w.key.k1) : c + 1;
+        if (g > 1 && !rv) {                                         // :117-121
           rv = inf = true;
           tinf = t;
           atomicAdd(&st[wv][k][1], 1u);
+        }
+        if (g <= c) {                                               // :112-115
+          cr = true;
+          atomicAdd(&st[wv][k][2], 1u);
+          if (c > g) atomicAdd(&st[wv][k][0], c - g);
         }
       }
       if (cr && !(cw & bit)) atomicOr(&cwg[wi], bit);
@@ -1488,7 +1408,8 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand_sh(const WinState w, ui
         if (j < c) gm |= 1u << ((mm[j] & 31) >> 2);
       uint32_t vn, c3drop;
       node_key(w.tlog, w.tmask, w.key, v, K_DROP, vn, c3drop);
-      uint32_t keep = 0;
+      const uint32_t c3crash = (c3drop & 0xFFFFFFu) | (K_CRASH << 24);
+      uint32_t keep = 0, crash = 0;  // bit j: slot j kept / its message carries a crash roll
 #pragma unroll
       for (uint32_t g = 0; g < (kWinMaxStride + 3) / 4; ++g)
         if ((gm >> g) & 1) {
@@ -1497,18 +1418,20 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand_sh(const WinState w, ui
                    ((int32_t)uniform(r.y, 100u) >= w.kd ? 2u : 0u) |
                    ((int32_t)uniform(r.z, 100u) >= w.kd ? 4u : 0u) |
                    ((int32_t)uniform(r.w, 100u) >= w.kd ? 8u : 0u)) << (4 * g);
+          if (w.kc > 0) {  // :180, keyed by the sender's slots
+            const u32x4 q = philox(vn, t, g, c3crash, w.key.k0, w.key.k1);
+            crash |= (((int32_t)uniform(q.x, 100u) < w.kc ? 1u : 0u) |
+                      ((int32_t)uniform(q.y, 100u) < w.kc ? 2u : 0u) |
+                      ((int32_t)uniform(q.z, 100u) < w.kc ? 4u : 0u) |
+                      ((int32_t)uniform(q.w, 100u) < w.kc ? 8u : 0u)) << (4 * g);
+          }
         }
 #pragma unroll
       for (uint32_t j = 0; j < MAXS; ++j) {
         const uint32_t ent = mm[j];
         if (j < c && ((keep >> (ent & 31)) & 1)) {                       // kept: :145
           const uint32_t tl = ent >> 5, bin = tl >> kCoarseShift;
-          uint32_t roll0 = 0;
-          if (w.kc > 0) {
-            uint32_t un, c3crash;
-            node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + tl, K_CRASH, un, c3crash);
-            roll0 = (int32_t)uniform(philox(un, t, 0, c3crash, w.key.k0, w.key.k1).x, 100u) < w.kc;
-          }
+          const uint32_t roll0 = (crash >> (ent & 31)) & 1;
           mt[j] = bin | (atomicAdd(&sm.cnt[bin], 1u) << 8);
           mm[j] = (tl & ((1u << kCoarseShift) - 1)) | (k << kCoarseShift) | (roll0 << kRoll0Coarse);
           ++sent;

@@ -8,11 +8,12 @@
  * delay/drop/crash), so its per-tick counters and bitsets equal
  * or_engine_step's bit for bit whatever the thread count:
  *   phase A (parallel over the fire slot's words): every firing node draws
- *     its drops and counts one arrival per kept send (atomic add); the first
- *     arrival at a node lists it in the thread's touched list;
- *   phase B (parallel over the touched nodes): rule A6 -- ordinals 0..k-1 of
- *     the receive case, with keyed crash rolls -- then Broadcast() of the
- *     newly received (atomic OR into the fire ring).
+ *     its drops and its messages' crash rolls and counts one arrival (and its
+ *     roll) per kept send (atomic add); the first arrival at a node lists it
+ *     in the thread's touched list;
+ *   phase B (parallel over the touched nodes): rule A6 -- k receipts, their
+ *     crash rolls and the keyed first-crash position -- then Broadcast() of
+ *     the newly received (atomic OR into the fire ring).
  * Flood model only (the reference's); no node-range sharding.
  */
 #include <omp.h>
@@ -157,13 +158,17 @@ int om_engine_step(om_engine* e, uint32_t ticks, or_tick_stats* out) {
           ++fired;
           const uint32_t d = e->deg[v];
           const uint32_t* row = e->ids + (uint64_t)v * e->stride;
-          uint32_t rnd[4] = {0, 0, 0, 0};
+          uint32_t rnd[4] = {0, 0, 0, 0}, rc[4] = {0, 0, 0, 0};
           for (uint32_t j = 0; j < d; ++j) {
-            if ((j & 3) == 0) draw4(e->key, v, (uint32_t)t, j >> 2, OR_K_DROP, e->p.trial, rnd);
+            if ((j & 3) == 0) {
+              draw4(e->key, v, (uint32_t)t, j >> 2, OR_K_DROP, e->p.trial, rnd);
+              if (e->kc > 0) draw4(e->key, v, (uint32_t)t, j >> 2, OR_K_CRASH, e->p.trial, rc);
+            }
             if ((int32_t)or_uniform(rnd[j & 3], 100) < e->kd) continue; /* :144, :172 */
             const uint32_t u = row[j];                                   /* :145 */
             ++sent;
-            if (__atomic_fetch_add(&e->cnt[u], 1u, __ATOMIC_RELAXED) == 0) {
+            const uint32_t roll = e->kc > 0 && (int32_t)or_uniform(rc[j & 3], 100) < e->kc;  /* :180 */
+            if (__atomic_fetch_add(&e->cnt[u], 1u + (roll << 16), __ATOMIC_RELAXED) == 0) {
               if (nt == cap) {
                 cap *= 2;
                 uint32_t* g = (uint32_t*)realloc(tl, cap * 4);
@@ -178,32 +183,23 @@ int om_engine_step(om_engine* e, uint32_t ticks, or_tick_stats* out) {
         }
       }
       /* implicit barrier: every arrival is counted */
-      /* phase B: the receive case per touched node, ordinals in order (:107-123) */
+      /* phase B: the receive case per touched node (:107-123, rule A6) */
       for (uint64_t i = 0; i < nt; ++i) {
         const uint32_t u = tl[i];
-        const uint32_t k = e->cnt[u];
+        const uint32_t k = e->cnt[u] & 0xFFFFu, ones = e->cnt[u] >> 16;
         e->cnt[u] = 0;
-        uint32_t rnd[4] = {0, 0, 0, 0};
         const uint64_t bit = 1ull << (u & 63);
-        int crashed = (int)((__atomic_load_n(&e->crashed[u >> 6], __ATOMIC_RELAXED) & bit) != 0);
-        int received = (int)((__atomic_load_n(&e->received[u >> 6], __ATOMIC_RELAXED) & bit) != 0);
-        for (uint32_t o = 0; o < k; ++o) {
-          if (crashed) break;                                            /* :108 */
-          ++msgs;                                                        /* :111 */
-          if (e->kc > 0) {
-            if ((o & 3) == 0) draw4(e->key, u, (uint32_t)t, o >> 2, OR_K_CRASH, e->p.trial, rnd);
-            if ((int32_t)or_uniform(rnd[o & 3], 100) < e->kc) {          /* :112-115 */
-              __atomic_fetch_or(&e->crashed[u >> 6], bit, __ATOMIC_RELAXED);
-              crashed = 1;
-              ++ncrash;
-              break;
-            }
-          }
-          if (received) continue;                                        /* :117 */
-          __atomic_fetch_or(&e->received[u >> 6], bit, __ATOMIC_RELAXED);  /* :120 */
-          received = 1;
-          ++nrecv;                                                       /* :121 */
-          schedule(e, u, t);                                             /* :122 */
+        if (__atomic_load_n(&e->crashed[u >> 6], __ATOMIC_RELAXED) & bit) continue;   /* :108 */
+        const uint32_t g = ones ? or_first_crash(e->key, e->p.trial, u, (uint32_t)t, k, ones) : k + 1;
+        msgs += g <= k ? g : k;                                                       /* :111 */
+        if (g > 1 && !(__atomic_load_n(&e->received[u >> 6], __ATOMIC_RELAXED) & bit)) {  /* :117 */
+          __atomic_fetch_or(&e->received[u >> 6], bit, __ATOMIC_RELAXED);             /* :120 */
+          ++nrecv;                                                                    /* :121 */
+          schedule(e, u, t);                                                          /* :122 */
+        }
+        if (g <= k) {                                                                 /* :112-115 */
+          __atomic_fetch_or(&e->crashed[u >> 6], bit, __ATOMIC_RELAXED);
+          ++ncrash;
         }
       }
     }

@@ -42,6 +42,19 @@ uint32_t or_uniform(uint32_t r, uint32_t m) {
   return (uint32_t)(((uint64_t)r * (uint64_t)m) >> 32);
 }
 
+uint32_t or_first_crash(const uint32_t key[2], uint32_t trial, uint32_t u, uint32_t t, uint32_t k,
+                        uint32_t ones) {
+  if (k <= 1 || ones >= k) return 1;
+  uint32_t rnd[4] = {0, 0, 0, 0};
+  for (uint32_t g = 1;; ++g) {  /* ends by g = k - ones + 1, where U_ones < ones */
+    if (((g - 1) & 3) == 0) {
+      uint32_t ctr[4] = {u, t, (g - 1) >> 2, ((uint32_t)OR_K_ORDER << 24) | (trial & 0xFFFFFFu)};
+      or_philox(ctr, key, rnd);
+    }
+    if (or_uniform(rnd[(g - 1) & 3], k - g + 1) < ones) return g;
+  }
+}
+
 /* Go: int(rate*100) -- float64 multiply, truncation toward zero
  * (simulator.go:172,180).  0.001 -> 0, 0.1 -> 10, 0.29 -> 28. */
 int32_t or_threshold(double rate) {
@@ -425,46 +438,48 @@ int or_engine_step(or_engine* e, uint32_t ticks, or_tick_stats* out) {
         if (v >= e->lo && v < e->hi) ++fired;
         uint32_t d = e->deg[v];
         const uint32_t* row = e->ids + (uint64_t)v * e->stride;
-        uint32_t rnd[4] = {0, 0, 0, 0};
+        uint32_t rnd[4] = {0, 0, 0, 0}, rc[4] = {0, 0, 0, 0};
         for (uint32_t j = 0; j < d; ++j) {
           if ((j & 3) == 0) {
             uint32_t ctr[4] = {v, (uint32_t)t, j >> 2, c3of(OR_K_DROP, e->p.trial)};
             or_philox(ctr, e->key, rnd);
+            if (e->kc > 0) {  /* the messages' crash rolls (:180), same counter */
+              ctr[3] = c3of(OR_K_CRASH, e->p.trial);
+              or_philox(ctr, e->key, rc);
+            }
           }
           if ((int32_t)or_uniform(rnd[j & 3], 100) < e->kd) continue; /* :144,:172 */
           uint32_t u = row[j];                                         /* :145 */
           if (u < e->lo || u >= e->hi) continue;  /* another rank's target */
           ++sent;
-          if (e->cnt[u]++ == 0) e->touched[nt++] = u;
+          const uint32_t roll = e->kc > 0 && (int32_t)or_uniform(rc[j & 3], 100) < e->kc;
+          if (e->cnt[u] == 0) e->touched[nt++] = u;
+          e->cnt[u] += 1u + (roll << 16);  /* receipts | crash rolls << 16 */
         }
       }
     }
     e->pending -= fired;
-    /* Receipts, in ordinal order (simulator.go:107-123): the outcome depends
-     * only on the arrival count and the keyed rolls, not on who sent what. */
+    /* Receipts (simulator.go:107-123), rule A6: the k messages of a tick are
+     * taken in a uniformly random order; each is counted (:111) and rolls
+     * its own crash (:112-115), the first that does not crash informs the
+     * node (:117-122), and the node stops at the first crash.  So only k, the
+     * number of crash rolls among them and the keyed first-crash position
+     * matter -- not who sent what, nor the order atomics arrive in. */
     for (uint64_t i = 0; i < nt; ++i) {
       uint32_t u = e->touched[i];
-      uint32_t k = e->cnt[u];
+      const uint32_t k = e->cnt[u] & 0xFFFFu, ones = e->cnt[u] >> 16;
       e->cnt[u] = 0;
-      uint32_t rnd[4] = {0, 0, 0, 0};
-      for (uint32_t o = 0; o < k; ++o) {
-        if (BIT(e->crashed, u)) break;                          /* :108 */
-        ++msgs;                                                 /* :111 */
-        if (e->kc > 0) {
-          if ((o & 3) == 0) {
-            uint32_t ctr[4] = {u, (uint32_t)t, o >> 2, c3of(OR_K_CRASH, e->p.trial)};
-            or_philox(ctr, e->key, rnd);
-          }
-          if ((int32_t)or_uniform(rnd[o & 3], 100) < e->kc) {  /* :112-115 */
-            SETBIT(e->crashed, u);
-            ++e->crashed_cnt;
-            break;
-          }
-        }
-        if (BIT(e->received, u)) continue;                      /* :117 */
-        SETBIT(e->received, u);                                 /* :120 */
-        ++e->recv;                                              /* :121 */
-        schedule(e, u, t);                                      /* :122 */
+      if (BIT(e->crashed, u)) continue;                          /* :108 */
+      const uint32_t g = ones ? or_first_crash(e->key, e->p.trial, u, (uint32_t)t, k, ones) : k + 1;
+      msgs += g <= k ? g : k;                                    /* :111 */
+      if (g > 1 && !BIT(e->received, u)) {                       /* :117 */
+        SETBIT(e->received, u);                                  /* :120 */
+        ++e->recv;                                               /* :121 */
+        schedule(e, u, t);                                       /* :122 */
+      }
+      if (g <= k) {                                              /* :112-115 */
+        SETBIT(e->crashed, u);
+        ++e->crashed_cnt;
       }
     }
     if (out) {

@@ -40,12 +40,15 @@ enum {
   OR_K_SENDER = 1,  /* simulator.go:240  rand.Intn(len(GlobalView))          */
   OR_K_DELAY = 2,   /* simulator.go:167  RandomNetworkDelay, per Broadcast    */
   OR_K_DROP = 3,    /* simulator.go:172  RandomDrop, per friend slot          */
-  OR_K_CRASH = 4,   /* simulator.go:180  RandomCrash, per receipt             */
+  OR_K_CRASH = 4,   /* simulator.go:180  RandomCrash: one roll per message, keyed by its
+                     * sender's (node, fire tick, slot) like the drop           */
   OR_K_PICK = 5,    /* simulator.go:97   new-friend pick                      */
   OR_K_OVDELAY = 6, /* simulator.go:153,160 Breakup/Makeup delay              */
   OR_K_VICTIM = 7,  /* simulator.go:71   victim slot                          */
   OR_K_REPLACE = 8, /* simulator.go:86-89 replacement friend (rejection)      */
-  OR_K_PUSHPULL = 9 /* push-pull extension: peer pick + loss, per (node, round) */
+  OR_K_PUSHPULL = 9, /* push-pull extension: peer pick + loss, per (node, round) */
+  OR_K_ORDER = 10    /* simulator.go:107-115 receipt order: position of the first
+                      * crashing message among a (node, tick)'s receipts        */
 };
 
 /* Dissemination models (or_params.model). */
@@ -87,6 +90,13 @@ typedef struct or_window {
 int32_t or_threshold(double rate);
 /* Philox4x32-10, Random123 constants. */
 void or_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+/* Receipt order (rule A6): the 1-based position of the first crashing
+ * message when k receipts of node u at tick t, `ones` of them with a crash
+ * roll (1 <= ones <= k), are taken in a uniformly random order -- sequential
+ * draws U_{k-g+1} < ones from Philox{u, t, (g-1)/4, ORDER}, lane (g-1)%4.
+ * k == 1 or ones == k needs no draw (position 1). */
+uint32_t or_first_crash(const uint32_t key[2], uint32_t trial, uint32_t u, uint32_t t, uint32_t k,
+                        uint32_t ones);
 /* floor(r * m / 2^32): the uniform-in-[0,m) map shared with the HIP engine. */
 uint32_t or_uniform(uint32_t r, uint32_t m);
 /* Sender chosen as simulator.go:240 does, from the keyed stream. */
