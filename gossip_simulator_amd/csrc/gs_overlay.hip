@@ -226,9 +226,12 @@ __global__ __launch_bounds__(256) void k_process(const OvParams p, uint32_t t, c
 
 using DevBuf = OverlayWork::Buf;
 
+// Grown with 25 % headroom: a batched context rebuilds overlays batch after
+// batch, and a regrow (hipFree + hipMalloc of GB-sized buckets) cost up to
+// 1.7 s where the next batch's events outnumbered the first's by a little.
 static hipError_t grow(DevBuf& b, size_t bytes) {
   if (b.bytes >= bytes) return hipSuccess;
-  const size_t nb = std::max(bytes, b.bytes * 3 / 2);
+  const size_t nb = std::max(bytes + bytes / 4, b.bytes * 3 / 2);
   if (b.p) (void)hipFree(b.p);
   b.p = nullptr;
   b.bytes = 0;
