@@ -138,6 +138,7 @@ struct WinState {
   WinCtl* ctl;                   // device-driven windows (null: the host passes t0 / L)
   unsigned long long* stage;     // [slots][kStageWords] per-window results for the host (device-driven)
   uint32_t lstride;              // unit layout stride: units u = f * lstride + k
+  uint32_t slots;                // longest row in use (<= stride: rows may be padded for 16-B loads)
   // node-range shard: partitioned friend rows (prow[v]..prow[v+1] of pent, entry =
   // (target - base) << 5 | slot j) and the all-gathered window fire list
   const uint32_t* prow;

@@ -352,7 +352,18 @@ __device__ __forceinline__ void tstat_add(uint32_t* tstat, uint32_t key, uint32_
 template <uint32_t MAXS>
 __device__ __forceinline__ void load_row(const WinState& w, uint32_t v, uint32_t (&mm)[MAXS]) {
   const uint32_t S = w.stride;
-  if ((S & 1) == 0) {
+  if ((S & 3) == 0 && S >= 8 && MAXS >= 5 && MAXS <= 8) {  // 16-B aligned rows: uint4 + uint2 / uint4
+    const uint4 a = reinterpret_cast<const uint4*>(w.ids + (size_t)v * S)[0];
+    mm[0] = a.x; mm[1] = a.y; mm[2] = a.z; mm[3] = a.w;
+    if (MAXS > 4 && MAXS <= 6) {
+      const uint2 b = reinterpret_cast<const uint2*>(w.ids + (size_t)v * S)[2];
+      mm[4 % MAXS] = b.x;
+      if (MAXS > 5) mm[5 % MAXS] = b.y;
+    } else if (MAXS > 6) {
+      const uint4 b = reinterpret_cast<const uint4*>(w.ids + (size_t)v * S)[1];
+      mm[4 % MAXS] = b.x; mm[5 % MAXS] = b.y; mm[6 % MAXS] = b.z; mm[7 % MAXS] = b.w;
+    }
+  } else if ((S & 1) == 0) {
     const uint2* row = reinterpret_cast<const uint2*>(w.ids + (size_t)v * S);
 #pragma unroll
     for (uint32_t j = 0; j < MAXS; j += 2) {
@@ -1553,19 +1564,20 @@ hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, i
   // block * 4 * row slots, so 6-slot rows fit four workgroups per CU
   // GS_XNPT=2: two firing nodes per thread (experiment: LDS and VGPRs for 8 workgroups per CU)
   static const uint32_t npt = [] { const char* e = getenv("GS_XNPT"); return e && atoi(e) == 2 ? 2u : kExpandNpt; }();
-  const uint32_t per_round = w.stride <= 8 ? kExpandBlock * (w.stride <= 6 ? npt : kExpandNpt) : kExpandBlock;
+  const uint32_t rs = w.slots;  // rows may be padded past the longest one
+  const uint32_t per_round = rs <= 8 ? kExpandBlock * (rs <= 6 ? npt : kExpandNpt) : kExpandBlock;
   const uint64_t rounds = (Tn + per_round - 1) / per_round;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>(rounds, 8192);
   const dim3 grid(blocks ? blocks : 1), blk(kExpandBlock);
   const unsigned long long tn = Tn;
   const int st = mode == 1 ? 1 : 0;
-  if (w.stride <= 6 && npt == 2) {
+  if (rs <= 6 && npt == 2) {
     if (mode) hipLaunchKernelGGL((k_expand<true, 6, 2>), grid, blk, 0, s, w, t0, L, tn, st);
     else hipLaunchKernelGGL((k_expand<false, 6, 2>), grid, blk, 0, s, w, t0, L, tn, 0);
-  } else if (w.stride <= 6) {
+  } else if (rs <= 6) {
     if (mode) hipLaunchKernelGGL((k_expand<true, 6, kExpandNpt>), grid, blk, 0, s, w, t0, L, tn, st);
     else hipLaunchKernelGGL((k_expand<false, 6, kExpandNpt>), grid, blk, 0, s, w, t0, L, tn, 0);
-  } else if (w.stride <= 8) {
+  } else if (rs <= 8) {
     if (mode) hipLaunchKernelGGL((k_expand<true, 8, kExpandNpt>), grid, blk, 0, s, w, t0, L, tn, st);
     else hipLaunchKernelGGL((k_expand<false, 8, kExpandNpt>), grid, blk, 0, s, w, t0, L, tn, 0);
   } else {
