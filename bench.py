@@ -72,6 +72,17 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+def guarded(name, fn):
+    """An extension leg that raises is recorded as {"error": ...} so the
+    headline line still prints (every rank runs the same legs, so a
+    parameter error raises on all of them alike)."""
+    try:
+        return fn()
+    except Exception as e:  # noqa: BLE001 -- reported in the line, not hidden
+        log(f"{name} failed: {type(e).__name__}: {e}")
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -166,14 +177,15 @@ def main():
 
     ext = None
     if not a.no_extensions:
-        ext = {"flood_failed_1pct": flood_failed(a, sim)}
+        ext = {"flood_failed_1pct": guarded("flood_failed_1pct", lambda: flood_failed(a, sim))}
     sim.close()
     if not a.no_extensions:
-        ext.update(pushpull_runs(a, gs, rank, local))
+        pp = guarded("pushpull", lambda: pushpull_runs(a, gs, rank, local))
+        ext.update(pp if "error" not in pp else {"pushpull": pp})
         if not a.no_c3:
-            ext["c3_trials"] = c3_trials(a, gs, rank, world, local, dist)
+            ext["c3_trials"] = guarded("c3_trials", lambda: c3_trials(a, gs, rank, world, local, dist))
         if not a.no_c4:
-            ext["c4_sharded"] = c4_sharded(a, gs, rank, world, local, dist)
+            ext["c4_sharded"] = guarded("c4_sharded", lambda: c4_sharded(a, gs, rank, world, local, dist))
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_n > 0:
