@@ -73,6 +73,9 @@ def lib():
         L.or_philox.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
         L.or_uniform.argtypes = [C.c_uint32, C.c_uint32]
         L.or_uniform.restype = C.c_uint32
+        L.or_first_crash.argtypes = [P(C.c_uint32), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                     C.c_uint32]
+        L.or_first_crash.restype = C.c_uint32
         L.or_pick_sender.argtypes = [P(Params)]
         L.or_pick_sender.restype = C.c_uint64
         L.or_overlay.argtypes = [P(Params), C.c_void_p, C.c_void_p, P(Window), C.c_size_t,
@@ -108,6 +111,12 @@ def make_params(n=50000, fanout=5, fanin=6, delay_low=10, delay_high=20,
 
 def threshold(rate: float) -> int:
     return lib().or_threshold(rate)
+
+
+def first_crash(key, trial, u, t, k, ones):
+    """Rule A6's keyed first-crash position (gsoracle.h or_first_crash)."""
+    kk = (C.c_uint32 * 2)(*[int(x) & 0xFFFFFFFF for x in key])
+    return int(lib().or_first_crash(kk, trial, u, t, k, ones))
 
 
 def philox(ctr, key):

@@ -137,6 +137,40 @@ def test_crash_on_first_receipt(oracle):
     assert st[-1, 4] == 0 and st[-1, 5] == 2 and st[:, 3].sum() == 2
 
 
+def test_first_crash_restates_the_sequential_draws(oracle):
+    """or_first_crash: draws U_(k-g+1)(lane (g-1)%4 of Philox{u, t, (g-1)/4,
+    ORDER << 24 | trial}) < ones, g = 1, 2, ...; position 1 without a draw
+    when k == 1 or every receipt carries a roll."""
+    key = [0x1234, 0x5678]
+    for (u, t, k, ones) in [(3, 17, 5, 2), (99, 4, 7, 1), (12, 250, 19, 5), (0, 1, 3, 2)]:
+        g = 1
+        while True:
+            r = oracle.philox([u, t, (g - 1) // 4, (10 << 24) | 7], key)[(g - 1) % 4]
+            if (r * (k - g + 1)) >> 32 < ones:
+                break
+            g += 1
+        assert oracle.first_crash(key, 7, u, t, k, ones) == g
+    assert oracle.first_crash(key, 7, 5, 5, 1, 1) == 1
+    assert oracle.first_crash(key, 7, 5, 5, 6, 6) == 1
+
+
+@pytest.mark.parametrize("k,ones", [(2, 1), (5, 2), (6, 3)])
+def test_first_crash_law_is_a_uniform_order(oracle, k, ones):
+    """The reference takes a tick's receipts in a random order and stops at the
+    first crash: P(first crash at g) = C(k-g, ones-1) / C(k, ones).  The keyed
+    draw has that law (chi-square over 40,000 (u, t) keys)."""
+    from math import comb
+    from scipy.stats import chisquare
+    key = [0x5EED, 0]
+    n = 40_000
+    obs = np.zeros(k - ones + 1)
+    for i in range(n):
+        obs[oracle.first_crash(key, 0, i, 1 + i % 97, k, ones) - 1] += 1
+    exp = np.array([comb(k - g, ones - 1) / comb(k, ones) for g in range(1, k - ones + 2)]) * n
+    assert abs(exp.sum() - n) < 1e-6
+    assert chisquare(obs, exp).pvalue > 0.001
+
+
 def test_default_crashrate_quantises_to_zero(oracle):
     deg, ids, _, _ = oracle.overlay(oracle.make_params(n=3000))
     rows, e = oracle.run_to_coverage(oracle.make_params(n=3000), deg, ids)
