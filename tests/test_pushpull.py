@@ -156,6 +156,8 @@ def test_gpu_pushpull_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac, rounds,
         if failed is not None:
             sim.set_failed(failed)
         sim.broadcast_begin(-1)
+        # the sparse rounds' reverse table is built at begin unless dense-only
+        assert (sim.timing()["prep_ms"] > 0) == (rounds != "dense")
         for r in range(60):
             a, b = e.step(1), sim.step(1)
             assert np.array_equal(a, b), f"round {r + 1}:\n{a}\n{b}"
