@@ -20,6 +20,7 @@ GS_FLAG_TICK_ENGINE = 2
 GS_FLAG_PP_L2_ONLY = 4
 GS_FLAG_PP_DENSE = 8
 GS_FLAG_PP_EARLY = 16
+GS_MODEL_FLOOD, GS_MODEL_PUSHPULL = 0, 1
 GS_RUN_COVERED, GS_RUN_QUIESCENT, GS_RUN_MAX_TICKS, GS_RUN_RUNNING = 0, 1, 2, -1
 GS_COMM_ID_BYTES = 128
 

@@ -59,7 +59,7 @@ class Config:
         p.seed, p.trial, p.device = self.seed, self.trial, self.device
         if self.model not in ("flood", "pushpull"):
             raise ValueError(f"model must be 'flood' or 'pushpull', not {self.model!r}")
-        p.model = 1 if self.model == "pushpull" else 0
+        p.model = _lib.GS_MODEL_PUSHPULL if self.model == "pushpull" else _lib.GS_MODEL_FLOOD
         p.flags = self.flags()
         p.trials = max(1, int(self.trials))
         return p

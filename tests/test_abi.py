@@ -34,6 +34,21 @@ def test_exports_every_declared_symbol(L):
     assert lib.gs_version() == 3
 
 
+def test_header_constants_match_binding(L):
+    """Every #define GS_* / enum GS_* value in include/gossip.h equals the
+    ctypes binding's constant of the same name."""
+    with open(os.path.join(ROOT, "include", "gossip.h")) as f:
+        src = f.read()
+    defs = dict((k, int(v)) for k, v in re.findall(r"#define (GS_[A-Z0-9_]+) (\d+)u?\b", src))
+    defs.update((k, int(v)) for k, v in re.findall(r"\b(GS_[A-Z0-9_]+) = (-?\d+)", src))
+    assert len(defs) >= 15
+    missing = [k for k in defs if not hasattr(L, k)]
+    assert not [k for k in missing if k.startswith("GS_FLAG_") or k.startswith("GS_MODEL_")], missing
+    for k, v in defs.items():
+        if hasattr(L, k):
+            assert getattr(L, k) == v, (k, getattr(L, k), v)
+
+
 def test_struct_sizes_match_header(L):
     import ctypes as C
     assert C.sizeof(L.Params) == 8 + 4 * 4 + 8 + 8 + 8 + 4 + 4 + 4 + 4 + 8 + 8 + 4 * 8
