@@ -100,7 +100,8 @@ struct gs_ctx {
   uint32_t G = 1, rank = 0;
   uint64_t lo = 0, hi = 0, seg_per = 0;
   uint32_t* d_prow = nullptr;           // [n + 1] partitioned row starts
-  uint32_t* d_pent = nullptr;           // owned slots: (target - lo) << 5 | j
+  uint32_t* d_pent = nullptr;           // owned slots: (target - lo) << 5 | j, [n][pw]
+  uint32_t pw = 0;                      // partitioned row width
   Buf gfire;                            // multi-process: this rank's all-gather buffer
   unsigned long long* d_gcounts = nullptr;  // multi-process: [G][16] gathered fires per tick
   ncclComm_t comm = nullptr;
@@ -254,6 +255,7 @@ void refresh_window(gs_ctx* c) {
   w.stride_magic = c->st.stride_magic;
   w.prow = c->d_prow;
   w.pent = c->d_pent;
+  w.pw = c->pw;
 }
 
 uint32_t ring_slots(const gs_params& p) { return p.delay_high > 2 ? (uint32_t)p.delay_high : 2u; }
@@ -367,46 +369,40 @@ int seal_rows(gs_ctx* c, const uint8_t* deg, uint32_t* ids, uint64_t n) {
   return GS_OK;
 }
 
-// Shard c's partition of the sealed global table (ids, on c's device).
+// Shard c's partition of the sealed global table (ids, on c's device):
+// fixed-width rows of pw = (the most owned slots any node has, rounded up to
+// 4) entries, so k_expand_sh reads a firing node's owned slots with one
+// dependent load (no row index).
 int partition(gs_ctx* c, const uint32_t* ids) {
   const uint64_t n = c->p.n;
   if (c->d_prow) (void)hipFree(c->d_prow);
   if (c->d_pent) (void)hipFree(c->d_pent);
   c->d_prow = nullptr;
   c->d_pent = nullptr;
+  c->pw = 0;
   uint32_t* cnt = nullptr;
-  unsigned long long* off = nullptr;
-  void* tmp = nullptr;
-  size_t tb = 0;
   int rc = GS_OK;
-  unsigned long long total = 0;
-  uint32_t e = 0;
+  uint32_t mx = 0;
   auto bail = [&](int code, const std::string& m) { rc = fail(c, code, m); };
-  if (hipMalloc(&cnt, (n + 1) * 4) != hipSuccess || hipMalloc(&off, (n + 1) * 8) != hipSuccess ||
-      hipMalloc(&c->d_prow, (n + 1) * 4) != hipSuccess) {
-    bail(GS_ENOMEM, "cannot allocate the shard's row index");
+  if (hipMalloc(&cnt, (n + 1) * 4) != hipSuccess) {
+    bail(GS_ENOMEM, "cannot allocate the shard's slot counts");
   } else if (hipMemsetAsync(cnt + n, 0, 4, c->stream) != hipSuccess ||
              part_count(ids, n, c->st.stride, (uint32_t)c->lo, (uint32_t)c->hi, cnt, c->stream) != hipSuccess ||
-             part_scan(cnt, n, off, nullptr, tb, c->stream) != hipSuccess || hipMalloc(&tmp, tb) != hipSuccess ||
-             part_scan(cnt, n, off, tmp, tb, c->stream) != hipSuccess ||
-             hipMemsetAsync(c->d_err, 0, 4, c->stream) != hipSuccess ||
-             part_narrow(off, n, c->d_prow, c->d_err, c->stream) != hipSuccess ||
-             hipMemcpyAsync(&total, off + n, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-             hipMemcpyAsync(&e, c->d_err, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+             part_max(cnt, n, cnt + n, c->stream) != hipSuccess ||
+             hipMemcpyAsync(&mx, cnt + n, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
              hipStreamSynchronize(c->stream) != hipSuccess) {
-    bail(GS_EDEVICE, "building the shard's row index failed");
-  } else if (e) {
-    bail(GS_EINVAL, "a shard holds 2^32 or more friend slots: use more shards");
-  } else if (hipMalloc(&c->d_pent, std::max<unsigned long long>(total, 1) * 4) != hipSuccess) {
-    bail(GS_ENOMEM, "cannot allocate " + std::to_string(total) + " partitioned friend slots");
-  } else if (part_fill(ids, n, c->st.stride, (uint32_t)c->lo, (uint32_t)c->hi, c->d_prow, c->d_pent,
-                       c->stream) != hipSuccess ||
-             hipStreamSynchronize(c->stream) != hipSuccess) {
-    bail(GS_EDEVICE, "filling the shard's partition failed");
+    bail(GS_EDEVICE, "counting the shard's slots failed");
+  } else {
+    c->pw = std::max<uint32_t>(4, (mx + 3) & ~3u);
+    if (hipMalloc(&c->d_pent, n * c->pw * 4ull) != hipSuccess) {
+      bail(GS_ENOMEM, "cannot allocate " + std::to_string(n * c->pw) + " partitioned friend slots");
+    } else if (part_fill_fixed(ids, n, c->st.stride, (uint32_t)c->lo, (uint32_t)c->hi, c->pw, c->d_pent,
+                               c->stream) != hipSuccess ||
+               hipStreamSynchronize(c->stream) != hipSuccess) {
+      bail(GS_EDEVICE, "filling the shard's partition failed");
+    }
   }
   if (cnt) (void)hipFree(cnt);
-  if (off) (void)hipFree(off);
-  if (tmp) (void)hipFree(tmp);
   refresh_window(c);
   return rc;
 }
@@ -468,7 +464,7 @@ int ctx_setup(gs_ctx* c, const gs_params* params, int device, bool shard, uint32
             " shards of whole 16384-node buckets";
       return GS_EINVAL;
     }
-    if (c->seg_per > (1ull << 27)) { why = "a shard may own at most 2^27 nodes: use more shards"; return GS_EINVAL; }
+    if (c->seg_per >= (1ull << 27)) { why = "a shard may own fewer than 2^27 nodes: use more shards"; return GS_EINVAL; }
     c->lo = rank * c->seg_per;
     c->hi = std::min<uint64_t>(c->lo + c->seg_per, c->p.n);
     c->ntot = c->hi - c->lo;

@@ -141,8 +141,9 @@ struct WinState {
   uint32_t slots;                // longest row in use (<= stride: rows may be padded for 16-B loads)
   // node-range shard: partitioned friend rows (prow[v]..prow[v+1] of pent, entry =
   // (target - base) << 5 | slot j) and the all-gathered window fire list
-  const uint32_t* prow;
-  const uint32_t* pent;
+  const uint32_t* prow;          // (unused: rows are fixed-width, see pw)
+  const uint32_t* pent;          // [n][pw] owned slots (target - lo) << 5 | j, ~0u-padded
+  uint32_t pw;                   // partitioned row width (a multiple of 4)
   const uint32_t* gfire;         // [G][gseg] entries local_id << 4 | k, ~0u = padding
   uint64_t gseg;                 // entries per shard segment of gfire
   uint32_t G, rank;              // shards, this shard's index
@@ -202,6 +203,11 @@ hipError_t part_scan(const uint32_t* cnt, uint64_t n, unsigned long long* off, v
 hipError_t part_narrow(const unsigned long long* off, uint64_t n, uint32_t* prow, uint32_t* err, hipStream_t s);
 hipError_t part_fill(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
                      const uint32_t* prow, uint32_t* pent, hipStream_t s);
+// Fixed-width partition: *max_out = max over v of cnt[v]; then pent[v * pw ..]
+// = v's owned slots in slot order, ~0u-padded to pw.
+hipError_t part_max(const uint32_t* cnt, uint64_t n, uint32_t* max_out, hipStream_t s);
+hipError_t part_fill_fixed(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi, uint32_t pw,
+                           uint32_t* pent, hipStream_t s);
 hipError_t win_fire_compact(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, uint32_t* out,
                             uint64_t seg, hipStream_t s);
 hipError_t win_expand_sh(const WinState& w, uint32_t t0, uint32_t L, int mode, hipStream_t s);

@@ -1347,6 +1347,31 @@ __global__ void k_part_fill(const uint32_t* ids, uint64_t n, uint32_t stride, ui
   }
 }
 
+__global__ void k_part_max(const uint32_t* cnt, uint64_t n, uint32_t* max_out) {
+  uint32_t m = 0;
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x)
+    m = max(m, cnt[v]);
+#pragma unroll
+  for (uint32_t o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(max_out, m);
+}
+
+// pent[v * pw ..] = (target - lo) << 5 | j for the owned slots of v, in slot
+// order, then ~0u (shards hold < 2^27 nodes, so no entry is ~0u).
+__global__ void k_part_fill_fixed(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
+                                  uint32_t pw, uint32_t* pent) {
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
+       v += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t* row = pent + v * pw;
+    uint32_t pos = 0;
+    for (uint32_t j = 0; j < stride; ++j) {
+      const uint32_t x = ids[v * stride + j];
+      if (x >= lo && x < hi) row[pos++] = ((x - lo) << 5) | j;
+    }
+    for (; pos < pw; ++pos) row[pos] = ~0u;
+  }
+}
+
 // This shard's fires of the window as entries local_id << 4 | k at out[0, Tn),
 // out[Tn, seg) = ~0u (the all-gather moves seg entries per shard).
 __global__ void k_fire_compact(const WinState w, uint32_t t0, uint32_t L, unsigned long long Tn,
@@ -1403,11 +1428,18 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand_sh(const WinState w, ui
         v = r * w.seg_per + (e >> 4);
         k = e & 15;
         own = r == w.rank;
-        const uint32_t a = w.prow[v];
-        c = w.prow[v + 1] - a;
+        // fixed-width partitioned row: one dependent load, no row index
+        const uint4* pr = reinterpret_cast<const uint4*>(w.pent + (size_t)v * w.pw);
 #pragma unroll
-        for (uint32_t j = 0; j < MAXS; ++j)
-          if (j < c) mm[j] = w.pent[a + j];
+        for (uint32_t j = 0; j < MAXS; j += 4) {
+          const uint4 x = j < w.pw ? pr[j / 4] : make_uint4(~0u, ~0u, ~0u, ~0u);
+          mm[j] = x.x;
+          if (j + 1 < MAXS) mm[j + 1] = x.y;
+          if (j + 2 < MAXS) mm[j + 2] = x.z;
+          if (j + 3 < MAXS) mm[j + 3] = x.w;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < MAXS; ++j) c += mm[j] != ~0u ? 1u : 0u;  // owned slots come first
       }
     }
     uint32_t sent = 0;
@@ -1662,6 +1694,19 @@ hipError_t part_narrow(const unsigned long long* off, uint64_t n, uint32_t* prow
   return hipGetLastError();
 }
 
+hipError_t part_max(const uint32_t* cnt, uint64_t n, uint32_t* max_out, hipStream_t s) {
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_part_max, dim3(blocks ? blocks : 1), dim3(256), 0, s, cnt, n, max_out);
+  return hipGetLastError();
+}
+
+hipError_t part_fill_fixed(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi, uint32_t pw,
+                           uint32_t* pent, hipStream_t s) {
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_part_fill_fixed, dim3(blocks ? blocks : 1), dim3(256), 0, s, ids, n, stride, lo, hi, pw, pent);
+  return hipGetLastError();
+}
+
 hipError_t part_fill(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
                      const uint32_t* prow, uint32_t* pent, hipStream_t s) {
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
@@ -1683,7 +1728,7 @@ hipError_t win_expand_sh(const WinState& w, uint32_t t0, uint32_t L, int mode, h
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((total + kExpandBlock - 1) / kExpandBlock, 8192);
   const dim3 grid(blocks ? blocks : 1), blk(kExpandBlock);
   const int st = mode == 1 ? 1 : 0;
-  if (w.stride <= 8) {
+  if (w.pw <= 8) {
     if (mode) hipLaunchKernelGGL((k_expand_sh<true, 8>), grid, blk, 0, s, w, t0, L, st);
     else hipLaunchKernelGGL((k_expand_sh<false, 8>), grid, blk, 0, s, w, t0, L, 0);
   } else {
