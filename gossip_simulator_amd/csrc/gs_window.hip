@@ -92,16 +92,36 @@ __global__ void k_units(const WinState w, uint32_t t0, uint32_t L) {
   }
   const uint32_t units = Ls * w.nfine;
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+  // 256-bucket tiles: the L fcount rows are read coalesced (bucket fastest),
+  // transposed in LDS and written bucket-major, coalesced.
+  __shared__ uint32_t s_tile[256 * (kMaxWindow + 1)];
+  uint32_t acc[kMaxWindow];
+#pragma unroll
+  for (uint32_t k = 0; k < kMaxWindow; ++k) acc[k] = 0;
   if (threadIdx.x < kMaxWindow) s_t[threadIdx.x] = 0;
+  if (tid == 0) w.usize[units] = 0;
   __syncthreads();
-  for (uint32_t u = tid; u <= units; u += nth) {
-    if (u == units) { w.usize[u] = 0; continue; }
-    const uint32_t f = u / Ls, k = u - f * Ls;
-    uint32_t c = 0;
-    if (k < L) c = w.fcount[(size_t)((t0 + k) % w.R) * w.nfine + f];
-    w.usize[u] = c;
-    if (c) atomicAdd(&s_t[k], c);
+  for (uint32_t f0 = blockIdx.x * 256; f0 < w.nfine; f0 += gridDim.x * 256) {
+    const uint32_t f = f0 + threadIdx.x;
+#pragma unroll
+    for (uint32_t k = 0; k < kMaxWindow; ++k) {
+      if (k >= Ls) break;
+      uint32_t c = 0;
+      if (k < L && f < w.nfine) c = w.fcount[(size_t)((t0 + k) % w.R) * w.nfine + f];
+      s_tile[threadIdx.x * (kMaxWindow + 1) + k] = c;
+      acc[k] += c;
+    }
+    __syncthreads();
+    const uint32_t nb = min(256u, w.nfine - f0), base = f0 * Ls;
+    for (uint32_t i = threadIdx.x; i < nb * Ls; i += 256) {
+      const uint32_t b = i / Ls, k = i - b * Ls;
+      w.usize[base + i] = s_tile[b * (kMaxWindow + 1) + k];
+    }
+    __syncthreads();
   }
+#pragma unroll
+  for (uint32_t k = 0; k < kMaxWindow; ++k)
+    if (acc[k]) atomicAdd(&s_t[k], acc[k]);
   __syncthreads();
   if (threadIdx.x < L && s_t[threadIdx.x]) atomicAdd(&w.tfires[threadIdx.x], (unsigned long long)s_t[threadIdx.x]);
   for (uint32_t i = tid; i < kRegions; i += nth) { w.chist[i] = 0; w.cfill[i] = 0; }
@@ -1538,8 +1558,8 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand_sh(const WinState w, ui
 }  // namespace
 
 hipError_t win_units(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s) {
-  const uint32_t units = std::max<uint32_t>(L * w.nfine + 1, w.nfine);
-  const uint32_t blocks = std::min<uint32_t>((units + 255) / 256, 4096);
+  (void)L;
+  const uint32_t blocks = std::max<uint32_t>(std::min<uint32_t>((w.nfine + 255) / 256, 4096), 1);
   hipLaunchKernelGGL(k_units, dim3(blocks), dim3(256), 0, s, w, t0, L);
   return hipGetLastError();
 }
