@@ -1176,6 +1176,18 @@ uint32_t pp_shift() {
   return (uint32_t)std::min(std::max(v, 0), 63);
 }
 
+// Dense rounds run bottom-up once |I| >= n * GS_PP_BOTTOM256 / 256 (default
+// 96), when the reverse table has packed slots and the failed mask (if any)
+// has fmask.
+unsigned long long pp_bottom_thr(const gs_ctx* c) {
+  const bool can = c->sp.ctl && pp_rslot_packed(c->st.stride) && (!c->failed || c->sp.fmask);
+  if (!can || (c->p.flags & GS_FLAG_PP_TOPDOWN)) return ~0ull;
+  if (c->p.flags & GS_FLAG_PP_BOTTOM) return 0;
+  const char* e = getenv("GS_PP_BOTTOM256");
+  const unsigned long long k = (unsigned long long)std::min(std::max(e ? atoi(e) : 96, 0), 256);
+  return k == 256 ? ~0ull : (unsigned long long)(((unsigned __int128)c->st.n * k) >> 8);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1200,7 +1212,7 @@ int gs_broadcast_begin(gs_ctx* c, int64_t sender) {
     RC(pp_prepare(c));
     const uint64_t n = c->st.n;
     const unsigned long long thr = (c->p.flags & GS_FLAG_PP_EARLY) ? n : (n >> pp_shift());
-    CK(c, pp_seed(c->st, c->d_next, (uint32_t)s, c->d_flag, c->sp, thr, c->stream));
+    CK(c, pp_seed(c->st, c->d_next, (uint32_t)s, c->d_flag, c->sp, thr, pp_bottom_thr(c), c->stream));
     uint32_t ok = 0;
     CK(c, hipMemcpyAsync(&ok, c->d_flag, 4, hipMemcpyDeviceToHost, c->stream));
     CK(c, hipStreamSynchronize(c->stream));
@@ -2164,6 +2176,15 @@ int gs_timing_get(gs_ctx* c, gs_timing* out) {
   if (!c || !out) return GS_EINVAL;
   *out = c->group ? c->mem[0]->timing : c->timing;  // a group: its first member's kernels
   if (c->group) out->overlay_ms = c->timing.overlay_ms;
+  out->pp_early_rounds = out->pp_bottom_rounds = 0;
+  if (c->pp && c->sp.ctl && c->begun) {
+    CK(c, hipSetDevice(c->dev));
+    PPCtl h;
+    CK(c, hipMemcpyAsync(&h, c->sp.ctl, offsetof(PPCtl, segcnt), hipMemcpyDeviceToHost, c->stream));
+    CK(c, hipStreamSynchronize(c->stream));
+    out->pp_early_rounds = h.nearly;
+    out->pp_bottom_rounds = h.nbottom;
+  }
   return GS_OK;
 }
 

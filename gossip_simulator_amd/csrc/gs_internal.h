@@ -230,7 +230,19 @@ inline uint64_t pp_summary_total_words(uint64_t W) { return 2 * pp_summary_words
 // (reverse table: in-edges (v, j) with ids[v*stride + j] = u, of node u at
 // [u ? rend[u-1] : 0, rend[u])).  The round's mode is decided on the device
 // (k_pp_mode) from PPCtl, so rounds stay queued without host syncs.
-enum PPMode : uint32_t { PP_DENSE = 0, PP_EARLY = 1 };
+// Dense rounds come in two directions.  Top-down (PP_DENSE, k_pp_round):
+// every informed caller's push is an atomicOr into its friend's word.
+// Bottom-up (PP_BOTTOM, k_ppb_round), once ninf > bthr: an uninformed live
+// node u finds the pushes it receives among its in-edges (v, j) -- v's keyed
+// pick is slot j, the call is kept and v is informed -- so the round issues no
+// global atomic and an informed caller reads no friend id at all.  Once
+// ninf >= bthr (dense rounds only: the early test comes first).  Needs the
+// reverse table with packed slots (stride <= 16) and, with a failure mask,
+// fmask (stride <= 8).
+enum PPMode : uint32_t { PP_DENSE = 0, PP_EARLY = 1, PP_BOTTOM = 2 };
+// rslot entries: slot j in bits 0..3 and deg(v) - 1 in bits 4..7 when
+// stride <= 16 (the caller's pick needs no deg[v] gather), else j alone.
+__host__ __device__ inline bool pp_rslot_packed(uint32_t stride) { return stride <= 16; }
 // The informed list is kPPSegs segments of seg_cap entries; workgroup b
 // appends to segment b % nseg (one counter per segment: a single append
 // counter saturated at ~1e8 atomics/s).  A full segment sets ovf: the round
@@ -239,12 +251,14 @@ constexpr uint32_t kPPSegs = 256;
 struct PPCtl {
   unsigned long long ninf;      // |I|: informed nodes (all modes)
   unsigned long long thr;       // early rounds while ninf <= thr
+  unsigned long long bthr;      // dense rounds bottom-up once ninf >= bthr (0: always, ~0: never)
   unsigned long long ncallers;  // live nodes with a non-empty row: calls per round
   unsigned long long seg_cap;   // entries per segment
   uint32_t nseg;                // segments in use (<= kPPSegs)
   uint32_t mode;                // PPMode of the current round
   uint32_t early_ok;            // the informed list is complete (never re-entered)
   uint32_t ovf;                 // a segment overflowed this round
+  uint32_t nearly, nbottom;     // rounds run sparse / bottom-up since the broadcast began (gs_timing)
   unsigned long long segcnt[kPPSegs];      // entries in segment s (incl. this round's appends)
   unsigned long long seglen[kPPSegs];      // entries at the start of this round
   unsigned long long segpre[kPPSegs + 1];  // prefix of seglen: list index -> segment
@@ -265,7 +279,7 @@ hipError_t pp_commit(const DevState& s, const unsigned long long* next, uint32_t
 // Sender informed unless failed; flag = 1 if informed.  Also initialises ctl
 // (counts live callers: a pass over deg and the failed mask).
 hipError_t pp_seed(const DevState& s, unsigned long long* next, uint32_t node, uint32_t* flag,
-                   const PPSparse& sp, unsigned long long thr, hipStream_t st);
+                   const PPSparse& sp, unsigned long long thr, unsigned long long bthr, hipStream_t st);
 // Reverse table: rend must hold n + 1 words of scratch-free u64 space; tmp /
 // tmp_bytes the hipcub scan workspace (pp_rev_scan_bytes).
 size_t pp_rev_scan_bytes(uint64_t n);

@@ -199,11 +199,158 @@ __global__ __launch_bounds__(kPPRoundBlock) void k_pp_round(const DevState s,
   block_add<kPPRoundBlock>(sh, v3, 3, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
 }
 
+// Bottom-up dense round (PPMode PP_BOTTOM, gs_internal.h).  Same draws,
+// outcomes and counters as k_pp_round.  A wave owns ranges of kPPRange words
+// (4096 nodes) and streams them a lane per node: an informed caller counts
+// its push (sent; msgs unless fmask marks the picked friend failed) and reads
+// nothing else; an uninformed live node joins the wave's LDS queue.  Each 64
+// queued nodes are resolved together, a lane each: the pull (friend id + the
+// friend's recv word) and the push receipts, found among the node's in-edges
+// (v, j) -- v's pick is recomputed from the packed slot byte (no deg gather),
+// and only a kept pick of slot j costs a gather of v's recv word.  So the
+// dependent-load chain runs for full waves of uninformed nodes however few
+// are left, and the range's newly informed gather in LDS and are stored, not
+// OR'ed (the wave owns its words).
+constexpr uint32_t kPPB = 4;        // words loaded together while streaming
+constexpr uint32_t kPPRange = 64;   // words per wave range (multiple of kPPB)
+constexpr uint32_t kPPQ = 128;      // queue entries per wave (<= 63 left + 64 appended)
+constexpr uint32_t kPPEdges = 4;    // in-edges loaded per batch
+constexpr uint32_t kPPWaves = kPPRoundBlock / 64;
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Resolves queue entries [0, cnt) (cnt <= 64), one per lane.  Entry = node
+// offset in the range (12 bits) | deg << 16.
+__device__ __forceinline__ void ppb_resolve(const DevState& s, const PPSparse& sp, uint32_t t, uint32_t c3,
+                                            const uint32_t* q, uint32_t cnt, uint64_t base,
+                                            unsigned long long* nb, uint64_t& sent, uint64_t& msgs) {
+  const uint32_t lane = threadIdx.x & 63;
+  if (lane >= cnt) return;
+  const uint32_t e = q[lane], loc = e & 0xFFFu, d = e >> 16;
+  const uint64_t v = base + loc;
+  const unsigned long long qb = v ? sp.rend[v - 1] : 0ull, qe = sp.rend[v];
+  bool pull = false;
+  uint32_t u = 0;
+  if (d > 0) {
+    const u32x4 r = philox((uint32_t)v, t, 0, c3, s.key.k0, s.key.k1);
+    if ((int32_t)uniform(r.y, 100u) >= s.kd) {
+      u = s.ids[v * s.stride + uniform(r.x, d)];
+      pull = true;
+    }
+  }
+  const unsigned long long Iu = pull ? s.recv[u >> 6] : 0ull;
+  bool got = false;
+  for (unsigned long long q0 = qb; q0 < qe && !got; q0 += kPPEdges) {
+    uint32_t src[kPPEdges], x[kPPEdges];
+#pragma unroll
+    for (uint32_t k = 0; k < kPPEdges; ++k) {
+      const bool in = q0 + k < qe;
+      src[k] = in ? sp.rsrc[q0 + k] : 0u;
+      x[k] = in ? sp.rslot[q0 + k] : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kPPEdges; ++k) {
+      if (q0 + k >= qe) break;
+      const u32x4 r = philox(src[k], t, 0, c3, s.key.k0, s.key.k1);
+      if (uniform(r.x, (x[k] >> 4) + 1) == (x[k] & 15u) && (int32_t)uniform(r.y, 100u) >= s.kd)
+        got |= ((s.recv[src[k] >> 6] >> (src[k] & 63)) & 1) != 0;
+    }
+  }
+  const bool pulled = pull && ((Iu >> (u & 63)) & 1);  // u informed => u live
+  if (pulled) {
+    ++sent;
+    ++msgs;
+  }
+  if (pulled || got) atomicOr(&nb[loc >> 6], 1ull << (loc & 63));
+}
+
+__global__ __launch_bounds__(kPPRoundBlock) void k_ppb_round(const DevState s, unsigned long long* __restrict__ next,
+                                                             const PPSparse sp, uint32_t t) {
+  __shared__ uint64_t sh[3 * kPPWaves];
+  __shared__ uint32_t s_q[kPPWaves][kPPQ];
+  __shared__ unsigned long long s_nb[kPPWaves][kPPRange];
+  if (sp.ctl->mode != PP_BOTTOM) return;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t* q = s_q[wv];
+  unsigned long long* nb = s_nb[wv];
+  const uint32_t c3 = ctr3(K_PUSHPULL, s.key.trial);
+  const uint8_t* __restrict__ fmask = sp.fmask;
+  uint64_t fired = 0, sent = 0, msgs = 0;
+  const uint64_t W = (s.n + 63) >> 6;
+  const uint64_t nrange = (W + kPPRange - 1) / kPPRange;
+  for (uint64_t rg = (uint64_t)blockIdx.x * kPPWaves + wv; rg < nrange; rg += (uint64_t)gridDim.x * kPPWaves) {
+    const uint64_t w0 = rg * kPPRange, base = w0 << 6;
+    nb[lane] = 0;
+    uint32_t qn = 0;  // wave-uniform
+    for (uint32_t wi = 0; wi < kPPRange; wi += kPPB) {
+      unsigned long long Iw[kPPB];
+      uint32_t d[kPPB], fm[kPPB];
+      bool live[kPPB];
+#pragma unroll
+      for (uint32_t i = 0; i < kPPB; ++i) {
+        const uint64_t word = w0 + wi + i, v = (word << 6) + lane;
+        const bool inb = word < W;
+        Iw[i] = inb ? s.recv[word] : ~0ull;
+        const unsigned long long Fw = inb ? s.crash[word] : ~0ull;
+        live[i] = v < s.n && !((Fw >> lane) & 1);
+        d[i] = live[i] ? s.deg[v] : 0u;
+        fm[i] = fmask && live[i] ? fmask[v] : 0u;
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < kPPB; ++i) {
+        const uint64_t v = ((w0 + wi + i) << 6) + lane;
+        const bool inf = (Iw[i] >> lane) & 1;
+        if (d[i] > 0) {
+          ++fired;
+          if (inf) {  // push: the receiver finds it
+            const u32x4 r = philox((uint32_t)v, t, 0, c3, s.key.k0, s.key.k1);
+            if ((int32_t)uniform(r.y, 100u) >= s.kd) {
+              ++sent;
+              if (!((fm[i] >> uniform(r.x, d[i])) & 1)) ++msgs;
+            }
+          }
+        }
+        const bool enq = live[i] && !inf;
+        const unsigned long long bal = __ballot(enq);
+        if (enq) {
+          const uint32_t at = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          q[at] = (uint32_t)(v - base) | d[i] << 16;
+        }
+        qn += (uint32_t)__popcll(bal);
+        if (qn >= 64) {
+          wave_lds_sync();
+          ppb_resolve(s, sp, t, c3, q, 64, base, nb, sent, msgs);
+          const uint32_t rest = qn - 64;
+          const uint32_t keep = lane < rest ? q[64 + lane] : 0u;
+          wave_lds_sync();
+          if (lane < rest) q[lane] = keep;
+          qn = rest;
+        }
+      }
+    }
+    wave_lds_sync();
+    if (qn) ppb_resolve(s, sp, t, c3, q, qn, base, nb, sent, msgs);
+    wave_lds_sync();
+    const uint64_t word = w0 + lane;
+    const unsigned long long x = nb[lane];
+    if (x && word < W) next[word] = s.recv[word] | x;
+    wave_lds_sync();  // nb and q are reused by the next range
+  }
+  const uint64_t v3[3] = {fired, sent, msgs};
+  const uint32_t f3[3] = {ST_FIRED, ST_SENT, ST_MSGS};
+  block_add<kPPRoundBlock>(sh, v3, 3, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
+}
+
 __global__ __launch_bounds__(kPPBlock) void k_pp_commit(const DevState s,
                                                         const unsigned long long* __restrict__ next,
                                                         uint32_t t, PPCtl* ctl) {
   __shared__ uint64_t sh[kPPBlock / 64];
-  if (ctl && ctl->mode != PP_DENSE) return;
+  if (ctl && ctl->mode == PP_EARLY) return;
   uint64_t newly = 0;
   for (uint64_t w = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; w < s.W;
        w += (uint64_t)gridDim.x * kPPBlock) {
@@ -247,7 +394,9 @@ __global__ __launch_bounds__(kPPSegs) void k_pp_mode(PPCtl* c) {
     }
     c->segpre[c->nseg] = a;
     const bool early = ok && c->ninf <= c->thr;
-    c->mode = early ? PP_EARLY : PP_DENSE;
+    c->mode = early ? PP_EARLY : c->ninf >= c->bthr ? PP_BOTTOM : PP_DENSE;
+    c->nearly += c->mode == PP_EARLY;
+    c->nbottom += c->mode == PP_BOTTOM;
     if (!early) c->early_ok = 0;  // |I| only grows: the list is never needed again
     (void)was_early;
   }
@@ -289,7 +438,7 @@ __global__ __launch_bounds__(kPPBlock) void k_ppe_round(const DevState s, unsign
   const unsigned long long nl = pre[nseg];
   const uint32_t myseg = blockIdx.x % nseg;
   const uint32_t c3 = ctr3(K_PUSHPULL, s.key.trial);
-  const bool cc = s.check_crashed;
+  const bool cc = s.check_crashed, packed = pp_rslot_packed(s.stride);
   uint64_t sent = 0, msgs = 0;
   const uint64_t G = (uint64_t)gridDim.x * kPPBlock;
   const uint64_t nlr = (nl + 63) & ~63ull;  // whole waves iterate together (pp_append)
@@ -329,13 +478,14 @@ __global__ __launch_bounds__(kPPBlock) void k_ppe_round(const DevState s, unsign
       uint32_t v = 0;
       if (q < e) {
         v = sp.rsrc[q];
-        const uint32_t j = sp.rslot[q];
+        const uint32_t x = sp.rslot[q];
+        const uint32_t j = packed ? x & 15u : x;
         ++q;
         const unsigned long long vb = 1ull << (v & 63);
         // v informed: its own list entry pushes; v failed: never calls
         if (!(s.recv[v >> 6] & vb) && !(cc && (s.crash[v >> 6] & vb))) {
           const u32x4 r = philox(v, t, 0, c3, s.key.k0, s.key.k1);
-          if (uniform(r.x, s.deg[v]) == j && (int32_t)uniform(r.y, 100u) >= s.kd) {
+          if (uniform(r.x, packed ? (x >> 4) + 1 : s.deg[v]) == j && (int32_t)uniform(r.y, 100u) >= s.kd) {
             ++sent;
             ++msgs;
             tk = !(atomicOr(&next[v >> 6], vb) & vb);
@@ -415,7 +565,7 @@ __global__ __launch_bounds__(kPPBlock) void k_rev_fill(const DevState s, unsigne
     for (uint32_t j = 0; j < d; ++j) {
       const unsigned long long at = atomicAdd(&rend[s.ids[v * s.stride + j]], 1ull);
       rsrc[at] = (uint32_t)v;
-      rslot[at] = (uint8_t)j;
+      rslot[at] = (uint8_t)(pp_rslot_packed(s.stride) ? j | (d - 1) << 4 : j);
     }
   }
 }
@@ -427,7 +577,7 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_fmask(const DevState s, const u
     if (!((s.crash[f >> 6] >> (f & 63)) & 1)) continue;
     for (unsigned long long q = f ? rend[f - 1] : 0ull; q < rend[f]; ++q) {
       const uint32_t v = rsrc[q];
-      atomicOr(&fm4[v >> 2], (1u << rslot[q]) << (8 * (v & 3)));
+      atomicOr(&fm4[v >> 2], (1u << (rslot[q] & 15u)) << (8 * (v & 3)));  // stride <= 8: packed
     }
   }
 }
@@ -459,7 +609,7 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_live_edges(const DevState s, ui
 // failed; flag[0] = 1 if it was informed.  ctl (zeroed, ncallers counted):
 // the informed list starts as the sender.
 __global__ void k_pp_seed(const DevState s, unsigned long long* next, uint32_t node, uint32_t* flag, PPSparse sp,
-                          unsigned long long thr) {
+                          unsigned long long thr, unsigned long long bthr) {
   const unsigned long long bit = 1ull << (node & 63);
   const bool ok = !(s.crash[node >> 6] & bit);
   if (ok) {
@@ -471,6 +621,7 @@ __global__ void k_pp_seed(const DevState s, unsigned long long* next, uint32_t n
     PPCtl* c = sp.ctl;
     c->ninf = ok ? 1 : 0;
     c->thr = thr;
+    c->bthr = bthr;
     c->nseg = (uint32_t)(s.n >> 12 < kPPSegs ? (s.n >> 12 ? s.n >> 12 : 1) : kPPSegs);
     c->seg_cap = (s.n + c->nseg - 1) / c->nseg;
     c->mode = PP_DENSE;
@@ -507,6 +658,11 @@ hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long l
       (uint32_t)std::min<uint64_t>((groups + kPPRoundBlock / 64 - 1) / (kPPRoundBlock / 64), 512);
   hipLaunchKernelGGL(k_pp_round, dim3(blocks), dim3(kPPRoundBlock), (size_t)2 * S2l * 8, st, s, next, sumA,
                      sumB, sum2, S2l, t, (const PPCtl*)sp.ctl, sp.fmask);
+  if (sp.ctl) {  // no-op unless the round is bottom-up
+    const uint64_t nrange = (s.W + kPPRange - 1) / kPPRange;
+    const uint32_t bblocks = (uint32_t)std::min<uint64_t>((nrange + kPPWaves - 1) / kPPWaves, 512);
+    hipLaunchKernelGGL(k_ppb_round, dim3(bblocks), dim3(kPPRoundBlock), 0, st, s, next, sp, t);
+  }
   return hipGetLastError();
 }
 
@@ -527,14 +683,14 @@ hipError_t pp_live_edges(const DevState& s, uint32_t* out, hipStream_t st) {
 }
 
 hipError_t pp_seed(const DevState& s, unsigned long long* next, uint32_t node, uint32_t* flag,
-                   const PPSparse& sp, unsigned long long thr, hipStream_t st) {
+                   const PPSparse& sp, unsigned long long thr, unsigned long long bthr, hipStream_t st) {
   if (sp.ctl) {
     hipError_t e = hipMemsetAsync(sp.ctl, 0, sizeof(PPCtl), st);
     if (e != hipSuccess) return e;
     const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.n + kPPBlock - 1) / kPPBlock, 4096);
     hipLaunchKernelGGL(k_pp_callers, dim3(blocks), dim3(kPPBlock), 0, st, s, sp.ctl);
   }
-  hipLaunchKernelGGL(k_pp_seed, dim3(1), dim3(1), 0, st, s, next, node, flag, sp, thr);
+  hipLaunchKernelGGL(k_pp_seed, dim3(1), dim3(1), 0, st, s, next, node, flag, sp, thr, bthr);
   return hipGetLastError();
 }
 

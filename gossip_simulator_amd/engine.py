@@ -38,18 +38,24 @@ class Config:
     model: str = "flood"    # "flood" (the reference) or "pushpull" (extension)
     trials: int = 1         # batched independent trials trial .. trial+trials-1 (config C3)
     pp_l2_only: bool = False  # push-pull: force the no-LDS summary path (tests)
-    pp_rounds: str = "auto"   # push-pull: "auto" (sparse early rounds while |I| <= n/256),
-                              # "dense" (every round streams the table), "early" (sparse at any |I|)
+    pp_rounds: str = "auto"   # push-pull: "auto" (sparse early rounds while |I| <= n/256, dense
+                              # rounds bottom-up once |I| >= 96n/256), "dense" (every round streams the
+                              # table top-down), "early" (sparse at any |I|), "topdown" (auto, but
+                              # dense rounds never bottom-up), "bottom" (every dense round bottom-up)
+
+    PP_ROUNDS = ("auto", "dense", "early", "topdown", "bottom")
 
     def flags(self, timing: bool | None = None) -> int:
-        if self.pp_rounds not in ("auto", "dense", "early"):
-            raise ValueError(f"pp_rounds must be 'auto', 'dense' or 'early', not {self.pp_rounds!r}")
+        if self.pp_rounds not in self.PP_ROUNDS:
+            raise ValueError(f"pp_rounds must be one of {self.PP_ROUNDS}, not {self.pp_rounds!r}")
         t = self.timing if timing is None else timing
         return (_lib.GS_FLAG_TIMING if t else 0) | \
             (_lib.GS_FLAG_TICK_ENGINE if self.engine == "tick" else 0) | \
             (_lib.GS_FLAG_PP_L2_ONLY if self.pp_l2_only else 0) | \
             (_lib.GS_FLAG_PP_DENSE if self.pp_rounds == "dense" else 0) | \
-            (_lib.GS_FLAG_PP_EARLY if self.pp_rounds == "early" else 0)
+            (_lib.GS_FLAG_PP_EARLY if self.pp_rounds == "early" else 0) | \
+            (_lib.GS_FLAG_PP_TOPDOWN if self.pp_rounds == "topdown" else 0) | \
+            (_lib.GS_FLAG_PP_BOTTOM if self.pp_rounds == "bottom" else 0)
 
     def to_params(self) -> Params:
         p = Params()

@@ -50,6 +50,9 @@ enum {
                                 * table, no sparse early rounds); same results, for tests */
 #define GS_FLAG_PP_EARLY 16u   /* push-pull: sparse early rounds at any informed count (default:
                                 * while |I| <= n/256); same results, for tests */
+#define GS_FLAG_PP_TOPDOWN 32u /* push-pull: dense rounds always push by atomics (default: bottom-up,
+                                * receivers scan their in-edges, once |I| >= 96n/256); same results */
+#define GS_FLAG_PP_BOTTOM 64u  /* push-pull: every dense round bottom-up; same results, for tests */
 
 /* Dissemination model (gs_params.model). */
 #define GS_MODEL_FLOOD 0u    /* the reference: every receipt re-broadcasts to all friends (simulator.go:107-149) */
@@ -117,6 +120,8 @@ typedef struct gs_timing {
   uint64_t exact_redos;    /* window engine: windows re-partitioned exactly   */
   double prep_ms;          /* push-pull: wall time of the last reverse-table / failed-slot-mask
                             * build (at gs_broadcast_begin, once per table / failure mask) */
+  uint64_t pp_early_rounds;  /* push-pull: rounds of this broadcast run sparse (informed list)   */
+  uint64_t pp_bottom_rounds; /* push-pull: dense rounds of this broadcast run bottom-up          */
 } gs_timing;
 
 /* gs_run status */

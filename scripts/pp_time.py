@@ -1,6 +1,6 @@
 """Push-pull timing probe (config C5 extension): one N-node GPU overlay, then
 timed gs_broadcast_begin + gs_run for each round mode, without and with 1 %
-failed nodes.  Usage (on the GPU box): python scripts/pp_time.py [n] [modes]"""
+failed nodes.  Usage (on the GPU box): python scripts/pp_time.py [n] [modes] [nofail|onlyfail]"""
 import os
 import sys
 import time
@@ -32,13 +32,14 @@ def run(sim):
 def main():
     n = int(float(sys.argv[1])) if len(sys.argv) > 1 else 1_000_000_000
     modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["auto", "dense"]
+    which = sys.argv[3] if len(sys.argv) > 3 else ""
     cfg = gs.Config(n=n, fanout=5, fanin=6, droprate=0.1, crashrate=0.01, seed=0x5EED, model="pushpull")
     with gs.Simulator(cfg) as sim:
         t0 = time.perf_counter()
         sim.build_overlay()
         print(f"overlay {time.perf_counter() - t0:.2f} s", flush=True)
         ref = None
-        for m in modes:
+        for m in modes if which != "onlyfail" else []:
             sim.cfg.pp_rounds = m
             sim.set_flags(False)
             run(sim)  # warmup (and the reverse-table build)
@@ -51,6 +52,8 @@ def main():
             ref = ref or key
             print(f"{m:6s} {dt * 1e3:8.1f} ms  rounds={tot['tick']} recv={tot['received']} msgs={tot['messages']} "
                   f"status={status} prep={prep:.1f} ms{same}", flush=True)
+        if which == "nofail":
+            return
         sim.set_failed(failed_mask(n, 0.01, 0x5EED + 1))
         ref = None
         for m in modes:

@@ -123,20 +123,22 @@ def test_oracle_known_answers(oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rounds", ["auto", "early", "dense"])
+@pytest.mark.parametrize("rounds", ["auto", "early", "dense", "topdown", "bottom"])
 @pytest.mark.parametrize("kw,stride,dlo,dhi,fail_frac", [
     (dict(PP, n=1), 2, 1, 2, 0.0),
     (dict(PP, n=2, drop_rate=0.0), 3, 0, 3, 0.0),
     (dict(PP, n=777), 6, 0, 6, 0.0),                        # ragged words, zero degrees
     (dict(PP, n=20000), 6, 5, 6, 0.01),                     # C5 shape, 1 % failed
     (dict(PP, n=20000, drop_rate=1.0), 6, 5, 6, 0.0),       # every call lost
+    (dict(PP, n=9000, drop_rate=0.05), 16, 1, 16, 0.0),     # widest packed slot bytes (j, deg <= 16)
     (dict(PP, n=65536 + 77, drop_rate=0.29, trial=5), 19, 18, 19, 0.03),  # wide rows
 ])
 def test_gpu_pushpull_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac, rounds, l2_only=False):
     """Per round bit-exact to the oracle: with the default round selection,
     with sparse early rounds forced for the whole run (informed list +
-    reverse table) and with dense rounds only (no reverse table, and the
-    failed-word gather instead of the failed-slot mask)."""
+    reverse table), with dense rounds only (no reverse table, and the
+    failed-word gather instead of the failed-slot mask), and with the dense
+    rounds forced top-down (atomic pushes) or bottom-up (in-edge scans)."""
     import gossip_simulator_amd as gs
     gs.load()
     n = kw["n"]
@@ -164,6 +166,16 @@ def test_gpu_pushpull_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac, rounds,
             assert sha(e.received()) == sha(sim.received()), f"informed set differs at round {r + 1}"
             if oracle.covered(int(a[0, 4]), n) or int(a[0, 4]) == 0:
                 break
+        tm = sim.timing()
+        # bottom-up needs packed slot bytes (stride <= 16) and, with failed
+        # nodes, the failed-slot mask (stride <= 8)
+        can_bottom = stride <= 16 and (fail_frac == 0 or stride <= 8)
+        if rounds in ("dense", "topdown") or not can_bottom:
+            assert tm["pp_bottom_rounds"] == 0
+        elif rounds == "bottom":
+            assert tm["pp_bottom_rounds"] == r + 1 - tm["pp_early_rounds"]
+        if rounds == "early":
+            assert tm["pp_early_rounds"] >= 1
 
 
 @pytest.mark.gpu
