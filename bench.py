@@ -272,8 +272,10 @@ def pushpull_runs(a, gs, rank, local):
     """C5 extension: push-pull gossip over the same
     overlay (same seed -> the same table, rebuilt in a push-pull context),
     without and with 1 % pre-failed nodes.  value = delivered transmissions / s
-    (calls not lost, whose receiver is live); k_pp_round roofline at 12
-    algorithmic bytes per call (4-B friend id + 8-B peer state word)."""
+    (calls not lost, whose receiver is live); the round's roofline (all its
+    kernels: sparse k_ppe_round, top-down k_pp_round or bottom-up k_ppb_round,
+    summaries, commit) at 12 algorithmic bytes per call (4-B friend id + 8-B
+    peer state word)."""
     cfg = gs.Config(n=a.n, fanout=a.fanout, fanin=a.fanin, delaylow=a.delaylow,
                     delayhigh=a.delayhigh, droprate=a.droprate, crashrate=a.crashrate,
                     seed=a.seed, trial=rank, device=local, model="pushpull")
@@ -299,7 +301,7 @@ def pushpull_runs(a, gs, rank, local):
             "calls_per_s": round(sum(r[0]["fired"] for r in runs) / dt, 1),
             "messages_per_step": tot["messages"], "received": tot["received"],
             "status": STATUS[status],
-            "roofline": {"bound": "hbm", "kernel": "k_pp_round (one launch per round)",
+            "roofline": {"bound": "hbm", "kernel": "one push-pull round (k_ppe_round | k_pp_round | k_ppb_round)",
                          "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 5),
                          "avg_launch_us": round(ms * 1e3 / max(rounds, 1), 2), "launches": rounds}}
