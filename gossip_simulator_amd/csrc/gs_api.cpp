@@ -248,6 +248,7 @@ void refresh_window(gs_ctx* c) {
   w.ids = c->st.ids;
   w.recv = c->st.recv;
   w.crash = c->st.crash;
+  w.rollw = c->st.rollw;
   w.stats = c->st.stats;
   w.err = c->d_err;
   w.stride = c->st.stride;
@@ -502,7 +503,8 @@ int ctx_setup(gs_ctx* c, const gs_params* params, int device, bool shard, uint32
                b_clist = tick ? al((size_t)s.R * kShards * s.CS * 4) : 0,
                b_ccount = tick ? al((size_t)s.R * kShards * kCounterStride * 4) : 0,
                b_stats = al((size_t)kStatSlots * kStatFields * 8);
-  const size_t total = 2 * b_bits + b_next + b_ring + b_cflag + b_clist + b_ccount + b_stats + 256;
+  const size_t b_roll = c->win ? b_bits : 0;
+  const size_t total = 2 * b_bits + b_roll + b_next + b_ring + b_cflag + b_clist + b_ccount + b_stats + 256;
   c->state_bytes = total;
   if (hipMalloc(&c->d_state, total) != hipSuccess) {
     why = "cannot allocate " + std::to_string(total) + " bytes of device state";
@@ -511,6 +513,7 @@ int ctx_setup(gs_ctx* c, const gs_params* params, int device, bool shard, uint32
   char* q = (char*)c->d_state;
   s.recv = (unsigned long long*)q; q += b_bits;
   s.crash = (unsigned long long*)q; q += b_bits;
+  s.rollw = b_roll ? (uint32_t*)q : nullptr; q += b_roll;
   c->d_next = b_next ? (unsigned long long*)q : nullptr;
   c->d_ppsum = b_next ? (unsigned long long*)(q + al(s.W * 8)) : nullptr;
   q += b_next;

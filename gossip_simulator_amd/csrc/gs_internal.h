@@ -53,6 +53,7 @@ struct DevState {
   const uint32_t* ids;
   unsigned long long* recv;
   unsigned long long* crash;
+  uint32_t* rollw;         // window engine: crash-roll marks of the window (cleared by k_resolve)
   uint32_t* cnt;
   unsigned long long* ring;
   uint32_t* cflag;
@@ -112,6 +113,7 @@ struct WinState {
   const uint32_t* ids;
   unsigned long long* recv;
   unsigned long long* crash;
+  uint32_t* rollw;               // [2W] nodes with a crash-roll receipt in the window (k_part2 -> k_resolve)
   unsigned long long* stats;
   uint32_t* err;
   uint32_t* fcount;              // [R][nfine] fire-list lengths
@@ -161,7 +163,7 @@ struct WinState {
   Key key;
 };
 constexpr uint32_t kStatShards = 256;
-constexpr uint32_t kStampPhases = 9;
+constexpr uint32_t kStampPhases = 10;
 // per-trial window counters (batched trials)
 enum TStat : uint32_t { TS_FIRED = 0, TS_SENT = 1, TS_DEAD = 2, TS_RECV = 3, TS_CRASH = 4 };
 constexpr uint32_t kTStatFields = 8;

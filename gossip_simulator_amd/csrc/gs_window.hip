@@ -715,8 +715,13 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8
     __syncthreads();
 #pragma unroll
     for (uint32_t r = 0; r < kPer; ++r)
-      if (m[r] != kEmptyMsg)
+      if (m[r] != kEmptyMsg) {
         ts.buf[ts.off[(m[r] >> kFineLog) & 255] + ((rank[r / 2] >> (16 * (r & 1))) & 0xFFFFu)] = m[r];
+        if ((m[r] >> kRoll0Coarse) & 1u) {  // a crash roll: its node is special in k_resolve
+          const uint32_t v = (c << kCoarseShift) | (m[r] & ((1u << kCoarseShift) - 1));
+          atomicOr(&w.rollw[v >> 5], 1u << (v & 31));
+        }
+      }
     if (mycnt) {
       if (at + mycnt > fe - fb) atomicOr(w.err, kErrFine);
       ts.gbase[tid] = fb + at;
@@ -737,24 +742,29 @@ constexpr uint32_t kResolveMaxBuckets = 256;  // buckets one persistent workgrou
 constexpr uint32_t kSmallMax = 256;           // buckets with <= this many receipts: k_resolve_small
 constexpr uint32_t kSmallBlock = 1024;        // k_resolve_small: 16 waves, one bucket each
 
-// Bit-parallel resolve (k_resolve): per tick k of the window, over the
-// receipts WITHOUT a crash roll b1 = nodes with >= 1, b2 = nodes with >= 2;
-// rl = nodes with a receipt that carries a crash roll.  The third and later
-// roll-free receipts of a (node, tick) and every crash-roll receipt (rare:
-// 1 % at crashrate 0.01) are listed per 32-node word (dlist, chained from
-// dhead).  The large path (resolve_tick) reuses the same LDS for per-node
-// counters and bit words.
+// Bit-parallel resolve (k_resolve).  Three kinds of node in a window:
+//   crashed before it: every receipt is uncounted (simulator.go:108), by tick;
+//   ROLLED: live, and a receipt in the window carries a crash roll (k_part2
+//     marks those nodes in w.rollw): the receipts are listed (dlist) and
+//     chained per 32-node word (dhead), and each (node, tick) group is
+//     replayed exactly (rule A6);
+//   plain: every receipt is counted and the first one informs the node
+//     (:111, :117-121), so a bit per (tick, node) is the whole state.
+// Per receipt: b1[k] |= bit (no-return LDS atomic) and reads of the c0 / r0
+// words.  A bucket whose list overflows takes the per-tick large path
+// (resolve_tick), which reuses the same LDS for per-node counters.
 constexpr uint32_t kBitWords = kFineNodes / 32;
-constexpr uint32_t kDupCap = 3840;     // listed receipts per bucket (more: large path)
+constexpr uint32_t kDupCap = 7680;     // listed receipts per bucket (more: large path)
+constexpr uint32_t kChainRegs = 8;     // a word's chain held in registers (longer: walked in LDS)
 struct ResolveLds {
   union {
     struct {                            // b1 .. dlist, then the infection list
       uint32_t b1[kBitTicks][kBitWords];
-      uint32_t b2[kBitTicks][kBitWords];
-      uint32_t rl[kBitTicks][kBitWords];
+      uint2 cr0[kBitWords];             // per word: crashed before the window, a crash-roll
+                                        // receipt in the window (from w.rollw)
+      uint32_t dhead[kBitWords];        // chain head per word: dlist index + 1, 0 = none
       uint32_t dlist[kDupCap];          // [0, ndup): loc | k << 14 | roll << 18 | next << 19
                                         // (next = index + 1, 0 = end)
-      uint32_t dhead[kBitWords];
     };
     struct {                            // large path
       uint32_t cnt[kFineNodes];         // per node at the current tick: arrivals | crash rolls << 16
@@ -766,6 +776,7 @@ struct ResolveLds {
   };
   uint32_t fc[kWinMaxRing];         // fire-list lengths of this bucket, per ring slot
   uint32_t st[kMaxWindow][4];       // dead (not counted), recv, crash per tick: whole launch
+  uint32_t dead[kMaxWindow];        // this bucket's receipts at nodes crashed before the window
   uint32_t blist[kResolveMaxBuckets];  // this workgroup's non-empty buckets
   uint32_t ndup;
   uint32_t ninf;
@@ -774,9 +785,10 @@ struct ResolveLds {
   uint32_t cls;
   unsigned long long stamp[2][kStampPhases];  // GS_STAMPS: [M >= 1024][phase] cycles (thread 0)
   unsigned long long tlast;
-};  // ~77 KB: two workgroups per CU
+};  // ~72 KB: two workgroups per CU
 static_assert(kBitTicks <= kMaxWindow, "window ticks fit the message format");
-static_assert((3 * kBitTicks * kBitWords + kDupCap) >= kFineNodes, "the infection list fits the bitmaps");
+static_assert(kDupCap < (1u << 13), "chain links fit 13 bits");
+static_assert(sizeof(uint32_t) * kFineNodes <= sizeof(((ResolveLds*)0)->cnt), "the infection list fits");
 
 // GS_STAMPS diagnostics: thread 0 adds the cycles since the last stamp to phase i.
 __device__ __forceinline__ void stamp(const WinState& w, ResolveLds& sm, uint32_t i) {
@@ -877,46 +889,21 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
-// One node with c >= 2 receipts at tick t, `ones` of them carrying a crash
-// roll (rule A6, simulator.go:107-123): counted up to and including the first
-// crash (first_crash), infected if a receipt came before it.
-__device__ __forceinline__ void replay_node(const WinState& w, uint32_t u, uint32_t t, uint32_t c,
-                                            uint32_t ones, uint32_t bit, uint32_t c3order, uint32_t& cw,
-                                            uint32_t& rw, uint32_t& infS, uint32_t& nd, uint32_t& nc,
-                                            uint32_t& ni) {
-  if (cw & bit) {  // crashed before this tick: nothing is counted (:108)
-    nd += c;
-    return;
-  }
-  const uint32_t g = ones ? first_crash(u, t, c, ones, c3order, w.key.k0, w.key.k1) : c + 1;
-  if (g > 1 && !(rw & bit)) {                                     // :117-121
-    rw |= bit;
-    infS |= bit;
-    ++ni;
-  }
-  if (g <= c) {                                                   // :112-115
-    cw |= bit;
-    ++nc;
-    nd += c - g;                                                  // the rest of the tick
-  }
-}
-
-// Adds the lanes' per-tick counters (infected | crashed << 16, and receipts not
-// counted) plus sm.st to the per-tick totals and, for a batched trial, to
-// tstat[trial]; leaves them zeroed.  Block-uniform call.
-__device__ __forceinline__ void flush_counts(const WinState& w, ResolveLds& sm, uint32_t (&acc_rc)[kBitTicks],
-                                             uint32_t (&acc_d)[kBitTicks], uint32_t L, uint32_t trial) {
+// Adds the lanes' per-tick infection counts plus sm.st (dead, recv, crash) to
+// the per-tick totals and, for a batched trial, to tstat[trial]; leaves them
+// zeroed.  Block-uniform call.
+// acc_ni[k / 2] holds tick k's count in bits 16 * (k & 1) (<= 32 per bucket,
+// <= 256 buckets per lane).
+__device__ __forceinline__ void flush_counts(const WinState& w, ResolveLds& sm, uint32_t (&acc_ni)[kBitTicks / 2],
+                                             uint32_t L, uint32_t trial) {
 #pragma unroll
   for (uint32_t k = 0; k < kBitTicks; ++k) {
     if (k >= L) continue;
-    const uint32_t rc = acc_rc[k];
-    const uint32_t sd = wave_sum(acc_d[k]), sr = wave_sum(rc & 0xFFFFu), sc = wave_sum(rc >> 16);
-    const uint32_t lane = lane_id();
-    const uint32_t v = lane == 0 ? sd : lane == 1 ? sr : sc;
-    if (lane < 3 && v) atomicAdd(&sm.st[k][lane], v);
-    acc_rc[k] = 0;
-    acc_d[k] = 0;
+    const uint32_t sr = wave_sum((acc_ni[k / 2] >> (16 * (k & 1))) & 0xFFFFu);
+    if (lane_id() == 0 && sr) atomicAdd(&sm.st[k][1], sr);
   }
+#pragma unroll
+  for (uint32_t k = 0; k < kBitTicks / 2; ++k) acc_ni[k] = 0;
   __syncthreads();
   const uint32_t tid = threadIdx.x;
   if (tid < L * 3) {
@@ -937,18 +924,25 @@ __device__ __forceinline__ void flush_counts(const WinState& w, ResolveLds& sm, 
   __syncthreads();
 }
 
+// chain entry x (loc | k << 14 | roll << 18 | next << 19) -> sort key
+// (node in word) << 5 | k << 1 | roll: groups (node, tick) in tick order per node
+__device__ __forceinline__ uint32_t chain_key(uint32_t x) {
+  return ((x & 31u) << 5) | (((x >> kFineLog) & (kMaxWindow - 1)) << 1) | ((x >> 18) & 1u);
+}
+
 // Persistent: workgroup g owns buckets g, g + G, g + 2G, ... (G = gridDim.x),
 // resolves its non-empty ones in turn, and adds its per-tick counters once at
 // the end.  Per bucket:
 //   stage    thread w owns bit word w (32 nodes): its recv/crash words in
-//            registers, its b1/b2/rl words and dup-chain head zeroed
-//   receipts every message sets its (tick, node) bit in b1 (atomicOr); a
-//            second receipt sets b2, later ones are chained under their
-//            word; a fired ordinal-0 roll sets rl
-//   ticks    per tick, thread w resolves its 32 nodes at once with bit ops
-//            (single receipts), counting chain entries only for b2 nodes; the
-//            infections of the tick are Broadcast() in the lane (:122, :141)
-// A bucket with more repeats than kDupCap takes the per-tick large path.
+//            registers, spec = crashed | marked in rollw (cleared here), its
+//            b1 words and chain head zeroed
+//   receipts every receipt sets its (tick, node) bit in b1; receipts at
+//            special nodes are listed, then chained under their word
+//   ticks    thread w resolves its plain nodes with bit ops, tick by tick
+//            (informed at the first receipt), then replays its special nodes'
+//            (node, tick) groups in order (rule A6, first_crash); the
+//            infections are Broadcast() (:122, :141)
+// A bucket with more special receipts than kDupCap takes the per-tick large path.
 __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
   __shared__ ResolveLds sm;
   const uint32_t tid = threadIdx.x, G = gridDim.x;
@@ -974,11 +968,11 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
   if (nb > 0) { fB = sm.blist[0]; mbB = w.fstart[fB]; MB = (uint32_t)w.ffill[fB]; }
   uint32_t* rwg = (uint32_t*)w.recv;
   uint32_t* cwg = (uint32_t*)w.crash;
-  // this lane's per-tick counters over all its buckets: infected | crashed << 16
-  // (each <= 32 per bucket and tick, <= 256 buckets), and receipts not counted
-  uint32_t acc_rc[kBitTicks], acc_d[kBitTicks];
+  // this lane's infections per tick over all its buckets
+  uint32_t acc_ni[kBitTicks / 2];
 #pragma unroll
-  for (uint32_t k = 0; k < kBitTicks; ++k) { acc_rc[k] = 0; acc_d[k] = 0; }
+  for (uint32_t k = 0; k < kBitTicks / 2; ++k) acc_ni[k] = 0;
+  static_assert(kBitTicks % 2 == 0 && 32 * kResolveMaxBuckets < 65536, "two 16-bit counts per register");
   for (uint32_t i = 0; i < nb; ++i) {
     const uint32_t f = fB, M = MB;
     const unsigned long long mb = mbB;
@@ -991,98 +985,198 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
     const uint32_t c3delay = (c3order & 0xFFFFFFu) | (K_DELAY << 24);
     const bool in = wi < w.W * 2;
     const uint32_t recv0 = in ? rwg[wi] : 0u, crash0 = in ? cwg[wi] : 0u;
+    const uint32_t roll0 = in ? w.rollw[wi] : 0u;
     const uint32_t fcv = tid < w.R ? w.fcount[(size_t)tid * w.nfine + f] : 0u;
     if (i + 1 < nb) { fB = sm.blist[i + 1]; mbB = w.fstart[fB]; MB = (uint32_t)w.ffill[fB]; }
+    if (roll0) w.rollw[wi] = 0u;  // consumed: the next window starts clear
+    const uint32_t rollw = roll0 & ~crash0;
 #pragma unroll
     for (uint32_t k = 0; k < kBitTicks; ++k)
-      if (k < L) { sm.b1[k][tid] = 0; sm.b2[k][tid] = 0; sm.rl[k][tid] = 0; }
+      if (k < L) sm.b1[k][tid] = 0;
+    sm.cr0[tid] = make_uint2(crash0, rollw);
     sm.dhead[tid] = 0;
     if (tid < w.R) sm.fc[tid] = fcv;
-    if (tid == 0) { sm.ndup = 0; sm.ninf = 0; sm.err = 0; sm.cls = M >= 1024 ? 1 : 0; }
+    if (tid < kMaxWindow) sm.dead[tid] = 0;
+    if (tid == 0) { sm.ndup = 0; sm.ninf = 0; sm.err = M >= (1u << 28) ? 3 : 0; sm.cls = M >= 1024 ? 1 : 0; }
     __syncthreads();
     stamp(w, sm, 1);
-    // receipts: (tick, node) bits; repeats chained under their word
+    // receipts: (tick, node) bits; uncounted receipts at crashed nodes by
+    // tick (8-bit fields per lane, flushed every 31 batches); receipts at
+    // rolled nodes listed.  The next batch's loads are issued before this
+    // batch's LDS work.
     const uint32_t* gm = w.fmsg + mb;
     constexpr uint32_t kU = 8;  // loads in flight per lane
-    for (uint32_t p0 = 0; p0 < M; p0 += kResolveBlock * kU) {
-      uint32_t m[kU];
+    constexpr uint32_t kBatch = kResolveBlock * kU;
+    auto ld = [&](uint32_t p0, uint32_t (&m)[kU]) {
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) {
         const uint32_t p = p0 + u * kResolveBlock + tid;
-        const uint32_t x = gm[p < M ? p : M - 1];  // branch-free (M >= 1)
-        m[u] = p < M ? x : ~0u;
+        // valid iff p < M (M >= 1); 32-bit byte offsets from the uniform base (M < 2^28)
+        m[u] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(gm) + ((p < M ? p : M - 1) << 2));
       }
+    };
+    unsigned long long dlo = 0, dhi = 0;  // uncounted receipts, ticks 0..7 / 8..15
+    auto flush_dead = [&]() {
+      while (dlo) {
+        const uint32_t b = __builtin_ctzll(dlo) >> 3;
+        atomicAdd(&sm.dead[b], (uint32_t)(dlo >> (8 * b)) & 255u);
+        dlo &= ~(255ull << (8 * b));
+      }
+      while (dhi) {
+        const uint32_t b = __builtin_ctzll(dhi) >> 3;
+        atomicAdd(&sm.dead[8 + b], (uint32_t)(dhi >> (8 * b)) & 255u);
+        dhi &= ~(255ull << (8 * b));
+      }
+    };
+    uint32_t m[kU];
+    ld(0, m);
+    for (uint32_t p0 = 0, nbat = 0; p0 < (sm.err == 3 ? 0u : M); p0 += kBatch, ++nbat) {
+      uint32_t mn[kU];
+      if (p0 + kBatch < M) ld(p0 + kBatch, mn);
+      uint2 sp[kU];
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) {
-        bool dup = false;
-        uint32_t loc = 0, k = 0, roll = 0;
-        if (m[u] != ~0u) {
-          loc = msg_loc(m[u]);
-          k = msg_tick(m[u]);
-          const uint32_t bit = 1u << (loc & 31);
-          roll = (m[u] >> kRoll0Fine) & 1;
-          if (roll) {  // a crash roll: flagged, and chained with its flag
-            atomicOr(&sm.rl[k][loc >> 5], bit);
-            dup = true;
-          } else if (atomicOr(&sm.b1[k][loc >> 5], bit) & bit) {
-            // thermometer: b1 = >= 1 receipt, b2 = >= 2; the third and later
-            // receipts of a (node, tick) are chained under their word
-            dup = (atomicOr(&sm.b2[k][loc >> 5], bit) & bit) != 0;
-          }
+        sp[u] = make_uint2(0, 0);
+        if (p0 + u * kResolveBlock + tid < M) {
+          const uint32_t loc = msg_loc(m[u]);
+          atomicOr(&sm.b1[msg_tick(m[u])][loc >> 5], 1u << (loc & 31));  // no return
+          sp[u] = sm.cr0[loc >> 5];
         }
-        if (!__ballot(dup)) continue;  // nothing to chain in this wave
-        const uint32_t at = wave_append(&sm.ndup, dup);
-        if (dup) {
-          if (at < kDupCap) {
-            const uint32_t prev = atomicExch(&sm.dhead[loc >> 5], at + 1);
-            sm.dlist[at] = loc | (k << kFineLog) | (roll << 18) | (prev << 19);
-          } else {
-            sm.err = 3;
-          }
+      }
+      uint32_t dm = 0;  // bit u: receipt u is at a rolled node
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t sh = msg_loc(m[u]) & 31, k = msg_tick(m[u]);
+        if ((sp[u].x >> sh) & 1u) {  // crashed before the window: not counted (:108)
+          if (k < 8) dlo += 1ull << (8 * k);
+          else dhi += 1ull << (8 * (k - 8));
         }
+        if ((sp[u].y >> sh) & 1u) dm |= 1u << u;
+      }
+      if (nbat % 31 == 30) flush_dead();
+      const uint32_t nd = __popc(dm);
+      if (__ballot(nd != 0)) {
+        uint32_t pre = 0, tot = 0;  // wave prefix of nd (<= 8)
+#pragma unroll
+        for (uint32_t bb = 0; bb < 4; ++bb) {
+          const unsigned long long bal = __ballot((nd >> bb) & 1u);
+          pre += mbcnt(bal) << bb;
+          tot += (uint32_t)__popcll(bal) << bb;
+        }
+        uint32_t base = 0;
+        if (lane_id() == 0) base = atomicAdd(&sm.ndup, tot);
+        uint32_t at = __builtin_amdgcn_readfirstlane(base) + pre;
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u)
+          if ((dm >> u) & 1u) {
+            if (at < kDupCap) sm.dlist[at] = m[u] & ((1u << 19) - 1);
+            else sm.err = 3;
+            ++at;
+          }
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) m[u] = mn[u];
+    }
+    flush_dead();
+    stamp(w, sm, 2);
+    __syncthreads();
+    // chain the listed receipts under their words
+    if (sm.err != 3) {
+      const uint32_t nd = sm.ndup;
+      for (uint32_t q = tid; q < nd; q += kResolveBlock) {
+        const uint32_t x = sm.dlist[q];
+        const uint32_t prev = atomicExch(&sm.dhead[msg_loc(x) >> 5], q + 1);
+        sm.dlist[q] = x | (prev << 19);
       }
     }
     __syncthreads();
-    stamp(w, sm, 2);
+    stamp(w, sm, 3);
     uint32_t rw = recv0, cw = crash0;
     if (sm.err != 3) {
+      if (tid < L && sm.dead[tid]) atomicAdd(&sm.st[tid][0], sm.dead[tid]);
       const uint32_t ubase = knode0 + tid * 32;
-      // ticks: thread tid resolves nodes 32*tid .. 32*tid+31, tick by tick
+      // plain nodes: informed at their first receipt, tick by tick
       uint32_t infk[kBitTicks], ninf = 0;  // infections per tick of this word
+      const uint32_t plain = ~(crash0 | rollw);
 #pragma unroll
       for (uint32_t k = 0; k < kBitTicks; ++k) {
         infk[k] = 0;
         if (k >= L) continue;
-        const uint32_t A = sm.b1[k][tid], D = sm.b2[k][tid], R = sm.rl[k][tid];
-        const uint32_t S = A & ~D & ~R;                  // one receipt at this tick, no crash roll
-        const uint32_t deadS = S & cw;                   // :108 crashed: not counted
-        uint32_t infS = S & ~cw & ~rw;                   // :117-121
+        const uint32_t infS = sm.b1[k][tid] & plain & ~rw;  // :117-121
         rw |= infS;
-        uint32_t nd = __popc(deadS), nc = 0, ni = __popc(infS);
-        const uint32_t t = t0 + k;
-        for (uint32_t dm = D | R; dm; dm &= dm - 1) {    // repeats or crash rolls at this tick
-          const uint32_t b = __builtin_ctz(dm), loc = tid * 32 + b;
-          uint32_t c = ((A >> b) & 1) + ((D >> b) & 1), ones = 0;
-          for (uint32_t q = sm.dhead[tid]; q;) {
-            const uint32_t e = sm.dlist[q - 1];
-            if ((e & ((1u << 18) - 1)) == (loc | (k << kFineLog))) {
-              ++c;
-              ones += (e >> 18) & 1;
-            }
-            q = e >> 19;
-          }
-          replay_node(w, ubase + b, t, c, ones, 1u << b, c3order, cw, rw, infS, nd, nc, ni);
-        }
-        // per-tick counters stay in the lane until the launch ends
-        acc_rc[k] += ni | (nc << 16);
-        acc_d[k] += nd;
         infk[k] = infS;
+      }
+      stamp(w, sm, 4);
+      // rolled nodes: (node, tick) groups in key order, counted exactly
+      const uint32_t h = sm.dhead[tid];
+      if (h) {
+        uint32_t e[kChainRegs];
+        uint32_t q = h;
+#pragma unroll
+        for (uint32_t j = 0; j < kChainRegs; ++j) {
+          e[j] = ~0u;
+          if (q) {
+            const uint32_t x = sm.dlist[q - 1];
+            e[j] = chain_key(x);
+            q = x >> 19;
+          }
+        }
+        const bool inreg = q == 0;  // else: walk the chain in LDS per group
+        uint32_t last = 0;          // groups with key >> 1 < last are done
+        while (true) {
+          uint32_t best = ~0u, c = 0, ones = 0;
+          if (inreg) {
+#pragma unroll
+            for (uint32_t j = 0; j < kChainRegs; ++j) {
+              const uint32_t k2 = e[j] >> 1;
+              if (e[j] != ~0u && k2 >= last) {
+                if (k2 < best) { best = k2; c = 1; ones = e[j] & 1u; }
+                else if (k2 == best) { ++c; ones += e[j] & 1u; }
+              }
+            }
+          } else {
+            for (uint32_t y = h; y;) {
+              const uint32_t x = sm.dlist[y - 1], ek = chain_key(x), k2 = ek >> 1;
+              if (k2 >= last) {
+                if (k2 < best) { best = k2; c = 1; ones = ek & 1u; }
+                else if (k2 == best) { ++c; ones += ek & 1u; }
+              }
+              y = x >> 19;
+            }
+          }
+          if (best == ~0u) break;
+          last = best + 1;
+          const uint32_t b = best >> 4, k = best & (kMaxWindow - 1), bit = 1u << b, t = t0 + k;
+          if (cw & bit) {  // crashed at an earlier tick of the window: nothing is counted (:108)
+            atomicAdd(&sm.st[k][0], c);
+            continue;
+          }
+          // rule A6: counted up to the first crash, informed if a receipt came first
+          const uint32_t g = ones ? first_crash(ubase + b, t, c, ones, c3order, w.key.k0, w.key.k1) : c + 1;
+          if (g > 1 && !(rw & bit)) {  // :117-121
+            rw |= bit;
+#pragma unroll
+            for (uint32_t kx = 0; kx < kBitTicks; ++kx)
+              if (kx == k) infk[kx] |= bit;
+          }
+          if (g <= c) {  // :112-115
+            cw |= bit;
+            atomicAdd(&sm.st[k][2], 1u);
+            if (c > g) atomicAdd(&sm.st[k][0], c - g);
+          }
+        }
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kBitTicks; ++k) {
+        const uint32_t ni = __popc(infk[k]);
+        acc_ni[k / 2] += ni << (16 * (k & 1));
         ninf += ni;
       }
-      stamp(w, sm, 3);
-      // infection list (loc | tick << 14) over the bitmaps, dead from here on
+      stamp(w, sm, 5);
       __syncthreads();
-      uint32_t* inf = &sm.b1[0][0];
+      stamp(w, sm, 6);
+      // infection list (loc | tick << 14) over the bitmaps, dead from here on
+      uint32_t* inf = &sm.cnt[0];
       {
         uint32_t pre = 0, tot = 0;
 #pragma unroll
@@ -1100,7 +1194,7 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
             inf[at++] = (tid * 32 + __builtin_ctz(x)) | (k << kFineLog);
       }
       __syncthreads();
-      stamp(w, sm, 4);
+      stamp(w, sm, 7);
       // Broadcast() of each infected node (:122, :141-142): fire at t + off
       const uint32_t ni_all = sm.ninf;
       for (uint32_t q = tid; q < ni_all; q += kResolveBlock) {
@@ -1127,20 +1221,20 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
       if (tid == 0 && sm.err == 1) atomicOr(w.err, kErrArrivals);
     }
     __syncthreads();
-    stamp(w, sm, 7);
+    stamp(w, sm, 8);
     if (in) {
       if (rw != recv0) rwg[wi] = rw;
       if (cw != crash0) cwg[wi] = cw;
     }
     if (tid < w.R) w.fcount[(size_t)tid * w.nfine + f] = sm.fc[tid];
-    stamp(w, sm, 8);
+    stamp(w, sm, 9);
     if (w.dbg && tid == 0) sm.stamp[sm.cls][0] += 1;
     // batched trials: the bucket's counters go to its trial's rows (a bucket
     // lies inside one trial) as well as to the per-tick totals
-    if (w.tstat) flush_counts(w, sm, acc_rc, acc_d, L, (uint32_t)(((uint64_t)w.base + node0) >> w.tlog));
+    if (w.tstat) flush_counts(w, sm, acc_ni, L, (uint32_t)(((uint64_t)w.base + node0) >> w.tlog));
   }
   if (w.dbg && tid < 2 * kStampPhases) atomicAdd(&w.dbg[tid], (&sm.stamp[0][0])[tid]);
-  if (!w.tstat) flush_counts(w, sm, acc_rc, acc_d, L, ~0u);
+  if (!w.tstat) flush_counts(w, sm, acc_ni, L, ~0u);
 }
 
 // Small buckets (1..kSmallMax receipts in the window): one wave per bucket.
@@ -1158,7 +1252,7 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
 template <uint32_t E>
 __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t t0, uint32_t L, uint32_t f,
                                                      unsigned long long M, uint32_t (&st)[16][kMaxWindow][4],
-                                                     uint32_t* skw);
+                                                     uint32_t* skw, uint32_t* fcw);
 
 // One launch for both sizes: each wave takes one bucket and the E = 1 or
 // E = 4 body by its receipt count (wave-uniform).
@@ -1166,6 +1260,7 @@ __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w,
   constexpr uint32_t kWaves = kSmallBlock / 64;
   __shared__ uint32_t st[kWaves][kMaxWindow][4];  // per wave: dead (not counted), recv, crash per tick
   __shared__ uint32_t sk[kWaves][64 * 4];          // each wave's sorted keys
+  __shared__ uint32_t fcw[kWaves][kWinMaxRing];    // each wave's bucket: fire-list lengths per ring slot
   const uint32_t tid = threadIdx.x, wv = tid >> 6;
   L = win_live(w, t0, L);
   if (!L) return;
@@ -1174,8 +1269,8 @@ __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w,
   __syncthreads();
   const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
   const unsigned long long M = f < w.nfine ? w.ffill[f] : 0ull;
-  if (M > 0 && M <= 64) resolve_small_bucket<1>(w, t0, L, f, M, st, sk[wv]);
-  else if (M > 64 && M <= 256) resolve_small_bucket<4>(w, t0, L, f, M, st, sk[wv]);
+  if (M > 0 && M <= 64) resolve_small_bucket<1>(w, t0, L, f, M, st, sk[wv], fcw[wv]);
+  else if (M > 64 && M <= 256) resolve_small_bucket<4>(w, t0, L, f, M, st, sk[wv], fcw[wv]);
   __syncthreads();
   if (tid < L * 3) {
     const uint32_t k = tid / 3, fld = tid - k * 3;
@@ -1194,10 +1289,14 @@ __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w,
 template <uint32_t E>
 __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t t0, uint32_t L, uint32_t f,
                                                      unsigned long long M, uint32_t (&st)[16][kMaxWindow][4],
-                                                     uint32_t* skw) {
+                                                     uint32_t* skw, uint32_t* fcw) {
   constexpr uint32_t N = 64 * E;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   {
+    // the bucket's fire-list lengths, staged in this wave's LDS: infections
+    // take their list positions with LDS atomics instead of same-address
+    // global atomics (one wave owns the bucket)
+    for (uint32_t s = lane; s < w.R; s += 64) fcw[s] = w.fcount[(size_t)s * w.nfine + f];
     uint32_t knode0, c3order;  // keys of the bucket's nodes (one trial per bucket)
     node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + (f << kFineLog), K_ORDER, knode0, c3order);
     const uint32_t c3delay = (c3order & 0xFFFFFFu) | (K_DELAY << 24);
@@ -1210,6 +1309,8 @@ __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t
       if (i < M) {
         const uint32_t m = gm[i];
         key[r] = (msg_loc(m) << 5) | (msg_tick(m) << 1) | ((m >> kRoll0Fine) & 1u);
+        // k_part2 marked the node of a crash roll for k_resolve: clear it here
+        if ((m >> kRoll0Fine) & 1u) w.rollw[((f << kFineLog) + msg_loc(m)) >> 5] = 0u;
       }
     }
 #pragma unroll
@@ -1243,6 +1344,7 @@ __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     uint32_t* rwg = (uint32_t*)w.recv;
     uint32_t* cwg = (uint32_t*)w.crash;
+    bool any_inf = false;
 #pragma unroll
     for (uint32_t r = 0; r < E; ++r) {
       const uint32_t i = r * 64 + lane;
@@ -1280,14 +1382,20 @@ __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t
       }
       if (cr && !(cw & bit)) atomicOr(&cwg[wi], bit);
       if (inf) {  // Broadcast() (:122, :141-142): fire at tinf + off
+        any_inf = true;
         atomicOr(&rwg[wi], bit);
         const uint32_t off = fire_offset(w.delay_low, w.delay_span,
                                          philox(u, tinf, 0, c3delay, w.key.k0, w.key.k1).x);
         const uint32_t slot = (tinf + off) % w.R;
-        const uint32_t pos = atomicAdd(&w.fcount[(size_t)slot * w.nfine + f], 1u);
+        const uint32_t pos = atomicAdd(&fcw[slot], 1u);
         w.flist[((size_t)slot * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (__ballot(any_inf))
+      for (uint32_t s = lane; s < w.R; s += 64) w.fcount[(size_t)s * w.nfine + f] = fcw[s];
     if (w.tstat) {  // batched trials: this bucket's counters go to its trial's rows
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
