@@ -79,6 +79,7 @@ struct gs_ctx {
   WinState ws{};
   void* d_win = nullptr;      // fcount + small per-window buffers
   void* d_flist = nullptr;    // [R][nfine][16384] u16
+  void* d_rlmsg = nullptr;    // [nfine][kRolledCap] k_resolve's rolled receipts
   size_t fcount_bytes = 0;
   Buf gmap, cmsg, fmsg, tmp;
   unsigned long long* h_cap = nullptr;  // pinned [257] coarse region plan
@@ -180,8 +181,9 @@ int alloc_window(gs_ctx* c) {
                b_small = al(kRegions * 8) * 2 + al((kRegions + 1) * 8) + al((kRegions + 1) * 4) + al(kMaxWindow * 8),
                b_fhist = al(((size_t)w.ncoarse * 256 + 1) * 8), b_fbase = al(((size_t)w.nfine + 1) * 8),
                b_ffill = al((size_t)w.nfine * 8),
-               b_sst = al((size_t)kStatShards * kMaxWindow * kStatFields * 8);
-  const size_t total = b_fc + 2 * b_units + b_small + b_fhist + b_fbase + b_ffill + b_sst;
+               b_sst = al((size_t)kStatShards * kMaxWindow * kStatFields * 8),
+               b_rlcnt = al((size_t)w.nfine * 4);
+  const size_t total = b_fc + 2 * b_units + b_small + b_fhist + b_fbase + b_ffill + b_sst + b_rlcnt;
   if (hipMalloc(&c->d_win, total) != hipSuccess)
     return fail(c, GS_ENOMEM, "cannot allocate window-engine buffers");
   const size_t flist = (size_t)w.R * w.nfine * kFineNodes * 2;
@@ -201,6 +203,10 @@ int alloc_window(gs_ctx* c) {
   w.fstart = (unsigned long long*)q; q += b_fbase;
   w.ffill = (unsigned long long*)q; q += b_ffill;
   w.sstats = (unsigned long long*)q; q += b_sst;
+  w.rlcnt = (uint32_t*)q; q += b_rlcnt;
+  if (hipMalloc(&c->d_rlmsg, (size_t)w.nfine * kRolledCap * 4) != hipSuccess)
+    return fail(c, GS_ENOMEM, "cannot allocate the rolled-receipt lists");
+  w.rlmsg = (uint32_t*)c->d_rlmsg;
   w.dbg = nullptr;
   if (getenv("GS_STAMPS") && hipMalloc(&w.dbg, 2 * kStampPhases * 8) == hipSuccess)
     (void)hipMemset(w.dbg, 0, 2 * kStampPhases * 8);
@@ -578,7 +584,7 @@ void destroy_one(gs_ctx* c) {
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   overlay_free(&c->ovw);
   for (void* ptr : {(void*)c->d_deg, (void*)c->d_ids, c->d_state, (void*)c->d_cnt, (void*)c->d_failed, c->d_win,
-                    c->d_flist, (void*)c->d_tstat, (void*)c->d_prow, (void*)c->d_pent, (void*)c->d_gcounts})
+                    c->d_flist, c->d_rlmsg, (void*)c->d_tstat, (void*)c->d_prow, (void*)c->d_pent, (void*)c->d_gcounts})
     if (ptr) (void)hipFree(ptr);
   for (Buf* b : {&c->gmap, &c->cmsg, &c->fmsg, &c->tmp, &c->gfire, &c->pp_rend, &c->pp_rsrc, &c->pp_rslot,
                  &c->pp_ilist, &c->pp_fmask, &c->pp_scan, &c->pp_ctlb})

@@ -92,6 +92,7 @@ constexpr uint32_t kWinMaxRing = 256;
 constexpr uint32_t kWinMaxStride = 32;          // friends-row length the window engine takes
 constexpr uint32_t kEmptyMsg = 0xFFFFFFFFu;
 constexpr uint32_t kPartTile = 16384;           // messages per partition tile (runs of ~64 per fine bucket)
+constexpr uint32_t kRolledCap = 1024;           // rolled receipts per bucket k_resolve lists (more: its large path)
 constexpr uint32_t kBitTicks = 10;              // window length k_resolve's per-tick bitmaps hold
 constexpr uint32_t kWinSlotsPerBucket = 1u << 16;  // window cut: friend slots per fine bucket
                                                 // (bounds the message buffers, not LDS)
@@ -114,6 +115,8 @@ struct WinState {
   unsigned long long* recv;
   unsigned long long* crash;
   uint32_t* rollw;               // [2W] nodes with a crash-roll receipt in the window (k_part2 -> k_resolve)
+  uint32_t* rlmsg;               // [nfine][kRolledCap] receipts at rolled nodes (k_resolve -> k_resolve_rolled)
+  uint32_t* rlcnt;               // [nfine] their counts (zeroed by the consumer)
   unsigned long long* stats;
   uint32_t* err;
   uint32_t* fcount;              // [R][nfine] fire-list lengths

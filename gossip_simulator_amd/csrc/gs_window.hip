@@ -745,26 +745,22 @@ constexpr uint32_t kSmallBlock = 1024;        // k_resolve_small: 16 waves, one 
 // Bit-parallel resolve (k_resolve).  Three kinds of node in a window:
 //   crashed before it: every receipt is uncounted (simulator.go:108), by tick;
 //   ROLLED: live, and a receipt in the window carries a crash roll (k_part2
-//     marks those nodes in w.rollw): the receipts are listed (dlist) and
-//     chained per 32-node word (dhead), and each (node, tick) group is
-//     replayed exactly (rule A6);
+//     marks those nodes in w.rollw): the receipts are written to the bucket's
+//     rolled list (w.rlmsg, w.rlcnt) and replayed exactly (rule A6) by
+//     k_resolve_rolled after this kernel, sorted per wave like k_resolve_small;
 //   plain: every receipt is counted and the first one informs the node
 //     (:111, :117-121), so a bit per (tick, node) is the whole state.
-// Per receipt: b1[k] |= bit (no-return LDS atomic) and reads of the c0 / r0
-// words.  A bucket whose list overflows takes the per-tick large path
-// (resolve_tick), which reuses the same LDS for per-node counters.
+// Per receipt: b1[k] |= bit (no-return LDS atomic) and a read of the word's
+// (crashed, rolled) pair.  A bucket whose rolled list overflows takes the
+// per-tick large path (resolve_tick), which reuses the same LDS for per-node
+// counters.
 constexpr uint32_t kBitWords = kFineNodes / 32;
-constexpr uint32_t kDupCap = 7680;     // listed receipts per bucket (more: large path)
-constexpr uint32_t kChainRegs = 8;     // a word's chain held in registers (longer: walked in LDS)
 struct ResolveLds {
   union {
     struct {                            // b1 .. dlist, then the infection list
       uint32_t b1[kBitTicks][kBitWords];
       uint2 cr0[kBitWords];             // per word: crashed before the window, a crash-roll
                                         // receipt in the window (from w.rollw)
-      uint32_t dhead[kBitWords];        // chain head per word: dlist index + 1, 0 = none
-      uint32_t dlist[kDupCap];          // [0, ndup): loc | k << 14 | roll << 18 | next << 19
-                                        // (next = index + 1, 0 = end)
     };
     struct {                            // large path
       uint32_t cnt[kFineNodes];         // per node at the current tick: arrivals | crash rolls << 16
@@ -787,7 +783,6 @@ struct ResolveLds {
   unsigned long long tlast;
 };  // ~72 KB: two workgroups per CU
 static_assert(kBitTicks <= kMaxWindow, "window ticks fit the message format");
-static_assert(kDupCap < (1u << 13), "chain links fit 13 bits");
 static_assert(sizeof(uint32_t) * kFineNodes <= sizeof(((ResolveLds*)0)->cnt), "the infection list fits");
 
 // GS_STAMPS diagnostics: thread 0 adds the cycles since the last stamp to phase i.
@@ -924,12 +919,6 @@ __device__ __forceinline__ void flush_counts(const WinState& w, ResolveLds& sm, 
   __syncthreads();
 }
 
-// chain entry x (loc | k << 14 | roll << 18 | next << 19) -> sort key
-// (node in word) << 5 | k << 1 | roll: groups (node, tick) in tick order per node
-__device__ __forceinline__ uint32_t chain_key(uint32_t x) {
-  return ((x & 31u) << 5) | (((x >> kFineLog) & (kMaxWindow - 1)) << 1) | ((x >> 18) & 1u);
-}
-
 // Persistent: workgroup g owns buckets g, g + G, g + 2G, ... (G = gridDim.x),
 // resolves its non-empty ones in turn, and adds its per-tick counters once at
 // the end.  Per bucket:
@@ -942,7 +931,7 @@ __device__ __forceinline__ uint32_t chain_key(uint32_t x) {
 //            (informed at the first receipt), then replays its special nodes'
 //            (node, tick) groups in order (rule A6, first_crash); the
 //            infections are Broadcast() (:122, :141)
-// A bucket with more special receipts than kDupCap takes the per-tick large path.
+// A bucket with more rolled receipts than kRolledCap takes the per-tick large path.
 __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
   __shared__ ResolveLds sm;
   const uint32_t tid = threadIdx.x, G = gridDim.x;
@@ -994,7 +983,6 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
     for (uint32_t k = 0; k < kBitTicks; ++k)
       if (k < L) sm.b1[k][tid] = 0;
     sm.cr0[tid] = make_uint2(crash0, rollw);
-    sm.dhead[tid] = 0;
     if (tid < w.R) sm.fc[tid] = fcv;
     if (tid < kMaxWindow) sm.dead[tid] = 0;
     if (tid == 0) { sm.ndup = 0; sm.ninf = 0; sm.err = M >= (1u << 28) ? 3 : 0; sm.cls = M >= 1024 ? 1 : 0; }
@@ -1069,7 +1057,7 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
 #pragma unroll
         for (uint32_t u = 0; u < kU; ++u)
           if ((dm >> u) & 1u) {
-            if (at < kDupCap) sm.dlist[at] = m[u] & ((1u << 19) - 1);
+            if (at < kRolledCap) w.rlmsg[(size_t)f * kRolledCap + at] = m[u] & ((1u << 19) - 1);
             else sm.err = 3;
             ++at;
           }
@@ -1080,21 +1068,12 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
     flush_dead();
     stamp(w, sm, 2);
     __syncthreads();
-    // chain the listed receipts under their words
-    if (sm.err != 3) {
-      const uint32_t nd = sm.ndup;
-      for (uint32_t q = tid; q < nd; q += kResolveBlock) {
-        const uint32_t x = sm.dlist[q];
-        const uint32_t prev = atomicExch(&sm.dhead[msg_loc(x) >> 5], q + 1);
-        sm.dlist[q] = x | (prev << 19);
-      }
-    }
-    __syncthreads();
+    // the rolled list goes to k_resolve_rolled (none on the large path)
+    if (tid == 0) w.rlcnt[f] = sm.err == 3 ? 0u : min(sm.ndup, kRolledCap);
     stamp(w, sm, 3);
     uint32_t rw = recv0, cw = crash0;
     if (sm.err != 3) {
       if (tid < L && sm.dead[tid]) atomicAdd(&sm.st[tid][0], sm.dead[tid]);
-      const uint32_t ubase = knode0 + tid * 32;
       // plain nodes: informed at their first receipt, tick by tick
       uint32_t infk[kBitTicks], ninf = 0;  // infections per tick of this word
       const uint32_t plain = ~(crash0 | rollw);
@@ -1107,65 +1086,6 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
         infk[k] = infS;
       }
       stamp(w, sm, 4);
-      // rolled nodes: (node, tick) groups in key order, counted exactly
-      const uint32_t h = sm.dhead[tid];
-      if (h) {
-        uint32_t e[kChainRegs];
-        uint32_t q = h;
-#pragma unroll
-        for (uint32_t j = 0; j < kChainRegs; ++j) {
-          e[j] = ~0u;
-          if (q) {
-            const uint32_t x = sm.dlist[q - 1];
-            e[j] = chain_key(x);
-            q = x >> 19;
-          }
-        }
-        const bool inreg = q == 0;  // else: walk the chain in LDS per group
-        uint32_t last = 0;          // groups with key >> 1 < last are done
-        while (true) {
-          uint32_t best = ~0u, c = 0, ones = 0;
-          if (inreg) {
-#pragma unroll
-            for (uint32_t j = 0; j < kChainRegs; ++j) {
-              const uint32_t k2 = e[j] >> 1;
-              if (e[j] != ~0u && k2 >= last) {
-                if (k2 < best) { best = k2; c = 1; ones = e[j] & 1u; }
-                else if (k2 == best) { ++c; ones += e[j] & 1u; }
-              }
-            }
-          } else {
-            for (uint32_t y = h; y;) {
-              const uint32_t x = sm.dlist[y - 1], ek = chain_key(x), k2 = ek >> 1;
-              if (k2 >= last) {
-                if (k2 < best) { best = k2; c = 1; ones = ek & 1u; }
-                else if (k2 == best) { ++c; ones += ek & 1u; }
-              }
-              y = x >> 19;
-            }
-          }
-          if (best == ~0u) break;
-          last = best + 1;
-          const uint32_t b = best >> 4, k = best & (kMaxWindow - 1), bit = 1u << b, t = t0 + k;
-          if (cw & bit) {  // crashed at an earlier tick of the window: nothing is counted (:108)
-            atomicAdd(&sm.st[k][0], c);
-            continue;
-          }
-          // rule A6: counted up to the first crash, informed if a receipt came first
-          const uint32_t g = ones ? first_crash(ubase + b, t, c, ones, c3order, w.key.k0, w.key.k1) : c + 1;
-          if (g > 1 && !(rw & bit)) {  // :117-121
-            rw |= bit;
-#pragma unroll
-            for (uint32_t kx = 0; kx < kBitTicks; ++kx)
-              if (kx == k) infk[kx] |= bit;
-          }
-          if (g <= c) {  // :112-115
-            cw |= bit;
-            atomicAdd(&sm.st[k][2], 1u);
-            if (c > g) atomicAdd(&sm.st[k][0], c - g);
-          }
-        }
-      }
 #pragma unroll
       for (uint32_t k = 0; k < kBitTicks; ++k) {
         const uint32_t ni = __popc(infk[k]);
@@ -1249,28 +1169,50 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
 // nodes Broadcast() (:122, :141-142) into the bucket's fire lists.
 // Instance E takes buckets with 64*(E/4) < M <= 64*E receipts (E = 1, 4);
 // k_resolve takes the rest.  The launches touch disjoint buckets.
-template <uint32_t E>
+// The same body replays the rolled receipts k_resolve listed per bucket
+// (k_resolve_rolled: the rolled nodes' receipts of a dense bucket, up to
+// kRolledCap, E = 1, 4 or 16); a rolled node is live when the window starts,
+// and its recv/crash bits are untouched by k_resolve, so the replay is the
+// same receive case from the same state.
+template <uint32_t E, bool ROLLED>
 __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t t0, uint32_t L, uint32_t f,
-                                                     unsigned long long M, uint32_t (&st)[16][kMaxWindow][4],
-                                                     uint32_t* skw, uint32_t* fcw);
+                                                     const uint32_t* gm, unsigned long long M,
+                                                     uint32_t (&st)[16][kMaxWindow][4], uint32_t* skw,
+                                                     uint32_t* fcw);
 
-// One launch for both sizes: each wave takes one bucket and the E = 1 or
-// E = 4 body by its receipt count (wave-uniform).
+// One launch for all sizes: each wave takes one bucket and the body by its
+// receipt count (wave-uniform).
+template <bool ROLLED>
 __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w, uint32_t t0, uint32_t L) {
   constexpr uint32_t kWaves = kSmallBlock / 64;
+  constexpr uint32_t kEmax = ROLLED ? 16 : 4;
   __shared__ uint32_t st[kWaves][kMaxWindow][4];  // per wave: dead (not counted), recv, crash per tick
-  __shared__ uint32_t sk[kWaves][64 * 4];          // each wave's sorted keys
+  __shared__ uint32_t sk[kWaves][64 * kEmax];      // each wave's sorted keys
   __shared__ uint32_t fcw[kWaves][kWinMaxRing];    // each wave's bucket: fire-list lengths per ring slot
   const uint32_t tid = threadIdx.x, wv = tid >> 6;
   L = win_live(w, t0, L);
   if (!L) return;
   static_assert(kWaves * kMaxWindow * 4 == kSmallBlock, "one counter per thread");
+  static_assert(kRolledCap == 64 * 16, "the rolled bodies cover 1..kRolledCap");
   (&st[0][0][0])[tid] = 0;
   __syncthreads();
   const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
-  const unsigned long long M = f < w.nfine ? w.ffill[f] : 0ull;
-  if (M > 0 && M <= 64) resolve_small_bucket<1>(w, t0, L, f, M, st, sk[wv], fcw[wv]);
-  else if (M > 64 && M <= 256) resolve_small_bucket<4>(w, t0, L, f, M, st, sk[wv], fcw[wv]);
+  unsigned long long M = 0;
+  const uint32_t* gm = nullptr;
+  if (f < w.nfine) {
+    if (ROLLED) {
+      M = w.rlcnt[f];
+      gm = w.rlmsg + (size_t)f * kRolledCap;
+    } else {
+      M = w.ffill[f];
+      gm = w.fmsg + w.fstart[f];
+    }
+  }
+  if (M > 0 && M <= 64) resolve_small_bucket<1, ROLLED>(w, t0, L, f, gm, M, st, sk[wv], fcw[wv]);
+  else if (M > 64 && M <= 256) resolve_small_bucket<4, ROLLED>(w, t0, L, f, gm, M, st, sk[wv], fcw[wv]);
+  else if (ROLLED && M > 256 && M <= kRolledCap)
+    resolve_small_bucket<ROLLED ? 16 : 1, ROLLED>(w, t0, L, f, gm, M, st, sk[wv], fcw[wv]);
+  if (ROLLED && M && (threadIdx.x & 63) == 0) w.rlcnt[f] = 0;  // consumed
   __syncthreads();
   if (tid < L * 3) {
     const uint32_t k = tid / 3, fld = tid - k * 3;
@@ -1286,10 +1228,11 @@ __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w,
   }
 }
 
-template <uint32_t E>
+template <uint32_t E, bool ROLLED>
 __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t t0, uint32_t L, uint32_t f,
-                                                     unsigned long long M, uint32_t (&st)[16][kMaxWindow][4],
-                                                     uint32_t* skw, uint32_t* fcw) {
+                                                     const uint32_t* gm, unsigned long long M,
+                                                     uint32_t (&st)[16][kMaxWindow][4], uint32_t* skw,
+                                                     uint32_t* fcw) {
   constexpr uint32_t N = 64 * E;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   {
@@ -1300,7 +1243,6 @@ __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t
     uint32_t knode0, c3order;  // keys of the bucket's nodes (one trial per bucket)
     node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + (f << kFineLog), K_ORDER, knode0, c3order);
     const uint32_t c3delay = (c3order & 0xFFFFFFu) | (K_DELAY << 24);
-    const uint32_t* gm = w.fmsg + w.fstart[f];
     uint32_t key[E];  // loc << 5 | k << 1 | crash roll; ~0u sorts last
 #pragma unroll
     for (uint32_t r = 0; r < E; ++r) {
@@ -1310,7 +1252,7 @@ __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t
         const uint32_t m = gm[i];
         key[r] = (msg_loc(m) << 5) | (msg_tick(m) << 1) | ((m >> kRoll0Fine) & 1u);
         // k_part2 marked the node of a crash roll for k_resolve: clear it here
-        if ((m >> kRoll0Fine) & 1u) w.rollw[((f << kFineLog) + msg_loc(m)) >> 5] = 0u;
+        if (!ROLLED && ((m >> kRoll0Fine) & 1u)) w.rollw[((f << kFineLog) + msg_loc(m)) >> 5] = 0u;
       }
     }
 #pragma unroll
@@ -1786,9 +1728,10 @@ hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s
   uint32_t G = std::min<uint32_t>(w.nfine, 2 * cus);
   G = std::max<uint32_t>(G, (w.nfine + kResolveMaxBuckets - 1) / kResolveMaxBuckets);
   const uint32_t gs = (w.nfine + kSmallBlock / 64 - 1) / (kSmallBlock / 64);
-  hipLaunchKernelGGL(k_resolve_small, dim3(gs), dim3(kSmallBlock), 0, s, w, t0, L);
+  hipLaunchKernelGGL(k_resolve_small<false>, dim3(gs), dim3(kSmallBlock), 0, s, w, t0, L);
   static_assert(kSmallMax == 64 * 4, "the two bodies cover 1..kSmallMax");
   hipLaunchKernelGGL(k_resolve, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
+  hipLaunchKernelGGL(k_resolve_small<true>, dim3(gs), dim3(kSmallBlock), 0, s, w, t0, L);  // k_resolve_rolled
   return hipGetLastError();
 }
 
