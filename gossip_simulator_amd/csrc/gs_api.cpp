@@ -90,6 +90,7 @@ struct gs_ctx {
   unsigned long long* h_stage = nullptr;  // pinned copy
   std::vector<hipEvent_t> wev;            // one per staging slot
   bool async_off = false;                 // GS_SYNC_WINDOWS=1: host-driven windows only (A/B tests)
+  bool winlog = false;                    // GS_WINLOG=1: one stderr line per device-driven window
   // trials: `trials` per context (batched when > 1), ids trial << tlog | node
   uint32_t trials = 1, tlog = 32;
   uint64_t ntot = 0;                    // nodes in this context's id space
@@ -541,6 +542,7 @@ int ctx_setup(gs_ctx* c, const gs_params* params, int device, bool shard, uint32
   }
   c->tacc.assign(c->trials, TrialAcc{});
   c->async_off = getenv("GS_SYNC_WINDOWS") != nullptr;
+  c->winlog = getenv("GS_WINLOG") != nullptr;
   if (hipMemsetAsync(c->d_state, 0, total, c->stream) != hipSuccess ||
       (c->d_cnt && hipMemsetAsync(c->d_cnt, 0, s.n * 4, c->stream) != hipSuccess) ||
       hipHostMalloc((void**)&c->h_stats, (size_t)kStatSlots * kStatFields * 8) != hipSuccess ||
@@ -1513,6 +1515,7 @@ int run_async(gs_ctx* c, uint64_t tend, uint32_t poll, uint64_t max_ticks, OnTic
       *what = 1;
       return GS_OK;
     }
+    if (c->winlog) fprintf(stderr, "[win] t0=%u L=%u Tn=%llu stop=%llu\n", t0, L, st[4], st[2]);
     for (uint32_t k = 0; k < L; ++k) on_tick((uint64_t)t0 + k, st + 8 + (size_t)k * kStatFields);
     if (st[2]) *stop = (uint32_t)st[2];
     if (st[2] || L == 0 || (uint64_t)t0 + L >= tend) *what = 1;

@@ -15,8 +15,8 @@ def s(n):
         return ""
     if m.group(1) == "k_resolve" and m.group(2) and m.group(2) != "<0>":
         return "probe"
-    if m.group(1) == "k_resolve_small" and m.group(2) == "<true>":
-        return "rolled"  # k_resolve_rolled: after k_resolve, same window
+    if m.group(1) == "k_resolve_rolled" or (m.group(1) == "k_resolve_small" and m.group(2) == "<true>"):
+        return "rolled"  # the rolled-node replay after k_resolve, same window
     return m.group(1)
 
 

@@ -12,7 +12,7 @@ import csv
 import json
 import sys
 
-KERNELS = ("gs::k_expand", "gs::k_part2", "gs::k_resolve_small", "gs::k_resolve")
+KERNELS = ("gs::k_expand", "gs::k_part2", "gs::k_resolve_small", "gs::k_resolve", "gs::k_resolve_rolled")
 
 
 def main():
