@@ -962,6 +962,31 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
 #pragma unroll
   for (uint32_t k = 0; k < kBitTicks / 2; ++k) acc_ni[k] = 0;
   static_assert(kBitTicks % 2 == 0 && 32 * kResolveMaxBuckets < 65536, "two 16-bit counts per register");
+  constexpr uint32_t kU = 8;  // loads in flight per lane
+  constexpr uint32_t kBatch = kResolveBlock * kU;
+  // messages p0 + u * kResolveBlock + tid of a bucket (gm, M): raw loads, valid
+  // iff the index is < M (M >= 1); 32-bit byte offsets from the uniform base
+  // (M < 2^28)
+  auto ld = [&](const uint32_t* gm, uint32_t M, uint32_t p0, uint32_t (&m)[kU]) {
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint32_t p = p0 + u * kResolveBlock + tid;
+      m[u] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(gm) + ((p < M ? p : M - 1) << 2));
+    }
+  };
+  // the next bucket's state words and first batch of messages are loaded
+  // while this bucket finishes (from the end of its receipts)
+  uint32_t pm[kU], p_recv0 = 0, p_crash0 = 0, p_roll0 = 0, p_fcv = 0;
+  auto prefetch = [&](uint32_t f, uint32_t M, unsigned long long mb) {
+    const uint64_t wi = ((uint64_t)(f << kFineLog) >> 5) + tid;
+    const bool in = wi < w.W * 2;
+    p_recv0 = in ? rwg[wi] : 0u;
+    p_crash0 = in ? cwg[wi] : 0u;
+    p_roll0 = in ? w.rollw[wi] : 0u;
+    p_fcv = tid < w.R ? w.fcount[(size_t)tid * w.nfine + f] : 0u;
+    ld(w.fmsg + mb, M, 0, pm);
+  };
+  if (nb > 0) prefetch(fB, MB, mbB);
   for (uint32_t i = 0; i < nb; ++i) {
     const uint32_t f = fB, M = MB;
     const unsigned long long mb = mbB;
@@ -973,9 +998,7 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
     node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + node0, K_ORDER, knode0, c3order);
     const uint32_t c3delay = (c3order & 0xFFFFFFu) | (K_DELAY << 24);
     const bool in = wi < w.W * 2;
-    const uint32_t recv0 = in ? rwg[wi] : 0u, crash0 = in ? cwg[wi] : 0u;
-    const uint32_t roll0 = in ? w.rollw[wi] : 0u;
-    const uint32_t fcv = tid < w.R ? w.fcount[(size_t)tid * w.nfine + f] : 0u;
+    const uint32_t recv0 = p_recv0, crash0 = p_crash0, roll0 = p_roll0, fcv = p_fcv;
     if (i + 1 < nb) { fB = sm.blist[i + 1]; mbB = w.fstart[fB]; MB = (uint32_t)w.ffill[fB]; }
     if (roll0) w.rollw[wi] = 0u;  // consumed: the next window starts clear
     const uint32_t rollw = roll0 & ~crash0;
@@ -993,16 +1016,6 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
     // rolled nodes listed.  The next batch's loads are issued before this
     // batch's LDS work.
     const uint32_t* gm = w.fmsg + mb;
-    constexpr uint32_t kU = 8;  // loads in flight per lane
-    constexpr uint32_t kBatch = kResolveBlock * kU;
-    auto ld = [&](uint32_t p0, uint32_t (&m)[kU]) {
-#pragma unroll
-      for (uint32_t u = 0; u < kU; ++u) {
-        const uint32_t p = p0 + u * kResolveBlock + tid;
-        // valid iff p < M (M >= 1); 32-bit byte offsets from the uniform base (M < 2^28)
-        m[u] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(gm) + ((p < M ? p : M - 1) << 2));
-      }
-    };
     unsigned long long dlo = 0, dhi = 0;  // uncounted receipts, ticks 0..7 / 8..15
     auto flush_dead = [&]() {
       while (dlo) {
@@ -1017,10 +1030,11 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
       }
     };
     uint32_t m[kU];
-    ld(0, m);
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) m[u] = pm[u];
     for (uint32_t p0 = 0, nbat = 0; p0 < (sm.err == 3 ? 0u : M); p0 += kBatch, ++nbat) {
       uint32_t mn[kU];
-      if (p0 + kBatch < M) ld(p0 + kBatch, mn);
+      if (p0 + kBatch < M) ld(gm, M, p0 + kBatch, mn);
       uint2 sp[kU];
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) {
@@ -1068,6 +1082,7 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
     flush_dead();
     stamp(w, sm, 2);
     __syncthreads();
+    if (i + 1 < nb) prefetch(fB, MB, mbB);
     // the rolled list goes to k_resolve_rolled (none on the large path)
     if (tid == 0) w.rlcnt[f] = sm.err == 3 ? 0u : min(sm.ndup, kRolledCap);
     stamp(w, sm, 3);
