@@ -91,7 +91,10 @@ constexpr uint32_t kRegions = 256 * kCoarseSub;
 constexpr uint32_t kWinMaxRing = 256;
 constexpr uint32_t kWinMaxStride = 32;          // friends-row length the window engine takes
 constexpr uint32_t kEmptyMsg = 0xFFFFFFFFu;
-constexpr uint32_t kPartTile = 16384;           // messages per partition tile (runs of ~64 per fine bucket)
+#ifndef GS_PART_TILE
+#define GS_PART_TILE 16384
+#endif
+constexpr uint32_t kPartTile = GS_PART_TILE;    // messages per partition tile (runs of ~64 per fine bucket)
 constexpr uint32_t kRolledCap = 1024;           // rolled receipts per bucket k_resolve lists (more: its large path)
 constexpr uint32_t kBitTicks = 10;              // window length k_resolve's per-tick bitmaps hold
 constexpr uint32_t kWinSlotsPerBucket = 1u << 16;  // window cut: friend slots per fine bucket

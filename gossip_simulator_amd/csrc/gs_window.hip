@@ -642,7 +642,10 @@ __global__ void k_plan(const WinState w, bool exact) {
 }
 
 // LDS counting sort of one tile by an 8-bit digit, then coalesced runs out.
-constexpr uint32_t kPartBlock = 1024;  // threads per partition tile (16 messages each)
+#ifndef GS_PART_BLOCK
+#define GS_PART_BLOCK 1024
+#endif
+constexpr uint32_t kPartBlock = GS_PART_BLOCK;  // threads per partition tile (16 messages each)
 static_assert(kPartTile % kPartBlock == 0, "whole messages per thread");
 
 // The tile holds coarse messages as they came: the fine digit (bits 14..21) is
