@@ -744,6 +744,7 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8
 constexpr uint32_t kResolveMaxBuckets = 256;  // buckets one persistent workgroup may own
 constexpr uint32_t kSmallMax = 256;           // buckets with <= this many receipts: k_resolve_small
 constexpr uint32_t kSmallBlock = 1024;        // k_resolve_small: 16 waves, one bucket each
+constexpr uint32_t kRolledBlock = 512;        // the rolled replay: 8 waves, one bucket each
 
 // Bit-parallel resolve (k_resolve).  Three kinds of node in a window:
 //   crashed before it: every receipt is uncounted (simulator.go:108), by tick;
@@ -1180,7 +1181,7 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
 // bucket holds a few dozen or hundred receipts, and the bit-parallel
 // k_resolve's fixed cost per bucket (512 bit words x L ticks, a chain of block
 // barriers) is what the window pays.  Here a wave holds the bucket's
-// receipts as E keys per lane (element r*64 + lane in register r), sorts them
+// receipts as E keys per lane (element lane*E + r in register r), sorts them
 // by (node, tick, roll0) with a bitonic network (shuffles across lanes,
 // swaps across registers), and the first element of every node's run replays
 // the receive case (simulator.go:107-123, rule A6) along the run; infected
@@ -1189,20 +1190,21 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
 // k_resolve takes the rest.  The launches touch disjoint buckets.
 // The same body replays the rolled receipts k_resolve listed per bucket
 // (k_resolve_rolled: the rolled nodes' receipts of a dense bucket, up to
-// kRolledCap, E = 1, 4 or 16); a rolled node is live when the window starts,
+// kRolledCap, E = 1, 4, 8 or 16); a rolled node is live when the window starts,
 // and its recv/crash bits are untouched by k_resolve, so the replay is the
 // same receive case from the same state.
 template <uint32_t E, bool ROLLED>
 __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t t0, uint32_t L, uint32_t f,
                                                      const uint32_t* gm, unsigned long long M,
-                                                     uint32_t (&st)[16][kMaxWindow][4], uint32_t* skw,
+                                                     uint32_t (*st)[kMaxWindow][4], uint32_t* skw,
                                                      uint32_t* fcw);
 
 // One launch for all sizes: each wave takes one bucket and the body by its
 // receipt count (wave-uniform).
 template <bool ROLLED>
-__global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w, uint32_t t0, uint32_t L) {
-  constexpr uint32_t kWaves = kSmallBlock / 64;
+__global__ __launch_bounds__(ROLLED ? kRolledBlock : kSmallBlock) void k_resolve_small(const WinState w, uint32_t t0,
+                                                                                       uint32_t L) {
+  constexpr uint32_t kWaves = (ROLLED ? kRolledBlock : kSmallBlock) / 64;
   constexpr uint32_t kEmax = ROLLED ? 16 : 4;
   __shared__ uint32_t st[kWaves][kMaxWindow][4];  // per wave: dead (not counted), recv, crash per tick
   __shared__ uint32_t sk[kWaves][64 * kEmax];      // each wave's sorted keys
@@ -1210,7 +1212,7 @@ __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w,
   const uint32_t tid = threadIdx.x, wv = tid >> 6;
   L = win_live(w, t0, L);
   if (!L) return;
-  static_assert(kWaves * kMaxWindow * 4 == kSmallBlock, "one counter per thread");
+  static_assert(kWaves * kMaxWindow * 4 == kWaves * 64, "one counter per thread");
   static_assert(kRolledCap == 64 * 16, "the rolled bodies cover 1..kRolledCap");
   (&st[0][0][0])[tid] = 0;
   __syncthreads();
@@ -1228,7 +1230,9 @@ __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w,
   }
   if (M > 0 && M <= 64) resolve_small_bucket<1, ROLLED>(w, t0, L, f, gm, M, st, sk[wv], fcw[wv]);
   else if (M > 64 && M <= 256) resolve_small_bucket<4, ROLLED>(w, t0, L, f, gm, M, st, sk[wv], fcw[wv]);
-  else if (ROLLED && M > 256 && M <= kRolledCap)
+  else if (ROLLED && M > 256 && M <= 512)
+    resolve_small_bucket<ROLLED ? 8 : 1, ROLLED>(w, t0, L, f, gm, M, st, sk[wv], fcw[wv]);
+  else if (ROLLED && M > 512 && M <= kRolledCap)
     resolve_small_bucket<ROLLED ? 16 : 1, ROLLED>(w, t0, L, f, gm, M, st, sk[wv], fcw[wv]);
   if (ROLLED && M && (threadIdx.x & 63) == 0) w.rlcnt[f] = 0;  // consumed
   __syncthreads();
@@ -1249,7 +1253,7 @@ __global__ __launch_bounds__(kSmallBlock) void k_resolve_small(const WinState w,
 template <uint32_t E, bool ROLLED>
 __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t t0, uint32_t L, uint32_t f,
                                                      const uint32_t* gm, unsigned long long M,
-                                                     uint32_t (&st)[16][kMaxWindow][4], uint32_t* skw,
+                                                     uint32_t (*st)[kMaxWindow][4], uint32_t* skw,
                                                      uint32_t* fcw) {
   constexpr uint32_t N = 64 * E;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1261,10 +1265,12 @@ __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t
     uint32_t knode0, c3order;  // keys of the bucket's nodes (one trial per bucket)
     node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + (f << kFineLog), K_ORDER, knode0, c3order);
     const uint32_t c3delay = (c3order & 0xFFFFFFu) | (K_DELAY << 24);
+    // element i = lane * E + r in key[r] (lane-major: the bitonic stages with
+    // j < E are register swaps, only those with j >= E shuffle across lanes)
     uint32_t key[E];  // loc << 5 | k << 1 | crash roll; ~0u sorts last
 #pragma unroll
     for (uint32_t r = 0; r < E; ++r) {
-      const uint32_t i = r * 64 + lane;
+      const uint32_t i = lane * E + r;
       key[r] = ~0u;
       if (i < M) {
         const uint32_t m = gm[i];
@@ -1277,42 +1283,55 @@ __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t
     for (uint32_t k = 2; k <= N; k <<= 1)
 #pragma unroll
       for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-        if (j < 64) {
+        if (j >= E) {  // partner in lane ^ (j / E), same register
 #pragma unroll
           for (uint32_t r = 0; r < E; ++r) {
-            const uint32_t i = r * 64 + lane;
-            const uint32_t o = __shfl_xor(key[r], j, 64);
+            const uint32_t i = lane * E + r;
+            const uint32_t o = __shfl_xor(key[r], j / E, 64);
             const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
             key[r] = keep_min ? min(key[r], o) : max(key[r], o);
           }
-        } else {
-          const uint32_t rj = j / 64;
+        } else {  // partner in register r ^ j of this lane
 #pragma unroll
           for (uint32_t r = 0; r < E; ++r) {
-            if (r & rj) continue;
-            const bool up = ((r * 64 + lane) & k) == 0;
-            const uint32_t a = key[r], b = key[r | rj];
+            if (r & j) continue;
+            const bool up = ((lane * E + r) & k) == 0;
+            const uint32_t a = key[r], b = key[r | j];
             key[r] = up ? min(a, b) : max(a, b);
-            key[r | rj] = up ? max(a, b) : min(a, b);
+            key[r | j] = up ? max(a, b) : min(a, b);
           }
         }
       }
 #pragma unroll
-    for (uint32_t r = 0; r < E; ++r) skw[r * 64 + lane] = key[r];
+    for (uint32_t r = 0; r < E; ++r) skw[lane * E + r] = key[r];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     uint32_t* rwg = (uint32_t*)w.recv;
     uint32_t* cwg = (uint32_t*)w.crash;
     bool any_inf = false;
+    // the run heads' recv / crash words, all loaded before any is used (a
+    // node's bits change only through its own run head)
+    uint32_t head = 0, cwv[E], rwv[E];
 #pragma unroll
     for (uint32_t r = 0; r < E; ++r) {
-      const uint32_t i = r * 64 + lane;
+      const uint32_t i = lane * E + r;
       const uint32_t loc = key[r] >> 5;
+      cwv[r] = rwv[r] = 0;
       if (key[r] == ~0u || (i > 0 && (skw[i - 1] >> 5) == loc)) continue;  // not a run head
+      head |= 1u << r;
+      const uint32_t wi = ((f << kFineLog) + loc) >> 5;
+      cwv[r] = cwg[wi];
+      rwv[r] = rwg[wi];
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < E; ++r) {
+      const uint32_t i = lane * E + r;
+      const uint32_t loc = key[r] >> 5;
+      if (!((head >> r) & 1u)) continue;
       const uint32_t wi = ((f << kFineLog) + loc) >> 5, bit = 1u << (loc & 31), u = knode0 + loc;
-      const uint32_t cw = cwg[wi];
-      bool rv = (rwg[wi] & bit) != 0, cr = (cw & bit) != 0, inf = false;
+      const uint32_t cw = cwv[r];
+      bool rv = (rwv[r] & bit) != 0, cr = (cw & bit) != 0, inf = false;
       uint32_t tinf = 0;
       for (uint32_t q = i; q < N;) {  // along the run, one (node, tick) group at a time
         const uint32_t e = skw[q];
@@ -1749,7 +1768,9 @@ hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s
   hipLaunchKernelGGL(k_resolve_small<false>, dim3(gs), dim3(kSmallBlock), 0, s, w, t0, L);
   static_assert(kSmallMax == 64 * 4, "the two bodies cover 1..kSmallMax");
   hipLaunchKernelGGL(k_resolve, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
-  hipLaunchKernelGGL(k_resolve_small<true>, dim3(gs), dim3(kSmallBlock), 0, s, w, t0, L);  // k_resolve_rolled
+  // k_resolve_rolled: 8-wave blocks (the E = 16 key arrays take 4 KB per wave)
+  hipLaunchKernelGGL(k_resolve_small<true>, dim3((w.nfine + kRolledBlock / 64 - 1) / (kRolledBlock / 64)),
+                     dim3(kRolledBlock), 0, s, w, t0, L);
   return hipGetLastError();
 }
 
