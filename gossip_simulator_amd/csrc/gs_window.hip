@@ -743,8 +743,14 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8
 
 constexpr uint32_t kResolveMaxBuckets = 256;  // buckets one persistent workgroup may own
 constexpr uint32_t kSmallMax = 256;           // buckets with <= this many receipts: k_resolve_small
-constexpr uint32_t kSmallBlock = 1024;        // k_resolve_small: 16 waves, one bucket each
-constexpr uint32_t kRolledBlock = 512;        // the rolled replay: 8 waves, one bucket each
+#ifndef GS_SMALL_BLOCK
+#define GS_SMALL_BLOCK 512
+#endif
+constexpr uint32_t kSmallBlock = GS_SMALL_BLOCK;  // k_resolve_small: 8 waves, one bucket each
+#ifndef GS_ROLLED_BLOCK
+#define GS_ROLLED_BLOCK 256
+#endif
+constexpr uint32_t kRolledBlock = GS_ROLLED_BLOCK;  // the rolled replay: 4 waves, one bucket each
 
 // Bit-parallel resolve (k_resolve).  Three kinds of node in a window:
 //   crashed before it: every receipt is uncounted (simulator.go:108), by tick;
@@ -1768,7 +1774,7 @@ hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s
   hipLaunchKernelGGL(k_resolve_small<false>, dim3(gs), dim3(kSmallBlock), 0, s, w, t0, L);
   static_assert(kSmallMax == 64 * 4, "the two bodies cover 1..kSmallMax");
   hipLaunchKernelGGL(k_resolve, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
-  // k_resolve_rolled: 8-wave blocks (the E = 16 key arrays take 4 KB per wave)
+  // k_resolve_rolled: small blocks (the E = 16 key arrays take 4 KB per wave; blocks finish independently)
   hipLaunchKernelGGL(k_resolve_small<true>, dim3((w.nfine + kRolledBlock / 64 - 1) / (kRolledBlock / 64)),
                      dim3(kRolledBlock), 0, s, w, t0, L);
   return hipGetLastError();
