@@ -1768,7 +1768,8 @@ hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s
       return (uint32_t)v;
     return 256u;
   }();
-  uint32_t G = std::min<uint32_t>(w.nfine, 2 * cus);
+  static const uint32_t per_cu = [] { const char* e = getenv("GS_RESOLVE_PER_CU"); return e ? (uint32_t)std::max(atoi(e), 1) : 2u; }();  // A/B knob
+  uint32_t G = std::min<uint32_t>(w.nfine, per_cu * cus);
   G = std::max<uint32_t>(G, (w.nfine + kResolveMaxBuckets - 1) / kResolveMaxBuckets);
   const uint32_t gs = (w.nfine + kSmallBlock / 64 - 1) / (kSmallBlock / 64);
   hipLaunchKernelGGL(k_resolve_small<false>, dim3(gs), dim3(kSmallBlock), 0, s, w, t0, L);
