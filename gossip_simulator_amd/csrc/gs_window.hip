@@ -1316,28 +1316,24 @@ __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t
     uint32_t* rwg = (uint32_t*)w.recv;
     uint32_t* cwg = (uint32_t*)w.crash;
     bool any_inf = false;
-    // the run heads' recv / crash words, all loaded before any is used (a
-    // node's bits change only through its own run head)
-    uint32_t head = 0, cwv[E], rwv[E];
+    // run heads of this lane's elements
+    uint32_t head = 0;
 #pragma unroll
     for (uint32_t r = 0; r < E; ++r) {
       const uint32_t i = lane * E + r;
-      const uint32_t loc = key[r] >> 5;
-      cwv[r] = rwv[r] = 0;
-      if (key[r] == ~0u || (i > 0 && (skw[i - 1] >> 5) == loc)) continue;  // not a run head
-      head |= 1u << r;
-      const uint32_t wi = ((f << kFineLog) + loc) >> 5;
-      cwv[r] = cwg[wi];
-      rwv[r] = rwg[wi];
+      if (key[r] != ~0u && !(i > 0 && (skw[i - 1] >> 5) == (key[r] >> 5))) head |= 1u << r;
     }
-#pragma unroll
+    // one run head at a time, keys re-read from LDS: the body (two Philox
+    // draws) is emitted once, not E times (the E = 16 instance's unrolled
+    // body outgrew the instruction cache)
+#pragma unroll 1
     for (uint32_t r = 0; r < E; ++r) {
-      const uint32_t i = lane * E + r;
-      const uint32_t loc = key[r] >> 5;
       if (!((head >> r) & 1u)) continue;
+      const uint32_t i = lane * E + r;
+      const uint32_t loc = skw[i] >> 5;
       const uint32_t wi = ((f << kFineLog) + loc) >> 5, bit = 1u << (loc & 31), u = knode0 + loc;
-      const uint32_t cw = cwv[r];
-      bool rv = (rwv[r] & bit) != 0, cr = (cw & bit) != 0, inf = false;
+      const uint32_t cw = cwg[wi];
+      bool rv = (rwg[wi] & bit) != 0, cr = (cw & bit) != 0, inf = false;
       uint32_t tinf = 0;
       for (uint32_t q = i; q < N;) {  // along the run, one (node, tick) group at a time
         const uint32_t e = skw[q];
