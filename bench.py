@@ -274,8 +274,9 @@ def pushpull_runs(a, gs, rank, local):
     without and with 1 % pre-failed nodes.  value = delivered transmissions / s
     (calls not lost, whose receiver is live); the round's roofline (all its
     kernels: sparse k_ppe_round, top-down k_pp_round or bottom-up k_ppb_round,
-    summaries, commit) at 12 algorithmic bytes per call (4-B friend id + 8-B
-    peer state word)."""
+    summaries, commit) at SURVEY.md 8(d)'s 8 algorithmic bytes per delivered
+    message; frac_12B_per_call charges 12 B (4-B friend id + 8-B peer state
+    word) to every call instead."""
     cfg = gs.Config(n=a.n, fanout=a.fanout, fanin=a.fanin, delaylow=a.delaylow,
                     delayhigh=a.delayhigh, droprate=a.droprate, crashrate=a.crashrate,
                     seed=a.seed, trial=rank, device=local, model="pushpull")
@@ -293,7 +294,9 @@ def pushpull_runs(a, gs, rank, local):
         rounds = int(tm["deliver_launches"])
         ms = tm["deliver_ms"]
         calls = tot["fired"]
-        ach = 12 * calls / (ms * 1e-3) / 1e9
+        # 8 algorithmic bytes per delivered push-pull message
+        ach = 8 * tot["messages"] / (ms * 1e-3) / 1e9
+        ach_call = 12 * calls / (ms * 1e-3) / 1e9
         log(f"push-pull: rounds={tot['tick']} sent={tot['sent']} {dt * 1e3 / len(runs):.1f} ms/run")
         out["pushpull"] = {
             "value": round(sum(r[0]["messages"] for r in runs) / dt, 1), "unit": "msgs/s",
@@ -302,8 +305,10 @@ def pushpull_runs(a, gs, rank, local):
             "messages_per_step": tot["messages"], "received": tot["received"],
             "status": STATUS[status],
             "roofline": {"bound": "hbm", "kernel": "one push-pull round (k_ppe_round | k_pp_round | k_ppb_round)",
+                         "bytes": "8 per delivered message (SURVEY.md 8(d))",
                          "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 5),
+                         "frac_12B_per_call": round(ach_call / HBM_PEAK_GBS, 5),
                          "avg_launch_us": round(ms * 1e3 / max(rounds, 1), 2), "launches": rounds}}
         sim.reset()
         sim.set_failed(failed_mask(a.n, 0.01, a.seed + 1))
@@ -459,17 +464,34 @@ def cpu_model():
     return "unknown"
 
 
+def cpu_limits():
+    """What this host lets the process use: affinity and the cgroup CPU quota."""
+    out = {"nproc": os.cpu_count()}
+    try:
+        out["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        q = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q and q[0] != "max":
+            out["cgroup_cpus"] = round(int(q[0]) / int(q[1]), 2)
+    except (OSError, ValueError, IndexError):
+        pass
+    return out
+
+
 def cpu_baseline(a, gs):
     """The all-core OpenMP port of the tick model (oracle/gsomp.c, bit-exact to
-    the restatement, checked in tests/test_omp_port.py) on this host's CPU
-    share: one whole broadcast at n = cpu_n with the same parameters, over a
-    table the GPU overlay built (copied to the host); times only the port's
-    tick loop, capped at 40 s.  msgs/s as the headline: delivered sends / time
+    the restatement, checked in tests/test_omp_port.py) on this host: one whole
+    broadcast at n = cpu_n with the same parameters, over a table the GPU
+    overlay built (copied to the host); times only the port's tick loop,
+    capped at 40 s.  `value` runs one OpenMP thread per host CPU (os.cpu_count());
+    the run at this GPU's CPU share (16 threads, the box's OMP_NUM_THREADS) is
+    reported beside it.  msgs/s as the headline: delivered sends / time
     (simulator.go:252-253 divides TotalMessage by the broadcast's time)."""
     from oracle import pyoracle as O
     O.build()
     n = a.cpu_n
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     cfg = gs.Config(n=n, fanout=a.fanout, fanin=a.fanin, delaylow=a.delaylow,
                     delayhigh=a.delayhigh, droprate=a.droprate, crashrate=a.crashrate,
                     seed=a.seed, trial=0, device=0)
@@ -479,29 +501,38 @@ def cpu_baseline(a, gs):
     p = O.make_params(n=n, fanout=a.fanout, fanin=a.fanin, delay_low=a.delaylow,
                       delay_high=a.delayhigh, drop_rate=a.droprate, crash_rate=a.crashrate,
                       seed=a.seed, trial=0)
-    e = O.OmpEngine(p, deg, ids, threads=threads)
-    del deg, ids
-    e.begin(-1)
-    sent = msgs = 0
-    t0 = time.perf_counter()
-    capped = False
-    while True:
-        st = e.step(10)
-        sent += int(st[:, 2].sum())
-        msgs += int(st[:, 3].sum())
-        if O.covered(int(st[-1, 4]), n) or int(st[-1, 6]) == 0:
-            break
-        if time.perf_counter() - t0 > 40:
-            capped = True
-            break
-    dt = time.perf_counter() - t0
-    log(f"cpu baseline: {e.threads} threads, n={n}: {sent / dt:.3e} msgs/s ({dt:.1f} s)")
-    return {"value": round(sent / dt, 1), "unit": "msgs/s", "cores": e.threads, "kind": "port",
-            "messages_per_s": round(msgs / dt, 1), "cpu_model": cpu_model(), "nproc": os.cpu_count(),
-            "sample": f"oracle/gsomp.c (OpenMP port of the tick model, {e.threads} threads = this GPU's host "
-                      f"CPU share), one broadcast at n={n} to {'the 40 s cap' if capped else '99% / quiescence'} "
-                      f"({sent} delivered sends in {dt:.2f} s), same params, GPU-built overlay; per-message work "
-                      f"does not depend on n, so the rate stands for N=1e9 (whose 24 GB table fits host RAM)"}
+
+    def run(threads):
+        e = O.OmpEngine(p, deg, ids, threads=threads)
+        e.begin(-1)
+        sent = msgs = 0
+        t0 = time.perf_counter()
+        capped = False
+        while True:
+            st = e.step(10)
+            sent += int(st[:, 2].sum())
+            msgs += int(st[:, 3].sum())
+            if O.covered(int(st[-1, 4]), n) or int(st[-1, 6]) == 0:
+                break
+            if time.perf_counter() - t0 > 40:
+                capped = True
+                break
+        dt = time.perf_counter() - t0
+        log(f"cpu baseline: {e.threads} threads, n={n}: {sent / dt:.3e} msgs/s ({dt:.1f} s)")
+        return e.threads, sent, msgs, dt, capped
+
+    share = int(os.environ.get("OMP_NUM_THREADS", "0")) or 16
+    allc = os.cpu_count() or share
+    th, sent, msgs, dt, capped = run(allc)
+    th16, sent16, _, dt16, capped16 = run(share) if share != allc else (th, sent, msgs, dt, capped)
+    return {"value": round(sent / dt, 1), "unit": "msgs/s", "cores": th, "kind": "port",
+            "messages_per_s": round(msgs / dt, 1), "cpu_model": cpu_model(), **cpu_limits(),
+            "gpu_share": {"threads": th16, "value": round(sent16 / dt16, 1), "s": round(dt16, 3),
+                          "capped": capped16},
+            "sample": f"oracle/gsomp.c (OpenMP port of the tick model) with {th} threads (one per host CPU), "
+                      f"one broadcast at n={n} to {'the 40 s cap' if capped else '99% / quiescence'} "
+                      f"({sent} delivered sends in {dt:.2f} s), same params, GPU-built overlay; gpu_share = the "
+                      f"same run with {th16} threads (this GPU's share of the host)"}
 
 
 if __name__ == "__main__":

@@ -83,7 +83,9 @@ struct gs_ctx {
   size_t fcount_bytes = 0;
   Buf gmap, cmsg, fmsg, tmp;
   unsigned long long* h_cap = nullptr;  // pinned [257] coarse region plan
-  unsigned long long* h_misc = nullptr; // pinned scratch (counts, flags)
+  unsigned long long* h_misc = nullptr; // pinned scratch (counts, flags): misc_words words
+  size_t misc_words = 0;                // >= kRegions and >= G * kMaxWindow (gathered fire counts)
+  uint32_t* h_err = nullptr;            // pinned copy of the error word (shard windows)
   // device-driven windows (run_async)
   WinCtl* d_ctl = nullptr;
   unsigned long long* d_stage = nullptr;  // [kSlots][kStageWords]
@@ -215,8 +217,10 @@ int alloc_window(gs_ctx* c) {
   c->fcount_bytes = (size_t)w.R * w.nfine * 4;
   if (hipMemsetAsync(c->d_win, 0, total, c->stream) != hipSuccess)
     return fail(c, GS_EDEVICE, "memset of window buffers failed");
+  c->misc_words = std::max<size_t>(4096, (size_t)c->G * kMaxWindow + 64);
   if (hipHostMalloc((void**)&c->h_cap, (kRegions + 1) * 8) != hipSuccess ||
-      hipHostMalloc((void**)&c->h_misc, 4096 * 8) != hipSuccess)
+      hipHostMalloc((void**)&c->h_misc, c->misc_words * 8) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_err, 64) != hipSuccess)
     return fail(c, GS_ENOMEM, "cannot allocate pinned window buffers");
   if (c->trials > 1) {
     const size_t tb = (size_t)c->trials * kMaxWindow * kTStatFields * 4;
@@ -494,10 +498,12 @@ int ctx_setup(gs_ctx* c, const gs_params* params, int device, bool shard, uint32
   s.key = Key{(uint32_t)c->p.seed, (uint32_t)(c->p.seed >> 32), c->p.trial};
   // Engine: the window engine unless the ring is too long for LDS, rows are
   // wider than 32 or the tick engine is forced; push-pull has its own kernels.
-  c->win = !c->pp && s.R <= kWinMaxRing && !(c->p.flags & GS_FLAG_TICK_ENGINE) && stride0 <= kWinMaxStride;
+  // (its coarse partition has 256 bins of 2^22 nodes: at most 2^30 nodes per context)
+  c->win = !c->pp && s.R <= kWinMaxRing && !(c->p.flags & GS_FLAG_TICK_ENGINE) && stride0 <= kWinMaxStride &&
+           s.n <= (1ull << (kCoarseShift + 8));
   if ((c->trials > 1 || shard) && !c->win) {
     why = "batched trials and node-range shards run on the window engine (delayhigh <= 256, "
-          "fanout/fanin <= 32, no GS_FLAG_TICK_ENGINE)";
+          "fanout/fanin <= 32, no GS_FLAG_TICK_ENGINE, at most 2^30 nodes per context or shard)";
     return GS_EINVAL;
   }
   // One state allocation, 256-B aligned sub-buffers; everything before
@@ -531,6 +537,7 @@ int ctx_setup(gs_ctx* c, const gs_params* params, int device, bool shard, uint32
   s.stats = (unsigned long long*)q; q += b_stats;
   c->d_err = (uint32_t*)q;
   c->d_flag = c->d_err + 1;
+  s.err = c->d_err;
   if (tick && s.kc > 0 && hipMalloc(&c->d_cnt, s.n * 4) != hipSuccess) {
     why = "cannot allocate arrival counters";
     return GS_ENOMEM;
@@ -591,7 +598,7 @@ void destroy_one(gs_ctx* c) {
   for (Buf* b : {&c->gmap, &c->cmsg, &c->fmsg, &c->tmp, &c->gfire, &c->pp_rend, &c->pp_rsrc, &c->pp_rslot,
                  &c->pp_ilist, &c->pp_fmask, &c->pp_scan, &c->pp_ctlb})
     if (b->p) (void)hipFree(b->p);
-  for (void* ptr : {(void*)c->h_cap, (void*)c->h_misc, (void*)c->h_stats, (void*)c->h_tstat, (void*)c->h_stage})
+  for (void* ptr : {(void*)c->h_cap, (void*)c->h_misc, (void*)c->h_err, (void*)c->h_stats, (void*)c->h_tstat, (void*)c->h_stage})
     if (ptr) (void)hipHostFree(ptr);
   for (void* ptr : {(void*)c->d_ctl, (void*)c->d_stage})
     if (ptr) (void)hipFree(ptr);
@@ -1693,12 +1700,12 @@ int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint
         CK(m, win_plan(w, false, m->stream));
         CK(m, win_part2(w, Tub, true, m->stream));
         if (e) CK(m, hipEventRecord(e[2], m->stream));
-        CK(m, hipMemcpyAsync(m->h_misc + 4090, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
+        CK(m, hipMemcpyAsync(m->h_err, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
       }
       RC(sync_all(ms));
       for (gs_ctx* m : ms) {  // regions sized from estimates: redo exactly on overflow
         WinState& w = m->ws;
-        uint32_t err = (uint32_t)m->h_misc[4090];
+        uint32_t err = *m->h_err;
         const unsigned long long Tub = Ftot * stride;
         if (err & kErrCoarse) {
           CK(m, hipMemsetAsync(w.chist, 0, kRegions * 8, m->stream));
@@ -1762,11 +1769,11 @@ int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint
   }
   for (gs_ctx* m : ms) {
     CK(m, hipSetDevice(m->dev));
-    CK(m, hipMemcpyAsync(m->h_misc + 4090, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
+    CK(m, hipMemcpyAsync(m->h_err, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
   }
   RC(sync_all(ms));
   for (gs_ctx* m : ms)
-    if (m->h_misc[4090] & 4) return fail(m, GS_EOVERFLOW, "too many arrivals at one node in one tick");
+    if (*m->h_err & kErrArrivals) return fail(m, GS_EOVERFLOW, "too many arrivals at one node in one tick");
   return GS_OK;
 }
 
@@ -1956,6 +1963,11 @@ int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
       CK(c, hipMemcpyAsync(c->h_tstat, c->d_tstat, (size_t)c->trials * kMaxWindow * kTStatFields * 4,
                            hipMemcpyDeviceToHost, c->stream));
     CK(c, hipStreamSynchronize(c->stream));
+    if (!c->win && !c->pp && !flood) {  // the tick engine's 16-bit receipt counts (MODE_COUNT)
+      uint32_t err = 0;
+      CK(c, hipMemcpy(&err, c->d_err, 4, hipMemcpyDeviceToHost));
+      if (err & kErrArrivals) return fail(c, GS_EOVERFLOW, "too many arrivals at one node in one tick");
+    }
     if (timing && !c->win) {
       for (uint32_t i = 0; i < batch; ++i) {
         hipEvent_t* e = &c->ev[(size_t)i * (flood || c->pp ? 2 : 4)];
@@ -2137,10 +2149,11 @@ namespace {
 // shard's own words at their global positions, batched trials trial-major.
 int read_bits(gs_ctx* c, int which, uint64_t* words, size_t nwords) {
   const uint64_t Wn = (c->p.n + 63) / 64;
-  if (c->group && c->gtrials) {
+  if (c->group && c->gtrials) {  // every member's trials, back to back: the caller's buffer holds them all
+    if (nwords < Wn * c->trials) return fail(c, GS_EINVAL, "need ceil(n/64) words per trial");
     uint64_t off = 0;
     for (gs_ctx* m : c->mem) {
-      if (read_bits(m, which, words + off * Wn, (size_t)m->trials * Wn)) return fail(c, GS_EINVAL, m->err);
+      if (read_bits(m, which, words + off * Wn, nwords - off * Wn)) return fail(c, GS_EINVAL, m->err);
       off += m->trials;
     }
     return GS_OK;

@@ -134,7 +134,10 @@ __device__ __forceinline__ void process_chunk(const DevState& st, uint32_t t, ui
         // the message's crash roll (:180), keyed by its sender's slot
         const uint32_t roll = (int32_t)uniform(lane_of(philox(v, t, j >> 2, ctr3(K_CRASH, st.key.trial),
                                                              st.key.k0, st.key.k1), j & 3), 100u) < st.kc;
-        atomicAdd(&st.cnt[u], 1u + (roll << 16));  // receipts | crash rolls << 16
+        // receipts | crash rolls << 16: the receipt count is 16 bits, so the
+        // 65536th arrival at one node in one tick is an overflow (GS_EOVERFLOW)
+        const uint32_t old = atomicAdd(&st.cnt[u], 1u + (roll << 16));
+        if ((old & 0xFFFFu) == 0xFFFFu) atomicOr(st.err, kErrArrivals);
       } else {
         const uint32_t k = atomicExch(&st.cnt[u], 0u);
         if (k) resolve_node(st, u, k & 0xFFFFu, k >> 16, t, c);

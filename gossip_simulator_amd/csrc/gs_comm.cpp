@@ -32,6 +32,7 @@ const Rccl& rccl() {
     g_rccl.get_unique_id = (decltype(g_rccl.get_unique_id))sym("ncclGetUniqueId");
     g_rccl.comm_init_rank = (decltype(g_rccl.comm_init_rank))sym("ncclCommInitRank");
     g_rccl.comm_destroy = (decltype(g_rccl.comm_destroy))sym("ncclCommDestroy");
+    g_rccl.comm_abort = (decltype(g_rccl.comm_abort))sym("ncclCommAbort");
     g_rccl.all_gather = (decltype(g_rccl.all_gather))sym("ncclAllGather");
     g_rccl.all_reduce = (decltype(g_rccl.all_reduce))sym("ncclAllReduce");
     g_rccl.error_string = (decltype(g_rccl.error_string))sym("ncclGetErrorString");

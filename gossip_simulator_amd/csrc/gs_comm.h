@@ -14,6 +14,7 @@ struct Rccl {
   ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
   ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
   ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                              hipStream_t) = nullptr;

@@ -60,6 +60,7 @@ struct DevState {
   uint32_t* clist;
   uint32_t* ccount;
   unsigned long long* stats;
+  uint32_t* err;           // error word (kErrArrivals: a 16-bit receipt count overflowed)
   uint64_t n, W;
   uint32_t C, CS, R, stride;
   uint32_t stride_magic;   // floor(2^32 / stride) + 1: exact q/stride for q < 2^18
@@ -182,7 +183,7 @@ __host__ __device__ __forceinline__ void node_key(uint32_t tlog, uint32_t tmask,
   c3 = ctr3(kind, key.trial + (uint32_t)(g >> tlog));
 }
 
-constexpr uint32_t kErrArrivals = 4;  // > 65535 arrivals at one node in one tick
+constexpr uint32_t kErrArrivals = 4;  // > 65535 arrivals at one node in one tick (both engines)
 constexpr uint32_t kErrCoarse = 8;    // a coarse region overflowed its estimate
 constexpr uint32_t kErrFine = 16;     // a fine region overflowed its estimate
 

@@ -141,7 +141,8 @@ int om_engine_step(om_engine* e, uint32_t ticks, or_tick_stats* out) {
     const uint64_t t = ++e->t;
     uint64_t* ring = e->ring + (t % e->R) * e->W;
     uint64_t fired = 0, sent = 0, msgs = 0, nrecv = 0, ncrash = 0;
-#pragma omp parallel num_threads(e->nth) reduction(+ : fired, sent, msgs, nrecv, ncrash)
+    int ovf = 0;
+#pragma omp parallel num_threads(e->nth) reduction(+ : fired, sent, msgs, nrecv, ncrash) reduction(| : ovf)
     {
       const int me = omp_get_thread_num();
       uint32_t* tl = e->touched[me];
@@ -168,7 +169,9 @@ int om_engine_step(om_engine* e, uint32_t ticks, or_tick_stats* out) {
             const uint32_t u = row[j];                                   /* :145 */
             ++sent;
             const uint32_t roll = e->kc > 0 && (int32_t)or_uniform(rc[j & 3], 100) < e->kc;  /* :180 */
-            if (__atomic_fetch_add(&e->cnt[u], 1u + (roll << 16), __ATOMIC_RELAXED) == 0) {
+            const uint32_t old = __atomic_fetch_add(&e->cnt[u], 1u + (roll << 16), __ATOMIC_RELAXED);
+            if ((old & 0xFFFFu) == 0xFFFFu) ovf = 1;  /* 16-bit receipt count: GS_EOVERFLOW */
+            if (old == 0) {
               if (nt == cap) {
                 cap *= 2;
                 uint32_t* g = (uint32_t*)realloc(tl, cap * 4);
@@ -203,6 +206,7 @@ int om_engine_step(om_engine* e, uint32_t ticks, or_tick_stats* out) {
         }
       }
     }
+    if (ovf) return OR_EOVERFLOW;  /* >= 65536 arrivals at one node in one tick */
     e->recv += nrecv;
     e->crashed_cnt += ncrash;
     e->pending = e->pending - fired + nrecv;

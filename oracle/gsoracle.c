@@ -454,7 +454,10 @@ int or_engine_step(or_engine* e, uint32_t ticks, or_tick_stats* out) {
           ++sent;
           const uint32_t roll = e->kc > 0 && (int32_t)or_uniform(rc[j & 3], 100) < e->kc;
           if (e->cnt[u] == 0) e->touched[nt++] = u;
-          e->cnt[u] += 1u + (roll << 16);  /* receipts | crash rolls << 16 */
+          /* receipts | crash rolls << 16: a 16-bit count, so >= 65536 arrivals at
+           * one node in one tick is an overflow (the engine returns GS_EOVERFLOW) */
+          if ((e->cnt[u] & 0xFFFFu) == 0xFFFFu) return OR_EOVERFLOW;
+          e->cnt[u] += 1u + (roll << 16);
         }
       }
     }

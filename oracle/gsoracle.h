@@ -51,6 +51,11 @@ enum {
                       * crashing message among a (node, tick)'s receipts        */
 };
 
+/* or_engine_step / om_engine_step: more than 65535 arrivals at one node in one
+ * tick overflow the 16-bit receipt count the engines pack (the HIP engine
+ * returns GS_EOVERFLOW for the same input). */
+#define OR_EOVERFLOW (-6)
+
 /* Dissemination models (or_params.model). */
 enum {
   OR_MODEL_FLOOD = 0,    /* the reference: push flooding (simulator.go:107-149)  */

@@ -16,6 +16,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "_build", "libgsoracle.so")
 _OMP_PATH = os.path.join(_HERE, "_build", "libgsomp.so")
+OR_EOVERFLOW = -6  # gsoracle.h: > 65535 arrivals at one node in one tick
 
 
 def build() -> str:
@@ -182,7 +183,10 @@ class Engine:
 
     def step(self, ticks: int = 1) -> np.ndarray:
         out = (TickStats * ticks)()
-        if lib().or_engine_step(self.h, ticks, out) != 0:
+        rc = lib().or_engine_step(self.h, ticks, out)
+        if rc == OR_EOVERFLOW:
+            raise OverflowError("or_engine_step: more than 65535 arrivals at one node in one tick")
+        if rc != 0:
             raise RuntimeError("or_engine_step failed")
         return np.array([[out[i].tick, out[i].fired, out[i].sent, out[i].messages,
                           out[i].received, out[i].crashed, out[i].pending]
@@ -274,7 +278,10 @@ class OmpEngine:
 
     def step(self, ticks: int = 1) -> np.ndarray:
         out = (TickStats * ticks)()
-        if omp_lib().om_engine_step(self.h, ticks, out) != 0:
+        rc = omp_lib().om_engine_step(self.h, ticks, out)
+        if rc == OR_EOVERFLOW:
+            raise OverflowError("om_engine_step: more than 65535 arrivals at one node in one tick")
+        if rc != 0:
             raise RuntimeError("om_engine_step failed")
         return np.array([[out[i].tick, out[i].fired, out[i].sent, out[i].messages,
                           out[i].received, out[i].crashed, out[i].pending]

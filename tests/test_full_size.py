@@ -11,7 +11,11 @@ implement the same tick model with no shared kernel code:
   broadcast is a scheduled one (pending never negative, 0 at quiescence);
 * the overlay respects fanout <= len(friends) <= fanin (simulator.go:68,80,96).
 Push-pull at N = 1e9: monotone informed set, pending == received, float32
-99 % reached, delivered <= calls.
+99 % reached, delivered <= calls; with a 1 % pre-failed mask the per-round
+counters and final bitsets are identical across the round selections auto /
+dense / topdown / bottom (independent kernels: sparse informed-list rounds,
+streamed top-down rounds with atomics, bottom-up in-edge scans).  The flood
+with the same 1 % mask: window engine vs tick engine, bit-exact per tick.
 """
 from __future__ import annotations
 
@@ -33,13 +37,24 @@ def sha(words: np.ndarray) -> str:
     return hashlib.sha256(words.tobytes()).hexdigest()
 
 
-def flood(engine: str):
+def failed_mask(frac: float, seed: int) -> np.ndarray:
+    """round(frac * N) node ids drawn uniformly (bench.py's failed_mask)."""
+    rng = np.random.default_rng(seed)
+    idx = rng.integers(0, N, size=int(round(frac * N)), dtype=np.int64)
+    w = np.zeros((N + 63) // 64, dtype=np.uint64)
+    np.bitwise_or.at(w, idx >> 6, np.left_shift(np.uint64(1), (idx & 63).astype(np.uint64)))
+    return w
+
+
+def flood(engine: str, mask=None):
     import gossip_simulator_amd as gs
     gs.load()
     cfg = gs.Config(n=N, fanout=5, fanin=6, droprate=0.1, crashrate=0.01, seed=0x5EED,
                     engine=engine)
     with gs.Simulator(cfg) as sim:
         _, stab = sim.build_overlay()
+        if mask is not None:
+            sim.set_failed(mask)
         if engine == "window":
             deg, _ = sim.read_peers()
             assert deg.min() >= 5 and deg.max() <= 6
@@ -85,3 +100,57 @@ def test_c5_pushpull_properties():
         assert (rows[:, 3] <= rows[:, 2]).all() and (rows[:, 2] <= rows[:, 1]).all()
         assert gs.covered(int(rec[-1]), N)
         assert popcount(sim.received()) == int(rec[-1])
+
+
+def test_c5_flood_failed_mask_window_vs_tick():
+    """C5's flood with 1 % of the nodes pre-failed (gs_set_failed): the two
+    engines agree per tick and on the final bitsets; failed nodes never count
+    nor forward (the crashed bitset holds the mask)."""
+    mask = failed_mask(0.01, 0x5EED + 1)
+    a = flood("window", mask)
+    b = flood("tick", mask)
+    assert np.array_equal(a[1], b[1]), "per-tick counters differ between the engines"
+    assert a[2] == b[2] and a[3] == b[3], "final bitsets differ between the engines"
+    nfail = popcount(mask)
+    assert a[5] >= nfail and 0.97 < a[4] / N < 0.99
+
+
+def pushpull_failed(pp_rounds: str, mask):
+    import gossip_simulator_amd as gs
+    gs.load()
+    cfg = gs.Config(n=N, fanout=5, fanin=6, droprate=0.1, crashrate=0.0, seed=0x5EED,
+                    model="pushpull", pp_rounds=pp_rounds)
+    with gs.Simulator(cfg) as sim:
+        sim.build_overlay()
+        sim.set_failed(mask)
+        sim.broadcast_begin(-1)
+        rows = []
+        while True:
+            r = sim.step(5)
+            rows.append(r)
+            if gs.covered(int(r[-1][4]), N) or len(rows) > 20:
+                break
+        tm = sim.timing()
+        rec = sim.received()
+        return np.concatenate(rows), sha(rec), popcount(rec), tm
+
+
+def test_c5_pushpull_failed_mask_round_modes_bit_exact():
+    mask = failed_mask(0.01, 0x5EED + 1)
+    ref = pushpull_failed("auto", mask)
+    rows, h, nrec, tm = ref
+    assert tm["pp_early_rounds"] > 0 and tm["pp_bottom_rounds"] > 0  # both special kernels ran
+    assert gs_covered(int(rows[-1][4]))
+    assert nrec == int(rows[-1][4])
+    rec = np.asarray(rows[:, 4], dtype=np.int64)
+    assert (np.diff(rec) >= 0).all() and (rows[:, 3] <= rows[:, 2]).all()
+    for mode in ("dense", "topdown", "bottom"):
+        got = pushpull_failed(mode, mask)
+        assert np.array_equal(got[0], rows), f"pp_rounds={mode}: per-round counters differ"
+        assert got[1] == h, f"pp_rounds={mode}: final informed set differs"
+        if mode == "dense":
+            assert got[3]["pp_early_rounds"] == 0 and got[3]["pp_bottom_rounds"] == 0
+
+
+def gs_covered(recv: int) -> bool:
+    return np.float32(recv) / np.float32(N) >= np.float32(0.99)

@@ -60,7 +60,7 @@ def c4_table(gs):
         return c, deg, ids, rows, sim.received(), sim.crashed()
 
 
-@pytest.mark.parametrize("G", [1, 2, 4])
+@pytest.mark.parametrize("G", [1, 2, 4, 8])
 def test_shards_match_unsharded_c4_shape(gs, c4_table, G):
     c, deg, ids, rows, recv, crash = c4_table
     with gs.Simulator(c, devices=[0] * G) as sim:
@@ -300,6 +300,32 @@ def test_gpu_native_rng_ks_1000_trials(gs, oracle):
     # power: a one-tick shift of the delay range is rejected at this size
     c = refsim_ticks(oracle, dict(KS_KW, delay_low=11, delay_high=21), KS_TRIALS, base=40_000)
     assert ks_2samp(a, c).pvalue < 0.01
+
+
+def refsim_degrees(oracle, n, runs, base=60_000):
+    """Friends-list lengths of `runs` or_refsim overlays (the Go-like event
+    model: one sequential stream, FIFO events), as a sample."""
+    p = oracle.make_params(n=n, seed=0x5EED)
+    ref = np.zeros(256, dtype=np.int64)
+    for s in range(runs):
+        ref += np.array(oracle.refsim(p, base + s).deg_hist[:256], dtype=np.int64)
+    return np.repeat(np.arange(256), ref)
+
+
+@pytest.mark.parametrize("n,trials", [(10_000, 40), (100_000, 8)])
+def test_gpu_overlay_degree_ks(gs, oracle, n, trials):
+    """KS (ks_2samp, p > 0.01) on overlay degrees, batched GPU
+    overlays (simulator.go:66-106 restated tick-synchronously) vs or_refsim, at
+    N = 1e4 and at C3's N = 1e5; a power check rejects fanin 7."""
+    with gs.Simulator(gs.Config(n=n, seed=0x5EED, trials=trials)) as sim:
+        sim.build_overlay()
+        deg, _ = sim.read_peers()
+    ref = refsim_degrees(oracle, n, trials)
+    res = ks_2samp(deg.astype(np.int64), ref)
+    assert res.pvalue > 0.01, (res, np.bincount(deg, minlength=8)[:8] / deg.size)
+    alt = np.concatenate([oracle.overlay(oracle.make_params(n=n, seed=0x5EED, fanin=7, trial=t))[0]
+                          for t in range(2)]).astype(np.int64)
+    assert ks_2samp(deg.astype(np.int64), alt).pvalue < 0.01
 
 
 def test_gpu_overlay_degree_histogram(gs, oracle):

@@ -6,7 +6,8 @@ overlay built.  Per-tick counters (fired, sent, TotalMessage, received,
 crashed, pending) and the final received / crashed bitsets must be identical.
 
 Config C5's parameters (fanout 5, fanin 6, delays 10-20, drop 0.1, crash 0.01)
-at N = 1e8, and C4's row shape (fanout 18, fanin 19) at N = 2e7: dense windows
+at N = 1e8, and config C4 as BASELINE.json names it (N = 1e8, fanout 18 =
+floor(ln 1e8), fanin 19; plus N = 2e7 of the same shape): dense windows
 with tens of thousands of receipts per 16384-node bucket, crashed and
 crash-rolled nodes in every bucket -- the k_resolve paths the small fixtures
 only touch lightly."""
@@ -20,7 +21,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n,fanout,fanin", [(100_000_000, 5, 6), (20_000_000, 18, 19)])
+@pytest.mark.parametrize("n,fanout,fanin", [(100_000_000, 5, 6), (20_000_000, 18, 19),
+                                            (100_000_000, 18, 19)])
 def test_window_engine_matches_port(oracle, n, fanout, fanin):
     import gossip_simulator_amd as gs
     gs.load()
@@ -29,7 +31,10 @@ def test_window_engine_matches_port(oracle, n, fanout, fanin):
     cfg = gs.Config(n=n, device=0, **kw)
     p = oracle.make_params(n=n, fanout=fanout, fanin=fanin, delay_low=10, delay_high=20, drop_rate=0.1,
                            crash_rate=0.01, seed=0x5EED, trial=3)
-    threads = min(16, os.cpu_count() or 1)
+    try:
+        threads = min(64, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        threads = min(16, os.cpu_count() or 1)
     with gs.Simulator(cfg) as sim:
         sim.build_overlay()
         deg, ids = sim.read_peers()

@@ -72,6 +72,24 @@ def test_overlay_degree_histograms_agree(oracle):
     assert np.abs(h_tick - h_ref).max() < 0.02, (h_tick, h_ref)
 
 
+def test_overlay_degrees_ks(oracle):
+    """SURVEY.md 8(c)4 on CPU: KS (p > 0.01) on overlay degrees, the tick-model
+    overlay (what the GPU builds, bit-exact) vs or_refsim, 40 overlays each at
+    N = 1e4; fanin 7 is rejected (power)."""
+    n, runs = 10_000, 40
+    a = np.concatenate([oracle.overlay(oracle.make_params(**dict(KW, n=n, trial=t)))[0]
+                        for t in range(runs)]).astype(np.int64)
+    p = oracle.make_params(**dict(KW, n=n))
+    h = np.zeros(256, dtype=np.int64)
+    for s in range(runs):
+        h += np.array(oracle.refsim(p, 60_000 + s).deg_hist[:256], dtype=np.int64)
+    b = np.repeat(np.arange(256), h)
+    assert ks_2samp(a, b).pvalue > 0.01
+    c = np.concatenate([oracle.overlay(oracle.make_params(**dict(KW, n=n, fanin=7, trial=t)))[0]
+                        for t in range(2)]).astype(np.int64)
+    assert ks_2samp(c, b).pvalue < 0.01
+
+
 def test_ks_detects_a_real_difference(oracle):
     """Power check: a changed delay range must be rejected."""
     a = tick_model_sample(oracle, KW, 150)
