@@ -35,6 +35,7 @@ EXPORTS = (
     "gs_format_float64", "gs_format_duration", "gs_threshold", "gs_philox",
     "gs_set_flags", "gs_reset", "gs_set_stream", "gs_create_multi", "gs_comm_unique_id",
     "gs_create_rank", "gs_shard_info", "gs_trial_results", "gs_set_trial",
+    "gs_create_rank_exchange", "gs_shard_timing",
 )
 
 
@@ -88,6 +89,15 @@ class Timing(C.Structure):
                 ("pp_early_rounds", C.c_uint64), ("pp_bottom_rounds", C.c_uint64)]
 
 
+# gs_exchange (gossip.h): host callbacks of a gs_create_rank_exchange rank
+ALL_GATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
+ALL_REDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t)
+
+
+class Exchange(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("all_gather", ALL_GATHER_FN), ("all_reduce_sum_u64", ALL_REDUCE_FN)]
+
+
 _lib = None
 
 
@@ -119,6 +129,7 @@ def load():
         "gs_read_received": ([ctx, vp, sz], C.c_int),
         "gs_read_crashed": ([ctx, vp, sz], C.c_int),
         "gs_timing_get": ([ctx, P(Timing)], C.c_int),
+        "gs_shard_timing": ([ctx, C.c_uint32, P(Timing)], C.c_int),
         "gs_format_float32": ([C.c_float, C.c_char_p, sz], sz),
         "gs_format_float64": ([C.c_double, C.c_char_p, sz], sz),
         "gs_format_duration": ([C.c_int64, C.c_char_p, sz], sz),
@@ -130,6 +141,7 @@ def load():
         "gs_create_multi": ([P(Params), P(C.c_int), C.c_int, P(vp)], C.c_int),
         "gs_comm_unique_id": ([C.c_char_p], C.c_int),
         "gs_create_rank": ([P(Params), C.c_int, C.c_int, C.c_int, C.c_char_p, P(vp)], C.c_int),
+        "gs_create_rank_exchange": ([P(Params), C.c_int, C.c_int, C.c_int, P(Exchange), P(vp)], C.c_int),
         "gs_shard_info": ([ctx, C.c_uint32, P(C.c_uint32), P(C.c_uint64), P(C.c_uint64)], C.c_int),
         "gs_trial_results": ([ctx, P(TrialStats), sz, P(sz)], C.c_int),
         "gs_set_trial": ([ctx, C.c_uint32], C.c_int),

@@ -103,12 +103,26 @@ struct gs_ctx {
   bool shard = false;
   uint32_t G = 1, rank = 0;
   uint64_t lo = 0, hi = 0, seg_per = 0;
-  uint32_t* d_prow = nullptr;           // [n + 1] partitioned row starts
-  uint32_t* d_pent = nullptr;           // owned slots: (target - lo) << 5 | j, [n][pw]
+  uint32_t* d_pent = nullptr;           // [n][pw]: owned-slot mask + owned targets - lo (or a spill offset)
+  uint32_t* d_pspill = nullptr;         // targets of the rows that do not fit pw - 1
   uint32_t pw = 0;                      // partitioned row width
+  uint64_t spilled = 0;                 // rows whose targets are in the spill array
   Buf gfire;                            // multi-process: this rank's all-gather buffer
   unsigned long long* d_gcounts = nullptr;  // multi-process: [G][16] gathered fires per tick
   ncclComm_t comm = nullptr;
+  // multi-process exchange done by the caller (gs_create_rank_exchange)
+  gs_exchange hx{};
+  bool has_hx = false;
+  char* h_xbuf = nullptr;               // pinned staging of the host exchanges
+  size_t h_xbytes = 0;
+  // push-pull node-range shard: the informed / failed sets by global id
+  // (G * segw words; shared by the members on one device, owned by a rank);
+  // st.recv / st.crash are this shard's slice of them
+  bool pp_shard = false, own_ig = false;
+  bool aborted = false;                 // a rank whose exchange failed (RCCL communicator aborted)
+  unsigned long long* d_ig = nullptr;
+  unsigned long long* d_fg = nullptr;
+  uint64_t segw = 0;
   // group (gs_create_multi)
   bool group = false, gtrials = false;
   std::vector<gs_ctx*> mem;
@@ -116,6 +130,7 @@ struct gs_ctx {
   std::vector<int> gdev_of;             // member -> index into gdevs
   std::vector<Buf> gbuf;                // one all-gather buffer per distinct device
   std::vector<hipEvent_t> gev_c, gev_x; // per member: compaction done; per device: copies done
+  std::vector<unsigned long long*> gig, gfg;  // push-pull shards: per distinct device, the replicated sets
   OverlayWork ovw;                      // overlay builder buffers, kept between builds
 };
 
@@ -265,9 +280,10 @@ void refresh_window(gs_ctx* c) {
   w.stride = c->st.stride;
   w.slots = c->row_slots && c->row_slots < c->st.stride ? c->row_slots : c->st.stride;
   w.stride_magic = c->st.stride_magic;
-  w.prow = c->d_prow;
   w.pent = c->d_pent;
+  w.pspill = c->d_pspill;
   w.pw = c->pw;
+  w.abort_on_err = c->shard ? 1u : 0u;
 }
 
 uint32_t ring_slots(const gs_params& p) { return p.delay_high > 2 ? (uint32_t)p.delay_high : 2u; }
@@ -381,40 +397,53 @@ int seal_rows(gs_ctx* c, const uint8_t* deg, uint32_t* ids, uint64_t n) {
   return GS_OK;
 }
 
-// Shard c's partition of the sealed global table (ids, on c's device):
-// fixed-width rows of pw = (the most owned slots any node has, rounded up to
-// 4) entries, so k_expand_sh reads a firing node's owned slots with one
-// dependent load (no row index).
+// Shard c's partition of the sealed global table (ids, on c's device), for
+// every node v: [owned-slot mask, owned targets - lo ...] in rows of pw words,
+// pw the smallest multiple of 4 that keeps 99.5 % of the rows inline (the
+// rest keep their targets in the spill array): k_expand_sh reads a firing
+// node's owned slots with one dependent load, and local ids are full 32-bit.
 int partition(gs_ctx* c, const uint32_t* ids) {
   const uint64_t n = c->p.n;
-  if (c->d_prow) (void)hipFree(c->d_prow);
+  if (c->d_pspill) (void)hipFree(c->d_pspill);
   if (c->d_pent) (void)hipFree(c->d_pent);
-  c->d_prow = nullptr;
+  c->d_pspill = nullptr;
   c->d_pent = nullptr;
   c->pw = 0;
   uint32_t* cnt = nullptr;
+  unsigned long long* hist = nullptr;  // [0, 33): rows by owned slots; [33]: spill fill
+  unsigned long long h[kWinMaxStride + 2] = {};
   int rc = GS_OK;
-  uint32_t mx = 0;
   auto bail = [&](int code, const std::string& m) { rc = fail(c, code, m); };
-  if (hipMalloc(&cnt, (n + 1) * 4) != hipSuccess) {
+  if (hipMalloc(&cnt, n * 4) != hipSuccess || hipMalloc(&hist, (kWinMaxStride + 2) * 8) != hipSuccess) {
     bail(GS_ENOMEM, "cannot allocate the shard's slot counts");
-  } else if (hipMemsetAsync(cnt + n, 0, 4, c->stream) != hipSuccess ||
+  } else if (hipMemsetAsync(hist, 0, (kWinMaxStride + 2) * 8, c->stream) != hipSuccess ||
              part_count(ids, n, c->st.stride, (uint32_t)c->lo, (uint32_t)c->hi, cnt, c->stream) != hipSuccess ||
-             part_max(cnt, n, cnt + n, c->stream) != hipSuccess ||
-             hipMemcpyAsync(&mx, cnt + n, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+             part_hist(cnt, n, hist, c->stream) != hipSuccess ||
+             hipMemcpyAsync(h, hist, sizeof h, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
              hipStreamSynchronize(c->stream) != hipSuccess) {
     bail(GS_EDEVICE, "counting the shard's slots failed");
   } else {
-    c->pw = std::max<uint32_t>(4, (mx + 3) & ~3u);
-    if (hipMalloc(&c->d_pent, n * c->pw * 4ull) != hipSuccess) {
+    uint32_t mx = 0;
+    for (uint32_t k = 0; k <= kWinMaxStride; ++k)
+      if (h[k]) mx = k;
+    uint64_t spilled = 0, spill_e = 0;
+    for (c->pw = 4;; c->pw += 4) {
+      spilled = spill_e = 0;
+      for (uint32_t k = c->pw; k <= kWinMaxStride; ++k) { spilled += h[k]; spill_e += (uint64_t)k * h[k]; }
+      if (c->pw > mx || spilled * 200 <= n) break;
+    }
+    c->spilled = spilled;
+    if (hipMalloc(&c->d_pent, n * c->pw * 4ull) != hipSuccess ||
+        hipMalloc(&c->d_pspill, std::max<uint64_t>(spill_e, 1) * 4) != hipSuccess) {
       bail(GS_ENOMEM, "cannot allocate " + std::to_string(n * c->pw) + " partitioned friend slots");
-    } else if (part_fill_fixed(ids, n, c->st.stride, (uint32_t)c->lo, (uint32_t)c->hi, c->pw, c->d_pent,
-                               c->stream) != hipSuccess ||
+    } else if (part_fill_mask(ids, n, c->st.stride, (uint32_t)c->lo, (uint32_t)c->hi, c->pw, c->d_pent, c->d_pspill,
+                              hist + kWinMaxStride + 1, c->stream) != hipSuccess ||
                hipStreamSynchronize(c->stream) != hipSuccess) {
       bail(GS_EDEVICE, "filling the shard's partition failed");
     }
   }
   if (cnt) (void)hipFree(cnt);
+  if (hist) (void)hipFree(hist);
   refresh_window(c);
   return rc;
 }
@@ -469,14 +498,18 @@ int ctx_setup(gs_ctx* c, const gs_params* params, int device, bool shard, uint32
   c->G = G;
   c->rank = rank;
   if (shard) {
-    if (c->pp) { why = "push-pull runs are not node-range sharded (shard trials instead)"; return GS_EINVAL; }
+    if (c->pp && !pp_rslot_packed(stride0)) {
+      why = "push-pull node-range shards need rows of at most 16 slots (bottom-up rounds)";
+      return GS_EINVAL;
+    }
     c->seg_per = (((c->p.n + G - 1) / G) + kFineNodes - 1) & ~(uint64_t)(kFineNodes - 1);
     if ((uint64_t)(G - 1) * c->seg_per >= c->p.n) {
       why = "n = " + std::to_string(c->p.n) + " is too small for " + std::to_string(G) +
             " shards of whole 16384-node buckets";
       return GS_EINVAL;
     }
-    if (c->seg_per >= (1ull << 27)) { why = "a shard may own fewer than 2^27 nodes: use more shards"; return GS_EINVAL; }
+    c->pp_shard = c->pp;
+    c->segw = c->seg_per / 64;
     c->lo = rank * c->seg_per;
     c->hi = std::min<uint64_t>(c->lo + c->seg_per, c->p.n);
     c->ntot = c->hi - c->lo;
@@ -501,7 +534,7 @@ int ctx_setup(gs_ctx* c, const gs_params* params, int device, bool shard, uint32
   // (its coarse partition has 256 bins of 2^22 nodes: at most 2^30 nodes per context)
   c->win = !c->pp && s.R <= kWinMaxRing && !(c->p.flags & GS_FLAG_TICK_ENGINE) && stride0 <= kWinMaxStride &&
            s.n <= (1ull << (kCoarseShift + 8));
-  if ((c->trials > 1 || shard) && !c->win) {
+  if ((c->trials > 1 || (shard && !c->pp)) && !c->win) {
     why = "batched trials and node-range shards run on the window engine (delayhigh <= 256, "
           "fanout/fanin <= 32, no GS_FLAG_TICK_ENGINE, at most 2^30 nodes per context or shard)";
     return GS_EINVAL;
@@ -538,6 +571,9 @@ int ctx_setup(gs_ctx* c, const gs_params* params, int device, bool shard, uint32
   c->d_err = (uint32_t*)q;
   c->d_flag = c->d_err + 1;
   s.err = c->d_err;
+  s.grecv = s.recv;  // a push-pull shard points these at the replicated sets (attach_pp_sets)
+  s.gcrash = s.crash;
+  s.gbase = 0;
   if (tick && s.kc > 0 && hipMalloc(&c->d_cnt, s.n * 4) != hipSuccess) {
     why = "cannot allocate arrival counters";
     return GS_ENOMEM;
@@ -569,6 +605,11 @@ void destroy_one(gs_ctx* c) {
         (void)hipSetDevice(c->gdevs[i]);
         (void)hipFree(c->gbuf[i].p);
       }
+    for (size_t i = 0; i < c->gdevs.size(); ++i) {
+      (void)hipSetDevice(c->gdevs[i]);
+      if (i < c->gig.size() && c->gig[i]) (void)hipFree(c->gig[i]);
+      if (i < c->gfg.size() && c->gfg[i]) (void)hipFree(c->gfg[i]);
+    }
     for (hipEvent_t e : c->gev_c) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->gev_x) (void)hipEventDestroy(e);
     delete c;
@@ -592,8 +633,13 @@ void destroy_one(gs_ctx* c) {
   }
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   overlay_free(&c->ovw);
+  if (c->own_ig) {
+    if (c->d_ig) (void)hipFree(c->d_ig);
+    if (c->d_fg) (void)hipFree(c->d_fg);
+  }
+  if (c->h_xbuf) (void)hipHostFree(c->h_xbuf);
   for (void* ptr : {(void*)c->d_deg, (void*)c->d_ids, c->d_state, (void*)c->d_cnt, (void*)c->d_failed, c->d_win,
-                    c->d_flist, c->d_rlmsg, (void*)c->d_tstat, (void*)c->d_prow, (void*)c->d_pent, (void*)c->d_gcounts})
+                    c->d_flist, c->d_rlmsg, (void*)c->d_tstat, (void*)c->d_pspill, (void*)c->d_pent, (void*)c->d_gcounts})
     if (ptr) (void)hipFree(ptr);
   for (Buf* b : {&c->gmap, &c->cmsg, &c->fmsg, &c->tmp, &c->gfire, &c->pp_rend, &c->pp_rsrc, &c->pp_rslot,
                  &c->pp_ilist, &c->pp_fmask, &c->pp_scan, &c->pp_ctlb})
@@ -645,6 +691,117 @@ int par_members(gs_ctx* g, F f) {
 void reset_counters(gs_ctx* c) {
   c->t = c->fired = c->sent = c->msgs = c->recv = c->crashed = c->pending = 0;
   for (TrialAcc& a : c->tacc) a = TrialAcc{};
+}
+
+// ---- multi-process exchange ----------------------------------
+// A rank context exchanges through RCCL (gs_create_rank) or the caller's host
+// callbacks (gs_create_rank_exchange); both are stream-ordered on c->stream.
+bool is_rank(const gs_ctx* c) { return c->comm != nullptr || c->has_hx; }
+
+bool grow_pinned(gs_ctx* c, size_t bytes) {
+  if (c->h_xbytes >= bytes) return true;
+  const size_t nb = std::max(bytes, c->h_xbytes + c->h_xbytes / 4);
+  if (c->h_xbuf) (void)hipHostFree(c->h_xbuf);
+  c->h_xbuf = nullptr;
+  c->h_xbytes = 0;
+  if (hipHostMalloc((void**)&c->h_xbuf, nb) != hipSuccess) return false;
+  c->h_xbytes = nb;
+  return true;
+}
+
+// In place: rank r's `bytes` at dbuf + r * bytes go to every rank.
+int x_all_gather(gs_ctx* c, void* dbuf, size_t bytes) {
+  if (c->comm) {
+    NCK(c, rccl().all_gather((char*)dbuf + (size_t)c->rank * bytes, dbuf, bytes, ncclUint8, c->comm, c->stream));
+    return GS_OK;
+  }
+  if (!grow_pinned(c, ((size_t)c->G + 1) * bytes)) return fail(c, GS_ENOMEM, "cannot allocate exchange staging");
+  char* send = c->h_xbuf + (size_t)c->G * bytes;
+  CK(c, hipMemcpyAsync(send, (char*)dbuf + (size_t)c->rank * bytes, bytes, hipMemcpyDeviceToHost, c->stream));
+  CK(c, hipStreamSynchronize(c->stream));
+  if (c->hx.all_gather(c->hx.user, send, c->h_xbuf, bytes))
+    return fail(c, GS_EDEVICE, "the exchange's all_gather callback failed");
+  CK(c, hipMemcpyAsync(dbuf, c->h_xbuf, (size_t)c->G * bytes, hipMemcpyHostToDevice, c->stream));
+  CK(c, hipStreamSynchronize(c->stream));
+  return GS_OK;
+}
+
+// In place: element-wise sum of `count` u64 over the ranks.
+int x_all_reduce(gs_ctx* c, unsigned long long* dbuf, size_t count) {
+  if (c->comm) {
+    NCK(c, rccl().all_reduce(dbuf, dbuf, count, ncclUint64, ncclSum, c->comm, c->stream));
+    return GS_OK;
+  }
+  if (!grow_pinned(c, count * 8)) return fail(c, GS_ENOMEM, "cannot allocate exchange staging");
+  CK(c, hipMemcpyAsync(c->h_xbuf, dbuf, count * 8, hipMemcpyDeviceToHost, c->stream));
+  CK(c, hipStreamSynchronize(c->stream));
+  if (c->hx.all_reduce_sum_u64(c->hx.user, (uint64_t*)c->h_xbuf, count))
+    return fail(c, GS_EDEVICE, "the exchange's all_reduce_sum_u64 callback failed");
+  CK(c, hipMemcpyAsync(dbuf, c->h_xbuf, count * 8, hipMemcpyHostToDevice, c->stream));
+  CK(c, hipStreamSynchronize(c->stream));
+  return GS_OK;
+}
+
+// A rank whose collective failed is torn down so that the other ranks' RCCL
+// calls fail instead of waiting for it (and torchrun-style launchers end the
+// job when this process exits with the error).
+int abort_rank(gs_ctx* c, int rc) {
+  if (rc && is_rank(c)) c->aborted = true;
+  if (rc && c->comm && rccl().ok && rccl().comm_abort) {
+    (void)rccl().comm_abort(c->comm);
+    c->comm = nullptr;
+  }
+  return rc;
+}
+
+// Push-pull shard c uses the replicated informed / failed sets ig / fg
+// (G * segw words each): its own nodes are words [rank * segw, ...).
+void attach_pp_sets(gs_ctx* c, unsigned long long* ig, unsigned long long* fg) {
+  c->d_ig = ig;
+  c->d_fg = fg;
+  DevState& s = c->st;
+  s.grecv = ig;
+  s.gcrash = fg;
+  s.gbase = c->lo;
+  s.recv = ig + (size_t)c->rank * c->segw;
+  s.crash = fg + (size_t)c->rank * c->segw;
+}
+
+int alloc_pp_sets(gs_ctx* c, uint64_t words, unsigned long long** ig, unsigned long long** fg);
+
+// The rest of a rank context once its exchange is set: gathered fire counts
+// (flood) or its own replicated sets (push-pull).
+int finish_rank(gs_ctx* c, gs_ctx** out) {
+  (void)hipSetDevice(c->dev);
+  if (hipMalloc(&c->d_gcounts, (size_t)c->G * kMaxWindow * 8 + (size_t)kMaxWindow * 8) != hipSuccess) {
+    destroy_one(c);
+    return GS_ENOMEM;
+  }
+  if (c->pp_shard) {
+    unsigned long long *ig = nullptr, *fg = nullptr;
+    if (alloc_pp_sets(c, (uint64_t)c->G * c->segw, &ig, &fg)) {
+      fprintf(stderr, "gs_create_rank: %s\n", c->err.c_str());
+      if (ig) (void)hipFree(ig);
+      if (fg) (void)hipFree(fg);
+      destroy_one(c);
+      return GS_ENOMEM;
+    }
+    c->own_ig = true;
+    attach_pp_sets(c, ig, fg);
+  }
+  *out = c;
+  return GS_OK;
+}
+
+// Allocates and zeroes a pair of replicated sets for G shards of segw words.
+int alloc_pp_sets(gs_ctx* c, uint64_t words, unsigned long long** ig, unsigned long long** fg) {
+  *ig = *fg = nullptr;
+  if (hipMalloc(ig, words * 8) != hipSuccess || hipMalloc(fg, words * 8) != hipSuccess)
+    return fail(c, GS_ENOMEM, "cannot allocate the replicated informed / failed sets");
+  CK(c, hipMemsetAsync(*ig, 0, words * 8, c->stream));
+  CK(c, hipMemsetAsync(*fg, 0, words * 8, c->stream));
+  CK(c, hipStreamSynchronize(c->stream));
+  return GS_OK;
 }
 
 }  // namespace
@@ -710,6 +867,23 @@ int gs_create_multi(const gs_params* params, const int* devices, int ndev, gs_ct
     }
   }
   g->gbuf.resize(g->gdevs.size());
+  g->pp = params->model == GS_MODEL_PUSHPULL;
+  if (g->pp && !g->gtrials) {  // push-pull shards: one pair of replicated sets per device
+    g->gig.assign(g->gdevs.size(), nullptr);
+    g->gfg.assign(g->gdevs.size(), nullptr);
+    for (size_t d = 0; d < g->gdevs.size(); ++d) {
+      std::vector<gs_ctx*> ms;
+      for (size_t i = 0; i < g->mem.size(); ++i)
+        if ((size_t)g->gdev_of[i] == d) ms.push_back(g->mem[i]);
+      (void)hipSetDevice(g->gdevs[d]);
+      if (alloc_pp_sets(ms[0], (uint64_t)g->mem.size() * ms[0]->segw, &g->gig[d], &g->gfg[d])) {
+        fprintf(stderr, "gs_create_multi: %s\n", ms[0]->err.c_str());
+        destroy_one(g);
+        return GS_ENOMEM;
+      }
+      for (gs_ctx* m : ms) attach_pp_sets(m, g->gig[d], g->gfg[d]);
+    }
+  }
   for (size_t i = 0; i < g->mem.size(); ++i) {
     hipEvent_t e;
     (void)hipSetDevice(g->mem[i]->dev);
@@ -781,12 +955,22 @@ int gs_create_rank(const gs_params* params, int device, int nranks, int rank, co
     destroy_one(c);
     return GS_EDEVICE;
   }
-  if (hipMalloc(&c->d_gcounts, (size_t)nranks * kMaxWindow * 8 + (size_t)kMaxWindow * 8) != hipSuccess) {
-    destroy_one(c);
-    return GS_ENOMEM;
-  }
-  *out = c;
-  return GS_OK;
+  return finish_rank(c, out);
+}
+
+int gs_create_rank_exchange(const gs_params* params, int device, int nranks, int rank, const gs_exchange* ex,
+                            gs_ctx** out) {
+  if (!out || !params || !ex || !ex->all_gather || !ex->all_reduce_sum_u64 || nranks < 1 || rank < 0 ||
+      rank >= nranks)
+    return GS_EINVAL;
+  *out = nullptr;
+  if (std::max<uint32_t>(1, params->trials) > 1) return gs_create_rank(params, device, nranks, rank, nullptr, out);
+  gs_ctx* c = nullptr;
+  int rc = create_one(params, device, true, (uint32_t)nranks, (uint32_t)rank, &c);
+  if (rc) return rc;
+  c->hx = *ex;
+  c->has_hx = true;
+  return finish_rank(c, out);
 }
 
 int gs_shard_info(const gs_ctx* c, uint32_t index, uint32_t* nshards, uint64_t* lo, uint64_t* hi) {
@@ -857,9 +1041,79 @@ int upload_table(gs_ctx* c, const uint8_t* deg, const uint32_t* ids, uint32_t st
   return validate_table(c, c->d_deg, c->d_ids, n, c->p.n);
 }
 
+// Push-pull shards: each member keeps the rows of its own nodes (its callers)
+// and the reverse table of its own nodes (in-edges from every caller), built
+// from the leader's full table, which is then dropped.
+int partition_pp(gs_ctx* leader, const std::vector<gs_ctx*>& ms) {
+  uint8_t* fdeg = leader->d_deg;
+  uint32_t* fids = leader->d_ids;
+  const uint32_t S = leader->st.stride;
+  const uint64_t N = leader->p.n;
+  leader->d_deg = nullptr;
+  leader->d_ids = nullptr;
+  leader->tab_stride = 0;
+  int rc = GS_OK;
+  for (gs_ctx* m : ms) {
+    const uint64_t n = m->ntot;
+    if (m->d_deg) (void)hipFree(m->d_deg);
+    if (m->d_ids) (void)hipFree(m->d_ids);
+    m->d_deg = nullptr;
+    m->d_ids = nullptr;
+    if (hipMalloc(&m->d_deg, n) != hipSuccess || hipMalloc(&m->d_ids, n * S * 4ull) != hipSuccess) {
+      rc = fail(m, GS_ENOMEM, "cannot allocate the shard's rows");
+      break;
+    }
+    m->tab_stride = 0;  // not the full-table shape: the next load reallocates
+    if ((rc = set_stride(m, S))) break;
+    refresh_state(m);
+    if (hipMemcpyAsync(m->d_deg, fdeg + m->lo, n, hipMemcpyDeviceToDevice, leader->stream) != hipSuccess ||
+        hipMemcpyAsync(m->d_ids, fids + m->lo * S, n * S * 4ull, hipMemcpyDeviceToDevice, leader->stream) !=
+            hipSuccess) {
+      rc = fail(m, GS_EDEVICE, "copying the shard's rows failed");
+      break;
+    }
+    // reverse table of [lo, hi): count + scan, then size the edge arrays
+    const size_t scan = pp_rev_range_scan_bytes(n);
+    if (!grow(m->pp_rend, (n + 1) * 8) || !grow(m->pp_scan, scan + 256) || !grow(m->pp_ctlb, sizeof(PPCtl))) {
+      rc = fail(m, GS_ENOMEM, "cannot allocate the shard's reverse table");
+      break;
+    }
+    unsigned long long* rend = (unsigned long long*)m->pp_rend.p;
+    if (pp_rev_count_range(fdeg, fids, N, S, m->lo, m->hi, rend, m->pp_scan.p, m->pp_scan.bytes, leader->stream) !=
+        hipSuccess) {
+      rc = fail(m, GS_EDEVICE, "counting the shard's in-edges failed");
+      break;
+    }
+    unsigned long long E = 0;
+    if (hipMemcpyAsync(&E, rend + n, 8, hipMemcpyDeviceToHost, leader->stream) != hipSuccess ||
+        hipStreamSynchronize(leader->stream) != hipSuccess) {
+      rc = fail(m, GS_EDEVICE, "reading the shard's in-edge count failed");
+      break;
+    }
+    if (!grow(m->pp_rsrc, std::max<uint64_t>(E, 1) * 4) || !grow(m->pp_rslot, std::max<uint64_t>(E, 1))) {
+      rc = fail(m, GS_ENOMEM, "cannot allocate the shard's in-edges");
+      break;
+    }
+    if (pp_rev_fill_range(fdeg, fids, N, S, m->lo, m->hi, rend, (uint32_t*)m->pp_rsrc.p, (uint8_t*)m->pp_rslot.p,
+                          leader->stream) != hipSuccess ||
+        hipStreamSynchronize(leader->stream) != hipSuccess) {
+      rc = fail(m, GS_EDEVICE, "filling the shard's in-edges failed");
+      break;
+    }
+    ++m->table_ver;
+    m->rev_ver = m->table_ver;
+    m->fm_tver = ~0ull;
+    m->peers = true;
+  }
+  (void)hipFree(fdeg);
+  (void)hipFree(fids);
+  return rc;
+}
+
 // Shards: partition every member on the leader's device from the leader's
 // sealed table, then drop the replicated table.
 int partition_from(gs_ctx* leader, const std::vector<gs_ctx*>& ms) {
+  if (leader->pp_shard) return partition_pp(leader, ms);
   for (gs_ctx* m : ms) {
     if (m != leader) {
       RC(set_stride(m, leader->st.stride));
@@ -1080,6 +1334,18 @@ int gs_set_failed(gs_ctx* c, const uint64_t* words, size_t nwords) {
     return GS_OK;
   }
   CK(c, hipSetDevice(c->dev));
+  if (c->pp_shard) {  // the replicated failed set: every word (k_ppb_round reads the callers' friends)
+    if (c->st.stride > 8) return fail(c, GS_EINVAL, "push-pull shards take a failure mask with rows <= 8 slots");
+    const uint64_t Wg = (c->p.n + 63) / 64;
+    std::vector<uint64_t> w(words, words + Wg);
+    if (c->p.n & 63) w[Wg - 1] &= (1ull << (c->p.n & 63)) - 1;
+    CK(c, hipMemcpyAsync(c->d_fg, w.data(), Wg * 8, hipMemcpyHostToDevice, c->stream));
+    CK(c, hipStreamSynchronize(c->stream));
+    c->failed = true;
+    c->st.check_crashed = 1;
+    ++c->fail_ver;
+    return GS_OK;
+  }
   const uint64_t W = c->st.W, w0 = c->lo / 64;  // this context's words (a shard's own range)
   std::vector<uint64_t> w(words + w0, words + w0 + W);
   if (c->ntot & 63) w[W - 1] &= (1ull << (c->ntot & 63)) - 1;
@@ -1144,6 +1410,22 @@ int begin_one(gs_ctx* c, uint64_t s, uint32_t* sched) {
 // not fit, leave the dense rounds only (same results).
 int pp_prepare(gs_ctx* c) {
   c->sp = PPSparse{};
+  if (c->pp_shard) {  // bottom-up rounds only: the partition built the reverse table
+    c->sp.ctl = (PPCtl*)c->pp_ctlb.p;
+    c->sp.rend = (const unsigned long long*)c->pp_rend.p;
+    c->sp.rsrc = (const uint32_t*)c->pp_rsrc.p;
+    c->sp.rslot = (const uint8_t*)c->pp_rslot.p;
+    if (c->failed) {
+      if (c->fm_tver != c->table_ver || c->fm_fver != c->fail_ver) {
+        if (!grow(c->pp_fmask, (c->st.n + 3) & ~3ull)) return fail(c, GS_ENOMEM, "cannot allocate the failed-slot mask");
+        CK(c, pp_fmask_rows(c->st, (uint8_t*)c->pp_fmask.p, c->stream));
+        c->fm_tver = c->table_ver;
+        c->fm_fver = c->fail_ver;
+      }
+      c->sp.fmask = (const uint8_t*)c->pp_fmask.p;
+    }
+    return GS_OK;
+  }
   if (c->p.flags & GS_FLAG_PP_DENSE) return GS_OK;
   const DevState& s = c->st;
   const uint64_t n = s.n, E = n * s.stride;
@@ -1206,12 +1488,165 @@ unsigned long long pp_bottom_thr(const gs_ctx* c) {
   return k == 256 ? ~0ull : (unsigned long long)(((unsigned __int128)c->st.n * k) >> 8);
 }
 
+// ---- push-pull node-range shards (SURVEY.md 8(e)2 for config C5) -------------
+// Every shard owns nodes [lo, hi): their rows (calls) and their in-edges
+// (pushes they receive), and a replicated copy of the informed set by global
+// id.  A round is bottom-up on the own nodes against the replicated set
+// (k_ppb_round: same draws and counters as the unsharded rounds, so the union
+// equals the unsharded run bit for bit); then the shards exchange their own
+// informed words: events only between members that share a device's arrays,
+// peer copies between devices, an all-gather between ranks.
+int pp_exchange(gs_ctx* acc, const std::vector<gs_ctx*>& ms) {
+  if (!acc->group) return x_all_gather(acc, acc->d_ig, acc->segw * 8);
+  const bool multi = acc->gdevs.size() > 1;
+  for (size_t i = 0; i < ms.size(); ++i) {
+    CK(ms[i], hipSetDevice(ms[i]->dev));
+    CK(ms[i], hipEventRecord(acc->gev_c[i], ms[i]->stream));
+  }
+  if (multi) {
+    for (size_t d = 0; d < acc->gdevs.size(); ++d) {
+      gs_ctx* L = nullptr;
+      for (size_t i = 0; i < ms.size() && !L; ++i)
+        if ((size_t)acc->gdev_of[i] == d) L = ms[i];
+      CK(L, hipSetDevice(L->dev));
+      for (size_t j = 0; j < ms.size(); ++j) {
+        const size_t dj = (size_t)acc->gdev_of[j];
+        if (dj == d) continue;
+        CK(L, hipStreamWaitEvent(L->stream, acc->gev_c[j], 0));
+        const size_t off = (size_t)ms[j]->rank * ms[j]->segw;
+        CK(L, hipMemcpyPeerAsync(acc->gig[d] + off, L->dev, acc->gig[dj] + off, ms[j]->dev, ms[j]->segw * 8,
+                                 L->stream));
+      }
+      CK(L, hipEventRecord(acc->gev_x[d], L->stream));
+    }
+  }
+  for (size_t i = 0; i < ms.size(); ++i) {
+    gs_ctx* m = ms[i];
+    CK(m, hipSetDevice(m->dev));
+    for (size_t j = 0; j < ms.size(); ++j)
+      if (j != i && acc->gdev_of[j] == acc->gdev_of[i]) CK(m, hipStreamWaitEvent(m->stream, acc->gev_c[j], 0));
+    if (multi) CK(m, hipStreamWaitEvent(m->stream, acc->gev_x[acc->gdev_of[i]], 0));
+  }
+  return GS_OK;
+}
+
+std::vector<gs_ctx*> shards_of(gs_ctx* c) { return c->group ? c->mem : std::vector<gs_ctx*>{c}; }
+
+// Members sharing a device share its informed set: no member may commit its
+// round's new bits into it while another member's round still reads it.
+int pp_barrier(gs_ctx* acc, const std::vector<gs_ctx*>& ms) {
+  if (!acc->group) return GS_OK;
+  for (size_t i = 0; i < ms.size(); ++i) {
+    CK(ms[i], hipSetDevice(ms[i]->dev));
+    CK(ms[i], hipEventRecord(acc->gev_c[i], ms[i]->stream));
+  }
+  for (size_t i = 0; i < ms.size(); ++i) {
+    CK(ms[i], hipSetDevice(ms[i]->dev));
+    for (size_t j = 0; j < ms.size(); ++j)
+      if (j != i && acc->gdev_of[j] == acc->gdev_of[i])
+        CK(ms[i], hipStreamWaitEvent(ms[i]->stream, acc->gev_c[j], 0));
+  }
+  return GS_OK;
+}
+
+// simulator.go:239-241 for the push-pull extension: the owner informs the
+// sender (unless failed), every shard resets its round control.
+int pp_shard_begin(gs_ctx* acc, uint64_t sender) {
+  std::vector<gs_ctx*> ms = shards_of(acc);
+  unsigned long long informed = 0;
+  for (gs_ctx* m : ms) {
+    CK(m, hipSetDevice(m->dev));
+    if (int rc = pp_prepare(m)) return fail(acc, rc, m->err);
+    const uint32_t node = sender >= m->lo && sender < m->hi ? (uint32_t)(sender - m->lo) : ~0u;
+    CK(m, pp_seed(m->st, m->d_next, node, m->d_flag, m->sp, 0ull, 0ull, m->stream));
+    uint32_t ok = 0;
+    CK(m, hipMemcpyAsync(&ok, m->d_flag, 4, hipMemcpyDeviceToHost, m->stream));
+    CK(m, hipStreamSynchronize(m->stream));
+    informed += ok;
+    reset_counters(m);
+    m->begun = true;
+  }
+  if (!acc->group) {  // every rank learns whether the owner informed the sender
+    unsigned long long* d = acc->d_gcounts;
+    CK(acc, hipMemcpyAsync(d, &informed, 8, hipMemcpyHostToDevice, acc->stream));
+    if (int rc = x_all_reduce(acc, d, 1)) return abort_rank(acc, rc);
+    CK(acc, hipMemcpyAsync(&informed, d, 8, hipMemcpyDeviceToHost, acc->stream));
+    CK(acc, hipStreamSynchronize(acc->stream));
+  }
+  if (int rc = pp_exchange(acc, ms)) return abort_rank(acc, rc);
+  acc->recv = acc->pending = informed;
+  acc->begun = true;
+  return GS_OK;
+}
+
+void account_tick(gs_ctx* c, uint64_t tick, const unsigned long long* s, gs_tick_stats* o);
+
+int pp_shard_step(gs_ctx* acc, uint32_t ticks, gs_tick_stats* out) {
+  std::vector<gs_ctx*> ms = shards_of(acc);
+  std::vector<unsigned long long> sum(kStatFields);
+  uint32_t done = 0;
+  while (done < ticks) {
+    const uint32_t batch = std::min<uint32_t>(ticks - done, kStatSlots);
+    const uint64_t t0 = acc->t + 1;
+    const uint32_t i0 = (uint32_t)(t0 % kStatSlots);
+    const uint32_t first = std::min<uint32_t>(batch, kStatSlots - i0);
+    for (gs_ctx* m : ms) {
+      CK(m, hipSetDevice(m->dev));
+      CK(m, hipMemsetAsync(m->st.stats + (size_t)i0 * kStatFields, 0, (size_t)first * kStatFields * 8, m->stream));
+      if (first < batch)
+        CK(m, hipMemsetAsync(m->st.stats, 0, (size_t)(batch - first) * kStatFields * 8, m->stream));
+    }
+    for (uint32_t i = 0; i < batch; ++i) {
+      const uint32_t tt = (uint32_t)(t0 + i);
+      for (gs_ctx* m : ms) {
+        CK(m, hipSetDevice(m->dev));
+        CK(m, pp_round_shard(m->st, m->d_next, tt, m->sp, m->stream));
+      }
+      RC(pp_barrier(acc, ms));
+      for (gs_ctx* m : ms) {
+        CK(m, hipSetDevice(m->dev));
+        CK(m, pp_commit(m->st, m->d_next, tt, m->sp, m->stream));
+      }
+      if (int rc = pp_exchange(acc, ms)) return abort_rank(acc, rc);
+    }
+    for (gs_ctx* m : ms) {
+      CK(m, hipSetDevice(m->dev));
+      unsigned long long* a = m->st.stats + (size_t)i0 * kStatFields;
+      if (is_rank(m)) {  // the global per-round counters on every rank
+        if (int rc = x_all_reduce(m, a, (size_t)first * kStatFields)) return abort_rank(m, rc);
+        if (first < batch)
+          if (int rc = x_all_reduce(m, m->st.stats, (size_t)(batch - first) * kStatFields)) return abort_rank(m, rc);
+      }
+      CK(m, hipMemcpyAsync(m->h_stats + (size_t)i0 * kStatFields, a, (size_t)first * kStatFields * 8,
+                           hipMemcpyDeviceToHost, m->stream));
+      if (first < batch)
+        CK(m, hipMemcpyAsync(m->h_stats, m->st.stats, (size_t)(batch - first) * kStatFields * 8,
+                             hipMemcpyDeviceToHost, m->stream));
+    }
+    for (gs_ctx* m : ms) {
+      CK(m, hipSetDevice(m->dev));
+      CK(m, hipStreamSynchronize(m->stream));
+    }
+    for (uint32_t i = 0; i < batch; ++i) {
+      const size_t row = (size_t)((t0 + i) % kStatSlots) * kStatFields;
+      for (uint32_t f = 0; f < kStatFields; ++f) {
+        sum[f] = 0;
+        for (gs_ctx* m : ms) sum[f] += m->h_stats[row + f];
+      }
+      account_tick(acc, t0 + i, sum.data(), out ? &out[done + i] : nullptr);
+    }
+    done += batch;
+  }
+  return GS_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 int gs_broadcast_begin(gs_ctx* c, int64_t sender) {
   if (!c) return GS_EINVAL;
+  if (c->aborted) return fail(c, GS_EDEVICE, "this rank's exchange failed earlier; the run is over");
   if (!c->peers) return fail(c, GS_EINVAL, "load peers or build the overlay first");
   if (c->begun) return fail(c, GS_EINVAL, "broadcast already begun");
   if (sender >= 0 && (uint64_t)sender >= c->p.n) return fail(c, GS_EINVAL, "sender out of range");
@@ -1225,6 +1660,7 @@ int gs_broadcast_begin(gs_ctx* c, int64_t sender) {
   }
   const bool batched = c->trials > 1;
   const uint64_t s = sender >= 0 ? (uint64_t)sender : batched ? ~0ull : keyed_sender(c->group ? c->mem[0] : c);
+  if (c->pp && (c->group || c->pp_shard)) return pp_shard_begin(c, s);
   if (c->pp) {  // push-pull: the sender is informed (unless failed)
     CK(c, hipSetDevice(c->dev));
     RC(pp_prepare(c));
@@ -1251,11 +1687,11 @@ int gs_broadcast_begin(gs_ctx* c, int64_t sender) {
     uint32_t k = 0;
     RC(begin_one(c, s, &k));
     scheduled = k;
-    if (c->comm) {  // every rank learns whether the owner scheduled the sender
+    if (is_rank(c)) {  // every rank learns whether the owner scheduled the sender
       unsigned long long* d = c->d_gcounts;  // scratch
       unsigned long long h = scheduled;
       CK(c, hipMemcpyAsync(d, &h, 8, hipMemcpyHostToDevice, c->stream));
-      NCK(c, rccl().all_reduce(d, d, 1, ncclUint64, ncclSum, c->comm, c->stream));
+      if (int rc = x_all_reduce(c, d, 1)) return abort_rank(c, rc);
       CK(c, hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, c->stream));
       CK(c, hipStreamSynchronize(c->stream));
       scheduled = h;
@@ -1269,7 +1705,7 @@ int gs_broadcast_begin(gs_ctx* c, int64_t sender) {
 
 int gs_set_stream(gs_ctx* c, void* hip_stream) {
   if (!c) return GS_EINVAL;
-  if (c->group || c->comm) return fail(c, GS_EINVAL, "multi-device contexts keep their own streams");
+  if (c->group || is_rank(c)) return fail(c, GS_EINVAL, "multi-device contexts keep their own streams");
   CK(c, hipSetDevice(c->dev));
   CK(c, hipStreamSynchronize(c->stream));
   c->stream = hip_stream ? (hipStream_t)hip_stream : c->own;
@@ -1568,10 +2004,17 @@ int sync_all(const std::vector<gs_ctx*>& ms) {
   return GS_OK;
 }
 
+// Fire counts of the window's units and their scan; with gather, tfires
+// (fires per tick, plus this shard's partition-overflow flag in slot 15) is
+// gathered: every rank's into d_gcounts, or the member's into its h_misc.
+constexpr uint32_t kFlagSlot = kMaxWindow - 1;
+static_assert(kFlagSlot >= kBitTicks, "the flag slot is past the window's ticks");
+
 int shard_units(gs_ctx* m, uint32_t t, uint32_t Lu, bool gather) {
   WinState& w = m->ws;
   CK(m, hipSetDevice(m->dev));
   CK(m, hipMemsetAsync(w.tfires, 0, kMaxWindow * 8, m->stream));
+  CK(m, hipMemcpyAsync(w.tfires + kFlagSlot, m->d_err, 4, hipMemcpyDeviceToDevice, m->stream));
   CK(m, win_units(w, t, Lu, m->stream));
   size_t need = 0;
   CK(m, win_scan_units(w, Lu, nullptr, need, m->stream));
@@ -1579,8 +2022,10 @@ int shard_units(gs_ctx* m, uint32_t t, uint32_t Lu, bool gather) {
   need = m->tmp.bytes;
   CK(m, win_scan_units(w, Lu, m->tmp.p, need, m->stream));
   if (!gather) return GS_OK;
-  if (m->comm) {
-    NCK(m, rccl().all_gather(w.tfires, m->d_gcounts, kMaxWindow, ncclUint64, m->comm, m->stream));
+  if (is_rank(m)) {
+    CK(m, hipMemcpyAsync(m->d_gcounts + (size_t)m->rank * kMaxWindow, w.tfires, kMaxWindow * 8,
+                         hipMemcpyDeviceToDevice, m->stream));
+    RC(x_all_gather(m, m->d_gcounts, kMaxWindow * 8));
     CK(m, hipMemcpyAsync(m->h_misc, m->d_gcounts, (size_t)m->G * kMaxWindow * 8, hipMemcpyDeviceToHost,
                          m->stream));
   } else {
@@ -1588,6 +2033,111 @@ int shard_units(gs_ctx* m, uint32_t t, uint32_t Lu, bool gather) {
   }
   return GS_OK;
 }
+
+// What the host keeps of a shard window until the next window's count sync
+// has shown that no shard's partition overflowed.
+struct ShardWin {
+  uint32_t t = 0, L = 0;
+  unsigned long long Tub = 0;  // bound on one shard's messages: every slot of every gathered fire
+  bool live = false;
+};
+
+// Expand + partition + consume + resolve of one window on shard m (its
+// gathered fire list in w.gfire).  Regions are sized from estimates; an
+// overflow sets the sticky flag, the later kernels of the window skip, and the
+// host redoes it exactly (shard_redo) before the next window.
+int shard_pipeline(gs_ctx* m, const ShardWin& sw, bool timing) {
+  WinState& w = m->ws;
+  CK(m, hipSetDevice(m->dev));
+  const unsigned long long Test =
+      (unsigned long long)((long double)sw.Tub * (long double)m->ntot / (long double)m->p.n);
+  plan_coarse(m, Test, nullptr);
+  const uint64_t fcap = sw.Tub + sw.Tub / 8 + (uint64_t)w.ncoarse * 256 * 513 + 16;
+  if (!grow(m->cmsg, (m->h_cap[kRegions] + 16) * 4) || !grow(m->fmsg, fcap * 4))
+    return fail(m, GS_ENOMEM, "cannot allocate " + std::to_string(sw.Tub) + " window messages");
+  w.cmsg = (uint32_t*)m->cmsg.p;
+  w.fmsg = (uint32_t*)m->fmsg.p;
+  w.tofs = 0;
+  if (timing)
+    while (m->ev.size() < 5) {
+      hipEvent_t ev;
+      CK(m, hipEventCreate(&ev));
+      m->ev.push_back(ev);
+    }
+  hipEvent_t* e = timing ? &m->ev[0] : nullptr;
+  CK(m, hipMemcpyAsync(w.ccap, m->h_cap, (kRegions + 1) * 8, hipMemcpyHostToDevice, m->stream));
+  if (e) CK(m, hipEventRecord(e[0], m->stream));
+  CK(m, win_expand_sh(w, sw.t, sw.L, 1, m->stream));
+  if (e) CK(m, hipEventRecord(e[1], m->stream));
+  CK(m, win_plan(w, false, m->stream));
+  CK(m, win_part2(w, sw.Tub, true, m->stream));
+  if (e) CK(m, hipEventRecord(e[2], m->stream));
+  CK(m, win_consume_sh(w, sw.t, sw.L, m->stream));
+  if (e) CK(m, hipEventRecord(e[3], m->stream));
+  CK(m, win_resolve(w, sw.t, sw.L, m->stream));
+  CK(m, win_stats_reduce(w, sw.t, sw.L, m->stream));
+  if (e) {
+    CK(m, hipEventRecord(e[4], m->stream));
+    CK(m, hipStreamSynchronize(m->stream));
+    float ms1 = 0, ms2 = 0, ms3 = 0;
+    CK(m, hipEventElapsedTime(&ms1, e[0], e[1]));
+    CK(m, hipEventElapsedTime(&ms2, e[1], e[2]));
+    CK(m, hipEventElapsedTime(&ms3, e[3], e[4]));
+    m->timing.expand_ms += ms1;
+    m->timing.part_ms += ms2;
+    m->timing.deliver_ms += ms1 + ms2;
+    m->timing.resolve_ms += ms3;
+    m->timing.deliver_launches += 1;
+    m->timing.resolve_launches += 1;
+    m->timing.windows += 1;
+  }
+  return GS_OK;
+}
+
+// Shard m's window sw overflowed a region: clear the flag, partition it again
+// with exact counts (its gathered fire list is still in place), consume and
+// resolve it.  Rank-local: no other shard takes part.
+int shard_redo(gs_ctx* m, const ShardWin& sw) {
+  WinState& w = m->ws;
+  CK(m, hipSetDevice(m->dev));
+  uint32_t e = 0;
+  CK(m, hipMemcpyAsync(&e, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
+  CK(m, hipStreamSynchronize(m->stream));
+  e &= ~(kErrCoarse | kErrFine);
+  CK(m, hipMemcpyAsync(m->d_err, &e, 4, hipMemcpyHostToDevice, m->stream));
+  CK(m, hipMemsetAsync(w.chist, 0, kRegions * 8, m->stream));
+  CK(m, hipMemsetAsync(w.cfill, 0, kRegions * 8, m->stream));
+  CK(m, hipMemsetAsync(w.ffill, 0, (size_t)w.nfine * 8, m->stream));
+  CK(m, win_expand_sh(w, sw.t, sw.L, 0, m->stream));
+  CK(m, hipMemcpyAsync(m->h_misc, w.chist, kRegions * 8, hipMemcpyDeviceToHost, m->stream));
+  CK(m, hipStreamSynchronize(m->stream));
+  plan_coarse(m, sw.Tub, m->h_misc);
+  if (!grow(m->cmsg, (m->h_cap[kRegions] + 16) * 4)) return fail(m, GS_ENOMEM, "cannot allocate the window messages");
+  w.cmsg = (uint32_t*)m->cmsg.p;
+  CK(m, hipMemcpyAsync(w.ccap, m->h_cap, (kRegions + 1) * 8, hipMemcpyHostToDevice, m->stream));
+  CK(m, win_expand_sh(w, sw.t, sw.L, 2, m->stream));
+  CK(m, win_plan(w, false, m->stream));
+  CK(m, hipMemsetAsync(w.fhist, 0, ((size_t)w.ncoarse * 256 + 1) * 8, m->stream));
+  CK(m, win_plan(w, true, m->stream));
+  CK(m, win_part2(w, sw.Tub, false, m->stream));
+  size_t need2 = 0;
+  CK(m, win_scan_fine(w, nullptr, need2, m->stream));
+  if (!grow(m->tmp, need2)) return fail(m, GS_ENOMEM, "cannot allocate scan scratch");
+  need2 = m->tmp.bytes;
+  CK(m, win_scan_fine(w, m->tmp.p, need2, m->stream));
+  CK(m, hipMemsetAsync(w.ffill, 0, (size_t)w.nfine * 8, m->stream));
+  CK(m, win_part2(w, sw.Tub, true, m->stream));
+  CK(m, win_consume_sh(w, sw.t, sw.L, m->stream));
+  CK(m, win_resolve(w, sw.t, sw.L, m->stream));
+  CK(m, win_stats_reduce(w, sw.t, sw.L, m->stream));
+  ++m->timing.exact_redos;
+  return GS_OK;
+}
+
+// Serial shard pipelines (GS_SHARD_SERIAL=1, in-process shards): each shard's
+// window runs alone on the device, so GS_FLAG_TIMING measures one shard's
+// device time per window (bench.py's in-process scaling proxy).
+bool shard_serial() { return getenv("GS_SHARD_SERIAL") != nullptr; }
 
 int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint32_t n, bool timing) {
   gs_ctx* m0 = ms[0];
@@ -1597,16 +2147,35 @@ int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint
   const uint32_t Lmax = std::min<uint32_t>(std::max<int32_t>(m0->p.delay_low, 1), kBitTicks);
   const uint64_t slot_budget = ((N + kFineNodes - 1) >> kFineLog) * (uint64_t)kWinSlotsPerBucket;
   std::vector<unsigned long long> cnt((size_t)G * kMaxWindow);
+  ShardWin prev;
   uint32_t done = 0;
-  while (done < n) {
-    const uint32_t Lw = std::min(Lmax, n - done);
-    const uint32_t t = (uint32_t)(t0 + done);
+  // 1. fire counts per tick (every shard's, gathered) and every shard's
+  //    overflow flag of the previous window: the one host sync per window
+  auto counts = [&](uint32_t t, uint32_t Lw) -> int {
     for (gs_ctx* m : ms) RC(shard_units(m, t, Lw, true));
     RC(sync_all(ms));
     for (uint32_t r = 0; r < G; ++r)
       for (uint32_t k = 0; k < kMaxWindow; ++k)
-        cnt[(size_t)r * kMaxWindow + k] = m0->comm ? m0->h_misc[(size_t)r * kMaxWindow + k]
-                                                   : (k < Lw ? ms[r]->h_misc[k] : 0ull);
+        cnt[(size_t)r * kMaxWindow + k] = is_rank(m0) ? m0->h_misc[(size_t)r * kMaxWindow + k] : ms[r]->h_misc[k];
+    return GS_OK;
+  };
+  auto flagged = [&]() {
+    for (uint32_t r = 0; r < G; ++r)
+      if (cnt[(size_t)r * kMaxWindow + kFlagSlot] & (kErrCoarse | kErrFine)) return true;
+    return false;
+  };
+  while (done < n) {
+    const uint32_t Lw = std::min(Lmax, n - done);
+    const uint32_t t = (uint32_t)(t0 + done);
+    RC(counts(t, Lw));
+    if (flagged()) {  // a shard's previous window overflowed: it redoes it, then every shard counts again
+      for (uint32_t r = 0; r < G; ++r) {
+        if (!(cnt[(size_t)r * kMaxWindow + kFlagSlot] & (kErrCoarse | kErrFine))) continue;
+        for (gs_ctx* m : ms)
+          if (m->rank == r) RC(shard_redo(m, prev));
+      }
+      RC(counts(t, Lw));
+    }
     auto F = [&](uint32_t k) {
       unsigned long long s = 0;
       for (uint32_t r = 0; r < G; ++r) s += cnt[(size_t)r * kMaxWindow + k];
@@ -1624,6 +2193,14 @@ int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint
       for (uint32_t k = 0; k < L; ++k) own[r] += cnt[(size_t)r * kMaxWindow + k];
       seg = std::max(seg, own[r]);
     }
+    const uint64_t segb = (seg * 5 + 15) & ~15ull;  // seg u32 ids + seg u8 ticks, 16-B aligned
+    unsigned long long Ftot = 0;
+    for (uint32_t k = 0; k < L; ++k) Ftot += F(k);
+    ShardWin sw;
+    sw.t = t;
+    sw.L = L;
+    sw.Tub = Ftot * stride;
+    sw.live = seg > 0;
     if (seg) {
       // 2. compaction into segment `rank` of the device's all-gather buffer
       for (size_t i = 0; i < ms.size(); ++i) {
@@ -1632,20 +2209,21 @@ int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint
         CK(m, hipSetDevice(m->dev));
         Buf* b = &m->gfire;
         if (acc->group) b = &acc->gbuf[acc->gdev_of[i]];
-        if (!grow(*b, (size_t)G * seg * 4)) return fail(m, GS_ENOMEM, "cannot allocate the window fire lists");
+        if (!grow(*b, (size_t)G * segb)) return fail(m, GS_ENOMEM, "cannot allocate the window fire lists");
         if (!grow(m->gmap, ((own[m->rank] + 63) / 64 + 1) * 4))
           return fail(m, GS_ENOMEM, "cannot allocate the group map");
         w.gmap = (uint32_t*)m->gmap.p;
-        w.gfire = (const uint32_t*)b->p;
+        w.gfire = (const uint8_t*)b->p;
         w.gseg = seg;
+        w.gsegb = segb;
+        uint8_t* mine = (uint8_t*)b->p + (size_t)m->rank * segb;
         CK(m, win_groupmap(w, L, m->stream));
-        CK(m, win_fire_compact(w, t, L, own[m->rank], (uint32_t*)b->p + (size_t)m->rank * seg, seg, m->stream));
+        CK(m, win_fire_compact(w, t, L, own[m->rank], (uint32_t*)mine, mine + seg * 4, seg, m->stream));
         if (acc->group) CK(m, hipEventRecord(acc->gev_c[i], m->stream));
       }
       // ... all-gathered
-      if (m0->comm) {
-        uint32_t* buf = (uint32_t*)m0->gfire.p;
-        NCK(m0, rccl().all_gather(buf + (size_t)m0->rank * seg, buf, seg, ncclUint32, m0->comm, m0->stream));
+      if (is_rank(m0)) {
+        RC(x_all_gather(m0, m0->gfire.p, segb));
       } else {
         // each device's leader copies the other devices' segments in; every
         // member waits for the compactions it reads
@@ -1664,114 +2242,39 @@ int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint
             CK(m, hipStreamWaitEvent(m->stream, acc->gev_c[j], 0));
             const int dj = acc->gdev_of[j];
             if (dj != d)
-              CK(m, hipMemcpyPeerAsync((uint32_t*)acc->gbuf[d].p + (size_t)ms[j]->rank * seg, m->dev,
-                                       (uint32_t*)acc->gbuf[dj].p + (size_t)ms[j]->rank * seg, ms[j]->dev,
-                                       seg * 4, m->stream));
+              CK(m, hipMemcpyPeerAsync((uint8_t*)acc->gbuf[d].p + (size_t)ms[j]->rank * segb, m->dev,
+                                       (uint8_t*)acc->gbuf[dj].p + (size_t)ms[j]->rank * segb, ms[j]->dev, segb,
+                                       m->stream));
           }
           CK(m, hipEventRecord(acc->gev_x[d], m->stream));
         }
       }
-      // 3. expand + partition
-      unsigned long long Ftot = 0;
-      for (uint32_t k = 0; k < L; ++k) Ftot += F(k);
+      // 3. expand, partition, consume, resolve on every shard (serially when timed in-process)
       for (gs_ctx* m : ms) {
-        WinState& w = m->ws;
+        RC(shard_pipeline(m, sw, timing));
+        if (shard_serial() && !is_rank(m)) CK(m, hipStreamSynchronize(m->stream));
+      }
+    } else {
+      for (gs_ctx* m : ms) {
         CK(m, hipSetDevice(m->dev));
-        const unsigned long long Tub = Ftot * stride;  // bound on this shard's messages
-        const unsigned long long Test = (unsigned long long)((long double)Tub * (long double)m->ntot / (long double)N);
-        plan_coarse(m, Test, nullptr);
-        const uint64_t fcap = Tub + Tub / 8 + (uint64_t)w.ncoarse * 256 * 513 + 16;
-        if (!grow(m->cmsg, (m->h_cap[kRegions] + 16) * 4) || !grow(m->fmsg, fcap * 4))
-          return fail(m, GS_ENOMEM, "cannot allocate " + std::to_string(Tub) + " window messages");
-        w.cmsg = (uint32_t*)m->cmsg.p;
-        w.fmsg = (uint32_t*)m->fmsg.p;
-        w.tofs = 0;
-        if (timing)
-          while (m->ev.size() < 5) {
-            hipEvent_t ev;
-            CK(m, hipEventCreate(&ev));
-            m->ev.push_back(ev);
-          }
-        hipEvent_t* e = timing ? &m->ev[0] : nullptr;
-        CK(m, hipMemcpyAsync(w.ccap, m->h_cap, (kRegions + 1) * 8, hipMemcpyHostToDevice, m->stream));
-        if (e) CK(m, hipEventRecord(e[0], m->stream));
-        CK(m, win_expand_sh(w, t, L, 1, m->stream));
-        if (e) CK(m, hipEventRecord(e[1], m->stream));
-        CK(m, win_plan(w, false, m->stream));
-        CK(m, win_part2(w, Tub, true, m->stream));
-        if (e) CK(m, hipEventRecord(e[2], m->stream));
-        CK(m, hipMemcpyAsync(m->h_err, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
-      }
-      RC(sync_all(ms));
-      for (gs_ctx* m : ms) {  // regions sized from estimates: redo exactly on overflow
-        WinState& w = m->ws;
-        uint32_t err = *m->h_err;
-        const unsigned long long Tub = Ftot * stride;
-        if (err & kErrCoarse) {
-          CK(m, hipMemsetAsync(w.chist, 0, kRegions * 8, m->stream));
-          CK(m, win_expand_sh(w, t, L, 0, m->stream));
-          CK(m, hipMemcpyAsync(m->h_misc, w.chist, kRegions * 8, hipMemcpyDeviceToHost, m->stream));
-          CK(m, hipStreamSynchronize(m->stream));
-          plan_coarse(m, Tub, m->h_misc);
-          if (!grow(m->cmsg, (m->h_cap[kRegions] + 16) * 4))
-            return fail(m, GS_ENOMEM, "cannot allocate the window messages");
-          w.cmsg = (uint32_t*)m->cmsg.p;
-          CK(m, hipMemcpyAsync(w.ccap, m->h_cap, (kRegions + 1) * 8, hipMemcpyHostToDevice, m->stream));
-          CK(m, hipMemsetAsync(w.cfill, 0, kRegions * 8, m->stream));
-          CK(m, win_expand_sh(w, t, L, 2, m->stream));
-          CK(m, win_plan(w, false, m->stream));
-          err = kErrFine;
-        }
-        if (err & kErrFine) {
-          CK(m, hipMemsetAsync(w.fhist, 0, ((size_t)w.ncoarse * 256 + 1) * 8, m->stream));
-          CK(m, win_plan(w, true, m->stream));
-          CK(m, win_part2(w, Tub, false, m->stream));
-          size_t need2 = 0;
-          CK(m, win_scan_fine(w, nullptr, need2, m->stream));
-          if (!grow(m->tmp, need2)) return fail(m, GS_ENOMEM, "cannot allocate scan scratch");
-          need2 = m->tmp.bytes;
-          CK(m, win_scan_fine(w, m->tmp.p, need2, m->stream));
-          CK(m, hipMemsetAsync(w.ffill, 0, (size_t)w.nfine * 8, m->stream));
-          CK(m, win_part2(w, Tub, true, m->stream));
-          ++m->timing.exact_redos;
-        }
+        CK(m, win_consume_sh(m->ws, t, L, m->stream));
       }
     }
-    for (gs_ctx* m : ms) {  // consume the window's fire lists, resolve own buckets
-      WinState& w = m->ws;
-      CK(m, hipSetDevice(m->dev));
-      const uint32_t s0 = t % w.R;
-      const uint32_t first = std::min(L, w.R - s0);
-      CK(m, hipMemsetAsync(w.fcount + (size_t)s0 * w.nfine, 0, (size_t)first * w.nfine * 4, m->stream));
-      if (first < L) CK(m, hipMemsetAsync(w.fcount, 0, (size_t)(L - first) * w.nfine * 4, m->stream));
-      if (!seg) continue;
-      hipEvent_t* e = timing ? &m->ev[0] : nullptr;
-      if (e) CK(m, hipEventRecord(e[3], m->stream));
-      CK(m, win_resolve(w, t, L, m->stream));
-      CK(m, win_stats_reduce(w, t, L, m->stream));
-      if (e) {
-        CK(m, hipEventRecord(e[4], m->stream));
-        CK(m, hipStreamSynchronize(m->stream));
-        float ms1 = 0, ms2 = 0, ms3 = 0;
-        CK(m, hipEventElapsedTime(&ms1, e[0], e[1]));
-        CK(m, hipEventElapsedTime(&ms2, e[1], e[2]));
-        CK(m, hipEventElapsedTime(&ms3, e[3], e[4]));
-        m->timing.expand_ms += ms1;
-        m->timing.part_ms += ms2;
-        m->timing.deliver_ms += ms1 + ms2;
-        m->timing.resolve_ms += ms3;
-        m->timing.deliver_launches += 1;
-        m->timing.resolve_launches += 1;
-        m->timing.windows += 1;
-      }
-    }
+    prev = sw;
     done += L;
   }
+  // the last window's overflow check (rank-local: the redo needs no exchange)
   for (gs_ctx* m : ms) {
     CK(m, hipSetDevice(m->dev));
     CK(m, hipMemcpyAsync(m->h_err, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
   }
   RC(sync_all(ms));
+  for (gs_ctx* m : ms)
+    if (*m->h_err & (kErrCoarse | kErrFine)) {
+      RC(shard_redo(m, prev));
+      CK(m, hipMemcpyAsync(m->h_err, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
+      CK(m, hipStreamSynchronize(m->stream));
+    }
   for (gs_ctx* m : ms)
     if (*m->h_err & kErrArrivals) return fail(m, GS_EOVERFLOW, "too many arrivals at one node in one tick");
   return GS_OK;
@@ -1816,11 +2319,9 @@ int shard_step(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint32_t ticks, gs_t
     for (gs_ctx* m : ms) {
       CK(m, hipSetDevice(m->dev));
       unsigned long long* a = m->st.stats + (size_t)i0 * kStatFields;
-      if (m->comm) {  // the global per-tick counters on every rank
-        NCK(m, rccl().all_reduce(a, a, (size_t)first * kStatFields, ncclUint64, ncclSum, m->comm, m->stream));
-        if (first < batch)
-          NCK(m, rccl().all_reduce(m->st.stats, m->st.stats, (size_t)(batch - first) * kStatFields, ncclUint64,
-                                   ncclSum, m->comm, m->stream));
+      if (is_rank(m)) {  // the global per-tick counters on every rank
+        RC(x_all_reduce(m, a, (size_t)first * kStatFields));
+        if (first < batch) RC(x_all_reduce(m, m->st.stats, (size_t)(batch - first) * kStatFields));
       }
       CK(m, hipMemcpyAsync(m->h_stats + (size_t)i0 * kStatFields, a, (size_t)first * kStatFields * 8,
                            hipMemcpyDeviceToHost, m->stream));
@@ -1866,6 +2367,7 @@ extern "C" {
 
 int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
   if (!c) return GS_EINVAL;
+  if (c->aborted) return fail(c, GS_EDEVICE, "this rank's exchange failed earlier; the run is over");
   if (!c->begun) return fail(c, GS_EINVAL, "gs_broadcast_begin first");
   if (c->group && c->gtrials) {
     std::vector<std::vector<gs_tick_stats>> rows(c->mem.size(), std::vector<gs_tick_stats>(ticks));
@@ -1893,8 +2395,9 @@ int gs_step(gs_ctx* c, uint32_t ticks, gs_tick_stats* out) {
     }
     return GS_OK;
   }
+  if (c->pp && (c->group || c->pp_shard)) return pp_shard_step(c, ticks, out);
   if (c->group) return shard_step(c, c->mem, ticks, out);
-  if (c->shard) return shard_step(c, {c}, ticks, out);
+  if (c->shard) return abort_rank(c, shard_step(c, {c}, ticks, out));
   CK(c, hipSetDevice(c->dev));
   if (async_ok(c) && ticks > 0) {  // device-driven windows
     uint32_t stop = 0, k = 0;
@@ -2007,6 +2510,26 @@ void snap_trial(const gs_ctx* c, uint32_t tr, int32_t status) {
 int pp_stalled(gs_ctx* c, bool* stalled) {
   *stalled = true;
   if (c->st.kd >= 100) return GS_OK;  // every call is lost (simulator.go:172 quantisation)
+  if (c->group || c->pp_shard) {  // shards: their own callers' edges against the replicated sets, summed
+    unsigned long long live = 0;
+    for (gs_ctx* m : shards_of(c)) {
+      CK(m, hipSetDevice(m->dev));
+      CK(m, pp_live_edges(m->st, m->d_err + 2, m->stream));
+      uint32_t h = 0;
+      CK(m, hipMemcpyAsync(&h, m->d_err + 2, 4, hipMemcpyDeviceToHost, m->stream));
+      CK(m, hipStreamSynchronize(m->stream));
+      live += h;
+    }
+    if (!c->group) {
+      unsigned long long* d = c->d_gcounts;
+      CK(c, hipMemcpyAsync(d, &live, 8, hipMemcpyHostToDevice, c->stream));
+      if (int rc = x_all_reduce(c, d, 1)) return abort_rank(c, rc);
+      CK(c, hipMemcpyAsync(&live, d, 8, hipMemcpyDeviceToHost, c->stream));
+      CK(c, hipStreamSynchronize(c->stream));
+    }
+    *stalled = live == 0;
+    return GS_OK;
+  }
   unsigned long long live = 0;
   CK(c, pp_live_edges(c->st, c->d_err + 2, c->stream));
   uint32_t h = 0;
@@ -2202,14 +2725,23 @@ int gs_timing_get(gs_ctx* c, gs_timing* out) {
   *out = c->group ? c->mem[0]->timing : c->timing;  // a group: its first member's kernels
   if (c->group) out->overlay_ms = c->timing.overlay_ms;
   out->pp_early_rounds = out->pp_bottom_rounds = 0;
-  if (c->pp && c->sp.ctl && c->begun) {
-    CK(c, hipSetDevice(c->dev));
+  gs_ctx* pc = c->group ? c->mem[0] : c;  // a group: its first shard's rounds (all shards run the same modes)
+  if (c->pp && pc->sp.ctl && c->begun) {
+    CK(pc, hipSetDevice(pc->dev));
     PPCtl h;
-    CK(c, hipMemcpyAsync(&h, c->sp.ctl, offsetof(PPCtl, segcnt), hipMemcpyDeviceToHost, c->stream));
-    CK(c, hipStreamSynchronize(c->stream));
+    CK(pc, hipMemcpyAsync(&h, pc->sp.ctl, offsetof(PPCtl, segcnt), hipMemcpyDeviceToHost, pc->stream));
+    CK(pc, hipStreamSynchronize(pc->stream));
     out->pp_early_rounds = h.nearly;
     out->pp_bottom_rounds = h.nbottom;
   }
+  return GS_OK;
+}
+
+int gs_shard_timing(gs_ctx* c, uint32_t index, gs_timing* out) {
+  if (!c || !out) return GS_EINVAL;
+  if (!c->group) return index == 0 ? gs_timing_get(c, out) : fail(c, GS_EINVAL, "no such shard");
+  if (index >= c->mem.size()) return fail(c, GS_EINVAL, "no such shard");
+  *out = c->mem[index]->timing;
   return GS_OK;
 }
 
@@ -2250,8 +2782,10 @@ int gs_reset(gs_ctx* c) {
     CK(c, hipMemsetAsync(c->d_state, 0, (char*)c->st.stats - (char*)c->d_state, c->stream));
     if (c->d_cnt) CK(c, hipMemsetAsync(c->d_cnt, 0, c->st.n * 4, c->stream));
     if (c->win) CK(c, hipMemsetAsync(c->ws.fcount, 0, c->fcount_bytes, c->stream));
-    if (c->failed)
+    if (c->failed && !c->pp_shard)
       CK(c, hipMemcpyAsync(c->st.crash, c->d_failed, c->st.W * 8, hipMemcpyDeviceToDevice, c->stream));
+    if (c->pp_shard)  // this shard's slice of the replicated informed set
+      CK(c, hipMemsetAsync(c->st.recv, 0, c->st.W * 8, c->stream));
     CK(c, hipStreamSynchronize(c->stream));
   }
   reset_counters(c);

@@ -61,6 +61,13 @@ struct DevState {
   uint32_t* ccount;
   unsigned long long* stats;
   uint32_t* err;           // error word (kErrArrivals: a 16-bit receipt count overflowed)
+  // Push-pull node-range shards: the informed and failed sets by GLOBAL node id
+  // (replicated on every shard, exchanged each round); recv / crash above are
+  // this shard's own slice of them, local node i = global gbase + i.  Every
+  // other context: grecv = recv, gcrash = crash, gbase = 0.
+  unsigned long long* grecv;
+  unsigned long long* gcrash;
+  uint64_t gbase;
   uint64_t n, W;
   uint32_t C, CS, R, stride;
   uint32_t stride_magic;   // floor(2^32 / stride) + 1: exact q/stride for q < 2^18
@@ -148,13 +155,13 @@ struct WinState {
   unsigned long long* stage;     // [slots][kStageWords] per-window results for the host (device-driven)
   uint32_t lstride;              // unit layout stride: units u = f * lstride + k
   uint32_t slots;                // longest row in use (<= stride: rows may be padded for 16-B loads)
-  // node-range shard: partitioned friend rows (prow[v]..prow[v+1] of pent, entry =
-  // (target - base) << 5 | slot j) and the all-gathered window fire list
-  const uint32_t* prow;          // (unused: rows are fixed-width, see pw)
-  const uint32_t* pent;          // [n][pw] owned slots (target - lo) << 5 | j, ~0u-padded
+  // node-range shard: partitioned friend rows and the all-gathered window fire list
+  const uint32_t* pent;          // [n][pw]: owned-slot mask, then the owned targets - lo (or a spill offset)
+  const uint32_t* pspill;        // targets of the rows with more than pw - 1 owned slots
   uint32_t pw;                   // partitioned row width (a multiple of 4)
-  const uint32_t* gfire;         // [G][gseg] entries local_id << 4 | k, ~0u = padding
-  uint64_t gseg;                 // entries per shard segment of gfire
+  uint32_t abort_on_err;         // host-driven shard windows: an overflowed window's later kernels skip
+  const uint8_t* gfire;          // [G] segments of gsegb bytes: gseg u32 global ids (~0u = padding), gseg u8 ticks
+  uint64_t gseg, gsegb;          // entries, bytes per shard segment of gfire
   uint32_t G, rank;              // shards, this shard's index
   uint32_t seg_per;              // nodes per shard (shard r owns [r*seg_per, ...))
   uint64_t n, W;
@@ -207,18 +214,12 @@ hipError_t win_stats_reduce(const WinState& w, uint32_t t0, uint32_t L, hipStrea
 // node-range shards
 hipError_t part_count(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
                       uint32_t* cnt, hipStream_t s);
-hipError_t part_scan(const uint32_t* cnt, uint64_t n, unsigned long long* off, void* tmp, size_t& tmp_bytes,
-                     hipStream_t s);
-hipError_t part_narrow(const unsigned long long* off, uint64_t n, uint32_t* prow, uint32_t* err, hipStream_t s);
-hipError_t part_fill(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
-                     const uint32_t* prow, uint32_t* pent, hipStream_t s);
-// Fixed-width partition: *max_out = max over v of cnt[v]; then pent[v * pw ..]
-// = v's owned slots in slot order, ~0u-padded to pw.
-hipError_t part_max(const uint32_t* cnt, uint64_t n, uint32_t* max_out, hipStream_t s);
-hipError_t part_fill_fixed(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi, uint32_t pw,
-                           uint32_t* pent, hipStream_t s);
-hipError_t win_fire_compact(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, uint32_t* out,
+hipError_t part_hist(const uint32_t* cnt, uint64_t n, unsigned long long* hist, hipStream_t s);
+hipError_t part_fill_mask(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi, uint32_t pw,
+                          uint32_t* pent, uint32_t* spill, unsigned long long* spill_n, hipStream_t s);
+hipError_t win_fire_compact(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, uint32_t* ids, uint8_t* ks,
                             uint64_t seg, hipStream_t s);
+hipError_t win_consume_sh(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
 hipError_t win_expand_sh(const WinState& w, uint32_t t0, uint32_t L, int mode, hipStream_t s);
 // Schedule local node `node` (batched: in every trial; ~0u: each trial's keyed sender) at `tick`.
 hipError_t win_schedule(const WinState& w, uint32_t node, uint32_t tick, uint32_t trials, uint32_t n,
@@ -297,6 +298,23 @@ hipError_t pp_rev_build(const DevState& s, unsigned long long* rend, uint32_t* r
 // fmask from the reverse table and the failed mask (stride <= 8).
 hipError_t pp_fmask_build(const DevState& s, const unsigned long long* rend, const uint32_t* rsrc,
                           const uint8_t* rslot, uint8_t* fmask, hipStream_t st);
+// Node-range shards of a push-pull run (SURVEY.md 8(e)2 for the C5 extension):
+// every round is bottom-up on the shard's own nodes [gbase, gbase + n) against
+// the replicated informed set (grecv), which the shards all-gather before
+// each round.  Reverse table of the targets in [lo, hi) from the full table
+// (deg/ids of nfull nodes; rend indexed by target - lo, rsrc global callers).
+// (count + scan: rend[0..n] = exclusive prefix, rend[n] = the range's in-edges;
+// then the fill, which leaves rend[i] = the end of target lo + i's edges)
+size_t pp_rev_range_scan_bytes(uint64_t n);
+hipError_t pp_rev_count_range(const uint8_t* deg, const uint32_t* ids, uint64_t nfull, uint32_t stride, uint64_t lo,
+                              uint64_t hi, unsigned long long* rend, void* tmp, size_t tmp_bytes, hipStream_t st);
+hipError_t pp_rev_fill_range(const uint8_t* deg, const uint32_t* ids, uint64_t nfull, uint32_t stride, uint64_t lo,
+                             uint64_t hi, unsigned long long* rend, uint32_t* rsrc, uint8_t* rslot, hipStream_t st);
+// fmask of the shard's own callers from their rows and the replicated failed set.
+hipError_t pp_fmask_rows(const DevState& s, uint8_t* fmask, hipStream_t st);
+// One sharded round: mode (always bottom-up) + k_ppb_round; commit with pp_commit.
+hipError_t pp_round_shard(const DevState& s, unsigned long long* next, uint32_t t, const PPSparse& sp,
+                          hipStream_t st);
 
 // Launchers (gs_broadcast.hip).
 hipError_t launch_tick(const DevState& st, uint32_t tick, int mode, hipStream_t s);

@@ -231,18 +231,18 @@ __device__ __forceinline__ void ppb_resolve(const DevState& s, const PPSparse& s
   const uint32_t lane = threadIdx.x & 63;
   if (lane >= cnt) return;
   const uint32_t e = q[lane], loc = e & 0xFFFu, d = e >> 16;
-  const uint64_t v = base + loc;
+  const uint64_t v = base + loc;  // local id (global s.gbase + v)
   const unsigned long long qb = v ? sp.rend[v - 1] : 0ull, qe = sp.rend[v];
   bool pull = false;
   uint32_t u = 0;
   if (d > 0) {
-    const u32x4 r = philox((uint32_t)v, t, 0, c3, s.key.k0, s.key.k1);
+    const u32x4 r = philox((uint32_t)(s.gbase + v), t, 0, c3, s.key.k0, s.key.k1);
     if ((int32_t)uniform(r.y, 100u) >= s.kd) {
       u = s.ids[v * s.stride + uniform(r.x, d)];
       pull = true;
     }
   }
-  const unsigned long long Iu = pull ? s.recv[u >> 6] : 0ull;
+  const unsigned long long Iu = pull ? s.grecv[u >> 6] : 0ull;  // u is a global id
   bool got = false;
   for (unsigned long long q0 = qb; q0 < qe && !got; q0 += kPPEdges) {
     uint32_t src[kPPEdges], x[kPPEdges];
@@ -257,7 +257,7 @@ __device__ __forceinline__ void ppb_resolve(const DevState& s, const PPSparse& s
       if (q0 + k >= qe) break;
       const u32x4 r = philox(src[k], t, 0, c3, s.key.k0, s.key.k1);
       if (uniform(r.x, (x[k] >> 4) + 1) == (x[k] & 15u) && (int32_t)uniform(r.y, 100u) >= s.kd)
-        got |= ((s.recv[src[k] >> 6] >> (src[k] & 63)) & 1) != 0;
+        got |= ((s.grecv[src[k] >> 6] >> (src[k] & 63)) & 1) != 0;
     }
   }
   const bool pulled = pull && ((Iu >> (u & 63)) & 1);  // u informed => u live
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(kPPRoundBlock) void k_ppb_round(const DevState s, u
         if (d[i] > 0) {
           ++fired;
           if (inf) {  // push: the receiver finds it
-            const u32x4 r = philox((uint32_t)v, t, 0, c3, s.key.k0, s.key.k1);
+            const u32x4 r = philox((uint32_t)(s.gbase + v), t, 0, c3, s.key.k0, s.key.k1);
             if ((int32_t)uniform(r.y, 100u) >= s.kd) {
               ++sent;
               if (!((fm[i] >> uniform(r.x, d[i])) & 1)) ++msgs;
@@ -595,14 +595,58 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_live_edges(const DevState s, ui
     const bool iv = (s.recv[v >> 6] & bit) != 0;
     const uint32_t d = s.deg[v];
     for (uint32_t j = 0; j < d; ++j) {
-      const uint32_t u = s.ids[v * s.stride + j];
+      const uint32_t u = s.ids[v * s.stride + j];  // global id
       const unsigned long long ub = 1ull << (u & 63);
-      const bool iu = (s.recv[u >> 6] & ub) != 0, fu = (s.crash[u >> 6] & ub) != 0;
+      const bool iu = (s.grecv[u >> 6] & ub) != 0, fu = (s.gcrash[u >> 6] & ub) != 0;
       if (iv ? (!iu && !fu) : iu) { ++cnt; break; }
     }
   }
   const uint32_t w = wave_sum64(cnt);
   if ((threadIdx.x & 63) == 0 && w) atomicAdd(out, w);
+}
+
+// ---- node-range shards ----------------------------------------------------------
+// In-edge counts of the targets in [lo, hi) over the full table (cnt indexed
+// by target - lo), then the fill (rend ends as the end of each target's edges).
+__global__ __launch_bounds__(kPPBlock) void k_rev_count_range(const uint8_t* deg, const uint32_t* ids, uint64_t n,
+                                                              uint32_t stride, uint64_t lo, uint64_t hi,
+                                                              unsigned long long* cnt) {
+  for (uint64_t v = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; v < n; v += (uint64_t)gridDim.x * kPPBlock) {
+    const uint32_t d = deg[v];
+    for (uint32_t j = 0; j < d; ++j) {
+      const uint32_t u = ids[v * stride + j];
+      if (u >= lo && u < hi) atomicAdd(&cnt[u - lo], 1ull);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kPPBlock) void k_rev_fill_range(const uint8_t* deg, const uint32_t* ids, uint64_t n,
+                                                             uint32_t stride, uint64_t lo, uint64_t hi,
+                                                             unsigned long long* rend, uint32_t* rsrc,
+                                                             uint8_t* rslot) {
+  for (uint64_t v = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; v < n; v += (uint64_t)gridDim.x * kPPBlock) {
+    const uint32_t d = deg[v];
+    for (uint32_t j = 0; j < d; ++j) {
+      const uint32_t u = ids[v * stride + j];
+      if (u < lo || u >= hi) continue;
+      const unsigned long long at = atomicAdd(&rend[u - lo], 1ull);
+      rsrc[at] = (uint32_t)v;
+      rslot[at] = (uint8_t)(pp_rslot_packed(stride) ? j | (d - 1) << 4 : j);
+    }
+  }
+}
+
+// fmask[v] bit j = friend j of own caller v is failed (replicated failed set).
+__global__ __launch_bounds__(kPPBlock) void k_pp_fmask_rows(const DevState s, uint8_t* fmask) {
+  for (uint64_t v = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; v < s.n; v += (uint64_t)gridDim.x * kPPBlock) {
+    const uint32_t d = s.deg[v];
+    uint32_t m = 0;
+    for (uint32_t j = 0; j < d; ++j) {
+      const uint32_t u = s.ids[v * s.stride + j];
+      if ((s.gcrash[u >> 6] >> (u & 63)) & 1) m |= 1u << j;
+    }
+    fmask[v] = (uint8_t)m;
+  }
 }
 
 // Sender (simulator.go:239-241 for the flood model): informed at begin unless
@@ -611,7 +655,7 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_live_edges(const DevState s, ui
 __global__ void k_pp_seed(const DevState s, unsigned long long* next, uint32_t node, uint32_t* flag, PPSparse sp,
                           unsigned long long thr, unsigned long long bthr) {
   const unsigned long long bit = 1ull << (node & 63);
-  const bool ok = !(s.crash[node >> 6] & bit);
+  const bool ok = node != ~0u && !(s.crash[node >> 6] & bit);  // ~0u: the sender is another shard's
   if (ok) {
     s.recv[node >> 6] |= bit;
     next[node >> 6] |= bit;
@@ -625,16 +669,21 @@ __global__ void k_pp_seed(const DevState s, unsigned long long* next, uint32_t n
     c->nseg = (uint32_t)(s.n >> 12 < kPPSegs ? (s.n >> 12 ? s.n >> 12 : 1) : kPPSegs);
     c->seg_cap = (s.n + c->nseg - 1) / c->nseg;
     c->mode = PP_DENSE;
-    c->early_ok = 1;
+    c->early_ok = sp.ilist ? 1 : 0;  // shards keep no informed list: never sparse
     c->segcnt[0] = ok ? 1 : 0;
-    if (ok) sp.ilist[0] = node;
+    if (ok && sp.ilist) sp.ilist[0] = node;
   }
 }
 
 }  // namespace
 
+// Every context sets grecv / gcrash (ctx_setup: = recv / crash; push-pull
+// shards: the replicated sets); a launch without them would fault.
+inline bool pp_state_ok(const DevState& s) { return s.recv && s.crash && s.grecv && s.gcrash; }
+
 hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long long* sum, uint32_t t,
                     bool l2_only_flag, const PPSparse& sp, hipStream_t st) {
+  if (!pp_state_ok(s) || !next) return hipErrorInvalidValue;
   if (sp.ctl) {
     hipLaunchKernelGGL(k_pp_mode, dim3(1), dim3(kPPSegs), 0, st, sp.ctl);
     // early rounds: the list grows at most ~(1 + in-degree)-fold per round;
@@ -675,6 +724,7 @@ hipError_t pp_commit(const DevState& s, const unsigned long long* next, uint32_t
 }
 
 hipError_t pp_live_edges(const DevState& s, uint32_t* out, hipStream_t st) {
+  if (!pp_state_ok(s)) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(out, 0, 4, st);
   if (e != hipSuccess) return e;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.n + kPPBlock - 1) / kPPBlock, 8192);
@@ -719,6 +769,44 @@ hipError_t pp_fmask_build(const DevState& s, const unsigned long long* rend, con
   if (e != hipSuccess) return e;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.n + kPPBlock - 1) / kPPBlock, 8192);
   hipLaunchKernelGGL(k_pp_fmask, dim3(blocks), dim3(kPPBlock), 0, st, s, rend, rsrc, rslot, (uint32_t*)fmask);
+  return hipGetLastError();
+}
+
+size_t pp_rev_range_scan_bytes(uint64_t n) { return pp_rev_scan_bytes(n); }
+
+hipError_t pp_rev_count_range(const uint8_t* deg, const uint32_t* ids, uint64_t nfull, uint32_t stride, uint64_t lo,
+                              uint64_t hi, unsigned long long* rend, void* tmp, size_t tmp_bytes, hipStream_t st) {
+  const uint64_t n = hi - lo;
+  hipError_t e = hipMemsetAsync(rend, 0, (n + 1) * 8, st);
+  if (e != hipSuccess) return e;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((nfull + kPPBlock - 1) / kPPBlock, 8192);
+  hipLaunchKernelGGL(k_rev_count_range, dim3(blocks), dim3(kPPBlock), 0, st, deg, ids, nfull, stride, lo, hi, rend);
+  return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, rend, rend, (int)(n + 1), st);
+}
+
+hipError_t pp_rev_fill_range(const uint8_t* deg, const uint32_t* ids, uint64_t nfull, uint32_t stride, uint64_t lo,
+                             uint64_t hi, unsigned long long* rend, uint32_t* rsrc, uint8_t* rslot, hipStream_t st) {
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((nfull + kPPBlock - 1) / kPPBlock, 8192);
+  hipLaunchKernelGGL(k_rev_fill_range, dim3(blocks), dim3(kPPBlock), 0, st, deg, ids, nfull, stride, lo, hi, rend,
+                     rsrc, rslot);
+  return hipGetLastError();
+}
+
+hipError_t pp_fmask_rows(const DevState& s, uint8_t* fmask, hipStream_t st) {
+  if (!pp_state_ok(s) || !fmask) return hipErrorInvalidValue;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.n + kPPBlock - 1) / kPPBlock, 8192);
+  hipLaunchKernelGGL(k_pp_fmask_rows, dim3(blocks), dim3(kPPBlock), 0, st, s, fmask);
+  return hipGetLastError();
+}
+
+hipError_t pp_round_shard(const DevState& s, unsigned long long* next, uint32_t t, const PPSparse& sp,
+                          hipStream_t st) {
+  if (!pp_state_ok(s) || !next || !sp.ctl || !sp.rend || !sp.rsrc || !sp.rslot || (s.check_crashed && !sp.fmask))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_pp_mode, dim3(1), dim3(kPPSegs), 0, st, sp.ctl);
+  const uint64_t nrange = (s.W + kPPRange - 1) / kPPRange;
+  const uint32_t bblocks = (uint32_t)std::min<uint64_t>((nrange + kPPWaves - 1) / kPPWaves, 512);
+  hipLaunchKernelGGL(k_ppb_round, dim3(bblocks ? bblocks : 1), dim3(kPPRoundBlock), 0, st, s, next, sp, t);
   return hipGetLastError();
 }
 

@@ -70,7 +70,7 @@ __device__ __forceinline__ uint32_t win_open(const WinState& w, uint32_t& t) {
 }
 // A kernel of an opened window: its start and length (0: skip the window).
 __device__ __forceinline__ uint32_t win_live(const WinState& w, uint32_t& t0, uint32_t L) {
-  if (!w.ctl) return L;
+  if (!w.ctl) return w.abort_on_err && win_abort(w) ? 0u : L;  // shards: a window that overflowed is redone
   if (win_abort(w)) return 0;
   t0 = w.ctl->t;
   return w.ctl->L;
@@ -126,7 +126,9 @@ __global__ void k_units(const WinState w, uint32_t t0, uint32_t L) {
   if (threadIdx.x < L && s_t[threadIdx.x]) atomicAdd(&w.tfires[threadIdx.x], (unsigned long long)s_t[threadIdx.x]);
   for (uint32_t i = tid; i < kRegions; i += nth) { w.chist[i] = 0; w.cfill[i] = 0; }
   for (uint32_t i = tid; i < w.nfine; i += nth) w.ffill[i] = 0;
-  if (tid == 0 && !w.ctl) *w.err &= ~(kErrCoarse | kErrFine);  // device-driven: sticky until the host redoes
+  // host-driven windows clear the overflow flags here; device-driven and shard
+  // windows keep them until the host has redone the window
+  if (tid == 0 && !w.ctl && !w.abort_on_err) *w.err &= ~(kErrCoarse | kErrFine);
 }
 
 // Device-driven windows: the cut (as the host-driven engine makes it: a
@@ -250,6 +252,7 @@ __device__ __forceinline__ unsigned long long* shard_row(const WinState& w, uint
 }
 
 __global__ void k_stats_reduce(const WinState w, uint32_t t0, uint32_t L) {
+  if (w.abort_on_err && win_abort(w)) return;  // the redo of the window reduces them
   const uint32_t tid = threadIdx.x;  // one (tick, field) pair per thread
   const uint32_t k = tid / kStatFields, fld = tid % kStatFields;
   if (k >= L) return;
@@ -571,6 +574,158 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
     unsigned long long* row = shard_row(w, k);
     if (v) atomicAdd(&row[fld ? ST_SENT : ST_FIRED], v);
     // every delivered send is a receipt; k_resolve subtracts the uncounted ones
+    if (v && fld) atomicAdd(&row[ST_MSGS], v);
+  }
+}
+
+// Expand for 8-slot rows (stride 8: C5's 6-slot rows padded to 8), a LANE
+// PAIR per firing node: lane 2p loads slots 0..3 of the row (16 B), lane
+// 2p + 1 slots 4..7, in one load instruction, and each draws the Philox of its
+// own 4-slot group (RandomDrop, :172; the crash rolls, :180) -- the same keys
+// as k_expand.  A row is then one 128-B-line request from one instruction
+// instead of two (uint4 + uint2) from one lane: on gfx950 random 64-B pieces
+// read by 4 lanes went at 4.9e10 lines/s against 3.8e10 for a lane's
+// two-load row (profiles/r03_fetch_calibration.json).  H half rows per lane
+// per round (128 * H firing nodes); the LDS partition is k_expand's.
+template <bool WRITE, uint32_t H>
+__global__ __launch_bounds__(kExpandBlock) void k_expand2(const WinState w, uint32_t t0, uint32_t L,
+                                                          unsigned long long Tn, int add_stats) {
+  __shared__ ExpandLds<kExpandBlock * H * 4> sm;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, hh = lane & 1;
+  uint32_t Ls = L;
+  if (w.ctl) {
+    L = win_live(w, t0, 0);
+    if (!L) return;
+    Tn = w.ctl->Tn;
+    Ls = w.lstride;
+  }
+  const uint32_t units = Ls * w.nfine;
+  constexpr uint32_t per_round = kExpandBlock / 2 * H;  // firing nodes per round
+  if (tid < kMaxWindow * 2) (&sm.acc[0][0])[tid] = 0;
+  const uint32_t reg = tid * kCoarseSub + (blockIdx.x & (kCoarseSub - 1));
+  const unsigned long long cbase = w.ccap[reg], cend = w.ccap[reg + 1];
+  sm.cend[tid] = cend;
+  const unsigned long long rounds = (Tn + per_round - 1) / per_round;
+  unsigned long long rbeg, rend, rstep;
+  xcd_rounds(rounds, rbeg, rend, rstep);
+  uint32_t accp[kBitTicks];
+#pragma unroll
+  for (uint32_t kx = 0; kx < kBitTicks; ++kx) accp[kx] = 0;
+  for (unsigned long long rd = rbeg; rd < rend; rd += rstep) {
+    sm.cnt[tid] = 0;
+    __syncthreads();
+    uint32_t mm[H][4], mt[H][4];
+    uint32_t vv[H], kk[H];
+#pragma unroll
+    for (uint32_t q = 0; q < H; ++q) {
+      // wave-uniform group of 32 consecutive firing indices (inside one 64-group of gmap)
+      const unsigned long long g0 =
+          rd * per_round + q * (kExpandBlock / 2) + __builtin_amdgcn_readfirstlane((tid & ~63u) >> 1);
+      const unsigned long long g = g0 + (lane >> 1);
+      vv[q] = ~0u;
+      kk[q] = 0;
+      if (g0 < Tn) {
+        const uint32_t u = unit_of_wave(w, g0, g < Tn ? g : Tn - 1, Tn, units);
+        if (g < Tn) {
+          const uint32_t f = u / Ls, k = u - f * Ls;
+          const uint32_t s = (t0 + k) % w.R;
+          const uint32_t i = (uint32_t)(g - w.unit_off[u]);
+          vv[q] = (f << kFineLog) + w.flist[((size_t)s * w.nfine + f) * kFineNodes + i];
+          kk[q] = k;
+        }
+      }
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < H; ++q) {
+      uint4 a = make_uint4(kEmptyMsg, kEmptyMsg, kEmptyMsg, kEmptyMsg);
+      if (vv[q] != ~0u) a = reinterpret_cast<const uint4*>(w.ids + (size_t)vv[q] * 8)[hh];  // all rows in flight
+      mm[q][0] = a.x; mm[q][1] = a.y; mm[q][2] = a.z; mm[q][3] = a.w;
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) mt[q][j] = ~0u;
+    }
+    uint32_t sentq[H];
+#pragma unroll
+    for (uint32_t q = 0; q < H; ++q) {
+      sentq[q] = 0;
+      if (vv[q] == ~0u) continue;
+      const uint32_t v = vv[q], k = kk[q], t = t0 + k;
+      uint32_t sent = 0;
+      if (mm[q][0] != kEmptyMsg) {  // rows are sealed: an empty first slot ends the list
+        uint32_t vn, c3drop;
+        node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + v, K_DROP, vn, c3drop);
+        const uint32_t c3crash = (c3drop & 0xFFFFFFu) | (K_CRASH << 24);
+        const u32x4 r = philox(vn, t, hh, c3drop, w.key.k0, w.key.k1);  // :144, :172
+        const u32x4 rc = w.kc > 0 ? philox(vn, t, hh, c3crash, w.key.k0, w.key.k1) : u32x4{~0u, ~0u, ~0u, ~0u};
+#pragma unroll
+        for (uint32_t jj = 0; jj < 4; ++jj) {
+          if (mm[q][jj] != kEmptyMsg && (int32_t)uniform(lane_of(r, jj), 100u) >= w.kd) {  // kept: :145
+            const uint32_t tgt = mm[q][jj], bin = tgt >> kCoarseShift;
+            const uint32_t roll0 = (int32_t)uniform(lane_of(rc, jj), 100u) < w.kc;
+            mt[q][jj] = bin | (atomicAdd(&sm.cnt[bin], 1u) << 8);
+            mm[q][jj] = (tgt & ((1u << kCoarseShift) - 1)) | (k << kCoarseShift) | (roll0 << kRoll0Coarse);
+            ++sent;
+          }
+        }
+      }
+      sentq[q] = sent;
+#pragma unroll
+      for (uint32_t kx = 0; kx < kBitTicks; ++kx)
+        if (kx == k) accp[kx] += (hh ? 0u : 1u) | (sent << 16);
+    }
+    if (WRITE && add_stats && w.tstat) {  // batched trials: fired/sent per (trial, tick)
+#pragma unroll
+      for (uint32_t q = 0; q < H; ++q) {
+        const uint32_t key = vv[q] == ~0u ? ~0u : (uint32_t)((uint64_t)vv[q] >> w.tlog) * kMaxWindow + w.tofs + kk[q];
+        tstat_add(w.tstat, key, TS_FIRED, hh ? 0u : 1u, TS_SENT, sentq[q]);
+      }
+    }
+    __syncthreads();
+    if (!WRITE) {
+      if (sm.cnt[tid]) atomicAdd(&w.chist[reg], (unsigned long long)sm.cnt[tid]);
+      continue;  // the next round's first barrier orders the reuse of sm.cnt
+    }
+    block_scan256(sm.cnt, sm.off);
+    const uint32_t mycnt = sm.cnt[tid];
+    unsigned long long at = 0;
+    if (mycnt) at = atomicAdd(&w.cfill[reg], (unsigned long long)mycnt);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < H; ++q)
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j)
+        if (mt[q][j] != ~0u) {
+          const uint32_t bin = mt[q][j] & 255, p = sm.off[bin] + (mt[q][j] >> 8);
+          sm.sorted[p] = mm[q][j];
+          sm.sbin[p] = (uint8_t)bin;
+        }
+    if (mycnt) {
+      if (at + mycnt > cend - cbase) atomicOr(w.err, kErrCoarse);
+      sm.gbase[tid] = cbase + at;
+    }
+    __syncthreads();
+    const uint32_t total = sm.off[256];
+    for (uint32_t p = tid; p < total; p += kExpandBlock) {
+      const uint32_t b = sm.sbin[p];
+      const unsigned long long pos = sm.gbase[b] + (p - sm.off[b]);
+      if (pos < sm.cend[b]) w.cmsg[pos] = sm.sorted[p];
+    }
+  }
+  if (!WRITE || !add_stats) return;  // an exact redo must not count the window twice
+#pragma unroll
+  for (uint32_t kx = 0; kx < kBitTicks; ++kx) {
+    if (kx >= L) continue;
+    const uint32_t fired = wave_sum32(accp[kx] & 0xFFFFu), sent = wave_sum32(accp[kx] >> 16);
+    if ((tid & 63) == 0) {
+      if (fired) atomicAdd(&sm.acc[kx][0], (unsigned long long)fired);
+      if (sent) atomicAdd(&sm.acc[kx][1], (unsigned long long)sent);
+    }
+  }
+  __syncthreads();
+  if (tid < L * 2) {
+    const uint32_t k = tid >> 1, fld = tid & 1;
+    const unsigned long long v = sm.acc[k][fld];
+    unsigned long long* row = shard_row(w, k);
+    if (v) atomicAdd(&row[fld ? ST_SENT : ST_FIRED], v);
     if (v && fld) atomicAdd(&row[ST_MSGS], v);
   }
 }
@@ -1411,12 +1566,17 @@ __global__ void k_schedule_win(const WinState w, uint32_t node, uint32_t t, uint
 
 // ---- node-range shards (config C4) -----------------
 // Shard r of G owns nodes [r * seg_per, min((r+1) * seg_per, N)).  It keeps,
-// for EVERY node v, only the friend slots whose target it owns (prow/pent,
-// built once from the replicated table), so per-window row reads and drop
-// draws shrink with G.  Every window the shards all-gather their firing lists
-// (gfire); each shard expands every firing node against its own partition and
-// resolves its own buckets with the kernels above (keys are global ids, so
-// the union over shards equals the unsharded run bit for bit).
+// for EVERY node v, only the friend slots whose target it owns, so per-window
+// row reads and drop draws shrink with G.  Row v of the partition is pw words:
+// word 0 = the owned-slot mask (bit j: friends[v][j] is owned), then the
+// owned targets (target - lo) in slot order -- inline when there are at most
+// pw - 1 of them, else word 1 is an offset into the spill array that holds
+// them (pw is chosen so that nearly every row is inline: one dependent load
+// per firing node).  Every window the shards all-gather their firing lists
+// (gfire: per shard a segment of global node ids, then their ticks as bytes);
+// each shard expands every firing node against its own partition and resolves
+// its own buckets with the kernels above (keys are global ids, so the union
+// over shards equals the unsharded run bit for bit).
 
 // cnt[v] = friend slots of v whose target lies in [lo, hi) (sealed rows: slots
 // past the list hold kEmptyMsg, which is never in range).
@@ -1433,84 +1593,87 @@ __global__ void k_part_count(const uint32_t* ids, uint64_t n, uint32_t stride, u
   }
 }
 
-// prow[v] = (uint32) off[v]; flags err if the total does not fit 32 bits.
-__global__ void k_part_narrow(const unsigned long long* off, uint64_t n, uint32_t* prow, uint32_t* err) {
-  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v <= n;
-       v += (uint64_t)gridDim.x * blockDim.x) {
-    const unsigned long long x = off[v];
-    if (x >> 32) atomicOr(err, 1u);
-    prow[v] = (uint32_t)x;
-  }
-}
-
-// pent[prow[v] ..] = (target - lo) << 5 | j for the owned slots of v, in slot order.
-__global__ void k_part_fill(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
-                            const uint32_t* prow, uint32_t* pent) {
-  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
-       v += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t pos = prow[v];
-    for (uint32_t j = 0; j < stride; ++j) {
-      const uint32_t x = ids[v * stride + j];
-      if (x >= lo && x < hi) pent[pos++] = ((x - lo) << 5) | j;
-    }
-  }
-}
-
-__global__ void k_part_max(const uint32_t* cnt, uint64_t n, uint32_t* max_out) {
-  uint32_t m = 0;
+// hist[c] = nodes with c owned slots (c <= kWinMaxStride).
+__global__ void k_part_hist(const uint32_t* cnt, uint64_t n, unsigned long long* hist) {
+  __shared__ uint32_t h[kWinMaxStride + 1];
+  if (threadIdx.x <= kWinMaxStride) h[threadIdx.x] = 0;
+  __syncthreads();
   for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x)
-    m = max(m, cnt[v]);
-#pragma unroll
-  for (uint32_t o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor(m, o, 64));
-  if ((threadIdx.x & 63) == 0 && m) atomicMax(max_out, m);
+    atomicAdd(&h[min(cnt[v], kWinMaxStride)], 1u);
+  __syncthreads();
+  if (threadIdx.x <= kWinMaxStride && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (unsigned long long)h[threadIdx.x]);
 }
 
-// pent[v * pw ..] = (target - lo) << 5 | j for the owned slots of v, in slot
-// order, then ~0u (shards hold < 2^27 nodes, so no entry is ~0u).
-__global__ void k_part_fill_fixed(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
-                                  uint32_t pw, uint32_t* pent) {
+// Row v = [mask, owned targets - lo ...] (inline, ~0u-padded to pw) or
+// [mask, spill offset] with the targets at spill[offset ..].
+__global__ void k_part_fill_mask(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
+                                 uint32_t pw, uint32_t* pent, uint32_t* spill, unsigned long long* spill_n) {
   for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
        v += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t* row = pent + v * pw;
-    uint32_t pos = 0;
+    const uint32_t* row = ids + v * stride;
+    uint32_t mask = 0, c = 0;
     for (uint32_t j = 0; j < stride; ++j) {
-      const uint32_t x = ids[v * stride + j];
-      if (x >= lo && x < hi) row[pos++] = ((x - lo) << 5) | j;
+      const uint32_t x = row[j];
+      if (x >= lo && x < hi) { mask |= 1u << j; ++c; }
     }
-    for (; pos < pw; ++pos) row[pos] = ~0u;
+    uint32_t* out = pent + v * pw;
+    out[0] = mask;
+    uint32_t* dst = out + 1;
+    uint32_t pos = 0;
+    if (c > pw - 1) {
+      const unsigned long long at = atomicAdd(spill_n, (unsigned long long)c);
+      out[1] = (uint32_t)at;
+      pos = 1;
+      dst = spill + at;
+      for (uint32_t j = 0, i = 0; j < stride; ++j) {
+        const uint32_t x = row[j];
+        if (x >= lo && x < hi) dst[i++] = x - lo;
+      }
+    } else {
+      for (uint32_t j = 0; j < stride; ++j) {
+        const uint32_t x = row[j];
+        if (x >= lo && x < hi) dst[pos++] = x - lo;
+      }
+      pos += 1;
+    }
+    for (uint32_t k = pos + (c > pw - 1 ? 1 : 0); k < pw; ++k) out[k] = ~0u;
   }
 }
 
-// This shard's fires of the window as entries local_id << 4 | k at out[0, Tn),
-// out[Tn, seg) = ~0u (the all-gather moves seg entries per shard).
-__global__ void k_fire_compact(const WinState w, uint32_t t0, uint32_t L, unsigned long long Tn,
-                               uint32_t* out, unsigned long long seg) {
+// This shard's fires of the window: global ids at ids[0, Tn), ticks at
+// ks[0, Tn); ids[Tn, seg) = ~0u (the all-gather moves whole segments).
+__global__ void k_fire_compact(const WinState w, uint32_t t0, uint32_t L, unsigned long long Tn, uint32_t* ids,
+                               uint8_t* ks, unsigned long long seg) {
   const uint32_t units = L * w.nfine;
   for (unsigned long long g = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; g < seg;
        g += (unsigned long long)gridDim.x * blockDim.x) {
-    uint32_t e = ~0u;
+    uint32_t e = ~0u, kk = 0;
     if (g < Tn) {
       const uint32_t u = unit_of(w, g, Tn, units);
       const uint32_t f = u / L, k = u - f * L;
       const uint32_t s = (t0 + k) % w.R;
       const uint32_t i = (uint32_t)(g - w.unit_off[u]);
-      e = (((f << kFineLog) + w.flist[((size_t)s * w.nfine + f) * kFineNodes + i]) << 4) | k;
+      e = w.base + (f << kFineLog) + w.flist[((size_t)s * w.nfine + f) * kFineNodes + i];
+      kk = k;
     }
-    out[g] = e;
+    ids[g] = e;
+    ks[g] = (uint8_t)kk;
   }
 }
 
 // Expand of a shard (Node.Broadcast, simulator.go:141-147): one thread per
-// all-gathered firing entry; its partitioned row (<= MAXS owned slots, slot
-// order) is read, RandomDrop (:144, :172) is drawn once per group of 4
-// ORIGINAL slots that holds an owned slot (same keys as the unsharded
-// expand), and kept targets leave through the coarse LDS partition of
-// k_expand.  Fired is counted by the firing node's owner only.
-template <bool WRITE, uint32_t MAXS>
+// all-gathered firing entry; its partitioned row is read (one dependent load
+// of the mask and up to 3 inline targets; the rest inline or from the spill
+// array), RandomDrop (:144, :172) is drawn once per group of 4 ORIGINAL slots
+// that holds an owned slot (the unsharded expand's keys), and kept targets
+// leave through the coarse LDS partition of k_expand.  Fired is counted by the
+// firing node's owner only.  MAXE: most owned slots of a row (8 or 32).
+template <bool WRITE, uint32_t MAXE>
 __global__ __launch_bounds__(kExpandBlock) void k_expand_sh(const WinState w, uint32_t t0, uint32_t L,
                                                             int add_stats) {
-  __shared__ ExpandLds<kExpandBlock * MAXS> sm;
+  __shared__ ExpandLds<kExpandBlock * MAXE> sm;
   const uint32_t tid = threadIdx.x;
+  if (w.abort_on_err && win_abort(w)) return;
   if (tid < kMaxWindow * 2) (&sm.acc[0][0])[tid] = 0;
   const uint32_t reg = tid * kCoarseSub + (blockIdx.x & (kCoarseSub - 1));  // bin tid, this XCD's sub-region
   const unsigned long long cbase = w.ccap[reg], cend = w.ccap[reg + 1];
@@ -1525,46 +1688,55 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand_sh(const WinState w, ui
   for (unsigned long long rd = rbeg; rd < rend; rd += rstep) {
     sm.cnt[tid] = 0;
     __syncthreads();
-    uint32_t mm[MAXS], mt[MAXS];
+    uint32_t mm[MAXE], mt[MAXE];
 #pragma unroll
-    for (uint32_t j = 0; j < MAXS; ++j) { mm[j] = 0; mt[j] = ~0u; }
+    for (uint32_t j = 0; j < MAXE; ++j) { mm[j] = ~0u; mt[j] = ~0u; }
     const unsigned long long idx = rd * kExpandBlock + tid;
-    uint32_t v = ~0u, k = 0, c = 0, own = 0;
+    uint32_t v = ~0u, k = 0, c = 0, own = 0, mask = 0;
     if (idx < total) {
-      const uint32_t e = w.gfire[idx];
+      const uint32_t r = (uint32_t)(idx / w.gseg);
+      const unsigned long long i = idx - (unsigned long long)r * w.gseg;
+      const uint8_t* seg = w.gfire + (size_t)r * w.gsegb;
+      const uint32_t e = reinterpret_cast<const uint32_t*>(seg)[i];
       if (e != ~0u) {
-        const uint32_t r = (uint32_t)(idx / w.gseg);
-        v = r * w.seg_per + (e >> 4);
-        k = e & 15;
+        v = e;
+        k = seg[w.gseg * 4 + i];
         own = r == w.rank;
-        // fixed-width partitioned row: one dependent load, no row index
         const uint4* pr = reinterpret_cast<const uint4*>(w.pent + (size_t)v * w.pw);
+        const uint4 h = pr[0];  // mask + up to 3 inline targets: one dependent load
+        mask = h.x;
+        c = __popc(mask);
+        if (c <= w.pw - 1) {
+          mm[0] = h.y;
+          if (MAXE > 1) mm[1 % MAXE] = h.z;
+          if (MAXE > 2) mm[2 % MAXE] = h.w;
 #pragma unroll
-        for (uint32_t j = 0; j < MAXS; j += 4) {
-          const uint4 x = j < w.pw ? pr[j / 4] : make_uint4(~0u, ~0u, ~0u, ~0u);
-          mm[j] = x.x;
-          if (j + 1 < MAXS) mm[j + 1] = x.y;
-          if (j + 2 < MAXS) mm[j + 2] = x.z;
-          if (j + 3 < MAXS) mm[j + 3] = x.w;
+          for (uint32_t j = 3; j < MAXE; j += 4) {
+            if (j >= c) break;
+            const uint4 x = pr[(j + 1) / 4];
+            mm[j] = x.x;
+            if (j + 1 < MAXE) mm[(j + 1) % MAXE] = x.y;
+            if (j + 2 < MAXE) mm[(j + 2) % MAXE] = x.z;
+            if (j + 3 < MAXE) mm[(j + 3) % MAXE] = x.w;
+          }
+        } else {  // spilled row: its targets at spill[h.y ..]
+          const uint32_t* sp = w.pspill + h.y;
+#pragma unroll
+          for (uint32_t j = 0; j < MAXE; ++j)
+            if (j < c) mm[j] = sp[j];
         }
-#pragma unroll
-        for (uint32_t j = 0; j < MAXS; ++j) c += mm[j] != ~0u ? 1u : 0u;  // owned slots come first
       }
     }
     uint32_t sent = 0;
     if (c) {
       const uint32_t t = t0 + k;
-      uint32_t gm = 0;  // groups of 4 original slots holding an owned slot
-#pragma unroll
-      for (uint32_t j = 0; j < MAXS; ++j)
-        if (j < c) gm |= 1u << ((mm[j] & 31) >> 2);
       uint32_t vn, c3drop;
       node_key(w.tlog, w.tmask, w.key, v, K_DROP, vn, c3drop);
       const uint32_t c3crash = (c3drop & 0xFFFFFFu) | (K_CRASH << 24);
       uint32_t keep = 0, crash = 0;  // bit j: slot j kept / its message carries a crash roll
 #pragma unroll
       for (uint32_t g = 0; g < (kWinMaxStride + 3) / 4; ++g)
-        if ((gm >> g) & 1) {
+        if ((mask >> (4 * g)) & 15u) {
           const u32x4 r = philox(vn, t, g, c3drop, w.key.k0, w.key.k1);   // :144, :172
           keep |= (((int32_t)uniform(r.x, 100u) >= w.kd ? 1u : 0u) |
                    ((int32_t)uniform(r.y, 100u) >= w.kd ? 2u : 0u) |
@@ -1578,14 +1750,17 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand_sh(const WinState w, ui
                       ((int32_t)uniform(q.w, 100u) < w.kc ? 8u : 0u)) << (4 * g);
           }
         }
+      uint32_t rest = mask;
 #pragma unroll
-      for (uint32_t j = 0; j < MAXS; ++j) {
-        const uint32_t ent = mm[j];
-        if (j < c && ((keep >> (ent & 31)) & 1)) {                       // kept: :145
-          const uint32_t tl = ent >> 5, bin = tl >> kCoarseShift;
-          const uint32_t roll0 = (crash >> (ent & 31)) & 1;
-          mt[j] = bin | (atomicAdd(&sm.cnt[bin], 1u) << 8);
-          mm[j] = (tl & ((1u << kCoarseShift) - 1)) | (k << kCoarseShift) | (roll0 << kRoll0Coarse);
+      for (uint32_t i = 0; i < MAXE; ++i) {
+        if (!rest) break;
+        const uint32_t j = __builtin_ctz(rest);  // the slot of owned entry i
+        rest &= rest - 1;
+        if ((keep >> j) & 1) {                                           // kept: :145
+          const uint32_t tl = mm[i], bin = tl >> kCoarseShift;
+          const uint32_t roll0 = (crash >> j) & 1;
+          mt[i] = bin | (atomicAdd(&sm.cnt[bin], 1u) << 8);
+          mm[i] = (tl & ((1u << kCoarseShift) - 1)) | (k << kCoarseShift) | (roll0 << kRoll0Coarse);
           ++sent;
         }
       }
@@ -1606,7 +1781,7 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand_sh(const WinState w, ui
     if (mycnt) at = atomicAdd(&w.cfill[reg], (unsigned long long)mycnt);
     __syncthreads();
 #pragma unroll
-    for (uint32_t j = 0; j < MAXS; ++j)
+    for (uint32_t j = 0; j < MAXE; ++j)
       if (mt[j] != ~0u) {
         const uint32_t bin = mt[j] & 255, p = sm.off[bin] + (mt[j] >> 8);
         sm.sorted[p] = mm[j];
@@ -1641,6 +1816,16 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand_sh(const WinState w, ui
     unsigned long long* row = shard_row(w, k);
     if (v) atomicAdd(&row[fld ? ST_SENT : ST_FIRED], v);
     if (v && fld) atomicAdd(&row[ST_MSGS], v);
+  }
+}
+
+// Shards: the window's fire lists are consumed (kept if the window overflowed
+// its partition: the host redoes it, and the redo consumes them).
+__global__ void k_consume_sh(const WinState w, uint32_t t0, uint32_t L) {
+  if (win_abort(w)) return;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < L * w.nfine; i += gridDim.x * blockDim.x) {
+    const uint32_t k = i / w.nfine, f = i - k * w.nfine;
+    w.fcount[(size_t)((t0 + k) % w.R) * w.nfine + f] = 0;
   }
 }
 
@@ -1712,6 +1897,21 @@ hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, i
   const dim3 grid(blocks ? blocks : 1), blk(kExpandBlock);
   const unsigned long long tn = Tn;
   const int st = mode == 1 ? 1 : 0;
+  // 8-slot rows (5..8-slot rows padded to 8): lane-pair rows, H = GS_XH (default 8) half rows per lane
+  static const uint32_t xh = [] { const char* e = getenv("GS_XH"); return e ? (uint32_t)atoi(e) : 8u; }();
+  if (w.stride == 8 && xh != 0) {  // every mode (an exact redo must count what the write pass writes)
+    const uint32_t pr = kExpandBlock / 2 * (xh == 4 ? 4 : 8);
+    const uint32_t b2 = (uint32_t)std::min<uint64_t>((Tn + pr - 1) / pr, 8192);
+    const dim3 g2(b2 ? b2 : 1);
+    if (xh == 4) {
+      if (mode) hipLaunchKernelGGL((k_expand2<true, 4>), g2, blk, 0, s, w, t0, L, tn, st);
+      else hipLaunchKernelGGL((k_expand2<false, 4>), g2, blk, 0, s, w, t0, L, tn, 0);
+    } else {
+      if (mode) hipLaunchKernelGGL((k_expand2<true, 8>), g2, blk, 0, s, w, t0, L, tn, st);
+      else hipLaunchKernelGGL((k_expand2<false, 8>), g2, blk, 0, s, w, t0, L, tn, 0);
+    }
+    return hipGetLastError();
+  }
   if (rs <= 6 && npt == 2) {
     if (mode) hipLaunchKernelGGL((k_expand<true, 6, 2>), grid, blk, 0, s, w, t0, L, tn, st);
     else hipLaunchKernelGGL((k_expand<false, 6, 2>), grid, blk, 0, s, w, t0, L, tn, 0);
@@ -1795,43 +1995,25 @@ hipError_t part_count(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t
   return hipGetLastError();
 }
 
-hipError_t part_scan(const uint32_t* cnt, uint64_t n, unsigned long long* off, void* tmp, size_t& tmp_bytes,
-                     hipStream_t s) {
-  // off[0..n] = exclusive prefix of cnt (cnt[n] must be 0)
-  return hipcub::DeviceScan::ExclusiveScan(tmp, tmp_bytes, cnt, off, hipcub::Sum(), 0ull, (int)(n + 1), s);
-}
-
-hipError_t part_narrow(const unsigned long long* off, uint64_t n, uint32_t* prow, uint32_t* err, hipStream_t s) {
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 256) / 256, 8192);
-  hipLaunchKernelGGL(k_part_narrow, dim3(blocks), dim3(256), 0, s, off, n, prow, err);
-  return hipGetLastError();
-}
-
-hipError_t part_max(const uint32_t* cnt, uint64_t n, uint32_t* max_out, hipStream_t s) {
+hipError_t part_hist(const uint32_t* cnt, uint64_t n, unsigned long long* hist, hipStream_t s) {
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_part_max, dim3(blocks ? blocks : 1), dim3(256), 0, s, cnt, n, max_out);
+  hipLaunchKernelGGL(k_part_hist, dim3(blocks ? blocks : 1), dim3(256), 0, s, cnt, n, hist);
   return hipGetLastError();
 }
 
-hipError_t part_fill_fixed(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi, uint32_t pw,
-                           uint32_t* pent, hipStream_t s) {
+hipError_t part_fill_mask(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi, uint32_t pw,
+                          uint32_t* pent, uint32_t* spill, unsigned long long* spill_n, hipStream_t s) {
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_part_fill_fixed, dim3(blocks ? blocks : 1), dim3(256), 0, s, ids, n, stride, lo, hi, pw, pent);
+  hipLaunchKernelGGL(k_part_fill_mask, dim3(blocks ? blocks : 1), dim3(256), 0, s, ids, n, stride, lo, hi, pw, pent,
+                     spill, spill_n);
   return hipGetLastError();
 }
 
-hipError_t part_fill(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
-                     const uint32_t* prow, uint32_t* pent, hipStream_t s) {
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_part_fill, dim3(blocks ? blocks : 1), dim3(256), 0, s, ids, n, stride, lo, hi, prow, pent);
-  return hipGetLastError();
-}
-
-hipError_t win_fire_compact(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, uint32_t* out,
+hipError_t win_fire_compact(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, uint32_t* ids, uint8_t* ks,
                             uint64_t seg, hipStream_t s) {
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((seg + 255) / 256, 8192);
   hipLaunchKernelGGL(k_fire_compact, dim3(blocks ? blocks : 1), dim3(256), 0, s, w, t0, L,
-                     (unsigned long long)Tn, out, (unsigned long long)seg);
+                     (unsigned long long)Tn, ids, ks, (unsigned long long)seg);
   return hipGetLastError();
 }
 
@@ -1841,13 +2023,19 @@ hipError_t win_expand_sh(const WinState& w, uint32_t t0, uint32_t L, int mode, h
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((total + kExpandBlock - 1) / kExpandBlock, 8192);
   const dim3 grid(blocks ? blocks : 1), blk(kExpandBlock);
   const int st = mode == 1 ? 1 : 0;
-  if (w.pw <= 8) {
+  if (w.stride <= 8) {
     if (mode) hipLaunchKernelGGL((k_expand_sh<true, 8>), grid, blk, 0, s, w, t0, L, st);
     else hipLaunchKernelGGL((k_expand_sh<false, 8>), grid, blk, 0, s, w, t0, L, 0);
   } else {
     if (mode) hipLaunchKernelGGL((k_expand_sh<true, kWinMaxStride>), grid, blk, 0, s, w, t0, L, st);
     else hipLaunchKernelGGL((k_expand_sh<false, kWinMaxStride>), grid, blk, 0, s, w, t0, L, 0);
   }
+  return hipGetLastError();
+}
+
+hipError_t win_consume_sh(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s) {
+  const uint32_t blocks = std::min<uint32_t>((L * w.nfine + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_consume_sh, dim3(blocks ? blocks : 1), dim3(256), 0, s, w, t0, L);
   return hipGetLastError();
 }
 

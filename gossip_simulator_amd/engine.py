@@ -89,7 +89,13 @@ class Simulator:
         self.L = _lib.load()
         self._p = cfg.to_params()
         h = C.c_void_p()
-        if _rank is not None:
+        if _rank is not None and len(_rank) == 4:  # host exchange: (nranks, rank, all_gather, all_reduce)
+            nranks, rank, ag, ar = _rank
+            self._xfns = self._exchange_fns(ag, ar)  # kept alive with the context
+            rc = self.L.gs_create_rank_exchange(C.byref(self._p), cfg.device, nranks, rank,
+                                                C.byref(self._xfns[2]), C.byref(h))
+            what = "gs_create_rank_exchange"
+        elif _rank is not None:
             nranks, rank, cid = _rank
             rc = self.L.gs_create_rank(C.byref(self._p), cfg.device, nranks, rank, cid, C.byref(h))
             what = "gs_create_rank"
@@ -117,6 +123,40 @@ class Simulator:
             t0 = cfg.trials * rank // nranks
             sim.trials = cfg.trials * (rank + 1) // nranks - t0
         return sim
+
+    @classmethod
+    def rank_exchange(cls, cfg: Config, nranks: int, rank: int, all_gather, all_reduce_sum):
+        """Rank `rank` of `nranks` processes with the exchange done by the caller
+        (gs_create_rank_exchange): all_gather(send: np.uint8 array) -> np.uint8
+        array of nranks * len(send) bytes, rank-major; all_reduce_sum(x:
+        np.uint64 array) -> the element-wise sum over the ranks."""
+        return cls(cfg, _rank=(nranks, rank, all_gather, all_reduce_sum))
+
+    @staticmethod
+    def _exchange_fns(all_gather, all_reduce_sum):
+        def ag(_user, send, recv, nbytes):
+            try:
+                src = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(send))
+                out = np.asarray(all_gather(src.copy()), dtype=np.uint8).ravel()
+                C.memmove(recv, out.ctypes.data, out.nbytes)
+                return 0
+            except Exception:  # noqa: BLE001 -- reported to the engine as a failed exchange
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        def ar(_user, buf, count):
+            try:
+                x = np.ctypeslib.as_array(buf, shape=(count,))
+                x[:] = np.asarray(all_reduce_sum(x.copy()), dtype=np.uint64)
+                return 0
+            except Exception:  # noqa: BLE001
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        f1, f2 = _lib.ALL_GATHER_FN(ag), _lib.ALL_REDUCE_FN(ar)
+        return f1, f2, _lib.Exchange(None, f1, f2)
 
     # -- plumbing --------------------------------------------------------
     def _check(self, rc: int, what: str):
@@ -248,6 +288,12 @@ class Simulator:
     def timing(self) -> dict:
         t = Timing()
         self._check(self.L.gs_timing_get(self.h, C.byref(t)), "gs_timing_get")
+        return {f: getattr(t, f) for f, _ in Timing._fields_}
+
+    def shard_timing(self, index: int) -> dict:
+        """Kernel timing of shard `index` (GS_FLAG_TIMING)."""
+        t = Timing()
+        self._check(self.L.gs_shard_timing(self.h, index, C.byref(t)), "gs_shard_timing")
         return {f: getattr(t, f) for f, _ in Timing._fields_}
 
 

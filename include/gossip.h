@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 3
+#define GS_ABI_VERSION 4
 
 enum {
   GS_OK = 0,
@@ -162,12 +162,30 @@ int gs_create_multi(const gs_params* params, const int* devices, int ndev, gs_ct
  * ships the GS_COMM_ID_BYTES bytes to every rank; each rank calls
  * gs_create_rank.  A flood run is then node-range sharded over the ranks with
  * an RCCL all-gather per window and an RCCL sum per gs_step (every rank's
- * gs_step/gs_run/gs_totals return the global counters); params.trials > 1
- * gives each rank its share of the trials (no communication, id may be NULL). */
+ * gs_step/gs_run/gs_totals return the global counters); a push-pull run
+ * (rows <= 16 slots) is node-range sharded with an all-gather of the informed
+ * set's owned words per round; params.trials > 1 gives each rank its share of
+ * the trials (no communication, id may be NULL).  gs_create_multi splits both
+ * models the same way over its devices. */
 #define GS_COMM_ID_BYTES 128
 int gs_comm_unique_id(uint8_t id[GS_COMM_ID_BYTES]);
 int gs_create_rank(const gs_params* params, int device, int nranks, int rank,
                    const uint8_t* id, gs_ctx** out);
+/* The same with the exchange done by the caller instead of RCCL (MPI, a
+ * torch.distributed group, a test harness): every rank calls it with the same
+ * nranks and its own rank, and the callbacks move HOST bytes between the
+ * ranks -- all_gather: `bytes` from every rank into recv (nranks * bytes,
+ * rank-major; send is this rank's part); all_reduce_sum_u64: element-wise sum
+ * over the ranks of count uint64, in place.  Both return 0 on success and are
+ * called by every rank in the same order.  Unlike every other argument the
+ * struct is kept: user and the callbacks must stay valid until gs_destroy. */
+typedef struct gs_exchange {
+  void* user;
+  int (*all_gather)(void* user, const void* send, void* recv, size_t bytes);
+  int (*all_reduce_sum_u64)(void* user, uint64_t* buf, size_t count);
+} gs_exchange;
+int gs_create_rank_exchange(const gs_params* params, int device, int nranks, int rank, const gs_exchange* ex,
+                            gs_ctx** out);
 /* Nodes [lo, hi) owned by shard `index` of a context (index < *nshards);
  * an unsharded context is one shard [0, n). */
 int gs_shard_info(const gs_ctx* ctx, uint32_t index, uint32_t* nshards, uint64_t* lo, uint64_t* hi);
@@ -227,6 +245,9 @@ int gs_read_received(gs_ctx* ctx, uint64_t* words, size_t nwords);
 int gs_read_crashed(gs_ctx* ctx, uint64_t* words, size_t nwords);
 
 int gs_timing_get(gs_ctx* ctx, gs_timing* out);
+/* The same for shard `index` of a sharded (or batched) context's members;
+ * index 0 of a one-device context is gs_timing_get. */
+int gs_shard_timing(gs_ctx* ctx, uint32_t index, gs_timing* out);
 /* Renumber the context's trial(s) to trial .. trial+trials-1 (Philox
  * counter word 3) between runs, keeping its device buffers: the overlay must
  * be built or loaded again before gs_broadcast_begin (config C3 runs batch

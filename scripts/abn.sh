@@ -1,16 +1,15 @@
 #!/bin/bash
-# A/B/C... in one gpurun call: the C5 flood bench (no extensions) once per
-# library build, twice round-robin.  Usage: bash scripts/abn.sh lib1.so lib2.so ...
-# ("main" = gossip_simulator_amd/libgossip_hip.so)
+# A/B/C... in one gpurun call: bench (no extensions) once per env setting, the
+# whole list twice (interleaved), one summary line each.
+# Usage: bash scripts/abn.sh "ENV_A=1" "ENV_B=1" ... [-- bench args]
 set -o pipefail
-mkdir -p gpurun_out/abn
-for pass in 1 2; do
-  for lib in "$@"; do
-    tag=$(basename "$lib" .so)
-    if [ "$lib" = main ]; then unset GS_LIB_PATH; else export GS_LIB_PATH=$PWD/gossip_simulator_amd/$lib; fi
-    timeout -k 10 300 python -u bench.py --steps 6 --warmup 1 --cpu-n 0 --no-extensions --no-c3 --no-c4 \
-      > gpurun_out/abn/${tag}_$pass.json 2>/dev/null || exit 1
-    python3 scripts/showbench.py gpurun_out/abn/${tag}_$pass.json | head -2 | sed "s/^/$pass $tag /"
+envs=(); while [ $# -gt 0 ] && [ "$1" != "--" ]; do envs+=("$1"); shift; done; [ "${1:-}" = "--" ] && shift
+mkdir -p gpurun_out
+for rep in 1 2; do
+  i=0
+  for e in "${envs[@]}"; do
+    i=$((i+1))
+    env $e timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --cpu-n 0 --no-extensions "$@" > gpurun_out/abn_${i}_$rep.json 2>gpurun_out/abn_${i}_$rep.err || { tail -3 gpurun_out/abn_${i}_$rep.err; exit 1; }
+    python3 scripts/showbench.py gpurun_out/abn_${i}_$rep.json | head -1 | sed "s/^/$rep [$e] /"
   done
 done
-unset GS_LIB_PATH

@@ -7,7 +7,12 @@
   shard_windows: per-window all-gather of the firing sets, per-poll sum of
   the counters) restated over oracle shards and gloo collectives -- must be
   bit-identical to the unsharded run.  The HIP path of the same protocol is
-  checked on the GPU (tests/test_gpu_multi.py).
+  checked on the GPU (tests/test_gpu_multi.py, and with two processes in
+  tests/test_rank_exchange.py).
+* Push-pull node-range sharding (config C5): the sharded round of
+  gs_api.cpp pp_shard_step (bottom-up on the shard's own nodes against the
+  replicated informed set, then an all-gather of the owned words) restated in
+  numpy over gloo -- must equal the oracle's unsharded pushpull_step per round.
 """
 from __future__ import annotations
 
@@ -118,6 +123,87 @@ def _sharded_worker(rank, world, port, kw, out_dir):
     dist.destroy_process_group()
 
 
+def pp_round_shard(O, p, deg, ids, inf, dead, t, lo, hi, rev):
+    """One sharded push-pull round restated (k_ppb_round on nodes [lo, hi)):
+    returns this shard's newly informed nodes and its (fired, sent, msgs)."""
+    key = [int(p.seed) & 0xFFFFFFFF, int(p.seed) >> 32]
+    kd = O.threshold(p.drop_rate)
+    c3 = (9 << 24) | int(p.trial)
+
+    def call(v):  # v's keyed pick slot and whether the call is kept
+        r = O.philox([v, t, 0, c3], key)
+        return (r[0] * int(deg[v])) >> 32, ((r[1] * 100) >> 32) >= kd
+
+    fired = sent = msgs = 0
+    new = []
+    for v in range(lo, hi):
+        if dead[v]:
+            continue
+        d = int(deg[v])
+        if d:
+            fired += 1
+            j, kept = call(v)
+            if inf[v]:
+                if kept:  # a push: counted by the caller, found by the receiver's owner
+                    sent += 1
+                    msgs += 0 if dead[int(ids[v, j])] else 1
+                continue
+            u = int(ids[v, j])
+            if kept and inf[u]:  # a pull from an informed friend
+                sent += 1
+                msgs += 1
+                new.append(v)
+                continue
+        if inf[v]:
+            continue
+        for (w, jw) in rev.get(v, ()):  # pushes v receives: its in-edges
+            if inf[w] and int(deg[w]) and call(w) == (jw, True):
+                new.append(v)
+                break
+    return new, fired, sent, msgs
+
+
+def _pp_sharded_worker(rank, world, port, kw, out_dir):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import pyoracle as O
+    from gossip_simulator_amd import dist as gd
+    p = O.make_params(**kw)
+    deg, ids, _, _ = O.overlay(p)
+    n = int(p.n)
+    lo, hi = gd.shard_range(n, rank, world)
+    dead = np.random.default_rng(3).random(n) < 0.02
+    rev = {}
+    for v in range(n):
+        for j in range(int(deg[v])):
+            u = int(ids[v, j])
+            if lo <= u < hi:
+                rev.setdefault(u, []).append((v, j))
+    inf = np.zeros(n, bool)
+    s = int(O.pick_sender(p))
+    inf[s] = not dead[s]
+    rows, recv = [], int(inf.sum())
+    for t in range(1, 31):
+        new, fired, sent, msgs = pp_round_shard(O, p, deg, ids, inf, dead, t, lo, hi, rev)
+        mine = np.zeros(hi - lo, bool)
+        mine[np.array(new, dtype=np.int64) - lo] = True
+        mine |= inf[lo:hi]
+        seg = gd.shard_range(n, 0, world)[1]  # every segment padded to the first (full) shard's size
+        part = torch.from_numpy(np.pad(mine, (0, seg - (hi - lo))))
+        got = [torch.zeros_like(part) for _ in range(world)]
+        dist.all_gather(got, part)
+        nxt = np.concatenate([g.numpy() for g in got])[:n]
+        c = torch.tensor([fired, sent, msgs], dtype=torch.int64)
+        dist.all_reduce(c)
+        recv += int((nxt & ~inf).sum())
+        inf = nxt
+        rows.append([t, *c.tolist(), recv, 0, recv])
+    np.save(os.path.join(out_dir, f"pp{rank}.npy"), np.array(rows, dtype=np.int64))
+    np.save(os.path.join(out_dir, f"ppinf{rank}.npy"), inf)
+    dist.destroy_process_group()
+
+
 def _trials_worker(rank, world, port, out_dir):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -159,6 +245,36 @@ def test_node_range_sharding_world2_bit_identical(oracle, tmp_path, kw):
     crash = np.load(tmp_path / "crash0.npy") | np.load(tmp_path / "crash1.npy")
     assert np.array_equal(recv, e.received()) and np.array_equal(crash, e.crashed())
     assert not (np.load(tmp_path / "recv0.npy") & np.load(tmp_path / "recv1.npy")).any()
+
+
+def test_pushpull_node_range_sharding_world2_bit_identical(oracle, tmp_path):
+    """Config C5's push-pull in two node-range shards (bottom-up rounds on the
+    own nodes, all-gather of the owned informed words): every round equals
+    the oracle's unsharded pushpull_step, 2 % of the nodes failed."""
+    kw = dict(n=20000, fanout=5, fanin=6, delay_low=10, delay_high=20, drop_rate=0.1, crash_rate=0.0,
+              seed=0x5EED, trial=0, model=1)
+    world = 2
+    mp.start_processes(_pp_sharded_worker, args=(world, free_port(), kw, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    a, b = np.load(tmp_path / "pp0.npy"), np.load(tmp_path / "pp1.npy")
+    assert np.array_equal(a, b)
+    p = oracle.make_params(**kw)
+    deg, ids, _, _ = oracle.overlay(p)
+    n = int(p.n)
+    dead = np.random.default_rng(3).random(n) < 0.02
+    w = np.zeros((n + 63) // 64, np.uint64)
+    idx = np.nonzero(dead)[0]
+    np.bitwise_or.at(w, idx // 64, np.left_shift(np.uint64(1), (idx % 64).astype(np.uint64)))
+    e = oracle.Engine(p, deg, ids)
+    e.set_failed(w)
+    e.begin(-1)
+    want = e.step(30).astype(np.int64)
+    want[:, 5] = 0
+    assert np.array_equal(a, want)
+    inf = np.load(tmp_path / "ppinf0.npy")
+    rec = e.received()
+    bits = (rec[np.arange(n) // 64] >> (np.arange(n) % 64).astype(np.uint64)) & np.uint64(1)
+    assert np.array_equal(inf, bits.astype(bool))
 
 
 def test_trial_sharding_world2_matches_serial(oracle, tmp_path):

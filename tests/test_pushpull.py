@@ -242,3 +242,83 @@ def test_gpu_pushpull_run_polls_like_oracle(oracle, fail_frac, rounds):
         assert int(sim.totals()["messages"]) == int(rows[:, 3].sum())
         assert status == (gs.GS_RUN_COVERED if oracle.covered(int(rows[-1][4]), n) else gs.GS_RUN_QUIESCENT)
         assert sha(sim.received()) == sha(e.received())
+
+
+# ---- node-range shards (SURVEY.md 8(e)2 for config C5) ------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw,stride,dlo,dhi,fail_frac,G", [
+    (dict(PP, n=20000), 6, 5, 6, 0.01, 2),                                  # C5 shape, 1 % failed
+    (dict(PP, n=65536 + 77, drop_rate=0.29, trial=5), 16, 1, 16, 0.0, 3),   # widest packed rows, 77-node shard
+    (dict(PP, n=50000, drop_rate=0.05), 8, 0, 8, 0.02, 2),                  # zero degrees, 8-slot fmask
+])
+def test_gpu_pushpull_shards_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac, G):
+    """G node-range shards of one push-pull run on one GPU (gs_create_multi):
+    every round is bottom-up on each shard's own nodes against the replicated
+    informed set, exchanged after the round; per round bit-exact to the
+    oracle's pushpull_step (oracle/gsoracle.c), as the unsharded engine is."""
+    import gossip_simulator_amd as gs
+    gs.load()
+    n = kw["n"]
+    deg, ids = random_table(n, stride, dlo, dhi, seed=n)
+    e = oracle.Engine(oracle.make_params(**kw), deg, ids)
+    failed = words_of(np.random.default_rng(1).random(n) < fail_frac) if fail_frac else None
+    if failed is not None:
+        e.set_failed(failed)
+    e.begin(-1)
+    cfg = gs.Config(n=n, fanout=kw["fanout"], fanin=kw["fanin"], delaylow=kw["delay_low"],
+                    delayhigh=kw["delay_high"], droprate=kw["drop_rate"], crashrate=kw["crash_rate"],
+                    seed=kw["seed"], trial=kw["trial"], model="pushpull")
+    with gs.Simulator(cfg, devices=[0] * G) as sim:
+        assert len(sim.shard_info()) == G
+        sim.load_peers(deg, ids)
+        if failed is not None:
+            sim.set_failed(failed)
+        sim.broadcast_begin(-1)
+        for r in range(60):
+            a, b = e.step(1), sim.step(1)
+            assert np.array_equal(a, b), f"round {r + 1}:\n{a}\n{b}"
+            assert sha(e.received()) == sha(sim.received()), f"informed set differs at round {r + 1}"
+            if oracle.covered(int(a[0, 4]), n) or int(a[0, 4]) == 0:
+                break
+        assert sim.timing()["pp_bottom_rounds"] == r + 1
+
+
+@pytest.fixture(scope="module")
+def pp_1e6():
+    """Push-pull at N = 1e6 over the GPU overlay, 1 % failed: the unsharded run."""
+    import gossip_simulator_amd as gs
+    gs.load()
+    n = 1_000_000
+    cfg = gs.Config(n=n, fanout=5, fanin=6, droprate=0.1, crashrate=0.0, seed=0x5EED, model="pushpull")
+    failed = words_of(np.random.default_rng(7).random(n) < 0.01)
+    with gs.Simulator(cfg) as sim:
+        sim.build_overlay()
+        deg, ids = sim.read_peers()
+        sim.set_failed(failed)
+        sim.broadcast_begin(-1)
+        rows = sim.step(45)
+        polls = None
+        rec = sim.received()
+        sim.reset()
+        sim.broadcast_begin(-1)
+        polls, status = sim.run(poll=5)
+    return cfg, deg, ids, failed, rows, rec, polls, status
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_gpu_pushpull_shards_match_unsharded_1e6(pp_1e6, G):
+    """N = 1e6 (C5 shape, 1 % failed) in G shards, per round and through
+    gs_run's poll and stop rule: identical to the unsharded run."""
+    import gossip_simulator_amd as gs
+    cfg, deg, ids, failed, rows, rec, polls, status = pp_1e6
+    with gs.Simulator(cfg, devices=[0] * G) as sim:
+        sim.load_peers(deg, ids)
+        sim.set_failed(failed)
+        sim.broadcast_begin(-1)
+        assert np.array_equal(sim.step(45), rows)
+        assert sha(sim.received()) == sha(rec)
+        sim.reset()
+        sim.broadcast_begin(-1)
+        p2, s2 = sim.run(poll=5)
+        assert s2 == status and np.array_equal(p2, polls)
