@@ -22,6 +22,7 @@ GS_FLAG_PP_DENSE = 8
 GS_FLAG_PP_EARLY = 16
 GS_FLAG_PP_TOPDOWN = 32
 GS_FLAG_PP_BOTTOM = 64
+GS_FLAG_PP_ANSWER = 128
 GS_MODEL_FLOOD, GS_MODEL_PUSHPULL = 0, 1
 GS_RUN_COVERED, GS_RUN_QUIESCENT, GS_RUN_MAX_TICKS, GS_RUN_RUNNING = 0, 1, 2, -1
 GS_COMM_ID_BYTES = 128
@@ -86,7 +87,8 @@ class Timing(C.Structure):
                 ("overlay_ms", C.c_double), ("expand_ms", C.c_double),
                 ("part_ms", C.c_double), ("windows", C.c_uint64), ("exact_redos", C.c_uint64),
                 ("prep_ms", C.c_double),
-                ("pp_early_rounds", C.c_uint64), ("pp_bottom_rounds", C.c_uint64)]
+                ("pp_early_rounds", C.c_uint64), ("pp_bottom_rounds", C.c_uint64),
+                ("pp_answer_rounds", C.c_uint64)]
 
 
 # gs_exchange (gossip.h): host callbacks of a gs_create_rank_exchange rank

@@ -1558,7 +1558,7 @@ int pp_shard_begin(gs_ctx* acc, uint64_t sender) {
     CK(m, hipSetDevice(m->dev));
     if (int rc = pp_prepare(m)) return fail(acc, rc, m->err);
     const uint32_t node = sender >= m->lo && sender < m->hi ? (uint32_t)(sender - m->lo) : ~0u;
-    CK(m, pp_seed(m->st, m->d_next, node, m->d_flag, m->sp, 0ull, 0ull, m->stream));
+    CK(m, pp_seed(m->st, m->d_next, node, m->d_flag, m->sp, 0ull, 0ull, ~0ull, m->stream));
     uint32_t ok = 0;
     CK(m, hipMemcpyAsync(&ok, m->d_flag, 4, hipMemcpyDeviceToHost, m->stream));
     CK(m, hipStreamSynchronize(m->stream));
@@ -1640,6 +1640,19 @@ int pp_shard_step(gs_ctx* acc, uint32_t ticks, gs_tick_stats* out) {
   return GS_OK;
 }
 
+// Dense rounds below the bottom-up threshold run pull-answer (informed nodes
+// answer the pulls among their in-edges) once |I| >= n * GS_PP_ANSWER256 / 256
+// (default 0: every such round; 256 = never, the top-down rounds), when the
+// reverse table has packed slots and the failed mask (if any) has fmask.
+unsigned long long pp_answer_thr(const gs_ctx* c) {
+  const bool can = c->sp.ctl && pp_rslot_packed(c->st.stride) && (!c->failed || c->sp.fmask);
+  if (!can || (c->p.flags & GS_FLAG_PP_TOPDOWN)) return ~0ull;
+  if (c->p.flags & GS_FLAG_PP_ANSWER) return 0;
+  const char* e = getenv("GS_PP_ANSWER256");
+  const unsigned long long k = (unsigned long long)std::min(std::max(e ? atoi(e) : 0, 0), 256);
+  return k == 256 ? ~0ull : (unsigned long long)(((unsigned __int128)c->st.n * k) >> 8);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1666,7 +1679,8 @@ int gs_broadcast_begin(gs_ctx* c, int64_t sender) {
     RC(pp_prepare(c));
     const uint64_t n = c->st.n;
     const unsigned long long thr = (c->p.flags & GS_FLAG_PP_EARLY) ? n : (n >> pp_shift());
-    CK(c, pp_seed(c->st, c->d_next, (uint32_t)s, c->d_flag, c->sp, thr, pp_bottom_thr(c), c->stream));
+    CK(c, pp_seed(c->st, c->d_next, (uint32_t)s, c->d_flag, c->sp, thr, pp_bottom_thr(c), pp_answer_thr(c),
+                  c->stream));
     uint32_t ok = 0;
     CK(c, hipMemcpyAsync(&ok, c->d_flag, 4, hipMemcpyDeviceToHost, c->stream));
     CK(c, hipStreamSynchronize(c->stream));
@@ -2724,7 +2738,7 @@ int gs_timing_get(gs_ctx* c, gs_timing* out) {
   if (!c || !out) return GS_EINVAL;
   *out = c->group ? c->mem[0]->timing : c->timing;  // a group: its first member's kernels
   if (c->group) out->overlay_ms = c->timing.overlay_ms;
-  out->pp_early_rounds = out->pp_bottom_rounds = 0;
+  out->pp_early_rounds = out->pp_bottom_rounds = out->pp_answer_rounds = 0;
   gs_ctx* pc = c->group ? c->mem[0] : c;  // a group: its first shard's rounds (all shards run the same modes)
   if (c->pp && pc->sp.ctl && c->begun) {
     CK(pc, hipSetDevice(pc->dev));
@@ -2733,6 +2747,7 @@ int gs_timing_get(gs_ctx* c, gs_timing* out) {
     CK(pc, hipStreamSynchronize(pc->stream));
     out->pp_early_rounds = h.nearly;
     out->pp_bottom_rounds = h.nbottom;
+    out->pp_answer_rounds = h.nanswer;
   }
   return GS_OK;
 }

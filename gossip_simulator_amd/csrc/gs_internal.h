@@ -249,7 +249,13 @@ inline uint64_t pp_summary_total_words(uint64_t W) { return 2 * pp_summary_words
 // ninf >= bthr (dense rounds only: the early test comes first).  Needs the
 // reverse table with packed slots (stride <= 16) and, with a failure mask,
 // fmask (stride <= 8).
-enum PPMode : uint32_t { PP_DENSE = 0, PP_EARLY = 1, PP_BOTTOM = 2 };
+// Pull-answer (PP_ANSWER, k_ppa_round), for the middle rounds between the
+// sparse and the bottom-up ones (ninf >= athr): informed nodes answer the
+// pulls -- an informed u scans its in-edges (v, j) and informs v when v's pick
+// is slot j, kept, and v is live and uninformed -- so the uninformed callers'
+// random gathers of their picks' words (most of which fail) are not made;
+// informed callers push as in the top-down round.
+enum PPMode : uint32_t { PP_DENSE = 0, PP_EARLY = 1, PP_BOTTOM = 2, PP_ANSWER = 3 };
 // rslot entries: slot j in bits 0..3 and deg(v) - 1 in bits 4..7 when
 // stride <= 16 (the caller's pick needs no deg[v] gather), else j alone.
 __host__ __device__ inline bool pp_rslot_packed(uint32_t stride) { return stride <= 16; }
@@ -262,6 +268,7 @@ struct PPCtl {
   unsigned long long ninf;      // |I|: informed nodes (all modes)
   unsigned long long thr;       // early rounds while ninf <= thr
   unsigned long long bthr;      // dense rounds bottom-up once ninf >= bthr (0: always, ~0: never)
+  unsigned long long athr;      // other dense rounds pull-answer once ninf >= athr (~0: never, top-down)
   unsigned long long ncallers;  // live nodes with a non-empty row: calls per round
   unsigned long long seg_cap;   // entries per segment
   uint32_t nseg;                // segments in use (<= kPPSegs)
@@ -269,6 +276,7 @@ struct PPCtl {
   uint32_t early_ok;            // the informed list is complete (never re-entered)
   uint32_t ovf;                 // a segment overflowed this round
   uint32_t nearly, nbottom;     // rounds run sparse / bottom-up since the broadcast began (gs_timing)
+  uint32_t nanswer, pad_;       // rounds run pull-answer
   unsigned long long segcnt[kPPSegs];      // entries in segment s (incl. this round's appends)
   unsigned long long seglen[kPPSegs];      // entries at the start of this round
   unsigned long long segpre[kPPSegs + 1];  // prefix of seglen: list index -> segment
@@ -289,7 +297,8 @@ hipError_t pp_commit(const DevState& s, const unsigned long long* next, uint32_t
 // Sender informed unless failed; flag = 1 if informed.  Also initialises ctl
 // (counts live callers: a pass over deg and the failed mask).
 hipError_t pp_seed(const DevState& s, unsigned long long* next, uint32_t node, uint32_t* flag,
-                   const PPSparse& sp, unsigned long long thr, unsigned long long bthr, hipStream_t st);
+                   const PPSparse& sp, unsigned long long thr, unsigned long long bthr, unsigned long long athr,
+                   hipStream_t st);
 // Reverse table: rend must hold n + 1 words of scratch-free u64 space; tmp /
 // tmp_bytes the hipcub scan workspace (pp_rev_scan_bytes).
 size_t pp_rev_scan_bytes(uint64_t n);

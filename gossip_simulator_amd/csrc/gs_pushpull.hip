@@ -346,6 +346,120 @@ __global__ __launch_bounds__(kPPRoundBlock) void k_ppb_round(const DevState s, u
   block_add<kPPRoundBlock>(sh, v3, 3, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
 }
 
+// Pull-answer round (PP_ANSWER): same draws, outcomes and counters as
+// k_pp_round.  A wave streams ranges of kPPRange words, a lane per node, and
+// queues its INFORMED nodes in LDS; each 64 queued nodes are resolved
+// together, a lane each: the node's own call (a push, as top-down: one
+// no-return atomicOr into its friend's word unless the friend is failed) and
+// the pulls it answers -- its in-edges (v, j) whose caller v picks slot j
+// (recomputed from the packed slot byte) and is not lost; only such an
+// in-edge costs a gather of v's recv / failed words (v must be live and
+// uninformed: its call is a pull from this informed node, counted here).
+// Every live caller is counted as fired from ctl->ncallers.
+__device__ __forceinline__ void ppa_resolve(const DevState& s, const PPSparse& sp, uint32_t t, uint32_t c3,
+                                            const uint32_t* q, uint32_t cnt, uint64_t base,
+                                            unsigned long long* __restrict__ next, uint64_t& sent, uint64_t& msgs) {
+  const uint32_t lane = threadIdx.x & 63;
+  if (lane >= cnt) return;
+  const uint32_t e = q[lane], loc = e & 0xFFFu, d = e >> 16;
+  const uint64_t u = base + loc;  // informed (so live)
+  const bool cc = s.check_crashed;
+  if (d > 0) {  // u's own call: a push
+    const u32x4 r = philox((uint32_t)(s.gbase + u), t, 0, c3, s.key.k0, s.key.k1);
+    if ((int32_t)uniform(r.y, 100u) >= s.kd) {
+      const uint32_t j = uniform(r.x, d);
+      const uint32_t w = s.ids[u * s.stride + j];
+      ++sent;
+      const bool dead = sp.fmask ? ((sp.fmask[u] >> j) & 1) != 0
+                                 : (cc && ((s.gcrash[w >> 6] >> (w & 63)) & 1));
+      if (!dead) {
+        ++msgs;
+        atomicOr(&next[w >> 6], 1ull << (w & 63));
+      }
+    }
+  }
+  const unsigned long long qb = u ? sp.rend[u - 1] : 0ull, qe = sp.rend[u];
+  for (unsigned long long q0 = qb; q0 < qe; q0 += kPPEdges) {
+    uint32_t src[kPPEdges], x[kPPEdges];
+#pragma unroll
+    for (uint32_t k = 0; k < kPPEdges; ++k) {
+      const bool in = q0 + k < qe;
+      src[k] = in ? sp.rsrc[q0 + k] : 0u;
+      x[k] = in ? sp.rslot[q0 + k] : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kPPEdges; ++k) {
+      if (q0 + k >= qe) break;
+      const u32x4 r = philox(src[k], t, 0, c3, s.key.k0, s.key.k1);
+      if (uniform(r.x, (x[k] >> 4) + 1) == (x[k] & 15u) && (int32_t)uniform(r.y, 100u) >= s.kd) {
+        const unsigned long long vb = 1ull << (src[k] & 63);
+        const bool iv = (s.grecv[src[k] >> 6] & vb) != 0;
+        const bool fv = cc && (s.gcrash[src[k] >> 6] & vb) != 0;
+        if (!iv && !fv) {  // v's pull from this informed node succeeds
+          ++sent;
+          ++msgs;
+          atomicOr(&next[src[k] >> 6], vb);
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kPPRoundBlock) void k_ppa_round(const DevState s, unsigned long long* __restrict__ next,
+                                                             const PPSparse sp, uint32_t t) {
+  __shared__ uint64_t sh[3 * kPPWaves];
+  __shared__ uint32_t s_q[kPPWaves][kPPQ];
+  PPCtl* c = sp.ctl;
+  if (c->mode != PP_ANSWER) return;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t* q = s_q[wv];
+  const uint32_t c3 = ctr3(K_PUSHPULL, s.key.trial);
+  uint64_t sent = 0, msgs = 0;
+  const uint64_t W = (s.n + 63) >> 6;
+  const uint64_t nrange = (W + kPPRange - 1) / kPPRange;
+  for (uint64_t rg = (uint64_t)blockIdx.x * kPPWaves + wv; rg < nrange; rg += (uint64_t)gridDim.x * kPPWaves) {
+    const uint64_t w0 = rg * kPPRange, base = w0 << 6;
+    uint32_t qn = 0;  // wave-uniform
+    for (uint32_t wi = 0; wi < kPPRange; wi += kPPB) {
+      unsigned long long Iw[kPPB];
+      uint32_t d[kPPB];
+#pragma unroll
+      for (uint32_t i = 0; i < kPPB; ++i) {
+        const uint64_t word = w0 + wi + i, v = (word << 6) + lane;
+        Iw[i] = word < W ? s.recv[word] : 0ull;
+        d[i] = ((Iw[i] >> lane) & 1) ? s.deg[v] : 0u;
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < kPPB; ++i) {
+        const uint64_t v = ((w0 + wi + i) << 6) + lane;
+        const bool enq = (Iw[i] >> lane) & 1;  // informed => live and in range
+        const unsigned long long bal = __ballot(enq);
+        if (enq) {
+          const uint32_t at = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          q[at] = (uint32_t)(v - base) | d[i] << 16;
+        }
+        qn += (uint32_t)__popcll(bal);
+        if (qn >= 64) {
+          wave_lds_sync();
+          ppa_resolve(s, sp, t, c3, q, 64, base, next, sent, msgs);
+          const uint32_t rest = qn - 64;
+          const uint32_t keep = lane < rest ? q[64 + lane] : 0u;
+          wave_lds_sync();
+          if (lane < rest) q[lane] = keep;
+          qn = rest;
+        }
+      }
+    }
+    wave_lds_sync();
+    if (qn) ppa_resolve(s, sp, t, c3, q, qn, base, next, sent, msgs);
+    wave_lds_sync();
+  }
+  const uint64_t v3[3] = {blockIdx.x == 0 && threadIdx.x == 0 ? c->ncallers : 0ull, sent, msgs};
+  const uint32_t f3[3] = {ST_FIRED, ST_SENT, ST_MSGS};
+  block_add<kPPRoundBlock>(sh, v3, 3, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
+}
+
 __global__ __launch_bounds__(kPPBlock) void k_pp_commit(const DevState s,
                                                         const unsigned long long* __restrict__ next,
                                                         uint32_t t, PPCtl* ctl) {
@@ -394,9 +508,10 @@ __global__ __launch_bounds__(kPPSegs) void k_pp_mode(PPCtl* c) {
     }
     c->segpre[c->nseg] = a;
     const bool early = ok && c->ninf <= c->thr;
-    c->mode = early ? PP_EARLY : c->ninf >= c->bthr ? PP_BOTTOM : PP_DENSE;
+    c->mode = early ? PP_EARLY : c->ninf >= c->bthr ? PP_BOTTOM : c->ninf >= c->athr ? PP_ANSWER : PP_DENSE;
     c->nearly += c->mode == PP_EARLY;
     c->nbottom += c->mode == PP_BOTTOM;
+    c->nanswer += c->mode == PP_ANSWER;
     if (!early) c->early_ok = 0;  // |I| only grows: the list is never needed again
     (void)was_early;
   }
@@ -653,7 +768,7 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_fmask_rows(const DevState s, ui
 // failed; flag[0] = 1 if it was informed.  ctl (zeroed, ncallers counted):
 // the informed list starts as the sender.
 __global__ void k_pp_seed(const DevState s, unsigned long long* next, uint32_t node, uint32_t* flag, PPSparse sp,
-                          unsigned long long thr, unsigned long long bthr) {
+                          unsigned long long thr, unsigned long long bthr, unsigned long long athr) {
   const unsigned long long bit = 1ull << (node & 63);
   const bool ok = node != ~0u && !(s.crash[node >> 6] & bit);  // ~0u: the sender is another shard's
   if (ok) {
@@ -666,6 +781,7 @@ __global__ void k_pp_seed(const DevState s, unsigned long long* next, uint32_t n
     c->ninf = ok ? 1 : 0;
     c->thr = thr;
     c->bthr = bthr;
+    c->athr = athr;
     c->nseg = (uint32_t)(s.n >> 12 < kPPSegs ? (s.n >> 12 ? s.n >> 12 : 1) : kPPSegs);
     c->seg_cap = (s.n + c->nseg - 1) / c->nseg;
     c->mode = PP_DENSE;
@@ -711,6 +827,7 @@ hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long l
     const uint64_t nrange = (s.W + kPPRange - 1) / kPPRange;
     const uint32_t bblocks = (uint32_t)std::min<uint64_t>((nrange + kPPWaves - 1) / kPPWaves, 512);
     hipLaunchKernelGGL(k_ppb_round, dim3(bblocks), dim3(kPPRoundBlock), 0, st, s, next, sp, t);
+    hipLaunchKernelGGL(k_ppa_round, dim3(bblocks), dim3(kPPRoundBlock), 0, st, s, next, sp, t);
   }
   return hipGetLastError();
 }
@@ -733,14 +850,15 @@ hipError_t pp_live_edges(const DevState& s, uint32_t* out, hipStream_t st) {
 }
 
 hipError_t pp_seed(const DevState& s, unsigned long long* next, uint32_t node, uint32_t* flag,
-                   const PPSparse& sp, unsigned long long thr, unsigned long long bthr, hipStream_t st) {
+                   const PPSparse& sp, unsigned long long thr, unsigned long long bthr, unsigned long long athr,
+                   hipStream_t st) {
   if (sp.ctl) {
     hipError_t e = hipMemsetAsync(sp.ctl, 0, sizeof(PPCtl), st);
     if (e != hipSuccess) return e;
     const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.n + kPPBlock - 1) / kPPBlock, 4096);
     hipLaunchKernelGGL(k_pp_callers, dim3(blocks), dim3(kPPBlock), 0, st, s, sp.ctl);
   }
-  hipLaunchKernelGGL(k_pp_seed, dim3(1), dim3(1), 0, st, s, next, node, flag, sp, thr, bthr);
+  hipLaunchKernelGGL(k_pp_seed, dim3(1), dim3(1), 0, st, s, next, node, flag, sp, thr, bthr, athr);
   return hipGetLastError();
 }
 

@@ -578,158 +578,6 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
   }
 }
 
-// Expand for 8-slot rows (stride 8: C5's 6-slot rows padded to 8), a LANE
-// PAIR per firing node: lane 2p loads slots 0..3 of the row (16 B), lane
-// 2p + 1 slots 4..7, in one load instruction, and each draws the Philox of its
-// own 4-slot group (RandomDrop, :172; the crash rolls, :180) -- the same keys
-// as k_expand.  A row is then one 128-B-line request from one instruction
-// instead of two (uint4 + uint2) from one lane: on gfx950 random 64-B pieces
-// read by 4 lanes went at 4.9e10 lines/s against 3.8e10 for a lane's
-// two-load row (profiles/r03_fetch_calibration.json).  H half rows per lane
-// per round (128 * H firing nodes); the LDS partition is k_expand's.
-template <bool WRITE, uint32_t H>
-__global__ __launch_bounds__(kExpandBlock) void k_expand2(const WinState w, uint32_t t0, uint32_t L,
-                                                          unsigned long long Tn, int add_stats) {
-  __shared__ ExpandLds<kExpandBlock * H * 4> sm;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, hh = lane & 1;
-  uint32_t Ls = L;
-  if (w.ctl) {
-    L = win_live(w, t0, 0);
-    if (!L) return;
-    Tn = w.ctl->Tn;
-    Ls = w.lstride;
-  }
-  const uint32_t units = Ls * w.nfine;
-  constexpr uint32_t per_round = kExpandBlock / 2 * H;  // firing nodes per round
-  if (tid < kMaxWindow * 2) (&sm.acc[0][0])[tid] = 0;
-  const uint32_t reg = tid * kCoarseSub + (blockIdx.x & (kCoarseSub - 1));
-  const unsigned long long cbase = w.ccap[reg], cend = w.ccap[reg + 1];
-  sm.cend[tid] = cend;
-  const unsigned long long rounds = (Tn + per_round - 1) / per_round;
-  unsigned long long rbeg, rend, rstep;
-  xcd_rounds(rounds, rbeg, rend, rstep);
-  uint32_t accp[kBitTicks];
-#pragma unroll
-  for (uint32_t kx = 0; kx < kBitTicks; ++kx) accp[kx] = 0;
-  for (unsigned long long rd = rbeg; rd < rend; rd += rstep) {
-    sm.cnt[tid] = 0;
-    __syncthreads();
-    uint32_t mm[H][4], mt[H][4];
-    uint32_t vv[H], kk[H];
-#pragma unroll
-    for (uint32_t q = 0; q < H; ++q) {
-      // wave-uniform group of 32 consecutive firing indices (inside one 64-group of gmap)
-      const unsigned long long g0 =
-          rd * per_round + q * (kExpandBlock / 2) + __builtin_amdgcn_readfirstlane((tid & ~63u) >> 1);
-      const unsigned long long g = g0 + (lane >> 1);
-      vv[q] = ~0u;
-      kk[q] = 0;
-      if (g0 < Tn) {
-        const uint32_t u = unit_of_wave(w, g0, g < Tn ? g : Tn - 1, Tn, units);
-        if (g < Tn) {
-          const uint32_t f = u / Ls, k = u - f * Ls;
-          const uint32_t s = (t0 + k) % w.R;
-          const uint32_t i = (uint32_t)(g - w.unit_off[u]);
-          vv[q] = (f << kFineLog) + w.flist[((size_t)s * w.nfine + f) * kFineNodes + i];
-          kk[q] = k;
-        }
-      }
-    }
-#pragma unroll
-    for (uint32_t q = 0; q < H; ++q) {
-      uint4 a = make_uint4(kEmptyMsg, kEmptyMsg, kEmptyMsg, kEmptyMsg);
-      if (vv[q] != ~0u) a = reinterpret_cast<const uint4*>(w.ids + (size_t)vv[q] * 8)[hh];  // all rows in flight
-      mm[q][0] = a.x; mm[q][1] = a.y; mm[q][2] = a.z; mm[q][3] = a.w;
-#pragma unroll
-      for (uint32_t j = 0; j < 4; ++j) mt[q][j] = ~0u;
-    }
-    uint32_t sentq[H];
-#pragma unroll
-    for (uint32_t q = 0; q < H; ++q) {
-      sentq[q] = 0;
-      if (vv[q] == ~0u) continue;
-      const uint32_t v = vv[q], k = kk[q], t = t0 + k;
-      uint32_t sent = 0;
-      if (mm[q][0] != kEmptyMsg) {  // rows are sealed: an empty first slot ends the list
-        uint32_t vn, c3drop;
-        node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + v, K_DROP, vn, c3drop);
-        const uint32_t c3crash = (c3drop & 0xFFFFFFu) | (K_CRASH << 24);
-        const u32x4 r = philox(vn, t, hh, c3drop, w.key.k0, w.key.k1);  // :144, :172
-        const u32x4 rc = w.kc > 0 ? philox(vn, t, hh, c3crash, w.key.k0, w.key.k1) : u32x4{~0u, ~0u, ~0u, ~0u};
-#pragma unroll
-        for (uint32_t jj = 0; jj < 4; ++jj) {
-          if (mm[q][jj] != kEmptyMsg && (int32_t)uniform(lane_of(r, jj), 100u) >= w.kd) {  // kept: :145
-            const uint32_t tgt = mm[q][jj], bin = tgt >> kCoarseShift;
-            const uint32_t roll0 = (int32_t)uniform(lane_of(rc, jj), 100u) < w.kc;
-            mt[q][jj] = bin | (atomicAdd(&sm.cnt[bin], 1u) << 8);
-            mm[q][jj] = (tgt & ((1u << kCoarseShift) - 1)) | (k << kCoarseShift) | (roll0 << kRoll0Coarse);
-            ++sent;
-          }
-        }
-      }
-      sentq[q] = sent;
-#pragma unroll
-      for (uint32_t kx = 0; kx < kBitTicks; ++kx)
-        if (kx == k) accp[kx] += (hh ? 0u : 1u) | (sent << 16);
-    }
-    if (WRITE && add_stats && w.tstat) {  // batched trials: fired/sent per (trial, tick)
-#pragma unroll
-      for (uint32_t q = 0; q < H; ++q) {
-        const uint32_t key = vv[q] == ~0u ? ~0u : (uint32_t)((uint64_t)vv[q] >> w.tlog) * kMaxWindow + w.tofs + kk[q];
-        tstat_add(w.tstat, key, TS_FIRED, hh ? 0u : 1u, TS_SENT, sentq[q]);
-      }
-    }
-    __syncthreads();
-    if (!WRITE) {
-      if (sm.cnt[tid]) atomicAdd(&w.chist[reg], (unsigned long long)sm.cnt[tid]);
-      continue;  // the next round's first barrier orders the reuse of sm.cnt
-    }
-    block_scan256(sm.cnt, sm.off);
-    const uint32_t mycnt = sm.cnt[tid];
-    unsigned long long at = 0;
-    if (mycnt) at = atomicAdd(&w.cfill[reg], (unsigned long long)mycnt);
-    __syncthreads();
-#pragma unroll
-    for (uint32_t q = 0; q < H; ++q)
-#pragma unroll
-      for (uint32_t j = 0; j < 4; ++j)
-        if (mt[q][j] != ~0u) {
-          const uint32_t bin = mt[q][j] & 255, p = sm.off[bin] + (mt[q][j] >> 8);
-          sm.sorted[p] = mm[q][j];
-          sm.sbin[p] = (uint8_t)bin;
-        }
-    if (mycnt) {
-      if (at + mycnt > cend - cbase) atomicOr(w.err, kErrCoarse);
-      sm.gbase[tid] = cbase + at;
-    }
-    __syncthreads();
-    const uint32_t total = sm.off[256];
-    for (uint32_t p = tid; p < total; p += kExpandBlock) {
-      const uint32_t b = sm.sbin[p];
-      const unsigned long long pos = sm.gbase[b] + (p - sm.off[b]);
-      if (pos < sm.cend[b]) w.cmsg[pos] = sm.sorted[p];
-    }
-  }
-  if (!WRITE || !add_stats) return;  // an exact redo must not count the window twice
-#pragma unroll
-  for (uint32_t kx = 0; kx < kBitTicks; ++kx) {
-    if (kx >= L) continue;
-    const uint32_t fired = wave_sum32(accp[kx] & 0xFFFFu), sent = wave_sum32(accp[kx] >> 16);
-    if ((tid & 63) == 0) {
-      if (fired) atomicAdd(&sm.acc[kx][0], (unsigned long long)fired);
-      if (sent) atomicAdd(&sm.acc[kx][1], (unsigned long long)sent);
-    }
-  }
-  __syncthreads();
-  if (tid < L * 2) {
-    const uint32_t k = tid >> 1, fld = tid & 1;
-    const unsigned long long v = sm.acc[k][fld];
-    unsigned long long* row = shard_row(w, k);
-    if (v) atomicAdd(&row[fld ? ST_SENT : ST_FIRED], v);
-    if (v && fld) atomicAdd(&row[ST_MSGS], v);
-  }
-}
-
 // Slots past a node's friends list become kEmptyMsg (the window engine's
 // expand reads rows without the length byte).
 __global__ void k_seal_rows(const uint8_t* deg, uint32_t* ids, uint64_t n, uint32_t stride) {
@@ -824,9 +672,12 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8
     uint32_t t0;
     if (!win_live(w, t0, 0)) return;
   }
+  // a sparse window has few tiles: the workgroups past them leave before
+  // staging the 8-KB tile prefix (the grid is sized for the densest window)
+  const uint32_t ntiles = w.tprefix[kRegions];
+  if (blockIdx.x >= ntiles) return;
   for (uint32_t i = tid; i <= kRegions; i += kPartBlock) s_tp[i] = w.tprefix[i];
   __syncthreads();
-  const uint32_t ntiles = s_tp[kRegions];
   for (uint32_t g = blockIdx.x; g < ntiles; g += gridDim.x) {
     uint32_t lo = 0, hi = kRegions - 1;  // coarse region r: s_tp[r] <= g < s_tp[r+1]
     while (lo < hi) {
@@ -939,6 +790,8 @@ struct ResolveLds {
   uint32_t st[kMaxWindow][4];       // dead (not counted), recv, crash per tick: whole launch
   uint32_t dead[kMaxWindow];        // this bucket's receipts at nodes crashed before the window
   uint32_t blist[kResolveMaxBuckets];  // this workgroup's non-empty buckets
+  unsigned long long bstart[kResolveMaxBuckets];  // their message region starts (fstart)
+  uint32_t bcnt[kResolveMaxBuckets];   // their message counts (ffill)
   uint32_t ndup;
   uint32_t ninf;
   uint32_t err;
@@ -1110,16 +963,23 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
   __syncthreads();
   {
     const uint32_t f = blockIdx.x + tid * G;
-    const bool ne = tid < kResolveMaxBuckets && f < w.nfine && w.ffill[f] > kSmallMax;  // small: k_resolve_small
+    const unsigned long long fl = tid < kResolveMaxBuckets && f < w.nfine ? w.ffill[f] : 0ull;
+    const bool ne = fl > kSmallMax;  // small: k_resolve_small
     const uint32_t at = wave_append(&sm.nb, ne);
-    if (ne) sm.blist[at] = f;
+    if (ne) {
+      // the bucket descriptors come from LDS later: a wait for them never waits
+      // for the vector loads in flight (the next bucket's prefetch)
+      sm.blist[at] = f;
+      sm.bstart[at] = w.fstart[f];
+      sm.bcnt[at] = (uint32_t)fl;
+    }
   }
   __syncthreads();
   const uint32_t nb = sm.nb;
   stamp(w, sm, 0);
   uint32_t fB = 0, MB = 0;
   unsigned long long mbB = 0;
-  if (nb > 0) { fB = sm.blist[0]; mbB = w.fstart[fB]; MB = (uint32_t)w.ffill[fB]; }
+  if (nb > 0) { fB = sm.blist[0]; mbB = sm.bstart[0]; MB = sm.bcnt[0]; }
   uint32_t* rwg = (uint32_t*)w.recv;
   uint32_t* cwg = (uint32_t*)w.crash;
   // this lane's infections per tick over all its buckets
@@ -1142,13 +1002,19 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
   // the next bucket's state words and first batch of messages are loaded
   // while this bucket finishes (from the end of its receipts)
   uint32_t pm[kU], p_recv0 = 0, p_crash0 = 0, p_roll0 = 0, p_fcv = 0;
+  bool p_in = false;
   auto prefetch = [&](uint32_t f, uint32_t M, unsigned long long mb) {
     const uint64_t wi = ((uint64_t)(f << kFineLog) >> 5) + tid;
     const bool in = wi < w.W * 2;
-    p_recv0 = in ? rwg[wi] : 0u;
-    p_crash0 = in ? cwg[wi] : 0u;
-    p_roll0 = in ? w.rollw[wi] : 0u;
-    p_fcv = tid < w.R ? w.fcount[(size_t)tid * w.nfine + f] : 0u;
+    // branch-free (clamped) loads, masked where they are used: a load in a
+    // branch, or a select right after it, makes the compiler wait for it at
+    // once, which serialises the prefetch with the rest of this bucket
+    const uint64_t wc = in ? wi : w.W * 2 - 1;
+    p_in = in;
+    p_recv0 = rwg[wc];
+    p_crash0 = cwg[wc];
+    p_roll0 = w.rollw[wc];
+    p_fcv = w.fcount[(size_t)(tid < w.R ? tid : 0u) * w.nfine + f];
     ld(w.fmsg + mb, M, 0, pm);
   };
   if (nb > 0) prefetch(fB, MB, mbB);
@@ -1163,8 +1029,9 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
     node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + node0, K_ORDER, knode0, c3order);
     const uint32_t c3delay = (c3order & 0xFFFFFFu) | (K_DELAY << 24);
     const bool in = wi < w.W * 2;
-    const uint32_t recv0 = p_recv0, crash0 = p_crash0, roll0 = p_roll0, fcv = p_fcv;
-    if (i + 1 < nb) { fB = sm.blist[i + 1]; mbB = w.fstart[fB]; MB = (uint32_t)w.ffill[fB]; }
+    const uint32_t recv0 = p_in ? p_recv0 : 0u, crash0 = p_in ? p_crash0 : 0u, roll0 = p_in ? p_roll0 : 0u;
+    const uint32_t fcv = tid < w.R ? p_fcv : 0u;
+    if (i + 1 < nb) { fB = sm.blist[i + 1]; mbB = sm.bstart[i + 1]; MB = sm.bcnt[i + 1]; }
     if (roll0) w.rollw[wi] = 0u;  // consumed: the next window starts clear
     const uint32_t rollw = roll0 & ~crash0;
 #pragma unroll
@@ -1897,21 +1764,6 @@ hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, i
   const dim3 grid(blocks ? blocks : 1), blk(kExpandBlock);
   const unsigned long long tn = Tn;
   const int st = mode == 1 ? 1 : 0;
-  // 8-slot rows (5..8-slot rows padded to 8): lane-pair rows, H = GS_XH (default 8) half rows per lane
-  static const uint32_t xh = [] { const char* e = getenv("GS_XH"); return e ? (uint32_t)atoi(e) : 8u; }();
-  if (w.stride == 8 && xh != 0) {  // every mode (an exact redo must count what the write pass writes)
-    const uint32_t pr = kExpandBlock / 2 * (xh == 4 ? 4 : 8);
-    const uint32_t b2 = (uint32_t)std::min<uint64_t>((Tn + pr - 1) / pr, 8192);
-    const dim3 g2(b2 ? b2 : 1);
-    if (xh == 4) {
-      if (mode) hipLaunchKernelGGL((k_expand2<true, 4>), g2, blk, 0, s, w, t0, L, tn, st);
-      else hipLaunchKernelGGL((k_expand2<false, 4>), g2, blk, 0, s, w, t0, L, tn, 0);
-    } else {
-      if (mode) hipLaunchKernelGGL((k_expand2<true, 8>), g2, blk, 0, s, w, t0, L, tn, st);
-      else hipLaunchKernelGGL((k_expand2<false, 8>), g2, blk, 0, s, w, t0, L, tn, 0);
-    }
-    return hipGetLastError();
-  }
   if (rs <= 6 && npt == 2) {
     if (mode) hipLaunchKernelGGL((k_expand<true, 6, 2>), grid, blk, 0, s, w, t0, L, tn, st);
     else hipLaunchKernelGGL((k_expand<false, 6, 2>), grid, blk, 0, s, w, t0, L, tn, 0);

@@ -41,9 +41,11 @@ class Config:
     pp_rounds: str = "auto"   # push-pull: "auto" (sparse early rounds while |I| <= n/256, dense
                               # rounds bottom-up once |I| >= 96n/256), "dense" (every round streams the
                               # table top-down), "early" (sparse at any |I|), "topdown" (auto, but
-                              # dense rounds never bottom-up), "bottom" (every dense round bottom-up)
+                              # dense rounds never bottom-up nor pull-answer), "bottom" (every dense round
+                              # bottom-up), "answer" (every dense round below the bottom-up threshold
+                              # pull-answer)
 
-    PP_ROUNDS = ("auto", "dense", "early", "topdown", "bottom")
+    PP_ROUNDS = ("auto", "dense", "early", "topdown", "bottom", "answer")
 
     def flags(self, timing: bool | None = None) -> int:
         if self.pp_rounds not in self.PP_ROUNDS:
@@ -55,7 +57,8 @@ class Config:
             (_lib.GS_FLAG_PP_DENSE if self.pp_rounds == "dense" else 0) | \
             (_lib.GS_FLAG_PP_EARLY if self.pp_rounds == "early" else 0) | \
             (_lib.GS_FLAG_PP_TOPDOWN if self.pp_rounds == "topdown" else 0) | \
-            (_lib.GS_FLAG_PP_BOTTOM if self.pp_rounds == "bottom" else 0)
+            (_lib.GS_FLAG_PP_BOTTOM if self.pp_rounds == "bottom" else 0) | \
+            (_lib.GS_FLAG_PP_ANSWER if self.pp_rounds == "answer" else 0)
 
     def to_params(self) -> Params:
         p = Params()

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 4
+#define GS_ABI_VERSION 5
 
 enum {
   GS_OK = 0,
@@ -53,6 +53,9 @@ enum {
 #define GS_FLAG_PP_TOPDOWN 32u /* push-pull: dense rounds always push by atomics (default: bottom-up,
                                 * receivers scan their in-edges, once |I| >= 96n/256); same results */
 #define GS_FLAG_PP_BOTTOM 64u  /* push-pull: every dense round bottom-up; same results, for tests */
+#define GS_FLAG_PP_ANSWER 128u /* push-pull: every dense round below the bottom-up threshold pull-answer
+                                * (informed nodes answer the pulls among their in-edges; the default
+                                * does too unless GS_PP_ANSWER256 is set); same results, for tests */
 
 /* Dissemination model (gs_params.model). */
 #define GS_MODEL_FLOOD 0u    /* the reference: every receipt re-broadcasts to all friends (simulator.go:107-149) */
@@ -122,6 +125,7 @@ typedef struct gs_timing {
                             * build (at gs_broadcast_begin, once per table / failure mask) */
   uint64_t pp_early_rounds;  /* push-pull: rounds of this broadcast run sparse (informed list)   */
   uint64_t pp_bottom_rounds; /* push-pull: dense rounds of this broadcast run bottom-up          */
+  uint64_t pp_answer_rounds; /* push-pull: dense rounds of this broadcast run pull-answer        */
 } gs_timing;
 
 /* gs_run status */

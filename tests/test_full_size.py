@@ -13,8 +13,9 @@ implement the same tick model with no shared kernel code:
 Push-pull at N = 1e9: monotone informed set, pending == received, float32
 99 % reached, delivered <= calls; with a 1 % pre-failed mask the per-round
 counters and final bitsets are identical across the round selections auto /
-dense / topdown / bottom (independent kernels: sparse informed-list rounds,
-streamed top-down rounds with atomics, bottom-up in-edge scans).  The flood
+dense / topdown / bottom / answer (independent kernels: sparse informed-list
+rounds, streamed top-down rounds with atomics, bottom-up in-edge scans,
+pull-answer in-edge scans of the informed).  The flood
 with the same 1 % mask: window engine vs tick engine, bit-exact per tick.
 """
 from __future__ import annotations
@@ -144,7 +145,7 @@ def test_c5_pushpull_failed_mask_round_modes_bit_exact():
     assert nrec == int(rows[-1][4])
     rec = np.asarray(rows[:, 4], dtype=np.int64)
     assert (np.diff(rec) >= 0).all() and (rows[:, 3] <= rows[:, 2]).all()
-    for mode in ("dense", "topdown", "bottom"):
+    for mode in ("dense", "topdown", "bottom", "answer"):
         got = pushpull_failed(mode, mask)
         assert np.array_equal(got[0], rows), f"pp_rounds={mode}: per-round counters differ"
         assert got[1] == h, f"pp_rounds={mode}: final informed set differs"

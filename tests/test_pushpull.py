@@ -123,7 +123,7 @@ def test_oracle_known_answers(oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rounds", ["auto", "early", "dense", "topdown", "bottom"])
+@pytest.mark.parametrize("rounds", ["auto", "early", "dense", "topdown", "bottom", "answer"])
 @pytest.mark.parametrize("kw,stride,dlo,dhi,fail_frac", [
     (dict(PP, n=1), 2, 1, 2, 0.0),
     (dict(PP, n=2, drop_rate=0.0), 3, 0, 3, 0.0),
@@ -171,9 +171,11 @@ def test_gpu_pushpull_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac, rounds,
         # nodes, the failed-slot mask (stride <= 8)
         can_bottom = stride <= 16 and (fail_frac == 0 or stride <= 8)
         if rounds in ("dense", "topdown") or not can_bottom:
-            assert tm["pp_bottom_rounds"] == 0
+            assert tm["pp_bottom_rounds"] == 0 and tm["pp_answer_rounds"] == 0
         elif rounds == "bottom":
             assert tm["pp_bottom_rounds"] == r + 1 - tm["pp_early_rounds"]
+        elif rounds == "answer":
+            assert tm["pp_answer_rounds"] + tm["pp_bottom_rounds"] == r + 1 - tm["pp_early_rounds"]
         if rounds == "early":
             assert tm["pp_early_rounds"] >= 1
 
