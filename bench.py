@@ -391,9 +391,10 @@ def c3_trials(a, gs, rank, world, local, dist):
 def c4_sharded(a, gs, rank, world, local, dist):
     """Config C4: N = 1e8, fanout 18 (floor(ln 1e8)), fanin 19, reference
     defaults otherwise; ONE broadcast with the node range sharded over the
-    ranks (gs_create_rank: per-window RCCL all-gather of the firing lists, per-
-    step RCCL sum of the counters) -- one shard through the same window driver
-    at --gpus 1.  value = delivered sends / wall time of the broadcast."""
+    ranks (gs_create_rank: each rank expands its own fires and the messages
+    move to their targets' owners by an RCCL all-to-all per window; per-step
+    RCCL sum of the counters) -- one shard through the same window driver at
+    --gpus 1.  value = delivered sends / wall time of the broadcast."""
     import torch
     from gossip_simulator_amd import dist as gd
     cfg = gs.Config(n=100_000_000, fanout=18, fanin=19, seed=a.seed, device=local)
@@ -438,12 +439,13 @@ def c4_sharded(a, gs, rank, world, local, dist):
                 "ticks": tot["tick"], "status": STATUS[status], "coverage": round(tot["received"] / cfg.n, 6),
                 "delivered_per_step": tot["sent"], "messages_per_step": tot["messages"],
                 "overlay_s": round(ov, 3),
-                "roofline": {"bound": "hbm", "kernel": "shard window pipeline k_expand_sh -> k_plan/k_part2 -> "
-                             "k_resolve (rank 0)", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
+                "roofline": {"bound": "hbm", "kernel": "shard window pipeline k_expand (owner bins) -> k_pack -> "
+                             "all-to-all -> k_plan/k_part2 -> k_resolve (rank 0)", "achieved": round(ach, 2),
+                             "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
                              "avg_launch_us": round(kern * 1e3 / launches, 2), "launches": launches,
-                             "kernels_total_ms": {"k_expand_sh": round(tm["expand_ms"], 3),
-                                                  "k_plan+k_part2": round(tm["part_ms"], 3),
+                             "kernels_total_ms": {"k_expand": round(tm["expand_ms"], 3),
+                                                  "k_pack+k_plan+k_part2": round(tm["part_ms"], 3),
                                                   "k_resolve": round(tm["resolve_ms"], 3)}}}
     finally:
         sim.close()
@@ -510,9 +512,11 @@ def shards_inproc(a, gs):
     config C4 (N = 1e8, fanout 18 / fanin 19) and G = 8 of C5's flood
     (N = 1e9), each shard's window pipeline run alone on the device
     (GS_SHARD_SERIAL=1) with HIP-event timing: per shard, the device time of
-    one broadcast; the slowest shard bounds a G-GPU run (plus its all-gathers,
-    not measured here).  DESIGN.md section 6 compares it with the per-rank
-    bytes model."""
+    one broadcast (expand of its own fires, pack, partition and resolve of
+    what it receives); the slowest shard bounds a G-GPU run (plus its
+    all-to-all transfers, not measured here: in-process shards read each
+    other's blocks in place).  DESIGN.md section 6 compares it with the
+    per-rank bytes model."""
     os.environ["GS_SHARD_SERIAL"] = "1"
     out = {}
     try:

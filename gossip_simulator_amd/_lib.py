@@ -96,8 +96,13 @@ ALL_GATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_siz
 ALL_REDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t)
 
 
+ALL_TO_ALLV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_size_t), C.c_void_p,
+                             C.POINTER(C.c_size_t))
+
+
 class Exchange(C.Structure):
-    _fields_ = [("user", C.c_void_p), ("all_gather", ALL_GATHER_FN), ("all_reduce_sum_u64", ALL_REDUCE_FN)]
+    _fields_ = [("user", C.c_void_p), ("all_gather", ALL_GATHER_FN), ("all_reduce_sum_u64", ALL_REDUCE_FN),
+                ("all_to_allv", ALL_TO_ALLV_FN)]
 
 
 _lib = None

@@ -103,12 +103,17 @@ struct gs_ctx {
   bool shard = false;
   uint32_t G = 1, rank = 0;
   uint64_t lo = 0, hi = 0, seg_per = 0;
-  uint32_t* d_pent = nullptr;           // [n][pw]: owned-slot mask + owned targets - lo (or a spill offset)
-  uint32_t* d_pspill = nullptr;         // targets of the rows that do not fit pw - 1
-  uint32_t pw = 0;                      // partitioned row width
-  uint64_t spilled = 0;                 // rows whose targets are in the spill array
-  Buf gfire;                            // multi-process: this rank's all-gather buffer
+  // owner expand: the receive layout of a window ([4][kRegions + 1]: region
+  // starts, ends, fills; the pack offsets of this shard's own send blocks),
+  // pinned host copy, and the receive-side WinState (kept for an exact redo)
+  unsigned long long* d_rtab = nullptr;
+  unsigned long long* h_rtab = nullptr;
+  WinState wr{};
+  uint64_t rtotal = 0;                  // messages received in the window
+  Buf xsend, xrecv;                     // multi-process: packed send blocks, received blocks
   unsigned long long* d_gcounts = nullptr;  // multi-process: [G][16] gathered fires per tick
+  unsigned long long* d_glay = nullptr;     // multi-process: [G][kRegions + 1] gathered region fills + error word
+  unsigned long long* h_glay = nullptr;     // pinned copy
   ncclComm_t comm = nullptr;
   // multi-process exchange done by the caller (gs_create_rank_exchange)
   gs_exchange hx{};
@@ -123,14 +128,24 @@ struct gs_ctx {
   unsigned long long* d_ig = nullptr;
   unsigned long long* d_fg = nullptr;
   uint64_t segw = 0;
+  // push-pull shards: the replica -- an unsharded push-pull context over the
+  // full table on this device (shared by the device's members; owned by the
+  // group, or by the rank) whose informed / failed sets ARE the replicated
+  // ones: it runs the sparse early rounds, identically on every device and
+  // rank, with no exchange (section 6.3 of DESIGN.md)
+  gs_ctx* rep = nullptr;
+  bool own_rep = false;
+  bool rep_live = false;                // the current broadcast's rounds still run on the replicas
+  uint32_t rep_rounds = 0;              // rounds run on the replicas since the broadcast began
   // group (gs_create_multi)
   bool group = false, gtrials = false;
   std::vector<gs_ctx*> mem;
   std::vector<int> gdevs;               // distinct devices, first-use order
   std::vector<int> gdev_of;             // member -> index into gdevs
-  std::vector<Buf> gbuf;                // one all-gather buffer per distinct device
-  std::vector<hipEvent_t> gev_c, gev_x; // per member: compaction done; per device: copies done
+  std::vector<Buf> gbuf;                // per distinct device: its members' send blocks, then blocks from other devices
+  std::vector<hipEvent_t> gev_c, gev_x; // per member: its part of an exchange done; per device: copies done
   std::vector<unsigned long long*> gig, gfg;  // push-pull shards: per distinct device, the replicated sets
+  std::vector<gs_ctx*> greps;           // push-pull shards: per distinct device, the replica
   OverlayWork ovw;                      // overlay builder buffers, kept between builds
 };
 
@@ -193,6 +208,17 @@ int alloc_window(gs_ctx* c) {
   w.G = c->G;
   w.rank = c->rank;
   w.seg_per = (uint32_t)c->seg_per;
+  w.csub = kCoarseSub;
+  w.ccap_end = nullptr;
+  if (c->shard) {  // owner expand (k_expand's coarse_bin)
+    w.owner = 1;
+    w.obins = 256 / c->G;
+    w.oseg_q = (uint32_t)(c->seg_per >> kFineLog);
+    w.oseg_magic = 0xFFFFFFFFu / w.oseg_q;
+    if (hipMalloc(&c->d_rtab, 4 * (kRegions + 1) * 8) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_rtab, 4 * (kRegions + 1) * 8) != hipSuccess)
+      return fail(c, GS_ENOMEM, "cannot allocate the shard's receive layout");
+  }
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t units = (size_t)kMaxWindow * w.nfine + 1;
   const size_t b_fc = al((size_t)w.R * w.nfine * 4), b_units = al(units * 8),
@@ -280,9 +306,6 @@ void refresh_window(gs_ctx* c) {
   w.stride = c->st.stride;
   w.slots = c->row_slots && c->row_slots < c->st.stride ? c->row_slots : c->st.stride;
   w.stride_magic = c->st.stride_magic;
-  w.pent = c->d_pent;
-  w.pspill = c->d_pspill;
-  w.pw = c->pw;
   w.abort_on_err = c->shard ? 1u : 0u;
 }
 
@@ -353,15 +376,6 @@ int alloc_table(gs_ctx* c, uint32_t stride) {
   return GS_OK;
 }
 
-void free_table(gs_ctx* c) {
-  if (c->d_deg) (void)hipFree(c->d_deg);
-  if (c->d_ids) (void)hipFree(c->d_ids);
-  c->d_deg = nullptr;
-  c->d_ids = nullptr;
-  c->tab_stride = 0;
-  refresh_state(c);
-}
-
 __global__ void k_validate_peers(const uint8_t* deg, const uint32_t* ids, uint64_t n, uint64_t bound,
                                  uint32_t stride, uint32_t* err) {
   for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
@@ -397,55 +411,26 @@ int seal_rows(gs_ctx* c, const uint8_t* deg, uint32_t* ids, uint64_t n) {
   return GS_OK;
 }
 
-// Shard c's partition of the sealed global table (ids, on c's device), for
-// every node v: [owned-slot mask, owned targets - lo ...] in rows of pw words,
-// pw the smallest multiple of 4 that keeps 99.5 % of the rows inline (the
-// rest keep their targets in the spill array): k_expand_sh reads a firing
-// node's owned slots with one dependent load, and local ids are full 32-bit.
-int partition(gs_ctx* c, const uint32_t* ids) {
-  const uint64_t n = c->p.n;
-  if (c->d_pspill) (void)hipFree(c->d_pspill);
-  if (c->d_pent) (void)hipFree(c->d_pent);
-  c->d_pspill = nullptr;
-  c->d_pent = nullptr;
-  c->pw = 0;
-  uint32_t* cnt = nullptr;
-  unsigned long long* hist = nullptr;  // [0, 33): rows by owned slots; [33]: spill fill
-  unsigned long long h[kWinMaxStride + 2] = {};
-  int rc = GS_OK;
-  auto bail = [&](int code, const std::string& m) { rc = fail(c, code, m); };
-  if (hipMalloc(&cnt, n * 4) != hipSuccess || hipMalloc(&hist, (kWinMaxStride + 2) * 8) != hipSuccess) {
-    bail(GS_ENOMEM, "cannot allocate the shard's slot counts");
-  } else if (hipMemsetAsync(hist, 0, (kWinMaxStride + 2) * 8, c->stream) != hipSuccess ||
-             part_count(ids, n, c->st.stride, (uint32_t)c->lo, (uint32_t)c->hi, cnt, c->stream) != hipSuccess ||
-             part_hist(cnt, n, hist, c->stream) != hipSuccess ||
-             hipMemcpyAsync(h, hist, sizeof h, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-             hipStreamSynchronize(c->stream) != hipSuccess) {
-    bail(GS_EDEVICE, "counting the shard's slots failed");
-  } else {
-    uint32_t mx = 0;
-    for (uint32_t k = 0; k <= kWinMaxStride; ++k)
-      if (h[k]) mx = k;
-    uint64_t spilled = 0, spill_e = 0;
-    for (c->pw = 4;; c->pw += 4) {
-      spilled = spill_e = 0;
-      for (uint32_t k = c->pw; k <= kWinMaxStride; ++k) { spilled += h[k]; spill_e += (uint64_t)k * h[k]; }
-      if (c->pw > mx || spilled * 200 <= n) break;
-    }
-    c->spilled = spilled;
-    if (hipMalloc(&c->d_pent, n * c->pw * 4ull) != hipSuccess ||
-        hipMalloc(&c->d_pspill, std::max<uint64_t>(spill_e, 1) * 4) != hipSuccess) {
-      bail(GS_ENOMEM, "cannot allocate " + std::to_string(n * c->pw) + " partitioned friend slots");
-    } else if (part_fill_mask(ids, n, c->st.stride, (uint32_t)c->lo, (uint32_t)c->hi, c->pw, c->d_pent, c->d_pspill,
-                              hist + kWinMaxStride + 1, c->stream) != hipSuccess ||
-               hipStreamSynchronize(c->stream) != hipSuccess) {
-      bail(GS_EDEVICE, "filling the shard's partition failed");
-    }
-  }
-  if (cnt) (void)hipFree(cnt);
-  if (hist) (void)hipFree(hist);
-  refresh_window(c);
-  return rc;
+// Shard c keeps the sealed rows of its own nodes [lo, hi) (copied from the
+// full table `deg` / `ids` of stride S on c's device): owner expand reads
+// only the rows of its own firing nodes.
+int own_rows(gs_ctx* c, const uint8_t* deg, const uint32_t* ids, uint32_t S, uint32_t row_slots, hipStream_t st) {
+  const uint64_t n = c->ntot;
+  if (c->d_deg) (void)hipFree(c->d_deg);
+  if (c->d_ids) (void)hipFree(c->d_ids);
+  c->d_deg = nullptr;
+  c->d_ids = nullptr;
+  c->tab_stride = 0;  // not the full-table shape: the next load reallocates
+  if (hipMalloc(&c->d_deg, n) != hipSuccess || hipMalloc(&c->d_ids, n * S * 4ull) != hipSuccess)
+    return fail(c, GS_ENOMEM, "cannot allocate the shard's rows");
+  RC(set_stride(c, S));
+  c->row_slots = row_slots;
+  refresh_state(c);
+  CK(c, hipMemcpyAsync(c->d_deg, deg + c->lo, n, hipMemcpyDeviceToDevice, st));
+  CK(c, hipMemcpyAsync(c->d_ids, ids + c->lo * S, n * S * 4ull, hipMemcpyDeviceToDevice, st));
+  CK(c, hipStreamSynchronize(st));
+  ++c->table_ver;
+  return GS_OK;
 }
 
 bool covered(uint64_t recv, uint64_t n) {
@@ -539,6 +524,12 @@ int ctx_setup(gs_ctx* c, const gs_params* params, int device, bool shard, uint32
           "fanout/fanin <= 32, no GS_FLAG_TICK_ENGINE, at most 2^30 nodes per context or shard)";
     return GS_EINVAL;
   }
+  // owner expand: every shard's range fits its 256 / G coarse bins of 2^22 nodes
+  if (shard && !c->pp && (G > 256 || ((c->seg_per + (1ull << kCoarseShift) - 1) >> kCoarseShift) > 256 / G)) {
+    why = "flood node-range shards: each of the G <= 256 shards' ranges must fit 256 / G bins of 2^22 nodes "
+          "(n up to about 2^30)";
+    return GS_EINVAL;
+  }
   // One state allocation, 256-B aligned sub-buffers; everything before
   // `stats` is per-broadcast state that gs_reset clears.
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -612,9 +603,11 @@ void destroy_one(gs_ctx* c) {
     }
     for (hipEvent_t e : c->gev_c) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->gev_x) (void)hipEventDestroy(e);
+    for (gs_ctx* r : c->greps) destroy_one(r);
     delete c;
     return;
   }
+  if (c->own_rep) destroy_one(c->rep);
   (void)hipSetDevice(c->dev);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm && rccl().ok) (void)rccl().comm_destroy(c->comm);
@@ -639,12 +632,14 @@ void destroy_one(gs_ctx* c) {
   }
   if (c->h_xbuf) (void)hipHostFree(c->h_xbuf);
   for (void* ptr : {(void*)c->d_deg, (void*)c->d_ids, c->d_state, (void*)c->d_cnt, (void*)c->d_failed, c->d_win,
-                    c->d_flist, c->d_rlmsg, (void*)c->d_tstat, (void*)c->d_pspill, (void*)c->d_pent, (void*)c->d_gcounts})
+                    c->d_flist, c->d_rlmsg, (void*)c->d_tstat, (void*)c->d_rtab, (void*)c->d_gcounts,
+                    (void*)c->d_glay})
     if (ptr) (void)hipFree(ptr);
-  for (Buf* b : {&c->gmap, &c->cmsg, &c->fmsg, &c->tmp, &c->gfire, &c->pp_rend, &c->pp_rsrc, &c->pp_rslot,
-                 &c->pp_ilist, &c->pp_fmask, &c->pp_scan, &c->pp_ctlb})
+  for (Buf* b : {&c->gmap, &c->cmsg, &c->fmsg, &c->tmp, &c->xsend, &c->xrecv, &c->pp_rend, &c->pp_rsrc,
+                 &c->pp_rslot, &c->pp_ilist, &c->pp_fmask, &c->pp_scan, &c->pp_ctlb})
     if (b->p) (void)hipFree(b->p);
-  for (void* ptr : {(void*)c->h_cap, (void*)c->h_misc, (void*)c->h_err, (void*)c->h_stats, (void*)c->h_tstat, (void*)c->h_stage})
+  for (void* ptr : {(void*)c->h_cap, (void*)c->h_misc, (void*)c->h_err, (void*)c->h_stats, (void*)c->h_tstat,
+                    (void*)c->h_stage, (void*)c->h_rtab, (void*)c->h_glay})
     if (ptr) (void)hipHostFree(ptr);
   for (void* ptr : {(void*)c->d_ctl, (void*)c->d_stage})
     if (ptr) (void)hipFree(ptr);
@@ -768,12 +763,15 @@ void attach_pp_sets(gs_ctx* c, unsigned long long* ig, unsigned long long* fg) {
 }
 
 int alloc_pp_sets(gs_ctx* c, uint64_t words, unsigned long long** ig, unsigned long long** fg);
+int make_replica(const gs_params* params, int dev, unsigned long long* ig, unsigned long long* fg, gs_ctx** out);
 
 // The rest of a rank context once its exchange is set: gathered fire counts
 // (flood) or its own replicated sets (push-pull).
 int finish_rank(gs_ctx* c, gs_ctx** out) {
   (void)hipSetDevice(c->dev);
-  if (hipMalloc(&c->d_gcounts, (size_t)c->G * kMaxWindow * 8 + (size_t)kMaxWindow * 8) != hipSuccess) {
+  if (hipMalloc(&c->d_gcounts, (size_t)c->G * kMaxWindow * 8 + (size_t)kMaxWindow * 8) != hipSuccess ||
+      (!c->pp_shard && (hipMalloc(&c->d_glay, (size_t)c->G * (kRegions + 1) * 8) != hipSuccess ||
+                        hipHostMalloc((void**)&c->h_glay, (size_t)c->G * (kRegions + 1) * 8) != hipSuccess))) {
     destroy_one(c);
     return GS_ENOMEM;
   }
@@ -788,6 +786,11 @@ int finish_rank(gs_ctx* c, gs_ctx** out) {
     }
     c->own_ig = true;
     attach_pp_sets(c, ig, fg);
+    if (make_replica(&c->p, c->dev, ig, fg, &c->rep)) {
+      destroy_one(c);
+      return GS_ENOMEM;
+    }
+    c->own_rep = c->rep != nullptr;
   }
   *out = c;
   return GS_OK;
@@ -801,6 +804,24 @@ int alloc_pp_sets(gs_ctx* c, uint64_t words, unsigned long long** ig, unsigned l
   CK(c, hipMemsetAsync(*ig, 0, words * 8, c->stream));
   CK(c, hipMemsetAsync(*fg, 0, words * 8, c->stream));
   CK(c, hipStreamSynchronize(c->stream));
+  return GS_OK;
+}
+
+// The replica of push-pull shards on device `dev` (gs_ctx::rep): an unsharded
+// push-pull context whose informed / failed sets are the replicated ig / fg.
+// It gets the full table at load time (partition_pp).  GS_PP_NO_REPLICA=1:
+// none (every round runs sharded bottom-up; A/B and memory-tight runs).
+int make_replica(const gs_params* params, int dev, unsigned long long* ig, unsigned long long* fg, gs_ctx** out) {
+  *out = nullptr;
+  if (getenv("GS_PP_NO_REPLICA")) return GS_OK;
+  gs_params rp = *params;
+  rp.trials = 1;
+  gs_ctx* r = nullptr;
+  RC(create_one(&rp, dev, false, 1, 0, &r));
+  r->st.recv = r->st.grecv = ig;
+  r->st.crash = r->st.gcrash = fg;
+  r->st.gbase = 0;
+  *out = r;
   return GS_OK;
 }
 
@@ -882,6 +903,13 @@ int gs_create_multi(const gs_params* params, const int* devices, int ndev, gs_ct
         return GS_ENOMEM;
       }
       for (gs_ctx* m : ms) attach_pp_sets(m, g->gig[d], g->gfg[d]);
+      gs_ctx* r = nullptr;
+      if (make_replica(params, g->gdevs[d], g->gig[d], g->gfg[d], &r)) {
+        destroy_one(g);
+        return GS_ENOMEM;
+      }
+      g->greps.push_back(r);
+      for (gs_ctx* m : ms) m->rep = r;
     }
   }
   for (size_t i = 0; i < g->mem.size(); ++i) {
@@ -963,6 +991,10 @@ int gs_create_rank_exchange(const gs_params* params, int device, int nranks, int
   if (!out || !params || !ex || !ex->all_gather || !ex->all_reduce_sum_u64 || nranks < 1 || rank < 0 ||
       rank >= nranks)
     return GS_EINVAL;
+  if (params->model == GS_MODEL_FLOOD && std::max<uint32_t>(1, params->trials) == 1 && !ex->all_to_allv) {
+    fprintf(stderr, "gs_create_rank_exchange: flood shards need the all_to_allv callback\n");
+    return GS_EINVAL;
+  }
   *out = nullptr;
   if (std::max<uint32_t>(1, params->trials) > 1) return gs_create_rank(params, device, nranks, rank, nullptr, out);
   gs_ctx* c = nullptr;
@@ -1047,7 +1079,7 @@ int upload_table(gs_ctx* c, const uint8_t* deg, const uint32_t* ids, uint32_t st
 int partition_pp(gs_ctx* leader, const std::vector<gs_ctx*>& ms) {
   uint8_t* fdeg = leader->d_deg;
   uint32_t* fids = leader->d_ids;
-  const uint32_t S = leader->st.stride;
+  const uint32_t S = leader->st.stride, slots = leader->row_slots;
   const uint64_t N = leader->p.n;
   leader->d_deg = nullptr;
   leader->d_ids = nullptr;
@@ -1105,6 +1137,20 @@ int partition_pp(gs_ctx* leader, const std::vector<gs_ctx*>& ms) {
     m->fm_tver = ~0ull;
     m->peers = true;
   }
+  gs_ctx* r = ms[0]->rep;
+  if (r && rc == GS_OK) {  // the full table stays on the device as the replica's
+    if (r->d_deg) (void)hipFree(r->d_deg);
+    if (r->d_ids) (void)hipFree(r->d_ids);
+    r->d_deg = fdeg;
+    r->d_ids = fids;
+    r->tab_stride = S;
+    r->row_slots = slots;
+    if ((rc = set_stride(r, S))) return fail(leader, rc, r->err);
+    refresh_state(r);
+    ++r->table_ver;
+    r->peers = true;
+    return GS_OK;
+  }
   (void)hipFree(fdeg);
   (void)hipFree(fids);
   return rc;
@@ -1114,16 +1160,19 @@ int partition_pp(gs_ctx* leader, const std::vector<gs_ctx*>& ms) {
 // sealed table, then drop the replicated table.
 int partition_from(gs_ctx* leader, const std::vector<gs_ctx*>& ms) {
   if (leader->pp_shard) return partition_pp(leader, ms);
+  uint8_t* fdeg = leader->d_deg;
+  uint32_t* fids = leader->d_ids;
+  const uint32_t S = leader->st.stride, slots = leader->row_slots;
+  leader->d_deg = nullptr;  // own_rows must not free the full table it copies from
+  leader->d_ids = nullptr;
+  int rc = GS_OK;
   for (gs_ctx* m : ms) {
-    if (m != leader) {
-      RC(set_stride(m, leader->st.stride));
-      CK(m, hipStreamSynchronize(leader->stream));
-    }
-    RC(partition(m, leader->d_ids));
+    if ((rc = own_rows(m, fdeg, fids, S, slots, leader->stream))) break;
     m->peers = true;
   }
-  free_table(leader);
-  return GS_OK;
+  (void)hipFree(fdeg);
+  (void)hipFree(fids);
+  return rc;
 }
 
 // Members sharing device d (group) or just c.
@@ -1344,6 +1393,11 @@ int gs_set_failed(gs_ctx* c, const uint64_t* words, size_t nwords) {
     c->failed = true;
     c->st.check_crashed = 1;
     ++c->fail_ver;
+    if (c->rep) {  // the replica reads the same replicated failed set
+      c->rep->failed = true;
+      c->rep->st.check_crashed = 1;
+      ++c->rep->fail_ver;
+    }
     return GS_OK;
   }
   const uint64_t W = c->st.W, w0 = c->lo / 64;  // this context's words (a shard's own range)
@@ -1532,6 +1586,18 @@ int pp_exchange(gs_ctx* acc, const std::vector<gs_ctx*>& ms) {
 
 std::vector<gs_ctx*> shards_of(gs_ctx* c) { return c->group ? c->mem : std::vector<gs_ctx*>{c}; }
 
+// The replicas of a push-pull shard group (one per device) or rank (one).
+std::vector<gs_ctx*> replicas_of(gs_ctx* c) {
+  std::vector<gs_ctx*> v;
+  if (c->group) {
+    for (gs_ctx* r : c->greps)
+      if (r) v.push_back(r);
+  } else if (c->rep) {
+    v.push_back(c->rep);
+  }
+  return v;
+}
+
 // Members sharing a device share its informed set: no member may commit its
 // round's new bits into it while another member's round still reads it.
 int pp_barrier(gs_ctx* acc, const std::vector<gs_ctx*>& ms) {
@@ -1549,11 +1615,32 @@ int pp_barrier(gs_ctx* acc, const std::vector<gs_ctx*>& ms) {
   return GS_OK;
 }
 
+uint32_t pp_shift();
+
 // simulator.go:239-241 for the push-pull extension: the owner informs the
-// sender (unless failed), every shard resets its round control.
+// sender (unless failed), every shard resets its round control; the replicas
+// (if any) start the broadcast's sparse early rounds.
 int pp_shard_begin(gs_ctx* acc, uint64_t sender) {
   std::vector<gs_ctx*> ms = shards_of(acc);
   unsigned long long informed = 0;
+  acc->rep_live = false;
+  acc->rep_rounds = 0;
+  std::vector<gs_ctx*> reps = replicas_of(acc);
+  bool sparse = !reps.empty();
+  for (gs_ctx* r : reps) {
+    CK(r, hipSetDevice(r->dev));
+    if (int rc = pp_prepare(r)) return fail(acc, rc, r->err);
+    if (!r->sp.ctl || !r->sp.ilist) sparse = false;  // no sparse-round buffers: the shards run every round
+  }
+  if (sparse)
+    for (gs_ctx* r : reps) {
+      CK(r, hipSetDevice(r->dev));
+      CK(r, hipMemsetAsync(r->d_next, 0, r->st.W * 8, r->stream));
+      CK(r, pp_seed(r->st, r->d_next, (uint32_t)sender, r->d_flag, r->sp, r->st.n >> pp_shift(), ~0ull, ~0ull,
+                    r->stream));
+      CK(r, hipStreamSynchronize(r->stream));
+    }
+  acc->rep_live = sparse;
   for (gs_ctx* m : ms) {
     CK(m, hipSetDevice(m->dev));
     if (int rc = pp_prepare(m)) return fail(acc, rc, m->err);
@@ -1583,6 +1670,7 @@ void account_tick(gs_ctx* c, uint64_t tick, const unsigned long long* s, gs_tick
 
 int pp_shard_step(gs_ctx* acc, uint32_t ticks, gs_tick_stats* out) {
   std::vector<gs_ctx*> ms = shards_of(acc);
+  std::vector<gs_ctx*> reps = replicas_of(acc);
   std::vector<unsigned long long> sum(kStatFields);
   uint32_t done = 0;
   while (done < ticks) {
@@ -1596,8 +1684,49 @@ int pp_shard_step(gs_ctx* acc, uint32_t ticks, gs_tick_stats* out) {
       if (first < batch)
         CK(m, hipMemsetAsync(m->st.stats, 0, (size_t)(batch - first) * kStatFields * 8, m->stream));
     }
+    for (gs_ctx* r : reps) {
+      CK(r, hipSetDevice(r->dev));
+      CK(r, hipMemsetAsync(r->st.stats + (size_t)i0 * kStatFields, 0, (size_t)first * kStatFields * 8, r->stream));
+      if (first < batch)
+        CK(r, hipMemsetAsync(r->st.stats, 0, (size_t)(batch - first) * kStatFields * 8, r->stream));
+    }
     for (uint32_t i = 0; i < batch; ++i) {
       const uint32_t tt = (uint32_t)(t0 + i);
+      if (acc->rep_live) {
+        // is this round a sparse early round on the replicas (k_pp_mode's test)?
+        gs_ctx* r0 = reps[0];
+        PPCtl h;
+        CK(r0, hipSetDevice(r0->dev));
+        CK(r0, hipMemcpyAsync(&h, r0->sp.ctl, offsetof(PPCtl, segcnt), hipMemcpyDeviceToHost, r0->stream));
+        CK(r0, hipStreamSynchronize(r0->stream));
+        if (h.early_ok && !h.ovf && h.ninf <= h.thr) {
+          // every replica runs the same round: the replicated sets stay equal with no exchange
+          for (gs_ctx* r : reps) {
+            CK(r, hipSetDevice(r->dev));
+            CK(r, pp_round(r->st, r->d_next, r->d_ppsum, tt, r->pp_l2_only, r->sp, r->stream));
+            CK(r, pp_commit(r->st, r->d_next, tt, r->sp, r->stream));
+          }
+          for (gs_ctx* r : reps) {
+            CK(r, hipSetDevice(r->dev));
+            CK(r, hipStreamSynchronize(r->stream));
+          }
+          // the round's counters, once: the group's first member / rank 0
+          if (acc->group || acc->rank == 0) {
+            const size_t row = (size_t)(tt % kStatSlots) * kStatFields;
+            CK(ms[0], hipSetDevice(ms[0]->dev));
+            CK(ms[0], hipMemcpyAsync(ms[0]->st.stats + row, r0->st.stats + row, kStatFields * 8,
+                                     hipMemcpyDeviceToDevice, ms[0]->stream));
+          }
+          ++acc->rep_rounds;
+          continue;
+        }
+        // the shards take over: each one's next = its slice of the replicated set
+        acc->rep_live = false;
+        for (gs_ctx* m : ms) {
+          CK(m, hipSetDevice(m->dev));
+          CK(m, hipMemcpyAsync(m->d_next, m->st.recv, m->st.W * 8, hipMemcpyDeviceToDevice, m->stream));
+        }
+      }
       for (gs_ctx* m : ms) {
         CK(m, hipSetDevice(m->dev));
         CK(m, pp_round_shard(m->st, m->d_next, tt, m->sp, m->stream));
@@ -2003,13 +2132,19 @@ int run_async(gs_ctx* c, uint64_t tend, uint32_t poll, uint64_t max_ticks, OnTic
 
 // ---- node-range shards ------------------------------------------------------
 // One window for shards `ms` (all shards of a group, or this rank's one shard
-// with an RCCL communicator), SURVEY.md section 8(e)2:
-//   1. each shard counts its fires per tick; the counts are gathered
-//      (host reads / RCCL all-gather) so every shard cuts the same window;
-//   2. each shard compacts its window fires; the lists are all-gathered
-//      (device copies / RCCL all-gather, in place);
-//   3. each shard expands EVERY firing node against its partition of the
-//      table and partitions / resolves its own buckets.
+// with an exchange), SURVEY.md section 8(e)2 -- owner expand:
+//   1. each shard counts its fires per tick; the counts are gathered, so every
+//      shard cuts the same window (host sync 1);
+//   2. each shard expands its OWN firing nodes (its own friend rows), binning
+//      every kept message by the shard that owns its target;
+//   3. the region fills and error words are gathered (host sync 2); a shard
+//      whose size estimate overflowed redoes its expand with exact counts;
+//   4. each shard packs the filled prefixes of its regions into one block per
+//      destination, and the blocks move to their owners (device copies, RCCL
+//      grouped send/recv, or the caller's all_to_allv);
+//   5. each shard partitions and resolves the messages it received.
+// Per shard, the expand reads 1/G of the window's rows and the resolve owns
+// 1/G of the buckets, so the work per shard shrinks with G.
 int sync_all(const std::vector<gs_ctx*>& ms) {
   for (gs_ctx* m : ms) {
     CK(m, hipSetDevice(m->dev));
@@ -2048,59 +2183,316 @@ int shard_units(gs_ctx* m, uint32_t t, uint32_t Lu, bool gather) {
   return GS_OK;
 }
 
-// What the host keeps of a shard window until the next window's count sync
-// has shown that no shard's partition overflowed.
+// Serial shard pipelines (GS_SHARD_SERIAL=1, in-process shards): each shard's
+// phases run alone on the device, so GS_FLAG_TIMING measures one shard's
+// device time per window (bench.py's in-process scaling proxy).
+bool shard_serial() { return getenv("GS_SHARD_SERIAL") != nullptr; }
+
+// A shard window the host keeps until the next window's count sync has shown
+// that no shard's receive-side partition overflowed.
 struct ShardWin {
   uint32_t t = 0, L = 0;
-  unsigned long long Tub = 0;  // bound on one shard's messages: every slot of every gathered fire
   bool live = false;
 };
 
-// Expand + partition + consume + resolve of one window on shard m (its
-// gathered fire list in w.gfire).  Regions are sized from estimates; an
-// overflow sets the sticky flag, the later kernels of the window skip, and the
-// host redoes it exactly (shard_redo) before the next window.
-int shard_pipeline(gs_ctx* m, const ShardWin& sw, bool timing) {
+// Coarse plan of shard c's outgoing messages (owner expand): bin b = d *
+// obins + k holds the targets in chunk k (2^22 nodes) of shard d's range;
+// each of its 8 sub-regions gets 1/8 of the chunk's node share of T plus 512,
+// or exactly `exact[region]`.  Bins past G * obins and empty chunks get none.
+void plan_coarse_owner(gs_ctx* c, uint64_t T, const unsigned long long* exact) {
+  const WinState& w = c->ws;
+  const uint64_t N = c->p.n;
+  unsigned long long a = 0;
+  for (uint32_t b = 0; b < 256; ++b) {
+    const uint32_t d = b / w.obins, k = b % w.obins;
+    uint64_t cnt = 0;
+    if (d < w.G) {
+      const uint64_t dlo = (uint64_t)d * c->seg_per, dhi = std::min<uint64_t>(dlo + c->seg_per, N);
+      const uint64_t lo = dlo + ((uint64_t)k << kCoarseShift);
+      const uint64_t hi = std::min<uint64_t>(dhi, lo + (1ull << kCoarseShift));
+      cnt = hi > lo ? hi - lo : 0;
+    }
+    const unsigned long long sub = cnt ? (unsigned long long)((double)T * (double)cnt / (double)N / kCoarseSub) + 512 : 0;
+    for (uint32_t x = 0; x < kCoarseSub; ++x) {
+      const uint32_t r = b * kCoarseSub + x;
+      c->h_cap[r] = a;
+      if (cnt) a += exact ? exact[r] : sub;
+    }
+  }
+  c->h_cap[kRegions] = a;
+}
+
+int shard_events(gs_ctx* m, size_t k) {
+  while (m->ev.size() < k) {
+    hipEvent_t ev;
+    CK(m, hipEventCreate(&ev));
+    m->ev.push_back(ev);
+  }
+  return GS_OK;
+}
+
+// Step 2 on shard m: expand its Tn own fires of window [t, t + L).
+int shard_expand(gs_ctx* m, uint32_t t, uint32_t L, uint64_t Tn, bool timing) {
   WinState& w = m->ws;
   CK(m, hipSetDevice(m->dev));
-  const unsigned long long Test =
-      (unsigned long long)((long double)sw.Tub * (long double)m->ntot / (long double)m->p.n);
-  plan_coarse(m, Test, nullptr);
-  const uint64_t fcap = sw.Tub + sw.Tub / 8 + (uint64_t)w.ncoarse * 256 * 513 + 16;
-  if (!grow(m->cmsg, (m->h_cap[kRegions] + 16) * 4) || !grow(m->fmsg, fcap * 4))
-    return fail(m, GS_ENOMEM, "cannot allocate " + std::to_string(sw.Tub) + " window messages");
+  plan_coarse_owner(m, Tn * w.slots, nullptr);
+  if (!grow(m->cmsg, (m->h_cap[kRegions] + 16) * 4) || !grow(m->gmap, ((Tn + 63) / 64 + 1) * 4))
+    return fail(m, GS_ENOMEM, "cannot allocate " + std::to_string(m->h_cap[kRegions]) + " window messages");
   w.cmsg = (uint32_t*)m->cmsg.p;
-  w.fmsg = (uint32_t*)m->fmsg.p;
+  w.gmap = (uint32_t*)m->gmap.p;
   w.tofs = 0;
-  if (timing)
-    while (m->ev.size() < 5) {
-      hipEvent_t ev;
-      CK(m, hipEventCreate(&ev));
-      m->ev.push_back(ev);
-    }
-  hipEvent_t* e = timing ? &m->ev[0] : nullptr;
   CK(m, hipMemcpyAsync(w.ccap, m->h_cap, (kRegions + 1) * 8, hipMemcpyHostToDevice, m->stream));
-  if (e) CK(m, hipEventRecord(e[0], m->stream));
-  CK(m, win_expand_sh(w, sw.t, sw.L, 1, m->stream));
-  if (e) CK(m, hipEventRecord(e[1], m->stream));
-  CK(m, win_plan(w, false, m->stream));
-  CK(m, win_part2(w, sw.Tub, true, m->stream));
-  if (e) CK(m, hipEventRecord(e[2], m->stream));
-  CK(m, win_consume_sh(w, sw.t, sw.L, m->stream));
-  if (e) CK(m, hipEventRecord(e[3], m->stream));
-  CK(m, win_resolve(w, sw.t, sw.L, m->stream));
-  CK(m, win_stats_reduce(w, sw.t, sw.L, m->stream));
-  if (e) {
-    CK(m, hipEventRecord(e[4], m->stream));
+  CK(m, win_groupmap(w, L, m->stream));
+  if (timing) {
+    RC(shard_events(m, 7));
+    CK(m, hipEventRecord(m->ev[0], m->stream));
+  }
+  CK(m, win_expand(w, t, L, Tn, 1, m->stream));
+  if (timing) CK(m, hipEventRecord(m->ev[1], m->stream));
+  return GS_OK;
+}
+
+// Step 3: lay[s * (kRegions + 1) + r] = shard s's fill of region r, and
+// lay[s * (kRegions + 1) + kRegions] = its error word.
+int gather_layouts(const std::vector<gs_ctx*>& ms, std::vector<unsigned long long>& lay) {
+  gs_ctx* m0 = ms[0];
+  const size_t K1 = kRegions + 1;
+  lay.assign((size_t)m0->G * K1, 0);
+  if (is_rank(m0)) {
+    gs_ctx* m = m0;
+    unsigned long long* mine = m->d_glay + (size_t)m->rank * K1;
+    CK(m, hipMemcpyAsync(mine, m->ws.cfill, kRegions * 8, hipMemcpyDeviceToDevice, m->stream));
+    CK(m, hipMemsetAsync(mine + kRegions, 0, 8, m->stream));
+    CK(m, hipMemcpyAsync(mine + kRegions, m->d_err, 4, hipMemcpyDeviceToDevice, m->stream));
+    RC(x_all_gather(m, m->d_glay, K1 * 8));
+    CK(m, hipMemcpyAsync(m->h_glay, m->d_glay, (size_t)m->G * K1 * 8, hipMemcpyDeviceToHost, m->stream));
     CK(m, hipStreamSynchronize(m->stream));
-    float ms1 = 0, ms2 = 0, ms3 = 0;
-    CK(m, hipEventElapsedTime(&ms1, e[0], e[1]));
-    CK(m, hipEventElapsedTime(&ms2, e[1], e[2]));
-    CK(m, hipEventElapsedTime(&ms3, e[3], e[4]));
-    m->timing.expand_ms += ms1;
-    m->timing.part_ms += ms2;
-    m->timing.deliver_ms += ms1 + ms2;
-    m->timing.resolve_ms += ms3;
+    std::copy(m->h_glay, m->h_glay + (size_t)m->G * K1, lay.begin());
+    return GS_OK;
+  }
+  for (gs_ctx* m : ms) {
+    CK(m, hipSetDevice(m->dev));
+    CK(m, hipMemcpyAsync(m->h_misc, m->ws.cfill, kRegions * 8, hipMemcpyDeviceToHost, m->stream));
+    CK(m, hipMemcpyAsync(m->h_err, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
+  }
+  RC(sync_all(ms));
+  for (gs_ctx* m : ms) {
+    std::copy(m->h_misc, m->h_misc + kRegions, lay.begin() + (size_t)m->rank * K1);
+    lay[(size_t)m->rank * K1 + kRegions] = *m->h_err;
+  }
+  return GS_OK;
+}
+
+// Clears the partition-overflow flags of m's error word (host round trip).
+int clear_part_flags(gs_ctx* m) {
+  uint32_t e = 0;
+  CK(m, hipMemcpyAsync(&e, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
+  CK(m, hipStreamSynchronize(m->stream));
+  e &= ~(kErrCoarse | kErrFine);
+  CK(m, hipMemcpyAsync(m->d_err, &e, 4, hipMemcpyHostToDevice, m->stream));
+  return GS_OK;
+}
+
+// Shard m's expand overflowed a region estimate: count its messages per
+// region, plan exactly and write them again (the stats were added by the
+// first pass).  Rank-local.
+int sender_redo(gs_ctx* m, uint32_t t, uint32_t L, uint64_t Tn) {
+  WinState& w = m->ws;
+  CK(m, hipSetDevice(m->dev));
+  RC(clear_part_flags(m));
+  CK(m, hipMemsetAsync(w.chist, 0, kRegions * 8, m->stream));
+  CK(m, hipMemsetAsync(w.cfill, 0, kRegions * 8, m->stream));
+  CK(m, win_expand(w, t, L, Tn, 0, m->stream));
+  CK(m, hipMemcpyAsync(m->h_misc, w.chist, kRegions * 8, hipMemcpyDeviceToHost, m->stream));
+  CK(m, hipStreamSynchronize(m->stream));
+  plan_coarse_owner(m, Tn * w.slots, m->h_misc);
+  if (!grow(m->cmsg, (m->h_cap[kRegions] + 16) * 4)) return fail(m, GS_ENOMEM, "cannot allocate the window messages");
+  w.cmsg = (uint32_t*)m->cmsg.p;
+  CK(m, hipMemcpyAsync(w.ccap, m->h_cap, (kRegions + 1) * 8, hipMemcpyHostToDevice, m->stream));
+  CK(m, win_expand(w, t, L, Tn, 2, m->stream));
+  ++m->timing.exact_redos;
+  return GS_OK;
+}
+
+// Step 4: packs every shard's blocks, moves them to their owners and sets
+// each shard's receive layout (m->wr, m->rtotal).  poff[s][r] = offset of
+// region r's fill in shard s's packed output; destination d's block is
+// regions [d * obins * 8, (d + 1) * obins * 8).
+int shard_exchange(gs_ctx* acc, const std::vector<gs_ctx*>& ms, const std::vector<unsigned long long>& lay,
+                   bool timing) {
+  gs_ctx* m0 = ms[0];
+  const uint32_t G = m0->G, B8 = m0->ws.obins * kCoarseSub, nreg = G * B8;
+  const size_t K1 = kRegions + 1;
+  std::vector<unsigned long long> poff((size_t)G * K1);
+  for (uint32_t s = 0; s < G; ++s) {
+    unsigned long long a = 0;
+    for (uint32_t r = 0; r < kRegions; ++r) {
+      poff[(size_t)s * K1 + r] = a;
+      a += lay[(size_t)s * K1 + r];
+    }
+    poff[(size_t)s * K1 + kRegions] = a;
+  }
+  auto bstart = [&](uint32_t s, uint32_t d) { return poff[(size_t)s * K1 + (size_t)d * B8]; };
+  auto bsize = [&](uint32_t s, uint32_t d) { return poff[(size_t)s * K1 + (size_t)(d + 1) * B8] - bstart(s, d); };
+  const bool rank = is_rank(m0);
+  // base[m][s]: where sender s's block for member m starts in m's receive buffer
+  std::vector<std::vector<unsigned long long>> base(ms.size(), std::vector<unsigned long long>(G, 0));
+  std::vector<uint32_t*> rbuf(ms.size(), nullptr), pout(ms.size(), nullptr);
+  if (rank) {
+    gs_ctx* m = m0;
+    const uint32_t me = m->rank;
+    unsigned long long rsum = 0;
+    for (uint32_t s = 0; s < G; ++s) { base[0][s] = rsum; rsum += bsize(s, me); }
+    if (!grow(m->xsend, (poff[(size_t)me * K1 + kRegions] + 16) * 4) || !grow(m->xrecv, (rsum + 16) * 4))
+      return fail(m, GS_ENOMEM, "cannot allocate the exchange buffers");
+    rbuf[0] = (uint32_t*)m->xrecv.p;
+    pout[0] = (uint32_t*)m->xsend.p;
+  } else {
+    // device D's buffer: its members' packed outputs, then the blocks its
+    // members receive from members on other devices
+    std::vector<unsigned long long> dtot(acc->gdevs.size(), 0), O(ms.size(), 0);
+    for (size_t i = 0; i < ms.size(); ++i) {
+      const int D = acc->gdev_of[i];
+      O[i] = dtot[D];
+      dtot[D] += poff[(size_t)ms[i]->rank * K1 + kRegions];
+    }
+    for (size_t i = 0; i < ms.size(); ++i) {
+      const int D = acc->gdev_of[i];
+      const uint32_t d = ms[i]->rank;
+      for (size_t j = 0; j < ms.size(); ++j) {
+        const uint32_t s = ms[j]->rank;
+        if (acc->gdev_of[j] == D) {
+          base[i][s] = O[j] + bstart(s, d);
+        } else {
+          base[i][s] = dtot[D];
+          dtot[D] += bsize(s, d);
+        }
+      }
+    }
+    for (size_t D = 0; D < acc->gdevs.size(); ++D) {
+      CK(acc, hipSetDevice(acc->gdevs[D]));
+      if (!grow(acc->gbuf[D], (dtot[D] + 16) * 4)) return fail(acc, GS_ENOMEM, "cannot allocate the exchange buffers");
+    }
+    for (size_t i = 0; i < ms.size(); ++i) {
+      rbuf[i] = (uint32_t*)acc->gbuf[acc->gdev_of[i]].p;
+      pout[i] = rbuf[i] + O[i];
+    }
+  }
+  // receive layouts (region = bin * (G * 8) + sender * 8 + sub) and pack offsets
+  for (size_t i = 0; i < ms.size(); ++i) {
+    gs_ctx* m = ms[i];
+    const uint32_t d = m->rank;
+    unsigned long long* rcap = m->h_rtab;
+    unsigned long long* rend = rcap + K1;
+    unsigned long long* rfill = rend + K1;
+    unsigned long long* mypoff = rfill + K1;
+    std::fill(m->h_rtab, m->h_rtab + 4 * K1, 0ull);
+    unsigned long long tot = 0;
+    for (uint32_t c = 0; c < m->ws.obins; ++c)
+      for (uint32_t s = 0; s < G; ++s)
+        for (uint32_t x = 0; x < kCoarseSub; ++x) {
+          const size_t rr = ((size_t)c * G + s) * kCoarseSub + x, sr = (size_t)d * B8 + c * kCoarseSub + x;
+          const unsigned long long f = lay[(size_t)s * K1 + sr];
+          rcap[rr] = base[i][s] + poff[(size_t)s * K1 + sr] - bstart(s, d);
+          rend[rr] = rcap[rr] + f;
+          rfill[rr] = f;
+          tot += f;
+        }
+    std::copy(poff.begin() + (size_t)d * K1, poff.begin() + (size_t)(d + 1) * K1, mypoff);
+    m->rtotal = tot;
+    WinState& wr = m->wr;
+    wr = m->ws;
+    wr.cmsg = rbuf[i];
+    wr.ccap = m->d_rtab;
+    wr.ccap_end = m->d_rtab + K1;
+    wr.cfill = m->d_rtab + 2 * K1;
+    wr.csub = G * kCoarseSub;
+    CK(m, hipSetDevice(m->dev));
+    CK(m, hipMemcpyAsync(m->d_rtab, m->h_rtab, 4 * K1 * 8, hipMemcpyHostToDevice, m->stream));
+    if (timing) CK(m, hipEventRecord(m->ev[2], m->stream));
+    CK(m, win_pack(m->ws, m->d_rtab + 3 * K1, nreg, pout[i], m->stream));
+    if (timing) CK(m, hipEventRecord(m->ev[3], m->stream));
+    if (!rank) CK(m, hipEventRecord(acc->gev_c[i], m->stream));
+    if (shard_serial() && !rank) CK(m, hipStreamSynchronize(m->stream));
+  }
+  if (rank) {
+    gs_ctx* m = m0;
+    const uint32_t me = m->rank;
+    if (m->comm) {
+      const Rccl& r = rccl();
+      NCK(m, r.group_start());
+      for (uint32_t p = 0; p < G; ++p) {
+        if (bsize(me, p))
+          NCK(m, r.send(pout[0] + bstart(me, p), bsize(me, p), ncclUint32, (int)p, m->comm, m->stream));
+        if (bsize(p, me))
+          NCK(m, r.recv(rbuf[0] + base[0][p], bsize(p, me), ncclUint32, (int)p, m->comm, m->stream));
+      }
+      NCK(m, r.group_end());
+    } else {
+      const unsigned long long ssum = poff[(size_t)me * K1 + kRegions];
+      unsigned long long rsum = 0;
+      std::vector<size_t> sb(G), rb(G);
+      for (uint32_t p = 0; p < G; ++p) {
+        sb[p] = bsize(me, p) * 4;
+        rb[p] = bsize(p, me) * 4;
+        rsum += bsize(p, me);
+      }
+      if (!grow_pinned(m, (ssum + rsum) * 4 + 16)) return fail(m, GS_ENOMEM, "cannot allocate exchange staging");
+      char* hs = m->h_xbuf;
+      char* hr = m->h_xbuf + ssum * 4;
+      CK(m, hipMemcpyAsync(hs, pout[0], ssum * 4, hipMemcpyDeviceToHost, m->stream));
+      CK(m, hipStreamSynchronize(m->stream));
+      if (m->hx.all_to_allv(m->hx.user, hs, sb.data(), hr, rb.data()))
+        return fail(m, GS_EDEVICE, "the exchange's all_to_allv callback failed");
+      CK(m, hipMemcpyAsync(rbuf[0], hr, rsum * 4, hipMemcpyHostToDevice, m->stream));
+      CK(m, hipStreamSynchronize(m->stream));
+    }
+    return GS_OK;
+  }
+  // group: every member waits for the packs it reads; blocks from other devices are copied in
+  for (size_t i = 0; i < ms.size(); ++i) {
+    gs_ctx* m = ms[i];
+    const int D = acc->gdev_of[i];
+    CK(m, hipSetDevice(m->dev));
+    for (size_t j = 0; j < ms.size(); ++j) {
+      if (j == i) continue;
+      CK(m, hipStreamWaitEvent(m->stream, acc->gev_c[j], 0));
+      const int Dj = acc->gdev_of[j];
+      const uint32_t s = ms[j]->rank;
+      if (Dj != D && bsize(s, m->rank))
+        CK(m, hipMemcpyPeerAsync(rbuf[i] + base[i][s], m->dev, pout[j] + bstart(s, m->rank), ms[j]->dev,
+                                 bsize(s, m->rank) * 4, m->stream));
+    }
+  }
+  return GS_OK;
+}
+
+// Step 5 on shard m: partition and resolve the received messages.
+int shard_receive(gs_ctx* m, const ShardWin& sw, bool timing) {
+  WinState& wr = m->wr;
+  CK(m, hipSetDevice(m->dev));
+  const uint64_t R = m->rtotal;
+  const uint64_t fcap = R + R / 8 + (uint64_t)wr.ncoarse * 256 * 513 + 16;
+  if (!grow(m->fmsg, fcap * 4)) return fail(m, GS_ENOMEM, "cannot allocate " + std::to_string(R) + " received messages");
+  wr.fmsg = m->ws.fmsg = (uint32_t*)m->fmsg.p;
+  if (timing) CK(m, hipEventRecord(m->ev[4], m->stream));
+  CK(m, win_plan(wr, false, m->stream));
+  CK(m, win_part2(wr, R, true, m->stream));
+  if (timing) CK(m, hipEventRecord(m->ev[5], m->stream));
+  CK(m, win_resolve(wr, sw.t, sw.L, m->stream));
+  CK(m, win_stats_reduce(wr, sw.t, sw.L, m->stream));
+  if (timing) {
+    CK(m, hipEventRecord(m->ev[6], m->stream));
+    CK(m, hipStreamSynchronize(m->stream));
+    float ex = 0, pk = 0, p2 = 0, rs = 0;
+    CK(m, hipEventElapsedTime(&ex, m->ev[0], m->ev[1]));
+    CK(m, hipEventElapsedTime(&pk, m->ev[2], m->ev[3]));
+    CK(m, hipEventElapsedTime(&p2, m->ev[4], m->ev[5]));
+    CK(m, hipEventElapsedTime(&rs, m->ev[5], m->ev[6]));
+    m->timing.expand_ms += ex;
+    m->timing.part_ms += pk + p2;
+    m->timing.deliver_ms += ex + pk + p2;
+    m->timing.resolve_ms += rs;
     m->timing.deliver_launches += 1;
     m->timing.resolve_launches += 1;
     m->timing.windows += 1;
@@ -2108,50 +2500,29 @@ int shard_pipeline(gs_ctx* m, const ShardWin& sw, bool timing) {
   return GS_OK;
 }
 
-// Shard m's window sw overflowed a region: clear the flag, partition it again
-// with exact counts (its gathered fire list is still in place), consume and
-// resolve it.  Rank-local: no other shard takes part.
-int shard_redo(gs_ctx* m, const ShardWin& sw) {
-  WinState& w = m->ws;
+// Shard m's receive-side partition of window sw overflowed: partition the
+// received messages (still in place) again with exact counts and resolve.
+int receiver_redo(gs_ctx* m, const ShardWin& sw) {
+  WinState& wr = m->wr;
   CK(m, hipSetDevice(m->dev));
-  uint32_t e = 0;
-  CK(m, hipMemcpyAsync(&e, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
-  CK(m, hipStreamSynchronize(m->stream));
-  e &= ~(kErrCoarse | kErrFine);
-  CK(m, hipMemcpyAsync(m->d_err, &e, 4, hipMemcpyHostToDevice, m->stream));
-  CK(m, hipMemsetAsync(w.chist, 0, kRegions * 8, m->stream));
-  CK(m, hipMemsetAsync(w.cfill, 0, kRegions * 8, m->stream));
-  CK(m, hipMemsetAsync(w.ffill, 0, (size_t)w.nfine * 8, m->stream));
-  CK(m, win_expand_sh(w, sw.t, sw.L, 0, m->stream));
-  CK(m, hipMemcpyAsync(m->h_misc, w.chist, kRegions * 8, hipMemcpyDeviceToHost, m->stream));
-  CK(m, hipStreamSynchronize(m->stream));
-  plan_coarse(m, sw.Tub, m->h_misc);
-  if (!grow(m->cmsg, (m->h_cap[kRegions] + 16) * 4)) return fail(m, GS_ENOMEM, "cannot allocate the window messages");
-  w.cmsg = (uint32_t*)m->cmsg.p;
-  CK(m, hipMemcpyAsync(w.ccap, m->h_cap, (kRegions + 1) * 8, hipMemcpyHostToDevice, m->stream));
-  CK(m, win_expand_sh(w, sw.t, sw.L, 2, m->stream));
-  CK(m, win_plan(w, false, m->stream));
-  CK(m, hipMemsetAsync(w.fhist, 0, ((size_t)w.ncoarse * 256 + 1) * 8, m->stream));
-  CK(m, win_plan(w, true, m->stream));
-  CK(m, win_part2(w, sw.Tub, false, m->stream));
-  size_t need2 = 0;
-  CK(m, win_scan_fine(w, nullptr, need2, m->stream));
-  if (!grow(m->tmp, need2)) return fail(m, GS_ENOMEM, "cannot allocate scan scratch");
-  need2 = m->tmp.bytes;
-  CK(m, win_scan_fine(w, m->tmp.p, need2, m->stream));
-  CK(m, hipMemsetAsync(w.ffill, 0, (size_t)w.nfine * 8, m->stream));
-  CK(m, win_part2(w, sw.Tub, true, m->stream));
-  CK(m, win_consume_sh(w, sw.t, sw.L, m->stream));
-  CK(m, win_resolve(w, sw.t, sw.L, m->stream));
-  CK(m, win_stats_reduce(w, sw.t, sw.L, m->stream));
+  RC(clear_part_flags(m));
+  const uint64_t R = m->rtotal;
+  CK(m, hipMemsetAsync(wr.ffill, 0, (size_t)wr.nfine * 8, m->stream));
+  CK(m, hipMemsetAsync(wr.fhist, 0, ((size_t)wr.ncoarse * 256 + 1) * 8, m->stream));
+  CK(m, win_plan(wr, true, m->stream));
+  CK(m, win_part2(wr, R, false, m->stream));
+  size_t need = 0;
+  CK(m, win_scan_fine(wr, nullptr, need, m->stream));
+  if (!grow(m->tmp, need)) return fail(m, GS_ENOMEM, "cannot allocate scan scratch");
+  need = m->tmp.bytes;
+  CK(m, win_scan_fine(wr, m->tmp.p, need, m->stream));
+  CK(m, hipMemsetAsync(wr.ffill, 0, (size_t)wr.nfine * 8, m->stream));
+  CK(m, win_part2(wr, R, true, m->stream));
+  CK(m, win_resolve(wr, sw.t, sw.L, m->stream));
+  CK(m, win_stats_reduce(wr, sw.t, sw.L, m->stream));
   ++m->timing.exact_redos;
   return GS_OK;
 }
-
-// Serial shard pipelines (GS_SHARD_SERIAL=1, in-process shards): each shard's
-// window runs alone on the device, so GS_FLAG_TIMING measures one shard's
-// device time per window (bench.py's in-process scaling proxy).
-bool shard_serial() { return getenv("GS_SHARD_SERIAL") != nullptr; }
 
 int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint32_t n, bool timing) {
   gs_ctx* m0 = ms[0];
@@ -2160,11 +2531,12 @@ int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint
   const uint32_t stride = m0->ws.stride;
   const uint32_t Lmax = std::min<uint32_t>(std::max<int32_t>(m0->p.delay_low, 1), kBitTicks);
   const uint64_t slot_budget = ((N + kFineNodes - 1) >> kFineLog) * (uint64_t)kWinSlotsPerBucket;
-  std::vector<unsigned long long> cnt((size_t)G * kMaxWindow);
+  const size_t K1 = kRegions + 1;
+  std::vector<unsigned long long> cnt((size_t)G * kMaxWindow), lay;
   ShardWin prev;
   uint32_t done = 0;
   // 1. fire counts per tick (every shard's, gathered) and every shard's
-  //    overflow flag of the previous window: the one host sync per window
+  //    overflow flag of the previous window
   auto counts = [&](uint32_t t, uint32_t Lw) -> int {
     for (gs_ctx* m : ms) RC(shard_units(m, t, Lw, true));
     RC(sync_all(ms));
@@ -2182,11 +2554,11 @@ int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint
     const uint32_t Lw = std::min(Lmax, n - done);
     const uint32_t t = (uint32_t)(t0 + done);
     RC(counts(t, Lw));
-    if (flagged()) {  // a shard's previous window overflowed: it redoes it, then every shard counts again
+    if (flagged()) {  // a shard's previous window overflowed its receive partition: it redoes it, then all count again
       for (uint32_t r = 0; r < G; ++r) {
         if (!(cnt[(size_t)r * kMaxWindow + kFlagSlot] & (kErrCoarse | kErrFine))) continue;
         for (gs_ctx* m : ms)
-          if (m->rank == r) RC(shard_redo(m, prev));
+          if (m->rank == r) RC(receiver_redo(m, prev));
       }
       RC(counts(t, Lw));
     }
@@ -2201,71 +2573,40 @@ int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint
     while (L < Lw && (Tn + F(L)) * stride <= slot_budget) Tn += F(L++);
     if (L < Lw)
       for (gs_ctx* m : ms) RC(shard_units(m, t, L, false));
-    unsigned long long seg = 0;
     std::vector<unsigned long long> own(G, 0);
+    unsigned long long Ftot = 0;
     for (uint32_t r = 0; r < G; ++r) {
       for (uint32_t k = 0; k < L; ++k) own[r] += cnt[(size_t)r * kMaxWindow + k];
-      seg = std::max(seg, own[r]);
+      Ftot += own[r];
     }
-    const uint64_t segb = (seg * 5 + 15) & ~15ull;  // seg u32 ids + seg u8 ticks, 16-B aligned
-    unsigned long long Ftot = 0;
-    for (uint32_t k = 0; k < L; ++k) Ftot += F(k);
     ShardWin sw;
     sw.t = t;
     sw.L = L;
-    sw.Tub = Ftot * stride;
-    sw.live = seg > 0;
-    if (seg) {
-      // 2. compaction into segment `rank` of the device's all-gather buffer
-      for (size_t i = 0; i < ms.size(); ++i) {
-        gs_ctx* m = ms[i];
-        WinState& w = m->ws;
-        CK(m, hipSetDevice(m->dev));
-        Buf* b = &m->gfire;
-        if (acc->group) b = &acc->gbuf[acc->gdev_of[i]];
-        if (!grow(*b, (size_t)G * segb)) return fail(m, GS_ENOMEM, "cannot allocate the window fire lists");
-        if (!grow(m->gmap, ((own[m->rank] + 63) / 64 + 1) * 4))
-          return fail(m, GS_ENOMEM, "cannot allocate the group map");
-        w.gmap = (uint32_t*)m->gmap.p;
-        w.gfire = (const uint8_t*)b->p;
-        w.gseg = seg;
-        w.gsegb = segb;
-        uint8_t* mine = (uint8_t*)b->p + (size_t)m->rank * segb;
-        CK(m, win_groupmap(w, L, m->stream));
-        CK(m, win_fire_compact(w, t, L, own[m->rank], (uint32_t*)mine, mine + seg * 4, seg, m->stream));
-        if (acc->group) CK(m, hipEventRecord(acc->gev_c[i], m->stream));
-      }
-      // ... all-gathered
-      if (is_rank(m0)) {
-        RC(x_all_gather(m0, m0->gfire.p, segb));
-      } else {
-        // each device's leader copies the other devices' segments in; every
-        // member waits for the compactions it reads
-        std::vector<int> done_dev(acc->gdevs.size(), 0);
-        for (size_t i = 0; i < ms.size(); ++i) {
-          gs_ctx* m = ms[i];
-          const int d = acc->gdev_of[i];
-          CK(m, hipSetDevice(m->dev));
-          if (done_dev[d]) {
-            CK(m, hipStreamWaitEvent(m->stream, acc->gev_x[d], 0));
-            continue;
-          }
-          done_dev[d] = 1;
-          for (size_t j = 0; j < ms.size(); ++j) {
-            if (j == i) continue;
-            CK(m, hipStreamWaitEvent(m->stream, acc->gev_c[j], 0));
-            const int dj = acc->gdev_of[j];
-            if (dj != d)
-              CK(m, hipMemcpyPeerAsync((uint8_t*)acc->gbuf[d].p + (size_t)ms[j]->rank * segb, m->dev,
-                                       (uint8_t*)acc->gbuf[dj].p + (size_t)ms[j]->rank * segb, ms[j]->dev, segb,
-                                       m->stream));
-          }
-          CK(m, hipEventRecord(acc->gev_x[d], m->stream));
-        }
-      }
-      // 3. expand, partition, consume, resolve on every shard (serially when timed in-process)
+    sw.live = Ftot > 0;
+    if (Ftot) {
+      // 2. expand own fires
       for (gs_ctx* m : ms) {
-        RC(shard_pipeline(m, sw, timing));
+        RC(shard_expand(m, t, L, own[m->rank], timing));
+        if (shard_serial() && !is_rank(m)) CK(m, hipStreamSynchronize(m->stream));
+      }
+      // 3. fills and overflow flags; exact redo of an overflowed expand
+      RC(gather_layouts(ms, lay));
+      bool redo = false;
+      for (uint32_t r = 0; r < G; ++r)
+        if (lay[(size_t)r * K1 + kRegions] & kErrCoarse) {
+          redo = true;
+          for (gs_ctx* m : ms)
+            if (m->rank == r) RC(sender_redo(m, t, L, own[r]));
+        }
+      if (redo) RC(gather_layouts(ms, lay));
+      for (gs_ctx* m : ms) {
+        CK(m, hipSetDevice(m->dev));
+        CK(m, win_consume_sh(m->ws, t, L, m->stream));
+      }
+      // 4. pack and move the blocks; 5. partition and resolve what arrived
+      RC(shard_exchange(acc, ms, lay, timing));
+      for (gs_ctx* m : ms) {
+        RC(shard_receive(m, sw, timing));
         if (shard_serial() && !is_rank(m)) CK(m, hipStreamSynchronize(m->stream));
       }
     } else {
@@ -2285,7 +2626,7 @@ int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint
   RC(sync_all(ms));
   for (gs_ctx* m : ms)
     if (*m->h_err & (kErrCoarse | kErrFine)) {
-      RC(shard_redo(m, prev));
+      RC(receiver_redo(m, prev));
       CK(m, hipMemcpyAsync(m->h_err, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
       CK(m, hipStreamSynchronize(m->stream));
     }
@@ -2749,6 +3090,7 @@ int gs_timing_get(gs_ctx* c, gs_timing* out) {
     out->pp_bottom_rounds = h.nbottom;
     out->pp_answer_rounds = h.nanswer;
   }
+  if (c->pp && c->begun) out->pp_early_rounds += c->rep_rounds;  // shards: the replicas' sparse rounds
   return GS_OK;
 }
 

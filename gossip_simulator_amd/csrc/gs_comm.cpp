@@ -35,6 +35,10 @@ const Rccl& rccl() {
     g_rccl.comm_abort = (decltype(g_rccl.comm_abort))sym("ncclCommAbort");
     g_rccl.all_gather = (decltype(g_rccl.all_gather))sym("ncclAllGather");
     g_rccl.all_reduce = (decltype(g_rccl.all_reduce))sym("ncclAllReduce");
+    g_rccl.send = (decltype(g_rccl.send))sym("ncclSend");
+    g_rccl.recv = (decltype(g_rccl.recv))sym("ncclRecv");
+    g_rccl.group_start = (decltype(g_rccl.group_start))sym("ncclGroupStart");
+    g_rccl.group_end = (decltype(g_rccl.group_end))sym("ncclGroupEnd");
     g_rccl.error_string = (decltype(g_rccl.error_string))sym("ncclGetErrorString");
     g_rccl.ok = ok;
     if (!ok) g_rccl.why = "librccl.so.1 lacks an entry point this engine needs";

@@ -139,7 +139,8 @@ struct WinState {
   uint32_t* cmsg;                // coarse regions: u_in_coarse | k << 22
   uint32_t* fmsg;                // fine regions:   u_in_fine   | k << 14
   unsigned long long* chist;     // [kRegions] exact coarse region counts (fallback)
-  unsigned long long* ccap;      // [kRegions + 1] coarse region starts, region = bin * 8 + sub
+  unsigned long long* ccap;      // [kRegions + 1] coarse region starts, region = bin * csub + sub
+  const unsigned long long* ccap_end;  // [kRegions] region ends (null: ccap[r + 1])
   unsigned long long* cfill;     // [kRegions] coarse region fill
   uint32_t* tprefix;             // [kRegions + 1] part2 tiles per coarse region (prefix)
   unsigned long long* fhist;     // [ncoarse*256 + 1] exact fine counts (fallback)
@@ -155,13 +156,16 @@ struct WinState {
   unsigned long long* stage;     // [slots][kStageWords] per-window results for the host (device-driven)
   uint32_t lstride;              // unit layout stride: units u = f * lstride + k
   uint32_t slots;                // longest row in use (<= stride: rows may be padded for 16-B loads)
-  // node-range shard: partitioned friend rows and the all-gathered window fire list
-  const uint32_t* pent;          // [n][pw]: owned-slot mask, then the owned targets - lo (or a spill offset)
-  const uint32_t* pspill;        // targets of the rows with more than pw - 1 owned slots
-  uint32_t pw;                   // partitioned row width (a multiple of 4)
+  // Regions per coarse bin: kCoarseSub, or G * kCoarseSub in a shard's receive
+  // layout (region = bin * csub + sender * kCoarseSub + sub)
+  uint32_t csub;
+  // node-range shard (owner expand): k_expand bins a kept message by its
+  // target's owner d and the 2^22-node chunk of d's range, bin = d * obins +
+  // chunk, message = target - d's first node within the chunk
+  uint32_t owner;                // 1: bin by owner
+  uint32_t obins;                // bins per owner (256 / G)
+  uint32_t oseg_q, oseg_magic;   // seg_per >> 14 and ceil(2^32 / oseg_q): owner d of a target
   uint32_t abort_on_err;         // host-driven shard windows: an overflowed window's later kernels skip
-  const uint8_t* gfire;          // [G] segments of gsegb bytes: gseg u32 global ids (~0u = padding), gseg u8 ticks
-  uint64_t gseg, gsegb;          // entries, bytes per shard segment of gfire
   uint32_t G, rank;              // shards, this shard's index
   uint32_t seg_per;              // nodes per shard (shard r owns [r*seg_per, ...))
   uint64_t n, W;
@@ -212,15 +216,10 @@ hipError_t win_seal_rows(const uint8_t* deg, uint32_t* ids, uint64_t n, uint32_t
                          hipStream_t s);
 hipError_t win_stats_reduce(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
 // node-range shards
-hipError_t part_count(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
-                      uint32_t* cnt, hipStream_t s);
-hipError_t part_hist(const uint32_t* cnt, uint64_t n, unsigned long long* hist, hipStream_t s);
-hipError_t part_fill_mask(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi, uint32_t pw,
-                          uint32_t* pent, uint32_t* spill, unsigned long long* spill_n, hipStream_t s);
-hipError_t win_fire_compact(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, uint32_t* ids, uint8_t* ks,
-                            uint64_t seg, hipStream_t s);
 hipError_t win_consume_sh(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
-hipError_t win_expand_sh(const WinState& w, uint32_t t0, uint32_t L, int mode, hipStream_t s);
+// Copies the first min(cfill[r], room) messages of every region r < nreg from
+// w.cmsg to out + poff[r] (the all-to-all's send blocks, back to back).
+hipError_t win_pack(const WinState& w, const unsigned long long* poff, uint32_t nreg, uint32_t* out, hipStream_t s);
 // Schedule local node `node` (batched: in every trial; ~0u: each trial's keyed sender) at `tick`.
 hipError_t win_schedule(const WinState& w, uint32_t node, uint32_t tick, uint32_t trials, uint32_t n,
                         hipStream_t s);

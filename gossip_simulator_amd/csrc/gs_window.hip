@@ -214,22 +214,10 @@ __global__ void k_groupmap(const WinState w, uint32_t L) {
   }
 }
 
-// Unit of firing index g: search [gmap[g/64], gmap[g/64 + 1]].
-__device__ __forceinline__ uint32_t unit_of(const WinState& w, unsigned long long g,
-                                            unsigned long long Tn, uint32_t units) {
-  const unsigned long long q = g >> 6;
-  uint32_t lo = w.gmap[q];
-  uint32_t hi = ((q + 1) << 6) < Tn ? w.gmap[q + 1] : units - 1;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi + 1) >> 1;
-    if (w.unit_off[mid] <= g) lo = mid; else hi = mid - 1;
-  }
-  return lo;
-}
-
-// The same for a wave whose 64 lanes hold the 64 consecutive firing indices
-// of group g0 / 64 (g0 wave-uniform): the group's unit bounds are two scalar
-// loads, and only a group that spans several units searches per lane.
+// Unit of firing index g (gmap[q] = unit holding firing index 64*q) for a
+// wave whose 64 lanes hold the 64 consecutive firing indices of group g0 / 64
+// (g0 wave-uniform): the group's unit bounds are two scalar loads, and only a
+// group that spans several units searches [gmap[q], gmap[q + 1]] per lane.
 __device__ __forceinline__ uint32_t unit_of_wave(const WinState& w, unsigned long long g0, unsigned long long g,
                                                  unsigned long long Tn, uint32_t units) {
   const unsigned long long q = g0 >> 6;
@@ -401,6 +389,25 @@ __device__ __forceinline__ void load_row(const WinState& w, uint32_t v, uint32_t
   }
 }
 
+// Coarse bin of target `t`; t becomes its index inside the bin.  Unsharded:
+// bin = t >> 22.  Owner expand (node-range shards): the target's owner d (the
+// shard whose range holds it: q = t >> 14 over seg_per >> 14, oseg_magic =
+// floor((2^32 - 1) / oseg_q) never overestimates and is at most one below)
+// and the 2^22-node chunk of d's range.
+__device__ __forceinline__ uint32_t coarse_bin(const WinState& w, uint32_t& t) {
+  if (!w.owner) {
+    const uint32_t b = t >> kCoarseShift;
+    t &= (1u << kCoarseShift) - 1;
+    return b;
+  }
+  const uint32_t q = t >> kFineLog;
+  uint32_t d = __umulhi(q, w.oseg_magic);
+  if ((d + 1) * w.oseg_q <= q) ++d;
+  const uint32_t off = t - d * w.seg_per;
+  t = off & ((1u << kCoarseShift) - 1);
+  return d * w.obins + (off >> kCoarseShift);
+}
+
 // Expand + coarse partition (Node.Broadcast, simulator.go:141-147).  Each
 // thread takes NPT firing nodes per round; their rows are all in flight before
 // any is used.  Kept targets are counting-sorted in LDS by coarse bucket and
@@ -504,10 +511,11 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
           const uint32_t j = jg * 4 + jj;
           if (j >= MAXS) break;
           if (mm[q][j] != kEmptyMsg && (int32_t)uniform(lane_of(r, jj), 100u) >= w.kd) {  // kept: :145
-            const uint32_t tgt = mm[q][j], bin = tgt >> kCoarseShift;
+            uint32_t loc = mm[q][j];
+            const uint32_t bin = coarse_bin(w, loc);
             const uint32_t roll0 = (int32_t)uniform(lane_of(rc, jj), 100u) < w.kc;
             mt[q][j] = bin | (atomicAdd(&sm.cnt[bin], 1u) << 8);
-            mm[q][j] = (tgt & ((1u << kCoarseShift) - 1)) | (k << kCoarseShift) | (roll0 << kRoll0Coarse);
+            mm[q][j] = loc | (k << kCoarseShift) | (roll0 << kRoll0Coarse);
             ++sent;
           }
         }
@@ -588,6 +596,15 @@ __global__ void k_seal_rows(const uint8_t* deg, uint32_t* ids, uint64_t n, uint3
   }
 }
 
+// End of coarse region r, and its messages (the fill capped at its size).
+__device__ __forceinline__ unsigned long long region_end(const WinState& w, uint32_t r) {
+  return w.ccap_end ? w.ccap_end[r] : w.ccap[r + 1];
+}
+__device__ __forceinline__ unsigned long long region_fill(const WinState& w, uint32_t r) {
+  const unsigned long long room = region_end(w, r) - w.ccap[r];
+  return w.cfill[r] < room ? w.cfill[r] : room;
+}
+
 // Fine regions inside each coarse region: capacity per fine bucket of coarse
 // c = cfill[c]*1.15/256 + 512 (fast path), or exact counts (fhist != null).
 __global__ void k_plan(const WinState w, bool exact) {
@@ -599,18 +616,15 @@ __global__ void k_plan(const WinState w, bool exact) {
     uint32_t t0;
     if (!win_live(w, t0, 0)) return;
   }
-  // messages of bucket c = the fills of its sub-regions (capped at their size);
-  // part2 tiles never cross a sub-region
+  // messages of bucket c = the fills of its csub sub-regions (capped at their
+  // size); part2 tiles never cross a sub-region
+  const uint32_t csub = w.csub;
   unsigned long long cnt = 0;
-  uint32_t tiles[kCoarseSub], ntile = 0;
-#pragma unroll
-  for (uint32_t x = 0; x < kCoarseSub; ++x) {
-    const uint32_t r = tid * kCoarseSub + x;
-    const unsigned long long room = w.ccap[r + 1] - w.ccap[r];
-    const unsigned long long f = w.cfill[r] < room ? w.cfill[r] : room;
+  uint32_t ntile = 0;
+  for (uint32_t x = 0; x < csub && tid * csub + x < kRegions; ++x) {
+    const unsigned long long f = region_fill(w, tid * csub + x);
     cnt += f;
-    tiles[x] = (uint32_t)((f + kPartTile - 1) / kPartTile);
-    ntile += tiles[x];
+    ntile += (uint32_t)((f + kPartTile - 1) / kPartTile);
   }
   const bool live = tid < w.ncoarse;
   // the last coarse bucket may hold fewer than 256 fine buckets
@@ -623,12 +637,12 @@ __global__ void k_plan(const WinState w, bool exact) {
   if (tid == 0)
     for (int i = 1; i <= 256; ++i) { s_base[i] += s_base[i - 1]; s_tp[i] += s_tp[i - 1]; }
   __syncthreads();
-  if (blockIdx.x == 0) {
+  if (blockIdx.x == 0) {  // every region < kRegions is written (256 * csub >= kRegions)
     uint32_t a = s_tp[tid];
-#pragma unroll
-    for (uint32_t x = 0; x < kCoarseSub; ++x) {
-      w.tprefix[tid * kCoarseSub + x] = a;
-      a += live ? tiles[x] : 0u;
+    for (uint32_t x = 0; x < csub && tid * csub + x < kRegions; ++x) {
+      const uint32_t r = tid * csub + x;
+      w.tprefix[r] = a;
+      a += live ? (uint32_t)((region_fill(w, r) + kPartTile - 1) / kPartTile) : 0u;
     }
     if (tid == 255) w.tprefix[kRegions] = s_tp[256];
   }
@@ -684,10 +698,9 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8
       const uint32_t mid = (lo + hi + 1) >> 1;
       if (s_tp[mid] <= g) lo = mid; else hi = mid - 1;
     }
-    const uint32_t r = lo, c = r / kCoarseSub;
+    const uint32_t r = lo, c = r / w.csub;
     const unsigned long long cb = w.ccap[r];
-    const unsigned long long fill = w.cfill[r] < w.ccap[r + 1] - cb ? w.cfill[r] : w.ccap[r + 1] - cb;
-    const unsigned long long ce = cb + fill;
+    const unsigned long long ce = cb + region_fill(w, r);
     const unsigned long long base = cb + (unsigned long long)(g - s_tp[r]) * kPartTile;
     if (tid < 256) ts.cnt[tid] = 0;
     __syncthreads();
@@ -1432,258 +1445,28 @@ __global__ void k_schedule_win(const WinState w, uint32_t node, uint32_t t, uint
 }
 
 // ---- node-range shards (config C4) -----------------
-// Shard r of G owns nodes [r * seg_per, min((r+1) * seg_per, N)).  It keeps,
-// for EVERY node v, only the friend slots whose target it owns, so per-window
-// row reads and drop draws shrink with G.  Row v of the partition is pw words:
-// word 0 = the owned-slot mask (bit j: friends[v][j] is owned), then the
-// owned targets (target - lo) in slot order -- inline when there are at most
-// pw - 1 of them, else word 1 is an offset into the spill array that holds
-// them (pw is chosen so that nearly every row is inline: one dependent load
-// per firing node).  Every window the shards all-gather their firing lists
-// (gfire: per shard a segment of global node ids, then their ticks as bytes);
-// each shard expands every firing node against its own partition and resolves
-// its own buckets with the kernels above (keys are global ids, so the union
-// over shards equals the unsharded run bit for bit).
+// Shard r of G owns nodes [r * seg_per, min((r+1) * seg_per, N)) and their
+// friend rows.  Every window it expands its OWN firing nodes with k_expand in
+// owner mode: a kept message is binned by the shard that owns its target
+// (bin = owner * obins + 2^22-node chunk of the owner's range), so the
+// coarse regions of owner d are one contiguous block of the message buffer.
+// k_pack moves each block's filled prefixes back to back; the blocks go to
+// their owners (all-to-all); each shard then partitions (k_plan / k_part2
+// over the receive layout: G senders x 8 sub-regions per bin) and resolves
+// its own buckets with the kernels above.  Keys are global ids, so the union
+// over shards equals the unsharded run bit for bit.
 
-// cnt[v] = friend slots of v whose target lies in [lo, hi) (sealed rows: slots
-// past the list hold kEmptyMsg, which is never in range).
-__global__ void k_part_count(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
-                             uint32_t* cnt) {
-  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
-       v += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t c = 0;
-    for (uint32_t j = 0; j < stride; ++j) {
-      const uint32_t x = ids[v * stride + j];
-      c += (x >= lo && x < hi) ? 1u : 0u;
-    }
-    cnt[v] = c;
-  }
-}
-
-// hist[c] = nodes with c owned slots (c <= kWinMaxStride).
-__global__ void k_part_hist(const uint32_t* cnt, uint64_t n, unsigned long long* hist) {
-  __shared__ uint32_t h[kWinMaxStride + 1];
-  if (threadIdx.x <= kWinMaxStride) h[threadIdx.x] = 0;
-  __syncthreads();
-  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x)
-    atomicAdd(&h[min(cnt[v], kWinMaxStride)], 1u);
-  __syncthreads();
-  if (threadIdx.x <= kWinMaxStride && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (unsigned long long)h[threadIdx.x]);
-}
-
-// Row v = [mask, owned targets - lo ...] (inline, ~0u-padded to pw) or
-// [mask, spill offset] with the targets at spill[offset ..].
-__global__ void k_part_fill_mask(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
-                                 uint32_t pw, uint32_t* pent, uint32_t* spill, unsigned long long* spill_n) {
-  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
-       v += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t* row = ids + v * stride;
-    uint32_t mask = 0, c = 0;
-    for (uint32_t j = 0; j < stride; ++j) {
-      const uint32_t x = row[j];
-      if (x >= lo && x < hi) { mask |= 1u << j; ++c; }
-    }
-    uint32_t* out = pent + v * pw;
-    out[0] = mask;
-    uint32_t* dst = out + 1;
-    uint32_t pos = 0;
-    if (c > pw - 1) {
-      const unsigned long long at = atomicAdd(spill_n, (unsigned long long)c);
-      out[1] = (uint32_t)at;
-      pos = 1;
-      dst = spill + at;
-      for (uint32_t j = 0, i = 0; j < stride; ++j) {
-        const uint32_t x = row[j];
-        if (x >= lo && x < hi) dst[i++] = x - lo;
-      }
-    } else {
-      for (uint32_t j = 0; j < stride; ++j) {
-        const uint32_t x = row[j];
-        if (x >= lo && x < hi) dst[pos++] = x - lo;
-      }
-      pos += 1;
-    }
-    for (uint32_t k = pos + (c > pw - 1 ? 1 : 0); k < pw; ++k) out[k] = ~0u;
-  }
-}
-
-// This shard's fires of the window: global ids at ids[0, Tn), ticks at
-// ks[0, Tn); ids[Tn, seg) = ~0u (the all-gather moves whole segments).
-__global__ void k_fire_compact(const WinState w, uint32_t t0, uint32_t L, unsigned long long Tn, uint32_t* ids,
-                               uint8_t* ks, unsigned long long seg) {
-  const uint32_t units = L * w.nfine;
-  for (unsigned long long g = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; g < seg;
-       g += (unsigned long long)gridDim.x * blockDim.x) {
-    uint32_t e = ~0u, kk = 0;
-    if (g < Tn) {
-      const uint32_t u = unit_of(w, g, Tn, units);
-      const uint32_t f = u / L, k = u - f * L;
-      const uint32_t s = (t0 + k) % w.R;
-      const uint32_t i = (uint32_t)(g - w.unit_off[u]);
-      e = w.base + (f << kFineLog) + w.flist[((size_t)s * w.nfine + f) * kFineNodes + i];
-      kk = k;
-    }
-    ids[g] = e;
-    ks[g] = (uint8_t)kk;
-  }
-}
-
-// Expand of a shard (Node.Broadcast, simulator.go:141-147): one thread per
-// all-gathered firing entry; its partitioned row is read (one dependent load
-// of the mask and up to 3 inline targets; the rest inline or from the spill
-// array), RandomDrop (:144, :172) is drawn once per group of 4 ORIGINAL slots
-// that holds an owned slot (the unsharded expand's keys), and kept targets
-// leave through the coarse LDS partition of k_expand.  Fired is counted by the
-// firing node's owner only.  MAXE: most owned slots of a row (8 or 32).
-template <bool WRITE, uint32_t MAXE>
-__global__ __launch_bounds__(kExpandBlock) void k_expand_sh(const WinState w, uint32_t t0, uint32_t L,
-                                                            int add_stats) {
-  __shared__ ExpandLds<kExpandBlock * MAXE> sm;
-  const uint32_t tid = threadIdx.x;
-  if (w.abort_on_err && win_abort(w)) return;
-  if (tid < kMaxWindow * 2) (&sm.acc[0][0])[tid] = 0;
-  const uint32_t reg = tid * kCoarseSub + (blockIdx.x & (kCoarseSub - 1));  // bin tid, this XCD's sub-region
-  const unsigned long long cbase = w.ccap[reg], cend = w.ccap[reg + 1];
-  sm.cend[tid] = cend;
-  const unsigned long long total = (unsigned long long)w.G * w.gseg;
-  const unsigned long long rounds = (total + kExpandBlock - 1) / kExpandBlock;
-  unsigned long long rbeg, rend, rstep;
-  xcd_rounds(rounds, rbeg, rend, rstep);
-  uint32_t accp[kBitTicks];
-#pragma unroll
-  for (uint32_t kx = 0; kx < kBitTicks; ++kx) accp[kx] = 0;
-  for (unsigned long long rd = rbeg; rd < rend; rd += rstep) {
-    sm.cnt[tid] = 0;
-    __syncthreads();
-    uint32_t mm[MAXE], mt[MAXE];
-#pragma unroll
-    for (uint32_t j = 0; j < MAXE; ++j) { mm[j] = ~0u; mt[j] = ~0u; }
-    const unsigned long long idx = rd * kExpandBlock + tid;
-    uint32_t v = ~0u, k = 0, c = 0, own = 0, mask = 0;
-    if (idx < total) {
-      const uint32_t r = (uint32_t)(idx / w.gseg);
-      const unsigned long long i = idx - (unsigned long long)r * w.gseg;
-      const uint8_t* seg = w.gfire + (size_t)r * w.gsegb;
-      const uint32_t e = reinterpret_cast<const uint32_t*>(seg)[i];
-      if (e != ~0u) {
-        v = e;
-        k = seg[w.gseg * 4 + i];
-        own = r == w.rank;
-        const uint4* pr = reinterpret_cast<const uint4*>(w.pent + (size_t)v * w.pw);
-        const uint4 h = pr[0];  // mask + up to 3 inline targets: one dependent load
-        mask = h.x;
-        c = __popc(mask);
-        if (c <= w.pw - 1) {
-          mm[0] = h.y;
-          if (MAXE > 1) mm[1 % MAXE] = h.z;
-          if (MAXE > 2) mm[2 % MAXE] = h.w;
-#pragma unroll
-          for (uint32_t j = 3; j < MAXE; j += 4) {
-            if (j >= c) break;
-            const uint4 x = pr[(j + 1) / 4];
-            mm[j] = x.x;
-            if (j + 1 < MAXE) mm[(j + 1) % MAXE] = x.y;
-            if (j + 2 < MAXE) mm[(j + 2) % MAXE] = x.z;
-            if (j + 3 < MAXE) mm[(j + 3) % MAXE] = x.w;
-          }
-        } else {  // spilled row: its targets at spill[h.y ..]
-          const uint32_t* sp = w.pspill + h.y;
-#pragma unroll
-          for (uint32_t j = 0; j < MAXE; ++j)
-            if (j < c) mm[j] = sp[j];
-        }
-      }
-    }
-    uint32_t sent = 0;
-    if (c) {
-      const uint32_t t = t0 + k;
-      uint32_t vn, c3drop;
-      node_key(w.tlog, w.tmask, w.key, v, K_DROP, vn, c3drop);
-      const uint32_t c3crash = (c3drop & 0xFFFFFFu) | (K_CRASH << 24);
-      uint32_t keep = 0, crash = 0;  // bit j: slot j kept / its message carries a crash roll
-#pragma unroll
-      for (uint32_t g = 0; g < (kWinMaxStride + 3) / 4; ++g)
-        if ((mask >> (4 * g)) & 15u) {
-          const u32x4 r = philox(vn, t, g, c3drop, w.key.k0, w.key.k1);   // :144, :172
-          keep |= (((int32_t)uniform(r.x, 100u) >= w.kd ? 1u : 0u) |
-                   ((int32_t)uniform(r.y, 100u) >= w.kd ? 2u : 0u) |
-                   ((int32_t)uniform(r.z, 100u) >= w.kd ? 4u : 0u) |
-                   ((int32_t)uniform(r.w, 100u) >= w.kd ? 8u : 0u)) << (4 * g);
-          if (w.kc > 0) {  // :180, keyed by the sender's slots
-            const u32x4 q = philox(vn, t, g, c3crash, w.key.k0, w.key.k1);
-            crash |= (((int32_t)uniform(q.x, 100u) < w.kc ? 1u : 0u) |
-                      ((int32_t)uniform(q.y, 100u) < w.kc ? 2u : 0u) |
-                      ((int32_t)uniform(q.z, 100u) < w.kc ? 4u : 0u) |
-                      ((int32_t)uniform(q.w, 100u) < w.kc ? 8u : 0u)) << (4 * g);
-          }
-        }
-      uint32_t rest = mask;
-#pragma unroll
-      for (uint32_t i = 0; i < MAXE; ++i) {
-        if (!rest) break;
-        const uint32_t j = __builtin_ctz(rest);  // the slot of owned entry i
-        rest &= rest - 1;
-        if ((keep >> j) & 1) {                                           // kept: :145
-          const uint32_t tl = mm[i], bin = tl >> kCoarseShift;
-          const uint32_t roll0 = (crash >> j) & 1;
-          mt[i] = bin | (atomicAdd(&sm.cnt[bin], 1u) << 8);
-          mm[i] = (tl & ((1u << kCoarseShift) - 1)) | (k << kCoarseShift) | (roll0 << kRoll0Coarse);
-          ++sent;
-        }
-      }
-    }
-    if (v != ~0u) {
-#pragma unroll
-      for (uint32_t kx = 0; kx < kBitTicks; ++kx)
-        if (kx == k) accp[kx] += own | (sent << 16);
-    }
-    __syncthreads();
-    if (!WRITE) {
-      if (sm.cnt[tid]) atomicAdd(&w.chist[reg], (unsigned long long)sm.cnt[tid]);
-      continue;
-    }
-    block_scan256(sm.cnt, sm.off);
-    const uint32_t mycnt = sm.cnt[tid];
-    unsigned long long at = 0;
-    if (mycnt) at = atomicAdd(&w.cfill[reg], (unsigned long long)mycnt);
-    __syncthreads();
-#pragma unroll
-    for (uint32_t j = 0; j < MAXE; ++j)
-      if (mt[j] != ~0u) {
-        const uint32_t bin = mt[j] & 255, p = sm.off[bin] + (mt[j] >> 8);
-        sm.sorted[p] = mm[j];
-        sm.sbin[p] = (uint8_t)bin;
-      }
-    if (mycnt) {
-      if (at + mycnt > cend - cbase) atomicOr(w.err, kErrCoarse);
-      sm.gbase[tid] = cbase + at;
-    }
-    __syncthreads();
-    const uint32_t tot = sm.off[256];
-    for (uint32_t p = tid; p < tot; p += kExpandBlock) {
-      const uint32_t b = sm.sbin[p];
-      const unsigned long long pos = sm.gbase[b] + (p - sm.off[b]);
-      if (pos < sm.cend[b]) w.cmsg[pos] = sm.sorted[p];
-    }
-  }
-  if (!WRITE || !add_stats) return;
-#pragma unroll
-  for (uint32_t kx = 0; kx < kBitTicks; ++kx) {
-    if (kx >= L) continue;
-    const uint32_t fired = wave_sum32(accp[kx] & 0xFFFFu), sent = wave_sum32(accp[kx] >> 16);
-    if ((tid & 63) == 0) {
-      if (fired) atomicAdd(&sm.acc[kx][0], (unsigned long long)fired);
-      if (sent) atomicAdd(&sm.acc[kx][1], (unsigned long long)sent);
-    }
-  }
-  __syncthreads();
-  if (tid < L * 2) {
-    const uint32_t k = tid >> 1, fld = tid & 1;
-    const unsigned long long v = sm.acc[k][fld];
-    unsigned long long* row = shard_row(w, k);
-    if (v) atomicAdd(&row[fld ? ST_SENT : ST_FIRED], v);
-    if (v && fld) atomicAdd(&row[ST_MSGS], v);
-  }
+// out[poff[r] ..] = the filled prefix of region r (< nreg), one region per
+// blockIdx.x, blockIdx.y strided over it.
+__global__ void k_pack(const WinState w, const unsigned long long* poff, uint32_t nreg, uint32_t* out) {
+  const uint32_t r = blockIdx.x;
+  if (r >= nreg) return;
+  const unsigned long long f = region_fill(w, r);
+  const uint32_t* src = w.cmsg + w.ccap[r];
+  uint32_t* dst = out + poff[r];
+  for (unsigned long long i = (unsigned long long)blockIdx.y * blockDim.x + threadIdx.x; i < f;
+       i += (unsigned long long)gridDim.y * blockDim.x)
+    dst[i] = src[i];
 }
 
 // Shards: the window's fire lists are consumed (kept if the window overflowed
@@ -1840,54 +1623,15 @@ hipError_t win_schedule(const WinState& w, uint32_t node, uint32_t tick, uint32_
   return hipGetLastError();
 }
 
-hipError_t part_count(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi,
-                      uint32_t* cnt, hipStream_t s) {
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_part_count, dim3(blocks ? blocks : 1), dim3(256), 0, s, ids, n, stride, lo, hi, cnt);
-  return hipGetLastError();
-}
-
-hipError_t part_hist(const uint32_t* cnt, uint64_t n, unsigned long long* hist, hipStream_t s) {
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_part_hist, dim3(blocks ? blocks : 1), dim3(256), 0, s, cnt, n, hist);
-  return hipGetLastError();
-}
-
-hipError_t part_fill_mask(const uint32_t* ids, uint64_t n, uint32_t stride, uint32_t lo, uint32_t hi, uint32_t pw,
-                          uint32_t* pent, uint32_t* spill, unsigned long long* spill_n, hipStream_t s) {
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_part_fill_mask, dim3(blocks ? blocks : 1), dim3(256), 0, s, ids, n, stride, lo, hi, pw, pent,
-                     spill, spill_n);
-  return hipGetLastError();
-}
-
-hipError_t win_fire_compact(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, uint32_t* ids, uint8_t* ks,
-                            uint64_t seg, hipStream_t s) {
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((seg + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_fire_compact, dim3(blocks ? blocks : 1), dim3(256), 0, s, w, t0, L,
-                     (unsigned long long)Tn, ids, ks, (unsigned long long)seg);
-  return hipGetLastError();
-}
-
-// mode 0: count coarse buckets only; 1: write + per-tick stats; 2: write only
-hipError_t win_expand_sh(const WinState& w, uint32_t t0, uint32_t L, int mode, hipStream_t s) {
-  const uint64_t total = (uint64_t)w.G * w.gseg;
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((total + kExpandBlock - 1) / kExpandBlock, 8192);
-  const dim3 grid(blocks ? blocks : 1), blk(kExpandBlock);
-  const int st = mode == 1 ? 1 : 0;
-  if (w.stride <= 8) {
-    if (mode) hipLaunchKernelGGL((k_expand_sh<true, 8>), grid, blk, 0, s, w, t0, L, st);
-    else hipLaunchKernelGGL((k_expand_sh<false, 8>), grid, blk, 0, s, w, t0, L, 0);
-  } else {
-    if (mode) hipLaunchKernelGGL((k_expand_sh<true, kWinMaxStride>), grid, blk, 0, s, w, t0, L, st);
-    else hipLaunchKernelGGL((k_expand_sh<false, kWinMaxStride>), grid, blk, 0, s, w, t0, L, 0);
-  }
-  return hipGetLastError();
-}
-
 hipError_t win_consume_sh(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s) {
   const uint32_t blocks = std::min<uint32_t>((L * w.nfine + 255) / 256, 2048);
   hipLaunchKernelGGL(k_consume_sh, dim3(blocks ? blocks : 1), dim3(256), 0, s, w, t0, L);
+  return hipGetLastError();
+}
+
+hipError_t win_pack(const WinState& w, const unsigned long long* poff, uint32_t nreg, uint32_t* out, hipStream_t s) {
+  if (!nreg) return hipSuccess;
+  hipLaunchKernelGGL(k_pack, dim3(nreg, 8), dim3(256), 0, s, w, poff, nreg, out);
   return hipGetLastError();
 }
 

@@ -92,11 +92,11 @@ class Simulator:
         self.L = _lib.load()
         self._p = cfg.to_params()
         h = C.c_void_p()
-        if _rank is not None and len(_rank) == 4:  # host exchange: (nranks, rank, all_gather, all_reduce)
-            nranks, rank, ag, ar = _rank
-            self._xfns = self._exchange_fns(ag, ar)  # kept alive with the context
+        if _rank is not None and len(_rank) == 5:  # host exchange: (nranks, rank, all_gather, all_reduce, all_to_allv)
+            nranks, rank, ag, ar, av = _rank
+            self._xfns = self._exchange_fns(nranks, ag, ar, av)  # kept alive with the context
             rc = self.L.gs_create_rank_exchange(C.byref(self._p), cfg.device, nranks, rank,
-                                                C.byref(self._xfns[2]), C.byref(h))
+                                                C.byref(self._xfns[-1]), C.byref(h))
             what = "gs_create_rank_exchange"
         elif _rank is not None:
             nranks, rank, cid = _rank
@@ -128,15 +128,18 @@ class Simulator:
         return sim
 
     @classmethod
-    def rank_exchange(cls, cfg: Config, nranks: int, rank: int, all_gather, all_reduce_sum):
+    def rank_exchange(cls, cfg: Config, nranks: int, rank: int, all_gather, all_reduce_sum, all_to_allv=None):
         """Rank `rank` of `nranks` processes with the exchange done by the caller
         (gs_create_rank_exchange): all_gather(send: np.uint8 array) -> np.uint8
         array of nranks * len(send) bytes, rank-major; all_reduce_sum(x:
-        np.uint64 array) -> the element-wise sum over the ranks."""
-        return cls(cfg, _rank=(nranks, rank, all_gather, all_reduce_sum))
+        np.uint64 array) -> the element-wise sum over the ranks;
+        all_to_allv(send: np.uint8 array, send_sizes, recv_sizes) -> np.uint8
+        array of sum(recv_sizes) bytes (blocks back to back in rank order; a
+        flood run needs it)."""
+        return cls(cfg, _rank=(nranks, rank, all_gather, all_reduce_sum, all_to_allv))
 
     @staticmethod
-    def _exchange_fns(all_gather, all_reduce_sum):
+    def _exchange_fns(nranks, all_gather, all_reduce_sum, all_to_allv):
         def ag(_user, send, recv, nbytes):
             try:
                 src = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(send))
@@ -158,8 +161,26 @@ class Simulator:
                 traceback.print_exc()
                 return 1
 
+        def av(_user, send, send_bytes, recv, recv_bytes):
+            try:
+                sb = [int(send_bytes[i]) for i in range(nranks)]
+                rb = [int(recv_bytes[i]) for i in range(nranks)]
+                src = np.ctypeslib.as_array((C.c_uint8 * sum(sb)).from_address(send)) if sum(sb) else \
+                    np.zeros(0, np.uint8)
+                out = np.asarray(all_to_allv(src.copy(), sb, rb), dtype=np.uint8).ravel()
+                if out.nbytes != sum(rb):
+                    raise ValueError(f"all_to_allv returned {out.nbytes} bytes, expected {sum(rb)}")
+                if out.nbytes:
+                    C.memmove(recv, out.ctypes.data, out.nbytes)
+                return 0
+            except Exception:  # noqa: BLE001
+                import traceback
+                traceback.print_exc()
+                return 1
+
         f1, f2 = _lib.ALL_GATHER_FN(ag), _lib.ALL_REDUCE_FN(ar)
-        return f1, f2, _lib.Exchange(None, f1, f2)
+        f3 = _lib.ALL_TO_ALLV_FN(av) if all_to_allv is not None else _lib.ALL_TO_ALLV_FN()
+        return f1, f2, f3, _lib.Exchange(None, f1, f2, f3)
 
     # -- plumbing --------------------------------------------------------
     def _check(self, rc: int, what: str):

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 5
+#define GS_ABI_VERSION 6
 
 enum {
   GS_OK = 0,
@@ -158,14 +158,18 @@ int gs_create(const gs_params* params, gs_ctx** out);
  * One context over ndev devices (entries may repeat: several shards or trial
  * batches on one GPU).  params.trials > 1: the trials are split over the
  * devices and run with no communication.  Otherwise ONE broadcast whose node
- * range is split into ndev shards (config C4): every window the shards
- * all-gather their firing lists (device-to-device copies) and sum their
- * counters; results are bit-identical to gs_create's. */
+ * range is split into ndev shards (config C4): every window each shard
+ * expands its own firing nodes and hands every other shard the messages
+ * addressed to its nodes (an all-to-all: device-to-device copies), then
+ * resolves its own nodes; counters are summed.  Results are bit-identical to
+ * gs_create's. */
 int gs_create_multi(const gs_params* params, const int* devices, int ndev, gs_ctx** out);
 /* Multi-process (one process per GPU): rank 0 calls gs_comm_unique_id and
  * ships the GS_COMM_ID_BYTES bytes to every rank; each rank calls
  * gs_create_rank.  A flood run is then node-range sharded over the ranks with
- * an RCCL all-gather per window and an RCCL sum per gs_step (every rank's
+ * an RCCL all-to-all of each window's messages (grouped send/recv, after an
+ * all-gather of the fire counts and the message layout) and an RCCL sum per
+ * gs_step (every rank's
  * gs_step/gs_run/gs_totals return the global counters); a push-pull run
  * (rows <= 16 slots) is node-range sharded with an all-gather of the informed
  * set's owned words per round; params.trials > 1 gives each rank its share of
@@ -180,13 +184,18 @@ int gs_create_rank(const gs_params* params, int device, int nranks, int rank,
  * nranks and its own rank, and the callbacks move HOST bytes between the
  * ranks -- all_gather: `bytes` from every rank into recv (nranks * bytes,
  * rank-major; send is this rank's part); all_reduce_sum_u64: element-wise sum
- * over the ranks of count uint64, in place.  Both return 0 on success and are
- * called by every rank in the same order.  Unlike every other argument the
- * struct is kept: user and the callbacks must stay valid until gs_destroy. */
+ * over the ranks of count uint64, in place; all_to_allv (flood runs): rank r
+ * gets send_bytes[r] bytes of send (the blocks lie back to back in rank
+ * order) and recv receives recv_bytes[r] bytes from every rank r, back to back
+ * in rank order.  All return 0 on success and are called by every rank in the
+ * same order.  Unlike every other argument the struct is kept: user and the
+ * callbacks must stay valid until gs_destroy. */
 typedef struct gs_exchange {
   void* user;
   int (*all_gather)(void* user, const void* send, void* recv, size_t bytes);
   int (*all_reduce_sum_u64)(void* user, uint64_t* buf, size_t count);
+  int (*all_to_allv)(void* user, const void* send, const size_t* send_bytes, void* recv,
+                     const size_t* recv_bytes);
 } gs_exchange;
 int gs_create_rank_exchange(const gs_params* params, int device, int nranks, int rank, const gs_exchange* ex,
                             gs_ctx** out);

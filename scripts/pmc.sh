@@ -19,4 +19,4 @@ for grp in \
   timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$out/p$i" -o run -- python3 bench.py $args > "$out/p$i.log" 2>&1 || { echo "pass $i ($grp) failed rc=$?"; tail -5 "$out/p$i.log"; exit 1; }
   echo "pass $i ok: $grp"
 done
-python3 scripts/pmc_summary.py "$out" > "$out/summary.csv" && rm -rf "$out"/p[0-9]*/ && python3 scripts/pmc_traffic.py "$out/summary.csv" "$out/pmc_traffic.json" $i > /dev/null
+python3 scripts/pmc_summary.py "$out" > "$out/summary.csv" && rm -rf "$out"/p[0-9]*/ && python3 scripts/pmc_traffic.py "$out/summary.csv" "$out/pmc_traffic.json" $i ${PMC_WINDOWS:-28} > /dev/null  # 28: the C5 broadcast's windows (gs_timing.windows)

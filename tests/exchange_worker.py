@@ -34,12 +34,18 @@ def main():
         dist.all_reduce(t)
         return t.numpy().view(np.uint64)
 
+    def all_to_allv(send: np.ndarray, send_sizes, recv_sizes) -> np.ndarray:
+        out = torch.empty(sum(recv_sizes), dtype=torch.uint8)
+        dist.all_to_all_single(out, torch.from_numpy(send), output_split_sizes=list(recv_sizes),
+                               input_split_sizes=list(send_sizes))
+        return out.numpy()
+
     z = np.load(os.path.join(d, "table.npz"))
     kw = {k: (z[k].item()) for k in ("n", "fanout", "fanin", "crashrate", "droprate")}
     cfg = gs.Config(n=int(kw["n"]), fanout=int(kw["fanout"]), fanin=int(kw["fanin"]),
                     crashrate=float(kw["crashrate"]), droprate=float(kw["droprate"]), seed=0x5EED,
                     model=model, device=0)
-    sim = gs.Simulator.rank_exchange(cfg, world, rank, all_gather, all_reduce)
+    sim = gs.Simulator.rank_exchange(cfg, world, rank, all_gather, all_reduce, all_to_allv)
     try:
         sim.load_peers(z["deg"], z["ids"])
         if "failed" in z:

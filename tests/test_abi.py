@@ -31,7 +31,7 @@ def test_exports_every_declared_symbol(L):
     for s in syms:
         assert hasattr(lib, s), f"{s} declared in include/gossip.h but not exported"
     assert sorted(L.EXPORTS) == syms
-    assert lib.gs_version() == 5
+    assert lib.gs_version() == 6
 
 
 def test_header_constants_match_binding(L):

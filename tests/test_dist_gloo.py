@@ -4,11 +4,15 @@
   oracle behind the batch interface the HIP engine exposes -- must reproduce
   the serial trials.
 * Node-range sharding: the library's window protocol (gs_api.cpp
-  shard_windows: per-window all-gather of the firing sets, per-poll sum of
-  the counters) restated over oracle shards and gloo collectives -- must be
-  bit-identical to the unsharded run.  The HIP path of the same protocol is
-  checked on the GPU (tests/test_gpu_multi.py, and with two processes in
-  tests/test_rank_exchange.py).
+  shard_windows: the same window cut on every shard from the gathered fire
+  counts, every message of the window delivered to the shard that owns its
+  target, per-poll sum of the counters) restated over oracle shards and gloo
+  collectives -- must be bit-identical to the unsharded run.  The HIP path
+  moves the messages themselves (owner expand + all-to-all); the restatement
+  all-gathers the firing sets and lets each shard deliver to its own nodes,
+  which is the same multiset of messages per shard.  The HIP path is checked
+  on the GPU (tests/test_gpu_multi.py, and with two processes exchanging
+  through gloo in tests/test_rank_exchange.py).
 * Push-pull node-range sharding (config C5): the sharded round of
   gs_api.cpp pp_shard_step (bottom-up on the shard's own nodes against the
   replicated informed set, then an all-gather of the owned words) restated in

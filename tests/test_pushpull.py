@@ -248,18 +248,23 @@ def test_gpu_pushpull_run_polls_like_oracle(oracle, fail_frac, rounds):
 
 # ---- node-range shards (SURVEY.md 8(e)2 for config C5) ------------------------
 @pytest.mark.gpu
+@pytest.mark.parametrize("replica", [True, False])
 @pytest.mark.parametrize("kw,stride,dlo,dhi,fail_frac,G", [
     (dict(PP, n=20000), 6, 5, 6, 0.01, 2),                                  # C5 shape, 1 % failed
     (dict(PP, n=65536 + 77, drop_rate=0.29, trial=5), 16, 1, 16, 0.0, 3),   # widest packed rows, 77-node shard
     (dict(PP, n=50000, drop_rate=0.05), 8, 0, 8, 0.02, 2),                  # zero degrees, 8-slot fmask
 ])
-def test_gpu_pushpull_shards_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac, G):
+def test_gpu_pushpull_shards_bit_exact(oracle, monkeypatch, kw, stride, dlo, dhi, fail_frac, G, replica):
     """G node-range shards of one push-pull run on one GPU (gs_create_multi):
-    every round is bottom-up on each shard's own nodes against the replicated
-    informed set, exchanged after the round; per round bit-exact to the
-    oracle's pushpull_step (oracle/gsoracle.c), as the unsharded engine is."""
+    the sparse early rounds on the device's replica (the full table, the
+    replicated sets; replica=False: GS_PP_NO_REPLICA=1, none), then every
+    round bottom-up on each shard's own nodes against the replicated informed
+    set, exchanged after the round; per round bit-exact to the oracle's
+    pushpull_step (oracle/gsoracle.c), as the unsharded engine is."""
     import gossip_simulator_amd as gs
     gs.load()
+    if not replica:
+        monkeypatch.setenv("GS_PP_NO_REPLICA", "1")
     n = kw["n"]
     deg, ids = random_table(n, stride, dlo, dhi, seed=n)
     e = oracle.Engine(oracle.make_params(**kw), deg, ids)
@@ -282,7 +287,9 @@ def test_gpu_pushpull_shards_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac, 
             assert sha(e.received()) == sha(sim.received()), f"informed set differs at round {r + 1}"
             if oracle.covered(int(a[0, 4]), n) or int(a[0, 4]) == 0:
                 break
-        assert sim.timing()["pp_bottom_rounds"] == r + 1
+        tm = sim.timing()
+        assert tm["pp_bottom_rounds"] + tm["pp_early_rounds"] == r + 1
+        assert (tm["pp_early_rounds"] >= 1) == replica
 
 
 @pytest.fixture(scope="module")
