@@ -539,9 +539,13 @@ def shards_inproc(a, gs):
                         tm = sim.shard_timing(i)
                         per.append(round(tm["expand_ms"] + tm["part_ms"] + tm["resolve_ms"], 3))
                     sim.set_flags(False)
+                    t0 = sim.shard_timing(0)
                     key = f"{name}_G{G}"
                     out[key] = {"n": n, "shard_ms": per, "max_ms": max(per), "sum_ms": round(sum(per), 3),
-                                "delivered": tot["sent"], "windows": int(sim.shard_timing(0)["windows"])}
+                                "delivered": tot["sent"], "windows": int(t0["windows"]),
+                                "shard0_phases_ms": {"expand": round(t0["expand_ms"], 3),
+                                                     "pack+plan+part2": round(t0["part_ms"], 3),
+                                                     "resolve": round(t0["resolve_ms"], 3)}}
                     log(f"in-process shards {key}: per-shard device ms {per}")
     finally:
         os.environ.pop("GS_SHARD_SERIAL", None)
@@ -549,16 +553,20 @@ def shards_inproc(a, gs):
 
 
 def pmc_traffic():
-    """HBM bytes per window launch (k_expand + k_part2 + k_resolve) from the
-    committed PMC pass (scripts/pmc.sh + scripts/pmc_traffic.py, FETCH_SIZE
-    doubled per MI355X_MICROARCH.md); counters cannot be read from inside the
-    timed process, so this is the profile of the same workload, not this run."""
+    """HBM bytes per window launch (k_expand + k_part2 + k_resolve*) from the
+    committed PMC passes (scripts/pmc.sh + scripts/pmc_traffic.py): reads =
+    the L2's memory read requests by size (every one was 128 B on gfx950,
+    calibrated on known byte counts: profiles/r03_fetch_calibration.json),
+    writes = WRITE_SIZE (exact in the same calibration); counters cannot be
+    read from inside the timed process, so this is the profile of the same
+    workload at this commit's kernels, not this run."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None, "no PMC profile committed"
     d = json.load(open(path))
-    return int(d["bytes_per_launch"]), (f"{os.path.relpath(path, ROOT)}: FETCH_SIZE*2 + WRITE_SIZE "
-                                        f"over {d['launches']} window launches of one broadcast")
+    return int(d["bytes_per_launch"]), (f"{os.path.relpath(path, ROOT)} (from {d['source']}): calibrated "
+                                        f"read requests + WRITE_SIZE over {d['launches']} window launches "
+                                        f"of one broadcast")
 
 
 def cpu_model():

@@ -187,6 +187,10 @@ bool grow(Buf& b, size_t bytes) {
     if (rc_) return rc_;      \
   } while (0)
 
+// A shard's receive layout (gs_ctx::d_rtab): region starts, ends, fills, its
+// own pack offsets ([kRegions + 1] each), then the source buffers (<= 257).
+constexpr size_t kRtabWords = 4 * (kRegions + 1) + 260;
+
 // Window-engine buffers.  Sizes at n = 1e9, R = 20: flist 40 GB (two bytes
 // per node per ring slot), fcount 4.9 MB; message buffers grow on demand.
 int alloc_window(gs_ctx* c) {
@@ -210,13 +214,14 @@ int alloc_window(gs_ctx* c) {
   w.seg_per = (uint32_t)c->seg_per;
   w.csub = kCoarseSub;
   w.ccap_end = nullptr;
+  w.csrc = nullptr;
   if (c->shard) {  // owner expand (k_expand's coarse_bin)
     w.owner = 1;
     w.obins = 256 / c->G;
     w.oseg_q = (uint32_t)(c->seg_per >> kFineLog);
     w.oseg_magic = 0xFFFFFFFFu / w.oseg_q;
-    if (hipMalloc(&c->d_rtab, 4 * (kRegions + 1) * 8) != hipSuccess ||
-        hipHostMalloc((void**)&c->h_rtab, 4 * (kRegions + 1) * 8) != hipSuccess)
+    if (hipMalloc(&c->d_rtab, kRtabWords * 8) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_rtab, kRtabWords * 8) != hipSuccess)
       return fail(c, GS_ENOMEM, "cannot allocate the shard's receive layout");
   }
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -1308,10 +1313,15 @@ int overlay_into(gs_ctx* c, uint64_t max_ticks, gs_window* win, size_t cap, size
   // a row never straddles two 128-B lines and k_expand gathers it with one
   // uint4 + one uint2 load instead of three uint2 loads (C5: 67.3 -> 66.3 ms
   // per broadcast).  gs_read_peers returns the unpadded rows.
+  // Rows of 9..31 slots (C4: fanin 19) are padded to a multiple of 4: 16-B
+  // aligned rows gathered with uint4 loads.
   c->row_slots = 0;
   if (c->win && stride > 4 && stride < 8) {
     c->row_slots = stride;
     stride = 8;
+  } else if (c->win && stride > 8 && (stride & 3)) {
+    c->row_slots = stride;
+    stride = (stride + 3) & ~3u;
   }
   RC(alloc_table(c, stride));
   const uint64_t n = table_n(c);
@@ -2314,38 +2324,50 @@ int sender_redo(gs_ctx* m, uint32_t t, uint32_t L, uint64_t Tn) {
   return GS_OK;
 }
 
-// Step 4: packs every shard's blocks, moves them to their owners and sets
-// each shard's receive layout (m->wr, m->rtotal).  poff[s][r] = offset of
-// region r's fill in shard s's packed output; destination d's block is
-// regions [d * obins * 8, (d + 1) * obins * 8).
+// Step 4: moves every block to its owner and sets each shard's receive
+// layout (m->wr, m->rtotal).  A block that stays on its device (in-process
+// shards of one device; a rank's block to itself) is read in place from its
+// sender's message buffer; the others are packed (filled prefixes back to
+// back) and sent: peer copies between devices, RCCL grouped send / receive
+// or the caller's all_to_allv between ranks.  Destination d's block of a
+// sender is its regions [d * obins * 8, (d + 1) * obins * 8).
 int shard_exchange(gs_ctx* acc, const std::vector<gs_ctx*>& ms, const std::vector<unsigned long long>& lay,
                    bool timing) {
   gs_ctx* m0 = ms[0];
   const uint32_t G = m0->G, B8 = m0->ws.obins * kCoarseSub, nreg = G * B8;
   const size_t K1 = kRegions + 1;
-  std::vector<unsigned long long> poff((size_t)G * K1);
+  const bool rank = is_rank(m0);
+  // a group's members are its shards in rank order
+  auto travels = [&](uint32_t s, uint32_t d) { return rank ? s != d : acc->gdev_of[s] != acc->gdev_of[d]; };
+  // poff[s][r]: offset of region r in sender s's packed output (~0: stays in place);
+  // blk[s][d]: messages of sender s for destination d
+  std::vector<unsigned long long> poff((size_t)G * K1, ~0ull), blk((size_t)G * G, 0), ptot(G, 0);
   for (uint32_t s = 0; s < G; ++s) {
     unsigned long long a = 0;
-    for (uint32_t r = 0; r < kRegions; ++r) {
+    for (uint32_t r = 0; r < nreg; ++r) {
+      const uint32_t d = r / B8;
+      const unsigned long long f = lay[(size_t)s * K1 + r];
+      blk[(size_t)s * G + d] += f;
+      if (!travels(s, d)) continue;
       poff[(size_t)s * K1 + r] = a;
-      a += lay[(size_t)s * K1 + r];
+      a += f;
     }
-    poff[(size_t)s * K1 + kRegions] = a;
+    ptot[s] = a;
   }
   auto bstart = [&](uint32_t s, uint32_t d) { return poff[(size_t)s * K1 + (size_t)d * B8]; };
-  auto bsize = [&](uint32_t s, uint32_t d) { return poff[(size_t)s * K1 + (size_t)(d + 1) * B8] - bstart(s, d); };
-  const bool rank = is_rank(m0);
-  // base[m][s]: where sender s's block for member m starts in m's receive buffer
-  std::vector<std::vector<unsigned long long>> base(ms.size(), std::vector<unsigned long long>(G, 0));
-  std::vector<uint32_t*> rbuf(ms.size(), nullptr), pout(ms.size(), nullptr);
+  auto bsize = [&](uint32_t s, uint32_t d) { return blk[(size_t)s * G + d]; };
+  // where each receiver finds the blocks that travel to it: in[i][s]; pack destinations pout[i]
+  std::vector<std::vector<unsigned long long>> in(ms.size(), std::vector<unsigned long long>(G, 0));
+  std::vector<uint32_t*> inbuf(ms.size(), nullptr), pout(ms.size(), nullptr);
   if (rank) {
     gs_ctx* m = m0;
     const uint32_t me = m->rank;
     unsigned long long rsum = 0;
-    for (uint32_t s = 0; s < G; ++s) { base[0][s] = rsum; rsum += bsize(s, me); }
-    if (!grow(m->xsend, (poff[(size_t)me * K1 + kRegions] + 16) * 4) || !grow(m->xrecv, (rsum + 16) * 4))
+    for (uint32_t s = 0; s < G; ++s)
+      if (s != me) { in[0][s] = rsum; rsum += bsize(s, me); }
+    if (!grow(m->xsend, (ptot[me] + 16) * 4) || !grow(m->xrecv, (rsum + 16) * 4))
       return fail(m, GS_ENOMEM, "cannot allocate the exchange buffers");
-    rbuf[0] = (uint32_t*)m->xrecv.p;
+    inbuf[0] = (uint32_t*)m->xrecv.p;
     pout[0] = (uint32_t*)m->xsend.p;
   } else {
     // device D's buffer: its members' packed outputs, then the blocks its
@@ -2354,31 +2376,26 @@ int shard_exchange(gs_ctx* acc, const std::vector<gs_ctx*>& ms, const std::vecto
     for (size_t i = 0; i < ms.size(); ++i) {
       const int D = acc->gdev_of[i];
       O[i] = dtot[D];
-      dtot[D] += poff[(size_t)ms[i]->rank * K1 + kRegions];
+      dtot[D] += ptot[i];
     }
-    for (size_t i = 0; i < ms.size(); ++i) {
-      const int D = acc->gdev_of[i];
-      const uint32_t d = ms[i]->rank;
-      for (size_t j = 0; j < ms.size(); ++j) {
-        const uint32_t s = ms[j]->rank;
-        if (acc->gdev_of[j] == D) {
-          base[i][s] = O[j] + bstart(s, d);
-        } else {
-          base[i][s] = dtot[D];
-          dtot[D] += bsize(s, d);
+    for (size_t i = 0; i < ms.size(); ++i)
+      for (uint32_t s = 0; s < G; ++s)
+        if (travels(s, (uint32_t)i)) {
+          const int D = acc->gdev_of[i];
+          in[i][s] = dtot[D];
+          dtot[D] += bsize(s, (uint32_t)i);
         }
-      }
-    }
     for (size_t D = 0; D < acc->gdevs.size(); ++D) {
+      if (!dtot[D]) continue;
       CK(acc, hipSetDevice(acc->gdevs[D]));
       if (!grow(acc->gbuf[D], (dtot[D] + 16) * 4)) return fail(acc, GS_ENOMEM, "cannot allocate the exchange buffers");
     }
     for (size_t i = 0; i < ms.size(); ++i) {
-      rbuf[i] = (uint32_t*)acc->gbuf[acc->gdev_of[i]].p;
-      pout[i] = rbuf[i] + O[i];
+      inbuf[i] = (uint32_t*)acc->gbuf[acc->gdev_of[i]].p;
+      pout[i] = inbuf[i] ? inbuf[i] + O[i] : nullptr;
     }
   }
-  // receive layouts (region = bin * (G * 8) + sender * 8 + sub) and pack offsets
+  // receive layouts (region = bin * (G * 8) + sender * 8 + sub), pack offsets, sources
   for (size_t i = 0; i < ms.size(); ++i) {
     gs_ctx* m = ms[i];
     const uint32_t d = m->rank;
@@ -2386,15 +2403,30 @@ int shard_exchange(gs_ctx* acc, const std::vector<gs_ctx*>& ms, const std::vecto
     unsigned long long* rend = rcap + K1;
     unsigned long long* rfill = rend + K1;
     unsigned long long* mypoff = rfill + K1;
-    std::fill(m->h_rtab, m->h_rtab + 4 * K1, 0ull);
+    const uint32_t** src = (const uint32_t**)(mypoff + K1);
+    std::fill(m->h_rtab, m->h_rtab + kRtabWords, 0ull);
+    // sources: rank: 0 = received blocks, 1 = own buffer; group: s = member s's buffer, G = received blocks
+    const uint32_t in_src = rank ? 0u : G;
+    if (rank) {
+      src[0] = inbuf[i];
+      src[1] = m->ws.cmsg;
+    } else {
+      for (uint32_t s = 0; s < G; ++s) src[s] = travels(s, d) ? nullptr : ms[s]->ws.cmsg;
+      src[G] = inbuf[i];
+    }
     unsigned long long tot = 0;
     for (uint32_t c = 0; c < m->ws.obins; ++c)
       for (uint32_t s = 0; s < G; ++s)
         for (uint32_t x = 0; x < kCoarseSub; ++x) {
           const size_t rr = ((size_t)c * G + s) * kCoarseSub + x, sr = (size_t)d * B8 + c * kCoarseSub + x;
           const unsigned long long f = lay[(size_t)s * K1 + sr];
-          rcap[rr] = base[i][s] + poff[(size_t)s * K1 + sr] - bstart(s, d);
-          rend[rr] = rcap[rr] + f;
+          unsigned long long at;
+          if (!travels(s, d))  // in place: the sender's own region start
+            at = ((unsigned long long)(rank ? 1u : s) << kSrcShift) | (rank ? m : ms[s])->h_cap[sr];
+          else
+            at = ((unsigned long long)in_src << kSrcShift) | (in[i][s] + poff[(size_t)s * K1 + sr] - bstart(s, d));
+          rcap[rr] = at;
+          rend[rr] = at + f;
           rfill[rr] = f;
           tot += f;
         }
@@ -2402,15 +2434,16 @@ int shard_exchange(gs_ctx* acc, const std::vector<gs_ctx*>& ms, const std::vecto
     m->rtotal = tot;
     WinState& wr = m->wr;
     wr = m->ws;
-    wr.cmsg = rbuf[i];
+    wr.cmsg = nullptr;
+    wr.csrc = (const uint32_t* const*)(m->d_rtab + 4 * K1);
     wr.ccap = m->d_rtab;
     wr.ccap_end = m->d_rtab + K1;
     wr.cfill = m->d_rtab + 2 * K1;
     wr.csub = G * kCoarseSub;
     CK(m, hipSetDevice(m->dev));
-    CK(m, hipMemcpyAsync(m->d_rtab, m->h_rtab, 4 * K1 * 8, hipMemcpyHostToDevice, m->stream));
+    CK(m, hipMemcpyAsync(m->d_rtab, m->h_rtab, kRtabWords * 8, hipMemcpyHostToDevice, m->stream));
     if (timing) CK(m, hipEventRecord(m->ev[2], m->stream));
-    CK(m, win_pack(m->ws, m->d_rtab + 3 * K1, nreg, pout[i], m->stream));
+    if (ptot[d]) CK(m, win_pack(m->ws, m->d_rtab + 3 * K1, nreg, pout[i], m->stream));
     if (timing) CK(m, hipEventRecord(m->ev[3], m->stream));
     if (!rank) CK(m, hipEventRecord(acc->gev_c[i], m->stream));
     if (shard_serial() && !rank) CK(m, hipStreamSynchronize(m->stream));
@@ -2422,46 +2455,44 @@ int shard_exchange(gs_ctx* acc, const std::vector<gs_ctx*>& ms, const std::vecto
       const Rccl& r = rccl();
       NCK(m, r.group_start());
       for (uint32_t p = 0; p < G; ++p) {
+        if (p == me) continue;
         if (bsize(me, p))
           NCK(m, r.send(pout[0] + bstart(me, p), bsize(me, p), ncclUint32, (int)p, m->comm, m->stream));
         if (bsize(p, me))
-          NCK(m, r.recv(rbuf[0] + base[0][p], bsize(p, me), ncclUint32, (int)p, m->comm, m->stream));
+          NCK(m, r.recv(inbuf[0] + in[0][p], bsize(p, me), ncclUint32, (int)p, m->comm, m->stream));
       }
       NCK(m, r.group_end());
     } else {
-      const unsigned long long ssum = poff[(size_t)me * K1 + kRegions];
       unsigned long long rsum = 0;
-      std::vector<size_t> sb(G), rb(G);
-      for (uint32_t p = 0; p < G; ++p) {
-        sb[p] = bsize(me, p) * 4;
-        rb[p] = bsize(p, me) * 4;
-        rsum += bsize(p, me);
-      }
-      if (!grow_pinned(m, (ssum + rsum) * 4 + 16)) return fail(m, GS_ENOMEM, "cannot allocate exchange staging");
+      std::vector<size_t> sb(G, 0), rb(G, 0);
+      for (uint32_t p = 0; p < G; ++p)
+        if (p != me) {
+          sb[p] = bsize(me, p) * 4;
+          rb[p] = bsize(p, me) * 4;
+          rsum += bsize(p, me);
+        }
+      if (!grow_pinned(m, (ptot[me] + rsum) * 4 + 16)) return fail(m, GS_ENOMEM, "cannot allocate exchange staging");
       char* hs = m->h_xbuf;
-      char* hr = m->h_xbuf + ssum * 4;
-      CK(m, hipMemcpyAsync(hs, pout[0], ssum * 4, hipMemcpyDeviceToHost, m->stream));
+      char* hr = m->h_xbuf + ptot[me] * 4;
+      CK(m, hipMemcpyAsync(hs, pout[0], ptot[me] * 4, hipMemcpyDeviceToHost, m->stream));
       CK(m, hipStreamSynchronize(m->stream));
       if (m->hx.all_to_allv(m->hx.user, hs, sb.data(), hr, rb.data()))
         return fail(m, GS_EDEVICE, "the exchange's all_to_allv callback failed");
-      CK(m, hipMemcpyAsync(rbuf[0], hr, rsum * 4, hipMemcpyHostToDevice, m->stream));
+      CK(m, hipMemcpyAsync(inbuf[0], hr, rsum * 4, hipMemcpyHostToDevice, m->stream));
       CK(m, hipStreamSynchronize(m->stream));
     }
     return GS_OK;
   }
-  // group: every member waits for the packs it reads; blocks from other devices are copied in
+  // group: blocks from other devices are copied in once their senders packed
+  // them (blocks on the same device were complete at the layout sync)
   for (size_t i = 0; i < ms.size(); ++i) {
     gs_ctx* m = ms[i];
-    const int D = acc->gdev_of[i];
     CK(m, hipSetDevice(m->dev));
-    for (size_t j = 0; j < ms.size(); ++j) {
-      if (j == i) continue;
-      CK(m, hipStreamWaitEvent(m->stream, acc->gev_c[j], 0));
-      const int Dj = acc->gdev_of[j];
-      const uint32_t s = ms[j]->rank;
-      if (Dj != D && bsize(s, m->rank))
-        CK(m, hipMemcpyPeerAsync(rbuf[i] + base[i][s], m->dev, pout[j] + bstart(s, m->rank), ms[j]->dev,
-                                 bsize(s, m->rank) * 4, m->stream));
+    for (uint32_t s = 0; s < G; ++s) {
+      if (!travels(s, (uint32_t)i) || !bsize(s, (uint32_t)i)) continue;
+      CK(m, hipStreamWaitEvent(m->stream, acc->gev_c[s], 0));
+      CK(m, hipMemcpyPeerAsync(inbuf[i] + in[i][s], m->dev, pout[s] + bstart(s, (uint32_t)i), ms[s]->dev,
+                               bsize(s, (uint32_t)i) * 4, m->stream));
     }
   }
   return GS_OK;

@@ -99,6 +99,8 @@ constexpr uint32_t kRegions = 256 * kCoarseSub;
 constexpr uint32_t kWinMaxRing = 256;
 constexpr uint32_t kWinMaxStride = 32;          // friends-row length the window engine takes
 constexpr uint32_t kEmptyMsg = 0xFFFFFFFFu;
+constexpr uint32_t kSrcShift = 56;                        // receive layout: source index of a region
+constexpr unsigned long long kSrcMask = (1ull << kSrcShift) - 1;
 #ifndef GS_PART_TILE
 #define GS_PART_TILE 16384
 #endif
@@ -159,6 +161,11 @@ struct WinState {
   // Regions per coarse bin: kCoarseSub, or G * kCoarseSub in a shard's receive
   // layout (region = bin * csub + sender * kCoarseSub + sub)
   uint32_t csub;
+  // receive layout: region starts / ends carry a source in bits 56..63, the
+  // buffer csrc[source] their offsets index (a sender's own message buffer,
+  // read in place, or the blocks received from other devices / ranks);
+  // null: every region indexes cmsg
+  const uint32_t* const* csrc;
   // node-range shard (owner expand): k_expand bins a kept message by its
   // target's owner d and the 2^22-node chunk of d's range, bin = d * obins +
   // chunk, message = target - d's first node within the chunk
@@ -218,7 +225,8 @@ hipError_t win_stats_reduce(const WinState& w, uint32_t t0, uint32_t L, hipStrea
 // node-range shards
 hipError_t win_consume_sh(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
 // Copies the first min(cfill[r], room) messages of every region r < nreg from
-// w.cmsg to out + poff[r] (the all-to-all's send blocks, back to back).
+// w.cmsg to out + poff[r] (the all-to-all's send blocks, back to back);
+// regions with poff[r] = ~0 stay where they are.
 hipError_t win_pack(const WinState& w, const unsigned long long* poff, uint32_t nreg, uint32_t* out, hipStream_t s);
 // Schedule local node `node` (batched: in every trial; ~0u: each trial's keyed sender) at `tick`.
 hipError_t win_schedule(const WinState& w, uint32_t node, uint32_t tick, uint32_t trials, uint32_t n,

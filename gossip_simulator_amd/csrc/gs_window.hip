@@ -374,6 +374,16 @@ __device__ __forceinline__ void load_row(const WinState& w, uint32_t v, uint32_t
       const uint4 b = reinterpret_cast<const uint4*>(w.ids + (size_t)v * S)[1];
       mm[4 % MAXS] = b.x; mm[5 % MAXS] = b.y; mm[6 % MAXS] = b.z; mm[7 % MAXS] = b.w;
     }
+  } else if ((S & 3) == 0 && MAXS > 8) {  // 16-B aligned longer rows: uint4 loads
+    const uint4* row = reinterpret_cast<const uint4*>(w.ids + (size_t)v * S);
+#pragma unroll
+    for (uint32_t j = 0; j < MAXS; j += 4) {
+      const uint4 x = j < S ? row[j / 4] : make_uint4(kEmptyMsg, kEmptyMsg, kEmptyMsg, kEmptyMsg);
+      mm[j] = x.x;
+      if (j + 1 < MAXS) mm[j + 1] = x.y;
+      if (j + 2 < MAXS) mm[j + 2] = x.z;
+      if (j + 3 < MAXS) mm[j + 3] = x.w;
+    }
   } else if ((S & 1) == 0) {
     const uint2* row = reinterpret_cast<const uint2*>(w.ids + (size_t)v * S);
 #pragma unroll
@@ -699,7 +709,12 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8
       if (s_tp[mid] <= g) lo = mid; else hi = mid - 1;
     }
     const uint32_t r = lo, c = r / w.csub;
-    const unsigned long long cb = w.ccap[r];
+    unsigned long long cb = w.ccap[r];
+    const uint32_t* msrc = w.cmsg;  // the region's messages (a receive layout names their buffer)
+    if (w.csrc) {
+      msrc = w.csrc[cb >> kSrcShift];
+      cb &= kSrcMask;
+    }
     const unsigned long long ce = cb + region_fill(w, r);
     const unsigned long long base = cb + (unsigned long long)(g - s_tp[r]) * kPartTile;
     if (tid < 256) ts.cnt[tid] = 0;
@@ -711,7 +726,7 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8
     for (uint32_t r = 0; r < kPer; ++r) {
       const unsigned long long x = base + r * kPartBlock + tid;
       // branch-free load (index clamped into the tile's region: base < ce)
-      const uint32_t m1 = w.cmsg[x < ce ? x : ce - 1];
+      const uint32_t m1 = msrc[x < ce ? x : ce - 1];
       m[r] = x < ce ? m1 : kEmptyMsg;
     }
 #pragma unroll
@@ -1450,17 +1465,18 @@ __global__ void k_schedule_win(const WinState w, uint32_t node, uint32_t t, uint
 // owner mode: a kept message is binned by the shard that owns its target
 // (bin = owner * obins + 2^22-node chunk of the owner's range), so the
 // coarse regions of owner d are one contiguous block of the message buffer.
-// k_pack moves each block's filled prefixes back to back; the blocks go to
-// their owners (all-to-all); each shard then partitions (k_plan / k_part2
-// over the receive layout: G senders x 8 sub-regions per bin) and resolves
-// its own buckets with the kernels above.  Keys are global ids, so the union
+// k_pack moves the filled prefixes of each block that leaves the device or
+// rank back to back; the blocks go to their owners (all-to-all); each shard
+// then partitions (k_plan / k_part2 over the receive layout: G senders x 8
+// sub-regions per bin, each region in its sender's buffer read in place or in
+// the received blocks) and resolves its own buckets with the kernels above.  Keys are global ids, so the union
 // over shards equals the unsharded run bit for bit.
 
 // out[poff[r] ..] = the filled prefix of region r (< nreg), one region per
 // blockIdx.x, blockIdx.y strided over it.
 __global__ void k_pack(const WinState w, const unsigned long long* poff, uint32_t nreg, uint32_t* out) {
   const uint32_t r = blockIdx.x;
-  if (r >= nreg) return;
+  if (r >= nreg || poff[r] == ~0ull) return;
   const unsigned long long f = region_fill(w, r);
   const uint32_t* src = w.cmsg + w.ccap[r];
   uint32_t* dst = out + poff[r];
@@ -1556,6 +1572,9 @@ hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, i
   } else if (rs <= 8) {
     if (mode) hipLaunchKernelGGL((k_expand<true, 8, kExpandNpt>), grid, blk, 0, s, w, t0, L, tn, st);
     else hipLaunchKernelGGL((k_expand<false, 8, kExpandNpt>), grid, blk, 0, s, w, t0, L, tn, 0);
+  } else if (rs <= 20) {  // C4's 19-slot rows: a 25-KB LDS stage, six workgroups per CU
+    if (mode) hipLaunchKernelGGL((k_expand<true, 20, 1>), grid, blk, 0, s, w, t0, L, tn, st);
+    else hipLaunchKernelGGL((k_expand<false, 20, 1>), grid, blk, 0, s, w, t0, L, tn, 0);
   } else {
     if (mode) hipLaunchKernelGGL((k_expand<true, kWinMaxStride, 1>), grid, blk, 0, s, w, t0, L, tn, st);
     else hipLaunchKernelGGL((k_expand<false, kWinMaxStride, 1>), grid, blk, 0, s, w, t0, L, tn, 0);
