@@ -12,6 +12,9 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 import gossip_simulator_amd as gs  # noqa: E402
 
+import torch  # noqa: E402
+
+torch.cuda.synchronize()  # the HIP runtime is up before the library's first call
 G = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 a = argparse.Namespace(n=1_000_000_000, fanout=5, fanin=6, delaylow=10, delayhigh=20, droprate=0.1,
                        seed=0x5EED, steps=8, pp_shards=G)
