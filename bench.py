@@ -190,6 +190,9 @@ def main():
             ext["c3_trials"] = guarded("c3_trials", lambda: c3_trials(a, gs, rank, world, local, dist))
         if not a.no_c4:
             ext["c4_sharded"] = guarded("c4_sharded", lambda: c4_sharded(a, gs, rank, world, local, dist))
+        if world > 1:
+            ext["c5_flood_sharded"] = guarded("c5_flood_sharded",
+                                              lambda: c5_flood_sharded(a, gs, rank, world, local, dist))
         ext["c5_pushpull_sharded"] = guarded("c5_pushpull_sharded",
                                              lambda: pushpull_sharded(a, gs, rank, world, local, dist))
         if world == 1 and a.shard_scaling:
@@ -388,16 +391,16 @@ def c3_trials(a, gs, rank, world, local, dist):
             "note": "measured: every trial's overlay + broadcast to its stopping poll, whole job"}
 
 
-def c4_sharded(a, gs, rank, world, local, dist):
-    """Config C4: N = 1e8, fanout 18 (floor(ln 1e8)), fanin 19, reference
-    defaults otherwise; ONE broadcast with the node range sharded over the
-    ranks (gs_create_rank: each rank expands its own fires and the messages
-    move to their targets' owners by an RCCL all-to-all per window; per-step
-    RCCL sum of the counters) -- one shard through the same window driver at
-    --gpus 1.  value = delivered sends / wall time of the broadcast."""
+def flood_sharded(a, gs, rank, world, local, dist, n, fanout, fanin, crashrate, name):
+    """ONE flood broadcast whose node range is sharded over the ranks
+    (gs_create_rank: each rank expands its own fires and the messages move to
+    their targets' owners by an RCCL all-to-all per window; per-step RCCL sum
+    of the counters) -- one shard through the same window driver at --gpus 1.
+    value = delivered sends / wall time of the broadcast (max over ranks)."""
     import torch
     from gossip_simulator_amd import dist as gd
-    cfg = gs.Config(n=100_000_000, fanout=18, fanin=19, seed=a.seed, device=local)
+    cfg = gs.Config(n=n, fanout=fanout, fanin=fanin, delaylow=a.delaylow, delayhigh=a.delayhigh,
+                    droprate=a.droprate, crashrate=crashrate, seed=a.seed, device=local)
     sim = gd.open_shard(cfg, rank, world) if world > 1 else gs.Simulator(cfg, devices=[local])
     try:
         t0 = time.perf_counter()
@@ -433,14 +436,16 @@ def c4_sharded(a, gs, rank, world, local, dist):
         launches = max(int(tm["resolve_launches"]), 1)
         shard_sent = tot["sent"] / world  # a shard's share of the deliveries (balanced ranges)
         ach = BYTES_PER_SEND * shard_sent / (kern * 1e-3) / 1e9 if kern > 0 else 0.0
-        log(f"C4 sharded x{world}: {dt * 1e3 / steps:.1f} ms per broadcast, {tot['sent'] / (dt / steps):.3e} msgs/s")
+        log(f"{name} sharded x{world}: {dt * 1e3 / steps:.1f} ms per broadcast, {tot['sent'] / (dt / steps):.3e} msgs/s")
         return {"value": round(tot["sent"] * steps / dt, 1), "unit": "msgs/s", "shards": world,
-                "ms_per_step": round(dt * 1e3 / steps, 3), "steps": steps, "n": cfg.n, "fanout": 18, "fanin": 19,
-                "ticks": tot["tick"], "status": STATUS[status], "coverage": round(tot["received"] / cfg.n, 6),
+                "ms_per_step": round(dt * 1e3 / steps, 3), "steps": steps, "n": cfg.n, "fanout": fanout,
+                "fanin": fanin, "ticks": tot["tick"], "status": STATUS[status],
+                "coverage": round(tot["received"] / cfg.n, 6),
                 "delivered_per_step": tot["sent"], "messages_per_step": tot["messages"],
                 "overlay_s": round(ov, 3),
                 "roofline": {"bound": "hbm", "kernel": "shard window pipeline k_expand (owner bins) -> k_pack -> "
-                             "all-to-all -> k_plan/k_part2 -> k_resolve (rank 0)", "achieved": round(ach, 2),
+                             "all-to-all -> k_plan/k_part2 -> k_resolve (rank 0; timed with GS_FLAG_TIMING, "
+                             "which synchronises every window)", "achieved": round(ach, 2),
                              "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
                              "avg_launch_us": round(kern * 1e3 / launches, 2), "launches": launches,
@@ -449,6 +454,19 @@ def c4_sharded(a, gs, rank, world, local, dist):
                                                   "k_resolve": round(tm["resolve_ms"], 3)}}}
     finally:
         sim.close()
+
+
+def c4_sharded(a, gs, rank, world, local, dist):
+    """Config C4: N = 1e8, fanout 18 (floor(ln 1e8)), fanin 19, reference
+    defaults otherwise (crashrate 0.001 -> threshold 0), sharded over the
+    ranks (flood_sharded)."""
+    return flood_sharded(a, gs, rank, world, local, dist, 100_000_000, 18, 19, 0.001, "C4")
+
+
+def c5_flood_sharded(a, gs, rank, world, local, dist):
+    """The headline workload (C5's flood at N = 1e9) as ONE broadcast sharded
+    over the ranks (--gpus > 1 only: at one GPU it is the headline itself)."""
+    return flood_sharded(a, gs, rank, world, local, dist, a.n, a.fanout, a.fanin, a.crashrate, "C5 flood")
 
 
 def pushpull_sharded(a, gs, rank, world, local, dist):

@@ -127,6 +127,13 @@ struct gs_ctx {
   bool aborted = false;                 // a rank whose exchange failed (RCCL communicator aborted)
   unsigned long long* d_ig = nullptr;
   unsigned long long* d_fg = nullptr;
+  // pull-answer rounds of push-pull shards: the round's informed set being
+  // built, by global id (shared like d_ig); a rank's staging for the bits the
+  // other ranks set in its range ([G][segw] words)
+  unsigned long long* d_gn = nullptr;
+  unsigned long long* d_gst = nullptr;
+  bool pp_answer = false;               // the current broadcast's sharded rounds still run pull-answer
+  bool pp_gn_ok = false;                // d_gn holds the replicated set (set at the first sharded round)
   uint64_t segw = 0;
   // push-pull shards: the replica -- an unsharded push-pull context over the
   // full table on this device (shared by the device's members; owned by the
@@ -144,7 +151,7 @@ struct gs_ctx {
   std::vector<int> gdev_of;             // member -> index into gdevs
   std::vector<Buf> gbuf;                // per distinct device: its members' send blocks, then blocks from other devices
   std::vector<hipEvent_t> gev_c, gev_x; // per member: its part of an exchange done; per device: copies done
-  std::vector<unsigned long long*> gig, gfg;  // push-pull shards: per distinct device, the replicated sets
+  std::vector<unsigned long long*> gig, gfg, ggn;  // push-pull shards: per distinct device, the replicated sets
   std::vector<gs_ctx*> greps;           // push-pull shards: per distinct device, the replica
   OverlayWork ovw;                      // overlay builder buffers, kept between builds
 };
@@ -605,6 +612,7 @@ void destroy_one(gs_ctx* c) {
       (void)hipSetDevice(c->gdevs[i]);
       if (i < c->gig.size() && c->gig[i]) (void)hipFree(c->gig[i]);
       if (i < c->gfg.size() && c->gfg[i]) (void)hipFree(c->gfg[i]);
+      if (i < c->ggn.size() && c->ggn[i]) (void)hipFree(c->ggn[i]);
     }
     for (hipEvent_t e : c->gev_c) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->gev_x) (void)hipEventDestroy(e);
@@ -634,6 +642,8 @@ void destroy_one(gs_ctx* c) {
   if (c->own_ig) {
     if (c->d_ig) (void)hipFree(c->d_ig);
     if (c->d_fg) (void)hipFree(c->d_fg);
+    if (c->d_gn) (void)hipFree(c->d_gn);
+    if (c->d_gst) (void)hipFree(c->d_gst);
   }
   if (c->h_xbuf) (void)hipHostFree(c->h_xbuf);
   for (void* ptr : {(void*)c->d_deg, (void*)c->d_ids, c->d_state, (void*)c->d_cnt, (void*)c->d_failed, c->d_win,
@@ -756,9 +766,10 @@ int abort_rank(gs_ctx* c, int rc) {
 
 // Push-pull shard c uses the replicated informed / failed sets ig / fg
 // (G * segw words each): its own nodes are words [rank * segw, ...).
-void attach_pp_sets(gs_ctx* c, unsigned long long* ig, unsigned long long* fg) {
+void attach_pp_sets(gs_ctx* c, unsigned long long* ig, unsigned long long* fg, unsigned long long* gn) {
   c->d_ig = ig;
   c->d_fg = fg;
+  c->d_gn = gn;
   DevState& s = c->st;
   s.grecv = ig;
   s.gcrash = fg;
@@ -767,7 +778,8 @@ void attach_pp_sets(gs_ctx* c, unsigned long long* ig, unsigned long long* fg) {
   s.crash = fg + (size_t)c->rank * c->segw;
 }
 
-int alloc_pp_sets(gs_ctx* c, uint64_t words, unsigned long long** ig, unsigned long long** fg);
+int alloc_pp_sets(gs_ctx* c, uint64_t words, unsigned long long** ig, unsigned long long** fg,
+                  unsigned long long** gn);
 int make_replica(const gs_params* params, int dev, unsigned long long* ig, unsigned long long* fg, gs_ctx** out);
 
 // The rest of a rank context once its exchange is set: gathered fire counts
@@ -781,16 +793,18 @@ int finish_rank(gs_ctx* c, gs_ctx** out) {
     return GS_ENOMEM;
   }
   if (c->pp_shard) {
-    unsigned long long *ig = nullptr, *fg = nullptr;
-    if (alloc_pp_sets(c, (uint64_t)c->G * c->segw, &ig, &fg)) {
+    unsigned long long *ig = nullptr, *fg = nullptr, *gn = nullptr, *gst = nullptr;
+    if (alloc_pp_sets(c, (uint64_t)c->G * c->segw, &ig, &fg, &gn) ||
+        alloc_pp_sets(c, (uint64_t)c->G * c->segw, &gst, nullptr, nullptr)) {
       fprintf(stderr, "gs_create_rank: %s\n", c->err.c_str());
-      if (ig) (void)hipFree(ig);
-      if (fg) (void)hipFree(fg);
+      for (unsigned long long* q : {ig, fg, gn, gst})
+        if (q) (void)hipFree(q);
       destroy_one(c);
       return GS_ENOMEM;
     }
     c->own_ig = true;
-    attach_pp_sets(c, ig, fg);
+    c->d_gst = gst;
+    attach_pp_sets(c, ig, fg, gn);
     if (make_replica(&c->p, c->dev, ig, fg, &c->rep)) {
       destroy_one(c);
       return GS_ENOMEM;
@@ -801,13 +815,17 @@ int finish_rank(gs_ctx* c, gs_ctx** out) {
   return GS_OK;
 }
 
-// Allocates and zeroes a pair of replicated sets for G shards of segw words.
-int alloc_pp_sets(gs_ctx* c, uint64_t words, unsigned long long** ig, unsigned long long** fg) {
-  *ig = *fg = nullptr;
-  if (hipMalloc(ig, words * 8) != hipSuccess || hipMalloc(fg, words * 8) != hipSuccess)
-    return fail(c, GS_ENOMEM, "cannot allocate the replicated informed / failed sets");
-  CK(c, hipMemsetAsync(*ig, 0, words * 8, c->stream));
-  CK(c, hipMemsetAsync(*fg, 0, words * 8, c->stream));
+// Allocates and zeroes up to three bitsets of `words` words (null outputs are
+// skipped): the replicated informed / failed sets and the pull-answer set.
+int alloc_pp_sets(gs_ctx* c, uint64_t words, unsigned long long** ig, unsigned long long** fg,
+                  unsigned long long** gn) {
+  for (unsigned long long** q : {ig, fg, gn}) {
+    if (!q) continue;
+    *q = nullptr;
+    if (hipMalloc(q, words * 8) != hipSuccess)
+      return fail(c, GS_ENOMEM, "cannot allocate the replicated informed / failed sets");
+    CK(c, hipMemsetAsync(*q, 0, words * 8, c->stream));
+  }
   CK(c, hipStreamSynchronize(c->stream));
   return GS_OK;
 }
@@ -897,17 +915,18 @@ int gs_create_multi(const gs_params* params, const int* devices, int ndev, gs_ct
   if (g->pp && !g->gtrials) {  // push-pull shards: one pair of replicated sets per device
     g->gig.assign(g->gdevs.size(), nullptr);
     g->gfg.assign(g->gdevs.size(), nullptr);
+    g->ggn.assign(g->gdevs.size(), nullptr);
     for (size_t d = 0; d < g->gdevs.size(); ++d) {
       std::vector<gs_ctx*> ms;
       for (size_t i = 0; i < g->mem.size(); ++i)
         if ((size_t)g->gdev_of[i] == d) ms.push_back(g->mem[i]);
       (void)hipSetDevice(g->gdevs[d]);
-      if (alloc_pp_sets(ms[0], (uint64_t)g->mem.size() * ms[0]->segw, &g->gig[d], &g->gfg[d])) {
+      if (alloc_pp_sets(ms[0], (uint64_t)g->mem.size() * ms[0]->segw, &g->gig[d], &g->gfg[d], &g->ggn[d])) {
         fprintf(stderr, "gs_create_multi: %s\n", ms[0]->err.c_str());
         destroy_one(g);
         return GS_ENOMEM;
       }
-      for (gs_ctx* m : ms) attach_pp_sets(m, g->gig[d], g->gfg[d]);
+      for (gs_ctx* m : ms) attach_pp_sets(m, g->gig[d], g->gfg[d], g->ggn[d]);
       gs_ctx* r = nullptr;
       if (make_replica(params, g->gdevs[d], g->gig[d], g->gfg[d], &r)) {
         destroy_one(g);
@@ -1627,6 +1646,57 @@ int pp_barrier(gs_ctx* acc, const std::vector<gs_ctx*>& ms) {
 
 uint32_t pp_shift();
 
+// The unsharded engine's bottom-up threshold (pp_bottom_thr) for n nodes.
+unsigned long long pp_bottom_thr_n(const gs_ctx* c, uint64_t n) {
+  if (c->p.flags & GS_FLAG_PP_BOTTOM) return 0;
+  const char* e = getenv("GS_PP_BOTTOM256");
+  const unsigned long long k = (unsigned long long)std::min(std::max(e ? atoi(e) : 96, 0), 256);
+  return k == 256 ? ~0ull : (unsigned long long)(((unsigned __int128)n * k) >> 8);
+}
+
+// A rank's pull-answer round set bits in other ranks' ranges of its d_gn:
+// slice p goes to rank p (all-to-all), and the slices this rank receives are
+// ORed into its own slice before the commit.
+int pp_answer_exchange(gs_ctx* c) {
+  const uint32_t G = c->G, me = c->rank;
+  const uint64_t sw = c->segw;
+  unsigned long long* own = c->d_gn + (size_t)me * sw;
+  if (c->comm) {
+    const Rccl& r = rccl();
+    NCK(c, r.group_start());
+    for (uint32_t p = 0; p < G; ++p) {
+      if (p == me) continue;
+      NCK(c, r.send(c->d_gn + (size_t)p * sw, sw, ncclUint64, (int)p, c->comm, c->stream));
+      NCK(c, r.recv(c->d_gst + (size_t)p * sw, sw, ncclUint64, (int)p, c->comm, c->stream));
+    }
+    NCK(c, r.group_end());
+  } else {
+    if (!grow_pinned(c, (size_t)2 * G * sw * 8)) return fail(c, GS_ENOMEM, "cannot allocate exchange staging");
+    char* hs = c->h_xbuf;
+    char* hr = c->h_xbuf + (size_t)G * sw * 8;
+    std::vector<size_t> sb(G, sw * 8), rb(G, sw * 8);
+    sb[me] = rb[me] = 0;
+    // send blocks back to back in rank order without this rank's own slice
+    size_t at = 0;
+    for (uint32_t p = 0; p < G; ++p)
+      if (p != me) {
+        CK(c, hipMemcpyAsync(hs + at, c->d_gn + (size_t)p * sw, sw * 8, hipMemcpyDeviceToHost, c->stream));
+        at += sw * 8;
+      }
+    CK(c, hipStreamSynchronize(c->stream));
+    if (c->hx.all_to_allv(c->hx.user, hs, sb.data(), hr, rb.data()))
+      return fail(c, GS_EDEVICE, "the exchange's all_to_allv callback failed");
+    at = 0;
+    for (uint32_t p = 0; p < G; ++p)
+      if (p != me) {
+        CK(c, hipMemcpyAsync(c->d_gst + (size_t)p * sw, hr + at, sw * 8, hipMemcpyHostToDevice, c->stream));
+        at += sw * 8;
+      }
+  }
+  CK(c, pp_or_slices(own, c->d_gst, G, sw, c->stream));  // the own slot of d_gst stays zero
+  return GS_OK;
+}
+
 // simulator.go:239-241 for the push-pull extension: the owner informs the
 // sender (unless failed), every shard resets its round control; the replicas
 // (if any) start the broadcast's sparse early rounds.
@@ -1651,6 +1721,14 @@ int pp_shard_begin(gs_ctx* acc, uint64_t sender) {
       CK(r, hipStreamSynchronize(r->stream));
     }
   acc->rep_live = sparse;
+  acc->pp_gn_ok = false;
+  // pull-answer sharded rounds: between ranks (their bits in other ranks' ranges
+  // move by an all-to-all) or among the shards of one device (one shared set);
+  // shards over several devices of one group run bottom-up only
+  const bool onedev = !acc->group || acc->gdevs.size() == 1;
+  bool answer = onedev && !getenv("GS_PP_SHARD_BOTTOM") && (!acc->has_hx || acc->hx.all_to_allv);
+  for (gs_ctx* m : ms) answer = answer && m->d_gn && (!m->failed || m->sp.fmask);
+  acc->pp_answer = answer;
   for (gs_ctx* m : ms) {
     CK(m, hipSetDevice(m->dev));
     if (int rc = pp_prepare(m)) return fail(acc, rc, m->err);
@@ -1730,21 +1808,43 @@ int pp_shard_step(gs_ctx* acc, uint32_t ticks, gs_tick_stats* out) {
           ++acc->rep_rounds;
           continue;
         }
-        // the shards take over: each one's next = its slice of the replicated set
-        acc->rep_live = false;
-        for (gs_ctx* m : ms) {
+        acc->rep_live = false;  // the shards take over
+      }
+      if (!acc->pp_gn_ok) {  // the round's set starts as the replicated set (per device / rank)
+        std::vector<int> done(acc->group ? acc->gdevs.size() : 1, 0);
+        for (size_t i = 0; i < ms.size(); ++i) {
+          gs_ctx* m = ms[i];
+          const int d = acc->group ? acc->gdev_of[i] : 0;
+          if (done[d]) continue;
+          done[d] = 1;
           CK(m, hipSetDevice(m->dev));
-          CK(m, hipMemcpyAsync(m->d_next, m->st.recv, m->st.W * 8, hipMemcpyDeviceToDevice, m->stream));
+          CK(m, hipMemcpyAsync(m->d_gn, m->d_ig, (size_t)m->G * m->segw * 8, hipMemcpyDeviceToDevice, m->stream));
         }
+        RC(pp_barrier(acc, ms));
+        acc->pp_gn_ok = true;
+      }
+      uint32_t mode = PP_BOTTOM;
+      if (acc->pp_answer) {  // pull-answer until |I| >= the unsharded engine's bottom-up threshold
+        gs_ctx* m0 = ms[0];  // every shard's copy of the replicated set is the same
+        unsigned long long* cnt = (unsigned long long*)(m0->d_err + 4);
+        unsigned long long ninf = 0;
+        CK(m0, hipSetDevice(m0->dev));
+        CK(m0, pp_count(m0->d_ig, (uint64_t)m0->G * m0->segw, cnt, m0->stream));
+        CK(m0, hipMemcpyAsync(&ninf, cnt, 8, hipMemcpyDeviceToHost, m0->stream));
+        CK(m0, hipStreamSynchronize(m0->stream));
+        if (ninf >= pp_bottom_thr_n(acc, acc->p.n)) acc->pp_answer = false;
+        else mode = PP_ANSWER;
       }
       for (gs_ctx* m : ms) {
         CK(m, hipSetDevice(m->dev));
-        CK(m, pp_round_shard(m->st, m->d_next, tt, m->sp, m->stream));
+        CK(m, pp_round_shard(m->st, m->d_gn + (size_t)m->rank * m->segw, m->d_gn, tt, m->sp, mode, m->stream));
       }
       RC(pp_barrier(acc, ms));
+      if (mode == PP_ANSWER && !acc->group)  // the bits this rank set in other ranks' ranges go to their owners
+        if (int rc = pp_answer_exchange(acc)) return abort_rank(acc, rc);
       for (gs_ctx* m : ms) {
         CK(m, hipSetDevice(m->dev));
-        CK(m, pp_commit(m->st, m->d_next, tt, m->sp, m->stream));
+        CK(m, pp_commit(m->st, m->d_gn + (size_t)m->rank * m->segw, tt, m->sp, m->stream));
       }
       if (int rc = pp_exchange(acc, ms)) return abort_rank(acc, rc);
     }

@@ -328,9 +328,16 @@ hipError_t pp_rev_fill_range(const uint8_t* deg, const uint32_t* ids, uint64_t n
                              uint64_t hi, unsigned long long* rend, uint32_t* rsrc, uint8_t* rslot, hipStream_t st);
 // fmask of the shard's own callers from their rows and the replicated failed set.
 hipError_t pp_fmask_rows(const DevState& s, uint8_t* fmask, hipStream_t st);
-// One sharded round: mode (always bottom-up) + k_ppb_round; commit with pp_commit.
-hipError_t pp_round_shard(const DevState& s, unsigned long long* next, uint32_t t, const PPSparse& sp,
-                          hipStream_t st);
+// One sharded round in `mode` (PP_BOTTOM: k_ppb_round into next, the shard's
+// own words; PP_ANSWER: k_ppa_round into gnext, a bitset by global id whose
+// bits in other shards' ranges go to their owners); commit with pp_commit.
+hipError_t pp_round_shard(const DevState& s, unsigned long long* next, unsigned long long* gnext, uint32_t t,
+                          const PPSparse& sp, uint32_t mode, hipStream_t st);
+// *out = popcount(words[0, nwords)) (stream-ordered).
+hipError_t pp_count(const unsigned long long* words, uint64_t nwords, unsigned long long* out, hipStream_t st);
+// dst[w] |= src[i * words + w] for i < nslices.
+hipError_t pp_or_slices(unsigned long long* dst, const unsigned long long* src, uint32_t nslices, uint64_t words,
+                        hipStream_t st);
 
 // Launchers (gs_broadcast.hip).
 hipError_t launch_tick(const DevState& st, uint32_t tick, int mode, hipStream_t s);

@@ -460,6 +460,47 @@ __global__ __launch_bounds__(kPPRoundBlock) void k_ppa_round(const DevState s, u
   block_add<kPPRoundBlock>(sh, v3, 3, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
 }
 
+// Shards: the round's mode, chosen by the host from the global informed count
+// (the same on every shard: the replicated set), and the round counters.
+__global__ void k_pp_set_mode(PPCtl* c, uint32_t mode) {
+  c->mode = mode;
+  c->nbottom += mode == PP_BOTTOM;
+  c->nanswer += mode == PP_ANSWER;
+}
+
+// *out = popcount of words[0, n) (n = 0: *out = 0).
+__global__ __launch_bounds__(kPPBlock) void k_pp_count(const unsigned long long* __restrict__ words,
+                                                       unsigned long long n, unsigned long long* out) {
+  __shared__ uint64_t sh[kPPBlock / 64];
+  if (n == 0) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *out = 0;
+    return;
+  }
+  uint64_t c = 0;
+  for (uint64_t w = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; w < n; w += (uint64_t)gridDim.x * kPPBlock)
+    c += (uint64_t)__popcll(words[w]);
+  const uint64_t ws = wave_sum64(c);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = ws;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t b = 0;
+    for (uint32_t k = 0; k < kPPBlock / 64; ++k) b += sh[k];
+    if (b) atomicAdd(out, (unsigned long long)b);
+  }
+}
+
+// dst[w] |= src[i * words + w] for every slice i < nslices (the bits other
+// shards set in this shard's range during a pull-answer round).
+__global__ __launch_bounds__(kPPBlock) void k_pp_or_slices(unsigned long long* __restrict__ dst,
+                                                           const unsigned long long* __restrict__ src,
+                                                           uint32_t nslices, uint64_t words) {
+  for (uint64_t w = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; w < words; w += (uint64_t)gridDim.x * kPPBlock) {
+    unsigned long long x = dst[w];
+    for (uint32_t i = 0; i < nslices; ++i) x |= src[(size_t)i * words + w];
+    dst[w] = x;
+  }
+}
+
 __global__ __launch_bounds__(kPPBlock) void k_pp_commit(const DevState s,
                                                         const unsigned long long* __restrict__ next,
                                                         uint32_t t, PPCtl* ctl) {
@@ -917,14 +958,32 @@ hipError_t pp_fmask_rows(const DevState& s, uint8_t* fmask, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t pp_round_shard(const DevState& s, unsigned long long* next, uint32_t t, const PPSparse& sp,
-                          hipStream_t st) {
-  if (!pp_state_ok(s) || !next || !sp.ctl || !sp.rend || !sp.rsrc || !sp.rslot || (s.check_crashed && !sp.fmask))
+hipError_t pp_round_shard(const DevState& s, unsigned long long* next, unsigned long long* gnext, uint32_t t,
+                          const PPSparse& sp, uint32_t mode, hipStream_t st) {
+  if (!pp_state_ok(s) || !next || !sp.ctl || !sp.rend || !sp.rsrc || !sp.rslot || (s.check_crashed && !sp.fmask) ||
+      (mode == PP_ANSWER && !gnext) || (mode != PP_ANSWER && mode != PP_BOTTOM))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_pp_mode, dim3(1), dim3(kPPSegs), 0, st, sp.ctl);
+  hipLaunchKernelGGL(k_pp_set_mode, dim3(1), dim3(1), 0, st, sp.ctl, mode);
   const uint64_t nrange = (s.W + kPPRange - 1) / kPPRange;
   const uint32_t bblocks = (uint32_t)std::min<uint64_t>((nrange + kPPWaves - 1) / kPPWaves, 512);
-  hipLaunchKernelGGL(k_ppb_round, dim3(bblocks ? bblocks : 1), dim3(kPPRoundBlock), 0, st, s, next, sp, t);
+  if (mode == PP_BOTTOM)
+    hipLaunchKernelGGL(k_ppb_round, dim3(bblocks ? bblocks : 1), dim3(kPPRoundBlock), 0, st, s, next, sp, t);
+  else
+    hipLaunchKernelGGL(k_ppa_round, dim3(bblocks ? bblocks : 1), dim3(kPPRoundBlock), 0, st, s, gnext, sp, t);
+  return hipGetLastError();
+}
+
+hipError_t pp_count(const unsigned long long* words, uint64_t nwords, unsigned long long* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_pp_count, dim3(1), dim3(1), 0, st, words, 0ull, out);  // zero the total
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((nwords + kPPBlock - 1) / kPPBlock, 2048);
+  hipLaunchKernelGGL(k_pp_count, dim3(blocks ? blocks : 1), dim3(kPPBlock), 0, st, words, nwords, out);
+  return hipGetLastError();
+}
+
+hipError_t pp_or_slices(unsigned long long* dst, const unsigned long long* src, uint32_t nslices, uint64_t words,
+                        hipStream_t st) {
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((words + kPPBlock - 1) / kPPBlock, 2048);
+  hipLaunchKernelGGL(k_pp_or_slices, dim3(blocks ? blocks : 1), dim3(kPPBlock), 0, st, dst, src, nslices, words);
   return hipGetLastError();
 }
 

@@ -13,10 +13,12 @@
   which is the same multiset of messages per shard.  The HIP path is checked
   on the GPU (tests/test_gpu_multi.py, and with two processes exchanging
   through gloo in tests/test_rank_exchange.py).
-* Push-pull node-range sharding (config C5): the sharded round of
-  gs_api.cpp pp_shard_step (bottom-up on the shard's own nodes against the
-  replicated informed set, then an all-gather of the owned words) restated in
-  numpy over gloo -- must equal the oracle's unsharded pushpull_step per round.
+* Push-pull node-range sharding (config C5): the sharded rounds of
+  gs_api.cpp pp_shard_step -- bottom-up on the shard's own nodes against the
+  replicated informed set, then an all-gather of the owned words; and
+  pull-answer, the shard's informed nodes informing nodes anywhere, whose
+  bits go to their owners -- restated in numpy over gloo; each must equal the
+  oracle's unsharded pushpull_step per round.
 """
 from __future__ import annotations
 
@@ -167,6 +169,81 @@ def pp_round_shard(O, p, deg, ids, inf, dead, t, lo, hi, rev):
     return new, fired, sent, msgs
 
 
+def pp_round_shard_answer(O, p, deg, ids, inf, dead, t, lo, hi, rev):
+    """One sharded pull-answer round restated (k_ppa_round on nodes [lo, hi)):
+    each own informed node pushes (its own row) and answers the pulls among its
+    in-edges; returns the nodes it informs ANYWHERE (they go to their owners)
+    and this shard's (fired, sent, msgs)."""
+    key = [int(p.seed) & 0xFFFFFFFF, int(p.seed) >> 32]
+    kd = O.threshold(p.drop_rate)
+    c3 = (9 << 24) | int(p.trial)
+
+    def call(v):
+        r = O.philox([v, t, 0, c3], key)
+        return (r[0] * int(deg[v])) >> 32, ((r[1] * 100) >> 32) >= kd
+
+    fired = sent = msgs = 0
+    new = []
+    for u in range(lo, hi):
+        if dead[u]:
+            continue
+        d = int(deg[u])
+        fired += d > 0
+        if not inf[u]:
+            continue
+        if d:
+            j, kept = call(u)
+            if kept:
+                sent += 1
+                w = int(ids[u, j])
+                if not dead[w]:
+                    msgs += 1
+                    new.append(w)
+        for (v, jv) in rev.get(u, ()):  # the pulls u answers: callers v anywhere
+            if not inf[v] and not dead[v] and call(v) == (jv, True):
+                sent += 1
+                msgs += 1
+                new.append(v)
+    return new, fired, sent, msgs
+
+
+def _pp_answer_worker(rank, world, port, kw, out_dir):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import pyoracle as O
+    from gossip_simulator_amd import dist as gd
+    p = O.make_params(**kw)
+    deg, ids, _, _ = O.overlay(p)
+    n = int(p.n)
+    lo, hi = gd.shard_range(n, rank, world)
+    dead = np.random.default_rng(3).random(n) < 0.02
+    rev = {}
+    for v in range(n):
+        for j in range(int(deg[v])):
+            u = int(ids[v, j])
+            if lo <= u < hi:
+                rev.setdefault(u, []).append((v, j))
+    inf = np.zeros(n, bool)
+    s = int(O.pick_sender(p))
+    inf[s] = not dead[s]
+    rows, recv = [], int(inf.sum())
+    for t in range(1, 31):
+        new, fired, sent, msgs = pp_round_shard_answer(O, p, deg, ids, inf, dead, t, lo, hi, rev)
+        mark = np.zeros(n, np.uint8)
+        mark[np.array(new, dtype=np.int64)] = 1
+        g = torch.from_numpy(mark)
+        dist.all_reduce(g, op=dist.ReduceOp.MAX)  # the bits every shard set, at their owners
+        nxt = inf | g.numpy().astype(bool)
+        c = torch.tensor([fired, sent, msgs], dtype=torch.int64)
+        dist.all_reduce(c)
+        recv += int((nxt & ~inf).sum())
+        inf = nxt
+        rows.append([t, *c.tolist(), recv, 0, recv])
+    np.save(os.path.join(out_dir, f"pa{rank}.npy"), np.array(rows, dtype=np.int64))
+    dist.destroy_process_group()
+
+
 def _pp_sharded_worker(rank, world, port, kw, out_dir):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -279,6 +356,33 @@ def test_pushpull_node_range_sharding_world2_bit_identical(oracle, tmp_path):
     rec = e.received()
     bits = (rec[np.arange(n) // 64] >> (np.arange(n) % 64).astype(np.uint64)) & np.uint64(1)
     assert np.array_equal(inf, bits.astype(bool))
+
+
+def test_pushpull_pull_answer_sharding_world2_bit_identical(oracle, tmp_path):
+    """The sharded pull-answer round (gs_api.cpp pp_shard_step, k_ppa_round on
+    each shard's informed nodes, their bits in other ranges sent to the owners)
+    restated over gloo, every round pull-answer: equal to the oracle's
+    unsharded pushpull_step per round, 2 % failed."""
+    kw = dict(n=20000, fanout=5, fanin=6, delay_low=10, delay_high=20, drop_rate=0.1, crash_rate=0.0,
+              seed=0x5EED, trial=0, model=1)
+    world = 2
+    mp.start_processes(_pp_answer_worker, args=(world, free_port(), kw, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    a, b = np.load(tmp_path / "pa0.npy"), np.load(tmp_path / "pa1.npy")
+    assert np.array_equal(a, b)
+    p = oracle.make_params(**kw)
+    deg, ids, _, _ = oracle.overlay(p)
+    n = int(p.n)
+    dead = np.random.default_rng(3).random(n) < 0.02
+    w = np.zeros((n + 63) // 64, np.uint64)
+    idx = np.nonzero(dead)[0]
+    np.bitwise_or.at(w, idx // 64, np.left_shift(np.uint64(1), (idx % 64).astype(np.uint64)))
+    e = oracle.Engine(p, deg, ids)
+    e.set_failed(w)
+    e.begin(-1)
+    want = e.step(30).astype(np.int64)
+    want[:, 5] = 0
+    assert np.array_equal(a, want)
 
 
 def test_trial_sharding_world2_matches_serial(oracle, tmp_path):

@@ -10,6 +10,10 @@ implement the same tick model with no shared kernel code:
   popcount(crashed bitset), messages <= delivered sends, every fired
   broadcast is a scheduled one (pending never negative, 0 at quiescence);
 * the overlay respects fanout <= len(friends) <= fanin (simulator.go:68,80,96).
+Node-range shards at full size (G in-process shards on the one GPU: the
+owner-expand flood with its all-to-all of messages, the push-pull replica +
+sharded bottom-up rounds) against the unsharded run, per tick and on the
+final bitsets.
 Push-pull at N = 1e9: monotone informed set, pending == received, float32
 99 % reached, delivered <= calls; with a 1 % pre-failed mask the per-round
 counters and final bitsets are identical across the round selections auto /
@@ -47,16 +51,16 @@ def failed_mask(frac: float, seed: int) -> np.ndarray:
     return w
 
 
-def flood(engine: str, mask=None):
+def flood(engine: str, mask=None, shards: int = 0):
     import gossip_simulator_amd as gs
     gs.load()
     cfg = gs.Config(n=N, fanout=5, fanin=6, droprate=0.1, crashrate=0.01, seed=0x5EED,
                     engine=engine)
-    with gs.Simulator(cfg) as sim:
+    with gs.Simulator(cfg, devices=[0] * shards if shards else None) as sim:
         _, stab = sim.build_overlay()
         if mask is not None:
             sim.set_failed(mask)
-        if engine == "window":
+        if engine == "window" and not shards:
             deg, _ = sim.read_peers()
             assert deg.min() >= 5 and deg.max() <= 6
             del deg
@@ -116,12 +120,12 @@ def test_c5_flood_failed_mask_window_vs_tick():
     assert a[5] >= nfail and 0.97 < a[4] / N < 0.99
 
 
-def pushpull_failed(pp_rounds: str, mask):
+def pushpull_failed(pp_rounds: str, mask, shards: int = 0):
     import gossip_simulator_amd as gs
     gs.load()
     cfg = gs.Config(n=N, fanout=5, fanin=6, droprate=0.1, crashrate=0.0, seed=0x5EED,
                     model="pushpull", pp_rounds=pp_rounds)
-    with gs.Simulator(cfg) as sim:
+    with gs.Simulator(cfg, devices=[0] * shards if shards else None) as sim:
         sim.build_overlay()
         sim.set_failed(mask)
         sim.broadcast_begin(-1)
@@ -155,3 +159,29 @@ def test_c5_pushpull_failed_mask_round_modes_bit_exact():
 
 def gs_covered(recv: int) -> bool:
     return np.float32(recv) / np.float32(N) >= np.float32(0.99)
+
+
+def test_c5_flood_shards_vs_unsharded_bit_exact():
+    """C5's flood at N = 1e9 in 8 node-range shards (owner expand, messages to
+    their targets' owners) and in 3 (ragged ranges, a partial coarse bin per
+    shard) with the 1 % mask: identical to the unsharded window engine per tick
+    and on the final bitsets."""
+    mask = failed_mask(0.01, 0x5EED + 1)
+    a = flood("window", mask)
+    for G in (8, 3):
+        b = flood("window", mask, shards=G)
+        assert a[0] == b[0]
+        assert np.array_equal(a[1], b[1]), f"G={G}: per-tick counters differ from the unsharded run"
+        assert a[2] == b[2] and a[3] == b[3], f"G={G}: final bitsets differ from the unsharded run"
+
+
+def test_c5_pushpull_shards_vs_unsharded_bit_exact():
+    """C5 as named (push-pull, N = 1e9) with the 1 % mask in 8 node-range
+    shards (the replica's sparse early rounds, then sharded bottom-up rounds):
+    identical to the unsharded run per round and on the informed set."""
+    mask = failed_mask(0.01, 0x5EED + 1)
+    rows, h, nrec, _ = pushpull_failed("auto", mask)
+    got = pushpull_failed("auto", mask, shards=8)
+    assert np.array_equal(got[0], rows), "per-round counters differ from the unsharded run"
+    assert got[1] == h and got[2] == nrec
+    assert got[3]["pp_early_rounds"] > 0 and got[3]["pp_bottom_rounds"] > 0

@@ -257,10 +257,12 @@ def test_gpu_pushpull_run_polls_like_oracle(oracle, fail_frac, rounds):
 def test_gpu_pushpull_shards_bit_exact(oracle, monkeypatch, kw, stride, dlo, dhi, fail_frac, G, replica):
     """G node-range shards of one push-pull run on one GPU (gs_create_multi):
     the sparse early rounds on the device's replica (the full table, the
-    replicated sets; replica=False: GS_PP_NO_REPLICA=1, none), then every
-    round bottom-up on each shard's own nodes against the replicated informed
-    set, exchanged after the round; per round bit-exact to the oracle's
-    pushpull_step (oracle/gsoracle.c), as the unsharded engine is."""
+    replicated sets; replica=False: GS_PP_NO_REPLICA=1, none), then
+    pull-answer rounds (each shard's informed nodes answer the pulls among
+    their in-edges, into one shared set) and bottom-up rounds on each shard's
+    own nodes against the replicated informed set, exchanged after the round;
+    per round bit-exact to the oracle's pushpull_step (oracle/gsoracle.c), as
+    the unsharded engine is."""
     import gossip_simulator_amd as gs
     gs.load()
     if not replica:
@@ -288,7 +290,7 @@ def test_gpu_pushpull_shards_bit_exact(oracle, monkeypatch, kw, stride, dlo, dhi
             if oracle.covered(int(a[0, 4]), n) or int(a[0, 4]) == 0:
                 break
         tm = sim.timing()
-        assert tm["pp_bottom_rounds"] + tm["pp_early_rounds"] == r + 1
+        assert tm["pp_bottom_rounds"] + tm["pp_early_rounds"] + tm["pp_answer_rounds"] == r + 1
         assert (tm["pp_early_rounds"] >= 1) == replica
 
 
@@ -315,11 +317,14 @@ def pp_1e6():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("G", [2, 4, 8])
-def test_gpu_pushpull_shards_match_unsharded_1e6(pp_1e6, G):
+@pytest.mark.parametrize("G,answer", [(2, True), (4, True), (8, True), (4, False)])
+def test_gpu_pushpull_shards_match_unsharded_1e6(pp_1e6, monkeypatch, G, answer):
     """N = 1e6 (C5 shape, 1 % failed) in G shards, per round and through
-    gs_run's poll and stop rule: identical to the unsharded run."""
+    gs_run's poll and stop rule: identical to the unsharded run (answer=False:
+    GS_PP_SHARD_BOTTOM=1, bottom-up sharded rounds only)."""
     import gossip_simulator_amd as gs
+    if not answer:
+        monkeypatch.setenv("GS_PP_SHARD_BOTTOM", "1")
     cfg, deg, ids, failed, rows, rec, polls, status = pp_1e6
     with gs.Simulator(cfg, devices=[0] * G) as sim:
         sim.load_peers(deg, ids)
@@ -331,3 +336,4 @@ def test_gpu_pushpull_shards_match_unsharded_1e6(pp_1e6, G):
         sim.broadcast_begin(-1)
         p2, s2 = sim.run(poll=5)
         assert s2 == status and np.array_equal(p2, polls)
+        assert (sim.timing()["pp_answer_rounds"] > 0) == answer
