@@ -264,8 +264,8 @@ int alloc_window(gs_ctx* c) {
     return fail(c, GS_ENOMEM, "cannot allocate the rolled-receipt lists");
   w.rlmsg = (uint32_t*)c->d_rlmsg;
   w.dbg = nullptr;
-  if (getenv("GS_STAMPS") && hipMalloc(&w.dbg, 2 * kStampPhases * 8) == hipSuccess)
-    (void)hipMemset(w.dbg, 0, 2 * kStampPhases * 8);
+  if (getenv("GS_STAMPS") && hipMalloc(&w.dbg, kDbgWords * 8) == hipSuccess)
+    (void)hipMemset(w.dbg, 0, kDbgWords * 8);
   w.flist = (uint16_t*)c->d_flist;
   c->fcount_bytes = (size_t)w.R * w.nfine * 4;
   if (hipMemsetAsync(c->d_win, 0, total, c->stream) != hipSuccess)
@@ -625,7 +625,13 @@ void destroy_one(gs_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm && rccl().ok) (void)rccl().comm_destroy(c->comm);
   if (c->ws.dbg) {
-    unsigned long long h[2 * kStampPhases];
+    unsigned long long h[kDbgWords];
+    if (hipMemcpy(h, c->ws.dbg, sizeof h, hipMemcpyDeviceToHost) == hipSuccess && h[kXStamp0]) {
+      const double r = 1e-3 / h[kXStamp0];  // k_expand phases (GS_XSTAMPS builds)
+      fprintf(stderr, "[stamps] k_expand: %llu rounds (wave 0), mean kcycles per round: lookup %.2f rows %.2f "
+              "draws %.2f scan+scatter %.2f barrier %.2f writeout %.2f\n", h[kXStamp0], h[kXStamp0 + 1] * r,
+              h[kXStamp0 + 2] * r, h[kXStamp0 + 3] * r, h[kXStamp0 + 4] * r, h[kXStamp0 + 5] * r, h[kXStamp0 + 6] * r);
+    }
     if (hipMemcpy(h, c->ws.dbg, sizeof h, hipMemcpyDeviceToHost) == hipSuccess)
       for (int cls = 0; cls < 2; ++cls) {  // k_resolve phases (GS_STAMPS=1), thread 0 of every workgroup
         const unsigned long long* d = h + cls * kStampPhases;

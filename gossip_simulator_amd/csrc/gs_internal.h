@@ -189,6 +189,8 @@ struct WinState {
 };
 constexpr uint32_t kStatShards = 256;
 constexpr uint32_t kStampPhases = 10;
+constexpr uint32_t kXStamp0 = 2 * kStampPhases;  // k_expand phases (GS_XSTAMPS builds) after k_resolve's
+constexpr uint32_t kDbgWords = kXStamp0 + 8;
 // per-trial window counters (batched trials)
 enum TStat : uint32_t { TS_FIRED = 0, TS_SENT = 1, TS_DEAD = 2, TS_RECV = 3, TS_CRASH = 4 };
 constexpr uint32_t kTStatFields = 8;

@@ -239,6 +239,24 @@ __device__ __forceinline__ unsigned long long* shard_row(const WinState& w, uint
   return w.sstats + ((size_t)(blockIdx.x & (kStatShards - 1)) * kMaxWindow + k) * kStatFields;
 }
 
+// GS_XSTAMPS builds (diagnostics, GS_STAMPS=1 at run time): wave 0 of every
+// k_expand workgroup waits for everything it issued and adds the cycles since
+// its last stamp to phase i (w.dbg[kXStamp0 + i]; i = 0 counts rounds).
+#ifdef GS_XSTAMPS
+__device__ __forceinline__ void xstamp(const WinState& w, unsigned long long& last, uint32_t i) {
+  if (w.dbg && threadIdx.x < 64) {
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0 && i) atomicAdd(&w.dbg[kXStamp0 + i], t - last);
+    if (threadIdx.x == 0 && i == 1) atomicAdd(&w.dbg[kXStamp0], 1ull);
+    last = t;
+  }
+}
+#define XSTAMP(i) xstamp(w, xlast, i)
+#else
+#define XSTAMP(i) ((void)0)
+#endif
+
 __global__ void k_stats_reduce(const WinState w, uint32_t t0, uint32_t L) {
   if (w.abort_on_err && win_abort(w)) return;  // the redo of the window reduces them
   const uint32_t tid = threadIdx.x;  // one (tick, field) pair per thread
@@ -472,9 +490,14 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
   uint32_t accp[kBitTicks];
 #pragma unroll
   for (uint32_t kx = 0; kx < kBitTicks; ++kx) accp[kx] = 0;
+#ifdef GS_XSTAMPS
+  unsigned long long xlast = 0;
+  XSTAMP(0);
+#endif
   for (unsigned long long rd = rbeg; rd < rend; rd += rstep) {
     sm.cnt[tid] = 0;
     __syncthreads();
+    XSTAMP(6);  // the previous round's write-out and this barrier
     uint32_t mm[NPT][MAXS], mt[NPT][MAXS];  // message, bin | rank << 8 (~0u = none)
     uint32_t vv[NPT], kk[NPT];
 #pragma unroll
@@ -494,12 +517,14 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
         }
       }
     }
+    XSTAMP(1);  // firing nodes looked up
 #pragma unroll
     for (uint32_t q = 0; q < NPT; ++q) {
 #pragma unroll
       for (uint32_t j = 0; j < MAXS; ++j) { mm[q][j] = kEmptyMsg; mt[q][j] = ~0u; }
       if (vv[q] != ~0u) load_row<MAXS>(w, vv[q], mm[q]);  // all rows in flight
     }
+    XSTAMP(2);  // rows gathered
     uint32_t sentq[NPT];
 #pragma unroll
     for (uint32_t q = 0; q < NPT; ++q) {
@@ -542,6 +567,7 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
         tstat_add(w.tstat, key, TS_FIRED, 1u, TS_SENT, sentq[q]);
       }
     }
+    XSTAMP(3);  // drop / crash draws and LDS ranks
     __syncthreads();
     if (!WRITE) {
       if (sm.cnt[tid]) atomicAdd(&w.chist[reg], (unsigned long long)sm.cnt[tid]);
@@ -567,7 +593,9 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
       if (at + mycnt > cend - cbase) atomicOr(w.err, kErrCoarse);
       sm.gbase[tid] = cbase + at;
     }
+    XSTAMP(4);  // scan, reservation, LDS scatter (wave 0's part)
     __syncthreads();
+    XSTAMP(5);  // waiting for the other waves
     const uint32_t total = sm.off[256];
     for (uint32_t p = tid; p < total; p += kExpandBlock) {
       const uint32_t b = sm.sbin[p];
