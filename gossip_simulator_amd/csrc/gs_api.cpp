@@ -238,8 +238,9 @@ int alloc_window(gs_ctx* c) {
                b_fhist = al(((size_t)w.ncoarse * 256 + 1) * 8), b_fbase = al(((size_t)w.nfine + 1) * 8),
                b_ffill = al((size_t)w.nfine * 8),
                b_sst = al((size_t)kStatShards * kMaxWindow * kStatFields * 8),
-               b_rlcnt = al((size_t)w.nfine * 4);
-  const size_t total = b_fc + 2 * b_units + b_small + b_fhist + b_fbase + b_ffill + b_sst + b_rlcnt;
+               b_rlcnt = al((size_t)w.nfine * 4),
+               b_tsum = al((size_t)w.ncoarse * kMaxWindow * 8) + al(((size_t)w.ncoarse + 1) * 8);
+  const size_t total = b_fc + 2 * b_units + b_small + b_fhist + b_fbase + b_ffill + b_sst + b_rlcnt + b_tsum;
   if (hipMalloc(&c->d_win, total) != hipSuccess)
     return fail(c, GS_ENOMEM, "cannot allocate window-engine buffers");
   const size_t flist = (size_t)w.R * w.nfine * kFineNodes * 2;
@@ -260,6 +261,8 @@ int alloc_window(gs_ctx* c) {
   w.ffill = (unsigned long long*)q; q += b_ffill;
   w.sstats = (unsigned long long*)q; q += b_sst;
   w.rlcnt = (uint32_t*)q; q += b_rlcnt;
+  w.tsum = (unsigned long long*)q; q += al((size_t)w.ncoarse * kMaxWindow * 8);
+  w.toff = (unsigned long long*)q; q += al(((size_t)w.ncoarse + 1) * 8);
   if (hipMalloc(&c->d_rlmsg, (size_t)w.nfine * kRolledCap * 4) != hipSuccess)
     return fail(c, GS_ENOMEM, "cannot allocate the rolled-receipt lists");
   w.rlmsg = (uint32_t*)c->d_rlmsg;
@@ -2186,19 +2189,15 @@ int run_async(gs_ctx* c, uint64_t tend, uint32_t poll, uint64_t max_ticks, OnTic
   // launch sizes: grid-stride kernels, sized for the dense windows
   const uint64_t Tn_bound = std::min<uint64_t>(c->ntot + 1, 4096ull * 1024),
                  T_bound = std::min<uint64_t>((c->ntot + 1) * w.stride, 2048ull * 16384);
-  size_t need = 0;
-  CK(c, win_scan_units_masked(w, nullptr, need, c->stream));
-  if (!grow(c->tmp, need)) return fail(c, GS_ENOMEM, "cannot allocate scan scratch");
   auto enqueue = [&](uint32_t slot) -> int {
+    // units (+ tile sums) -> cut (+ tile offsets) -> unit scan and group map
+    // inside the tiles; the rolled replay consumes the window's fire lists
     CK(c, win_units(w, 0, w.lstride, c->stream));
     CK(c, win_cut(w, budget, c->stream));
-    size_t nb = c->tmp.bytes;
-    CK(c, win_scan_units_masked(w, c->tmp.p, nb, c->stream));
-    CK(c, win_groupmap(w, w.lstride, c->stream));
+    CK(c, win_unitscan(w, c->stream));
     CK(c, win_expand(w, 0, w.lstride, Tn_bound, 1, c->stream));
     CK(c, win_plan(w, false, c->stream));
     CK(c, win_part2(w, T_bound, true, c->stream));
-    CK(c, win_consume(w, c->stream));
     CK(c, win_resolve(w, 0, w.lstride, c->stream));
     CK(c, win_close(w, slot, c->stream));
     CK(c, hipMemcpyAsync(c->h_stage + (size_t)slot * kStageWords, c->d_stage + (size_t)slot * kStageWords,

@@ -148,6 +148,8 @@ struct WinState {
   unsigned long long* fhist;     // [ncoarse*256 + 1] exact fine counts (fallback)
   unsigned long long* fstart;    // [nfine + 1] fine region starts
   unsigned long long* ffill;     // [nfine] fine region fill
+  unsigned long long* tsum;      // [ncoarse][kMaxWindow] fires per (256-bucket tile, tick) (k_units)
+  unsigned long long* toff;      // [ncoarse + 1] device-driven windows: firing index of each tile's first unit (k_cut)
   unsigned long long* sstats;    // [kStatShards][kMaxWindow][kStatFields] per-window partial counters
   unsigned long long* dbg;       // diagnostic phase stamps (GS_STAMPS=1), else null
   // batched trials: [trials][kMaxWindow][kTStatFields] per-window counters of every
@@ -187,7 +189,7 @@ struct WinState {
   uint32_t tlog, tmask;
   Key key;
 };
-constexpr uint32_t kStatShards = 256;
+constexpr uint32_t kStatShards = 32;  // per-window counter copies (k_close reads them all: 32 KB)
 constexpr uint32_t kStampPhases = 10;
 constexpr uint32_t kXStamp0 = 2 * kStampPhases;  // k_expand phases (GS_XSTAMPS builds) after k_resolve's
 constexpr uint32_t kDbgWords = kXStamp0 + 8;
@@ -210,8 +212,7 @@ constexpr uint32_t kErrFine = 16;     // a fine region overflowed its estimate
 hipError_t win_units(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
 // device-driven windows (w.ctl set, w.lstride = ctl->lmax)
 hipError_t win_cut(const WinState& w, unsigned long long budget, hipStream_t s);
-hipError_t win_scan_units_masked(const WinState& w, void* tmp, size_t& tmp_bytes, hipStream_t s);
-hipError_t win_consume(const WinState& w, hipStream_t s);
+hipError_t win_unitscan(const WinState& w, hipStream_t s);
 hipError_t win_close(const WinState& w, uint32_t slot, hipStream_t s);
 hipError_t win_scan_units(const WinState& w, uint32_t L, void* tmp, size_t& tmp_bytes, hipStream_t s);
 hipError_t win_groupmap(const WinState& w, uint32_t L, hipStream_t s);

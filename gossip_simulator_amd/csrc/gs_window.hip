@@ -76,6 +76,37 @@ __device__ __forceinline__ uint32_t win_live(const WinState& w, uint32_t& t0, ui
   return w.ctl->L;
 }
 
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
+#pragma unroll
+  for (uint32_t o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Exclusive scan of one u64 per thread over a 256-thread block (s: 4 words
+// of LDS); returns the thread's prefix, *total the block's sum.  Block-uniform.
+__device__ __forceinline__ unsigned long long block_exscan256_u64(unsigned long long v, unsigned long long* s,
+                                                                   unsigned long long* total) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned long long x = v;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s[wv] = x;
+  __syncthreads();
+  unsigned long long before = 0, all = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < 4; ++q) {
+    const unsigned long long t = s[q];
+    if (q < wv) before += t;
+    all += t;
+  }
+  __syncthreads();
+  *total = all;
+  return before + x - v;
+}
+
 // Units = (fine bucket f, tick k), bucket-major (u = f*Ls + k, Ls = the layout
 // stride: L, or lmax for device-driven windows): the L fire lists of one
 // bucket are expanded back to back, so friends-row lines that several ticks of
@@ -101,8 +132,10 @@ __global__ void k_units(const WinState w, uint32_t t0, uint32_t L) {
   if (threadIdx.x < kMaxWindow) s_t[threadIdx.x] = 0;
   if (tid == 0) w.usize[units] = 0;
   __syncthreads();
+  __shared__ uint32_t s_ts[kMaxWindow];  // this tile's fires per tick
   for (uint32_t f0 = blockIdx.x * 256; f0 < w.nfine; f0 += gridDim.x * 256) {
     const uint32_t f = f0 + threadIdx.x;
+    if (threadIdx.x < kMaxWindow) s_ts[threadIdx.x] = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kMaxWindow; ++k) {
       if (k >= Ls) break;
@@ -112,6 +145,16 @@ __global__ void k_units(const WinState w, uint32_t t0, uint32_t L) {
       acc[k] += c;
     }
     __syncthreads();
+    // per-tile sums for the device-driven unit scan (k_cut, k_unitscan)
+#pragma unroll
+    for (uint32_t k = 0; k < kMaxWindow; ++k) {
+      if (k < Ls) {
+        const uint32_t c = wave_sum32(s_tile[threadIdx.x * (kMaxWindow + 1) + k]);
+        if ((threadIdx.x & 63) == 0 && c) atomicAdd(&s_ts[k], c);
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < Ls) w.tsum[(size_t)(f0 >> 8) * kMaxWindow + threadIdx.x] = s_ts[threadIdx.x];
     const uint32_t nb = min(256u, w.nfine - f0), base = f0 * Ls;
     for (uint32_t i = threadIdx.x; i < nb * Ls; i += 256) {
       const uint32_t b = i / Ls, k = i - b * Ls;
@@ -138,12 +181,21 @@ __global__ void k_units(const WinState w, uint32_t t0, uint32_t L) {
 __global__ void k_cut(const WinState w, unsigned long long budget) {
   __shared__ unsigned long long s_sz[256];
   __shared__ unsigned long long s_T;
-  __shared__ uint32_t s_go;
+  __shared__ uint32_t s_go, s_L;
   WinCtl* c = w.ctl;
   const uint32_t b = threadIdx.x;  // 256 threads: thread b plans coarse bin b
+  __shared__ unsigned long long s_tf[kMaxWindow];
   if (win_abort(w)) return;  // keep ctl: the host redoes the failed window
   uint32_t t = 0;
   const uint32_t Lw = win_open(w, t);
+  // every load this kernel needs is issued up front (one latency, not a chain)
+  if (b < kMaxWindow) s_tf[b] = w.tfires[b];
+  unsigned long long ts[4][kMaxWindow];  // this thread's tiles' fires per tick
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j)
+#pragma unroll
+    for (uint32_t k = 0; k < kMaxWindow; ++k)
+      ts[j][k] = Lw && b * 4 + j < w.ncoarse ? w.tsum[(size_t)(b * 4 + j) * kMaxWindow + k] : 0ull;
   __syncthreads();
   if (b == 0) {
     s_go = Lw != 0;
@@ -152,11 +204,12 @@ __global__ void k_cut(const WinState w, unsigned long long budget) {
       c->Tn = 0;
     } else {
       uint32_t L = 1;
-      unsigned long long Tn = w.tfires[0];
-      while (L < Lw && (Tn + w.tfires[L]) * w.stride <= budget) Tn += w.tfires[L++];
+      unsigned long long Tn = s_tf[0];
+      while (L < Lw && (Tn + s_tf[L]) * w.stride <= budget) Tn += s_tf[L++];
       for (uint32_t k = 0; k < kMaxWindow; ++k) w.tfires[k] = 0;
       c->t = t;
       c->L = L;
+      s_L = L;
       c->tnext = t + L;
       c->Tn = Tn;
       c->T = Tn * w.stride;
@@ -165,6 +218,29 @@ __global__ void k_cut(const WinState w, unsigned long long budget) {
   }
   __syncthreads();
   if (!s_go) return;
+  {
+    // firing index of each 256-bucket tile's first unit (ticks >= L count as
+    // empty): k_unitscan finishes the scan inside the tiles (ncoarse <= 1024)
+    const uint32_t L = s_L, nt = w.ncoarse;
+    unsigned long long v[4], sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      v[j] = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < kMaxWindow; ++k) v[j] += k < L ? ts[j][k] : 0ull;
+      sum += v[j];
+    }
+    unsigned long long tot;
+    unsigned long long pre = block_exscan256_u64(sum, &s_sz[0], &tot);
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t tile = b * 4 + j;
+      if (tile < nt) w.toff[tile] = pre;
+      pre += v[j];
+    }
+    if (b == 0) w.toff[nt] = tot;
+    __syncthreads();
+  }
   // coarse regions: each sub-region gets 1/8 of its bin's node share of T,
   // plus 512 (plan_coarse on the host)
   const unsigned long long lo = (unsigned long long)b << kCoarseShift;
@@ -190,14 +266,36 @@ __global__ void k_cut(const WinState w, unsigned long long budget) {
   if (b == 255) w.ccap[kRegions] = total;
 }
 
-// Device-driven windows: the window's fire lists are consumed.
-__global__ void k_consume(const WinState w) {
-  uint32_t t0 = 0;
+// Device-driven windows: the unit scan inside each 256-bucket tile (thread =
+// bucket, its Ls units contiguous; ticks >= L count as empty), offset by the
+// tile's start from k_cut, and the group map of those units.  One block per
+// tile.  (Host-driven windows: hipcub scan + k_groupmap.)
+__global__ void k_unitscan(const WinState w) {
+  __shared__ unsigned long long s_x[4];
+  uint32_t t0;
   const uint32_t L = win_live(w, t0, 0);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < L * w.nfine; i += gridDim.x * blockDim.x) {
-    const uint32_t k = i / w.nfine, f = i - k * w.nfine;
-    w.fcount[(size_t)((t0 + k) % w.R) * w.nfine + f] = 0;
+  if (!L) return;
+  const uint32_t Ls = w.lstride, tile = blockIdx.x, f = tile * 256 + threadIdx.x;
+  unsigned long long sz[kMaxWindow], sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kMaxWindow; ++k) {
+    sz[k] = 0;
+    if (k < L && f < w.nfine) sz[k] = w.usize[(size_t)f * Ls + k];
+    sum += sz[k];
   }
+  unsigned long long tot;
+  unsigned long long a = w.toff[tile] + block_exscan256_u64(sum, s_x, &tot);
+  if (f >= w.nfine) return;
+#pragma unroll
+  for (uint32_t k = 0; k < kMaxWindow; ++k) {
+    if (k >= Ls) break;
+    const uint32_t u = f * Ls + k;
+    w.unit_off[u] = a;
+    const unsigned long long b = a + sz[k];
+    for (unsigned long long q = (a + 63) >> 6; (q << 6) < b; ++q) w.gmap[q] = u;
+    a = b;
+  }
+  if (f == w.nfine - 1) w.unit_off[(size_t)w.nfine * Ls] = a;
 }
 
 // gmap[q] = unit holding firing index 64*q.
@@ -232,9 +330,10 @@ __device__ __forceinline__ uint32_t unit_of_wave(const WinState& w, unsigned lon
 }
 
 // Per-tick counters are added into one of kStatShards copies (by workgroup)
-// and summed into the stats ring by k_stats_reduce: tens of thousands of
-// workgroups adding into the same few lines would serialise at the memory-side
-// atomic unit.
+// and summed into the stats ring by k_stats_reduce / k_close: thousands of
+// workgroups adding into the same few lines would serialise at the
+// memory-side atomic unit (32 copies take a dense window's few hundred
+// thousand adds at well under one per microsecond per address).
 __device__ __forceinline__ unsigned long long* shard_row(const WinState& w, uint32_t k) {
   return w.sstats + ((size_t)(blockIdx.x & (kStatShards - 1)) * kMaxWindow + k) * kStatFields;
 }
@@ -257,42 +356,55 @@ __device__ __forceinline__ void xstamp(const WinState& w, unsigned long long& la
 #define XSTAMP(i) ((void)0)
 #endif
 
-__global__ void k_stats_reduce(const WinState w, uint32_t t0, uint32_t L) {
-  if (w.abort_on_err && win_abort(w)) return;  // the redo of the window reduces them
-  const uint32_t tid = threadIdx.x;  // one (tick, field) pair per thread
-  const uint32_t k = tid / kStatFields, fld = tid % kStatFields;
-  if (k >= L) return;
-  unsigned long long sum = 0;
-  for (uint32_t sh = 0; sh < kStatShards; ++sh) {
-    unsigned long long* x = &w.sstats[((size_t)sh * kMaxWindow + k) * kStatFields + fld];
-    sum += *x;
-    *x = 0;
-  }
-  if (sum) w.stats[(size_t)((t0 + k) % kStatSlots) * kStatFields + fld] += sum;
-}
-
 // Device-driven windows: the window's per-tick counters (stats ring, and
 // staging slot `slot` for the host with the window's snapshot), the poll
 // rule's running state and, at a poll tick, gs_run's stop rule
 // (simulator.go:243-248: covered at float32 99 %; the engine also stops when
 // nothing is pending or max_ticks has passed).  One block of 128 threads.
-__global__ void k_close(const WinState w, uint32_t slot) {
+// Sum of stat shard field `i` (= tick * kStatFields + field) over the
+// kStatShards copies, leaving them zeroed: lane group of kCloseLanes lanes
+// per field, each lane kStatShards / kCloseLanes shards with all its loads
+// in flight together.
+constexpr uint32_t kCloseLanes = 8;
+__device__ __forceinline__ unsigned long long stat_shard_sum(const WinState& w, uint32_t i, uint32_t part) {
+  constexpr uint32_t kPer = kStatShards / kCloseLanes;
+  unsigned long long x[kPer], sum = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; ++j) x[j] = w.sstats[(size_t)(j * kCloseLanes + part) * kMaxWindow * kStatFields + i];
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; ++j) {
+    sum += x[j];
+    if (x[j]) w.sstats[(size_t)(j * kCloseLanes + part) * kMaxWindow * kStatFields + i] = 0;
+  }
+#pragma unroll
+  for (uint32_t o = 1; o < kCloseLanes; o <<= 1) sum += __shfl_xor(sum, o, 64);
+  return sum;
+}
+
+__global__ void k_stats_reduce(const WinState w, uint32_t t0, uint32_t L) {  // as k_close's block
+  if (w.abort_on_err && win_abort(w)) return;  // the redo of the window reduces them
+  const uint32_t i = threadIdx.x / kCloseLanes, part = threadIdx.x % kCloseLanes;
+  const uint32_t k = i / kStatFields, fld = i % kStatFields;
+  if (k >= L) return;
+  const unsigned long long sum = stat_shard_sum(w, i, part);
+  if (part == 0 && sum) w.stats[(size_t)((t0 + k) % kStatSlots) * kStatFields + fld] += sum;
+}
+
+__global__ void k_close(const WinState w, uint32_t slot) {  // kMaxWindow * kStatFields * kCloseLanes threads
   __shared__ unsigned long long rows[kMaxWindow][kStatFields];
   WinCtl* c = w.ctl;
   unsigned long long* st = w.stage + (size_t)slot * kStageWords;
   uint32_t t0 = 0;
   const uint32_t L = win_live(w, t0, 0);
-  const uint32_t tid = threadIdx.x, k = tid / kStatFields, fld = tid % kStatFields;
-  if (k < L) {
-    unsigned long long sum = 0;
-    for (uint32_t sh = 0; sh < kStatShards; ++sh) {
-      unsigned long long* x = &w.sstats[((size_t)sh * kMaxWindow + k) * kStatFields + fld];
-      sum += *x;
-      *x = 0;
+  const uint32_t i = threadIdx.x / kCloseLanes, part = threadIdx.x % kCloseLanes, tid = threadIdx.x;
+  const uint32_t k = i / kStatFields, fld = i % kStatFields;
+  if (k < L) {  // k is uniform over each lane group
+    const unsigned long long sum = stat_shard_sum(w, i, part);
+    if (part == 0) {
+      rows[k][fld] = sum;
+      w.stats[(size_t)((t0 + k) % kStatSlots) * kStatFields + fld] = sum;
+      st[8 + k * kStatFields + fld] = sum;
     }
-    rows[k][fld] = sum;
-    w.stats[(size_t)((t0 + k) % kStatSlots) * kStatFields + fld] = sum;
-    st[8 + k * kStatFields + fld] = sum;
   }
   __syncthreads();
   if (tid != 0) return;
@@ -324,8 +436,9 @@ struct ExpandLds {
   uint8_t sbin[SLOTS];
   uint32_t cnt[256];
   uint32_t off[257];
-  unsigned long long gbase[256];
+  unsigned long long gbase[256];          // bin b's message p goes to gbase[b] + p
   unsigned long long cend[256];           // end of coarse region b (ccap[b + 1])
+  uint32_t ovf;                           // a bin of this round overflowed its region
   unsigned long long acc[kMaxWindow][2];  // fired, sent per tick
 };
 
@@ -348,12 +461,6 @@ __device__ __forceinline__ void block_scan256(uint32_t* cnt, uint32_t* off) {
     off[4 * l + 3] = ex + a + b + c;
     if (l == 63) off[256] = x;
   }
-}
-
-__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
-#pragma unroll
-  for (uint32_t o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
 }
 
 // Batched trials: add (a, b) to fields (fa, fb) of row `key` of tstat
@@ -497,6 +604,7 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
   for (unsigned long long rd = rbeg; rd < rend; rd += rstep) {
     sm.cnt[tid] = 0;
     __syncthreads();
+    if (tid == 0) sm.ovf = 0;
     XSTAMP(6);  // the previous round's write-out and this barrier
     uint32_t mm[NPT][MAXS], mt[NPT][MAXS];  // message, bin | rank << 8 (~0u = none)
     uint32_t vv[NPT], kk[NPT];
@@ -590,17 +698,26 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
           sm.sbin[p] = (uint8_t)bin;
         }
     if (mycnt) {
-      if (at + mycnt > cend - cbase) atomicOr(w.err, kErrCoarse);
-      sm.gbase[tid] = cbase + at;
+      if (at + mycnt > cend - cbase) {
+        atomicOr(w.err, kErrCoarse);
+        sm.ovf = 1;
+      }
+      sm.gbase[tid] = cbase + at - sm.off[tid];
     }
     XSTAMP(4);  // scan, reservation, LDS scatter (wave 0's part)
     __syncthreads();
     XSTAMP(5);  // waiting for the other waves
     const uint32_t total = sm.off[256];
-    for (uint32_t p = tid; p < total; p += kExpandBlock) {
-      const uint32_t b = sm.sbin[p];
-      const unsigned long long pos = sm.gbase[b] + (p - sm.off[b]);
-      if (pos < sm.cend[b]) w.cmsg[pos] = sm.sorted[p];
+    // two LDS reads per message; the region bound is checked only in a round
+    // whose reservation overflowed (the window is then redone exactly)
+    if (!sm.ovf) {
+      for (uint32_t p = tid; p < total; p += kExpandBlock) w.cmsg[sm.gbase[sm.sbin[p]] + p] = sm.sorted[p];
+    } else {
+      for (uint32_t p = tid; p < total; p += kExpandBlock) {
+        const uint32_t b = sm.sbin[p];
+        const unsigned long long pos = sm.gbase[b] + p;
+        if (pos < sm.cend[b]) w.cmsg[pos] = sm.sorted[p];
+      }
     }
   }
   if (!WRITE || !add_stats) return;  // an exact redo must not count the window twice
@@ -659,28 +776,46 @@ __global__ void k_plan(const WinState w, bool exact) {
   const uint32_t csub = w.csub;
   unsigned long long cnt = 0;
   uint32_t ntile = 0;
-  for (uint32_t x = 0; x < csub && tid * csub + x < kRegions; ++x) {
-    const unsigned long long f = region_fill(w, tid * csub + x);
-    cnt += f;
-    ntile += (uint32_t)((f + kPartTile - 1) / kPartTile);
+  unsigned long long fl[kCoarseSub];  // unsharded layout (csub = 8): the fills' loads in flight together
+  if (csub == kCoarseSub) {
+#pragma unroll
+    for (uint32_t x = 0; x < kCoarseSub; ++x) fl[x] = region_fill(w, tid * kCoarseSub + x);
+#pragma unroll
+    for (uint32_t x = 0; x < kCoarseSub; ++x) {
+      cnt += fl[x];
+      ntile += (uint32_t)((fl[x] + kPartTile - 1) / kPartTile);
+    }
+  } else {
+    for (uint32_t x = 0; x < csub && tid * csub + x < kRegions; ++x) {
+      const unsigned long long f = region_fill(w, tid * csub + x);
+      cnt += f;
+      ntile += (uint32_t)((f + kPartTile - 1) / kPartTile);
+    }
   }
   const bool live = tid < w.ncoarse;
   // the last coarse bucket may hold fewer than 256 fine buckets
   const uint32_t nf = live ? min(256u, w.nfine - tid * 256) : 1u;
+  __shared__ unsigned long long s_x[4];
   s_cap[tid] = live ? (cnt + cnt / 8 + nf - 1) / nf + 512 : 0;
-  s_base[tid + 1] = s_cap[tid] * 256;
-  s_tp[tid + 1] = live ? ntile : 0;
-  if (tid == 0) { s_base[0] = 0; s_tp[0] = 0; }
-  __syncthreads();
-  if (tid == 0)
-    for (int i = 1; i <= 256; ++i) { s_base[i] += s_base[i - 1]; s_tp[i] += s_tp[i - 1]; }
+  unsigned long long tb, tt;
+  s_base[tid] = block_exscan256_u64(s_cap[tid] * 256, s_x, &tb);
+  s_tp[tid] = (uint32_t)block_exscan256_u64(live ? ntile : 0u, s_x, &tt);
+  if (tid == 0) { s_base[256] = tb; s_tp[256] = (uint32_t)tt; }
   __syncthreads();
   if (blockIdx.x == 0) {  // every region < kRegions is written (256 * csub >= kRegions)
     uint32_t a = s_tp[tid];
-    for (uint32_t x = 0; x < csub && tid * csub + x < kRegions; ++x) {
-      const uint32_t r = tid * csub + x;
-      w.tprefix[r] = a;
-      a += live ? (uint32_t)((region_fill(w, r) + kPartTile - 1) / kPartTile) : 0u;
+    if (csub == kCoarseSub) {
+#pragma unroll
+      for (uint32_t x = 0; x < kCoarseSub; ++x) {
+        w.tprefix[tid * kCoarseSub + x] = a;
+        a += live ? (uint32_t)((fl[x] + kPartTile - 1) / kPartTile) : 0u;
+      }
+    } else {
+      for (uint32_t x = 0; x < csub && tid * csub + x < kRegions; ++x) {
+        const uint32_t r = tid * csub + x;
+        w.tprefix[r] = a;
+        a += live ? (uint32_t)((region_fill(w, r) + kPartTile - 1) / kPartTile) : 0u;
+      }
     }
     if (tid == 255) w.tprefix[kRegions] = s_tp[256];
   }
@@ -709,8 +844,9 @@ struct TileSort {
   uint32_t buf[kPartTile];
   uint32_t cnt[256];
   uint32_t off[257];
-  unsigned long long gbase[256];
+  unsigned long long gbase[256];  // digit b's message p goes to gbase[b] + p
   unsigned long long gend[256];  // end of fine region b (fstart[c*256 + b + 1])
+  uint32_t ovf;                  // a fine region of this tile overflowed
 };
 
 // part2: coarse tiles -> fine regions; message = u_in_fine | k << 14.
@@ -747,6 +883,7 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8
     const unsigned long long base = cb + (unsigned long long)(g - s_tp[r]) * kPartTile;
     if (tid < 256) ts.cnt[tid] = 0;
     __syncthreads();
+    if (tid == 0) ts.ovf = 0;
     constexpr uint32_t kPer = kPartTile / kPartBlock;
     static_assert(kPartTile <= 65536 && kPer % 2 == 0, "two 16-bit ranks per register");
     uint32_t m[kPer], rank[kPer / 2] = {};
@@ -788,16 +925,28 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8
         }
       }
     if (mycnt) {
-      if (at + mycnt > fe - fb) atomicOr(w.err, kErrFine);
-      ts.gbase[tid] = fb + at;
+      if (at + mycnt > fe - fb) {
+        atomicOr(w.err, kErrFine);
+        ts.ovf = 1;
+      }
+      ts.gbase[tid] = fb + at - ts.off[tid];
       ts.gend[tid] = fe;
     }
     __syncthreads();
     const uint32_t total = ts.off[256];
-    for (uint32_t p = tid; p < total; p += kPartBlock) {
-      const uint32_t m1 = ts.buf[p], b = (m1 >> kFineLog) & 255;
-      const unsigned long long pos = ts.gbase[b] + (p - ts.off[b]);
-      if (pos < ts.gend[b]) w.fmsg[pos] = (m1 & (kFineNodes - 1)) | ((m1 >> kCoarseShift) << kFineLog);
+    // two LDS reads per message; the region bound is checked only in a tile
+    // whose reservation overflowed (the window is then redone exactly)
+    if (!ts.ovf) {
+      for (uint32_t p = tid; p < total; p += kPartBlock) {
+        const uint32_t m1 = ts.buf[p];
+        w.fmsg[ts.gbase[(m1 >> kFineLog) & 255] + p] = (m1 & (kFineNodes - 1)) | ((m1 >> kCoarseShift) << kFineLog);
+      }
+    } else {
+      for (uint32_t p = tid; p < total; p += kPartBlock) {
+        const uint32_t m1 = ts.buf[p], b = (m1 >> kFineLog) & 255;
+        const unsigned long long pos = ts.gbase[b] + p;
+        if (pos < ts.gend[b]) w.fmsg[pos] = (m1 & (kFineNodes - 1)) | ((m1 >> kCoarseShift) << kFineLog);
+      }
     }
     __syncthreads();
   }
@@ -1319,6 +1468,11 @@ __global__ __launch_bounds__(ROLLED ? kRolledBlock : kSmallBlock) void k_resolve
   else if (ROLLED && M > 512 && M <= kRolledCap)
     resolve_small_bucket<ROLLED ? 16 : 1, ROLLED>(w, t0, L, f, gm, M, st, sk[wv], fcw[wv]);
   if (ROLLED && M && (threadIdx.x & 63) == 0) w.rlcnt[f] = 0;  // consumed
+  // device-driven windows: the window's fire lists of the buckets the body
+  // did not take are consumed here (see resolve_small_bucket); k_resolve and
+  // the rolled replay run after this kernel
+  if (!ROLLED && w.ctl && !(M > 0 && M <= 256) && f < w.nfine && (threadIdx.x & 63) < L)
+    w.fcount[(size_t)((t0 + (threadIdx.x & 63)) % w.R) * w.nfine + f] = 0;
   __syncthreads();
   if (tid < L * 3) {
     const uint32_t k = tid / 3, fld = tid - k * 3;
@@ -1345,7 +1499,15 @@ __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t
     // the bucket's fire-list lengths, staged in this wave's LDS: infections
     // take their list positions with LDS atomics instead of same-address
     // global atomics (one wave owns the bucket)
-    for (uint32_t s = lane; s < w.R; s += 64) fcw[s] = w.fcount[(size_t)s * w.nfine + f];
+    // device-driven windows: k_resolve_small, the first kernel to append to
+    // the fire lists, consumes the window's (k_units counted them, k_expand
+    // read them): ring slots t0 .. t0 + L - 1 restart at 0 in every bucket
+    // before any infection of this window is appended (a short ring may
+    // reuse them)
+    const bool consume = !ROLLED && w.ctl;
+    const uint32_t s0 = t0 % w.R;
+    for (uint32_t s = lane; s < w.R; s += 64)
+      fcw[s] = consume && (s + w.R - s0) % w.R < L ? 0u : w.fcount[(size_t)s * w.nfine + f];
     uint32_t knode0, c3order;  // keys of the bucket's nodes (one trial per bucket)
     node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + (f << kFineLog), K_ORDER, knode0, c3order);
     const uint32_t c3delay = (c3order & 0xFFFFFFu) | (K_DELAY << 24);
@@ -1453,8 +1615,11 @@ __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (__ballot(any_inf))
+    if (__ballot(any_inf)) {
       for (uint32_t s = lane; s < w.R; s += 64) w.fcount[(size_t)s * w.nfine + f] = fcw[s];
+    } else if (consume && lane < L) {
+      w.fcount[(size_t)((t0 + lane) % w.R) * w.nfine + f] = 0;
+    }
     if (w.tstat) {  // batched trials: this bucket's counters go to its trial's rows
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -1537,31 +1702,13 @@ hipError_t win_cut(const WinState& w, unsigned long long budget, hipStream_t s) 
   return hipGetLastError();
 }
 
-// Device-driven windows: units of ticks >= ctl->L count as empty.
-struct MaskedUnits {
-  const unsigned long long* usize;
-  const WinCtl* ctl;
-  uint32_t lstride;
-  __device__ __forceinline__ unsigned long long operator()(const uint32_t& u) const {
-    return (u % lstride) < ctl->L ? usize[u] : 0ull;
-  }
-};
-
-hipError_t win_scan_units_masked(const WinState& w, void* tmp, size_t& tmp_bytes, hipStream_t s) {
-  hipcub::CountingInputIterator<uint32_t> it(0);
-  hipcub::TransformInputIterator<unsigned long long, MaskedUnits, hipcub::CountingInputIterator<uint32_t>> in(
-      it, MaskedUnits{w.usize, w.ctl, w.lstride});
-  return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, in, w.unit_off, (int)(w.lstride * w.nfine + 1), s);
-}
-
-hipError_t win_consume(const WinState& w, hipStream_t s) {
-  const uint32_t blocks = std::min<uint32_t>((w.lstride * w.nfine + 255) / 256, 2048);
-  hipLaunchKernelGGL(k_consume, dim3(blocks), dim3(256), 0, s, w);
+hipError_t win_unitscan(const WinState& w, hipStream_t s) {
+  hipLaunchKernelGGL(k_unitscan, dim3(w.ncoarse), dim3(256), 0, s, w);
   return hipGetLastError();
 }
 
 hipError_t win_close(const WinState& w, uint32_t slot, hipStream_t s) {
-  hipLaunchKernelGGL(k_close, dim3(1), dim3(kMaxWindow * kStatFields), 0, s, w, slot);
+  hipLaunchKernelGGL(k_close, dim3(1), dim3(kMaxWindow * kStatFields * kCloseLanes), 0, s, w, slot);
   return hipGetLastError();
 }
 
@@ -1587,7 +1734,19 @@ hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, i
   const uint32_t rs = w.slots;  // rows may be padded past the longest one
   const uint32_t per_round = rs <= 8 ? kExpandBlock * (rs <= 6 ? npt : kExpandNpt) : kExpandBlock;
   const uint64_t rounds = (Tn + per_round - 1) / per_round;
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>(rounds, 8192);
+  // persistent grid: four workgroups per CU (the LDS holds four), whatever the
+  // window's size -- a sparse window then costs one wave of workgroups, not
+  // several (GS_XGRID: A/B knob)
+  static const uint64_t cap = [] {
+    const char* e = getenv("GS_XGRID");
+    if (e) return (uint64_t)std::max(atoi(e), 8);
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      return (uint64_t)v * 4;
+    return (uint64_t)1024;
+  }();
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>(rounds, cap);
   const dim3 grid(blocks ? blocks : 1), blk(kExpandBlock);
   const unsigned long long tn = Tn;
   const int st = mode == 1 ? 1 : 0;
@@ -1660,7 +1819,7 @@ hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s
 }
 
 hipError_t win_stats_reduce(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s) {
-  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(kMaxWindow * kStatFields), 0, s, w, t0, L);
+  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(kMaxWindow * kStatFields * kCloseLanes), 0, s, w, t0, L);
   return hipGetLastError();
 }
 
