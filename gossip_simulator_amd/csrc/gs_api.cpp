@@ -89,7 +89,7 @@ struct gs_ctx {
   // device-driven windows (run_async)
   WinCtl* d_ctl = nullptr;
   unsigned long long* d_stage = nullptr;  // [kSlots][kStageWords]
-  unsigned long long* h_stage = nullptr;  // pinned copy
+  unsigned long long* h_stage = nullptr;  // pinned, mapped: d_stage is its device address
   std::vector<hipEvent_t> wev;            // one per staging slot
   bool async_off = false;                 // GS_SYNC_WINDOWS=1: host-driven windows only (A/B tests)
   bool winlog = false;                    // GS_WINLOG=1: one stderr line per device-driven window
@@ -665,8 +665,7 @@ void destroy_one(gs_ctx* c) {
   for (void* ptr : {(void*)c->h_cap, (void*)c->h_misc, (void*)c->h_err, (void*)c->h_stats, (void*)c->h_tstat,
                     (void*)c->h_stage, (void*)c->h_rtab, (void*)c->h_glay})
     if (ptr) (void)hipHostFree(ptr);
-  for (void* ptr : {(void*)c->d_ctl, (void*)c->d_stage})
-    if (ptr) (void)hipFree(ptr);
+  if (c->d_ctl) (void)hipFree(c->d_ctl);  // (d_stage maps h_stage)
   for (hipEvent_t e : c->wev) (void)hipEventDestroy(e);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
@@ -2138,8 +2137,10 @@ uint64_t cover_threshold(uint64_t n) {  // smallest r with covered(r, n)
 int async_setup(gs_ctx* c) {
   if (!c->d_ctl) {
     CK(c, hipMalloc(&c->d_ctl, sizeof(WinCtl)));
-    CK(c, hipMalloc(&c->d_stage, (size_t)kSlots * kStageWords * 8));
-    CK(c, hipHostMalloc((void**)&c->h_stage, (size_t)kSlots * kStageWords * 8));
+    // k_close writes each window's results straight into pinned host memory
+    // (no copy launch per window); d_stage is its device address
+    CK(c, hipHostMalloc((void**)&c->h_stage, (size_t)kSlots * kStageWords * 8, hipHostMallocMapped));
+    CK(c, hipHostGetDevicePointer((void**)&c->d_stage, c->h_stage, 0));
     for (uint32_t i = 0; i < kSlots; ++i) {
       hipEvent_t e;
       CK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -2200,8 +2201,6 @@ int run_async(gs_ctx* c, uint64_t tend, uint32_t poll, uint64_t max_ticks, OnTic
     CK(c, win_part2(w, T_bound, true, c->stream));
     CK(c, win_resolve(w, 0, w.lstride, c->stream));
     CK(c, win_close(w, slot, c->stream));
-    CK(c, hipMemcpyAsync(c->h_stage + (size_t)slot * kStageWords, c->d_stage + (size_t)slot * kStageWords,
-                         kStageWords * 8, hipMemcpyDeviceToHost, c->stream));
     CK(c, hipEventRecord(c->wev[slot], c->stream));
     return GS_OK;
   };

@@ -56,14 +56,27 @@ constexpr uint32_t kRoll0Fine = kFineLog + 4;
 __device__ __forceinline__ bool win_abort(const WinState& w) {
   return (*w.err & (kErrCoarse | kErrFine)) != 0;
 }
+// The window control block's first 32 bytes (t, L, tnext, tend, poll, pbase,
+// stop, lmax) and the error word, all loaded before any is tested: a kernel
+// of a window pays one load latency for them, not a chain of dependent ones.
+struct CtlView {
+  uint32_t t, L, tnext, tend, poll, pbase, stop, lmax, err;
+};
+__device__ __forceinline__ CtlView ctl_view(const WinState& w) {
+  static_assert(offsetof(WinCtl, t) == 0 && offsetof(WinCtl, lmax) == 28, "WinCtl's first 32 bytes");
+  const uint4* p = reinterpret_cast<const uint4*>(w.ctl);
+  const uint4 a = p[0], b = p[1];
+  const uint32_t e = *w.err;
+  return CtlView{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, e};
+}
 __device__ __forceinline__ uint32_t win_open(const WinState& w, uint32_t& t) {
-  const WinCtl* c = w.ctl;
-  if (win_abort(w) || c->stop) return 0;
-  t = c->tnext;
-  if (t >= c->tend) return 0;
-  uint32_t Lw = min(c->lmax, c->tend - t);
-  if (c->poll) {
-    const uint32_t P = c->pbase + c->poll * ((t - c->pbase + c->poll - 1) / c->poll);  // next poll tick
+  const CtlView c = ctl_view(w);
+  if ((c.err & (kErrCoarse | kErrFine)) || c.stop) return 0;
+  t = c.tnext;
+  if (t >= c.tend) return 0;
+  uint32_t Lw = min(c.lmax, c.tend - t);
+  if (c.poll) {
+    const uint32_t P = c.pbase + c.poll * ((t - c.pbase + c.poll - 1) / c.poll);  // next poll tick
     Lw = min(Lw, P - t + 1);
   }
   return Lw;
@@ -71,9 +84,10 @@ __device__ __forceinline__ uint32_t win_open(const WinState& w, uint32_t& t) {
 // A kernel of an opened window: its start and length (0: skip the window).
 __device__ __forceinline__ uint32_t win_live(const WinState& w, uint32_t& t0, uint32_t L) {
   if (!w.ctl) return w.abort_on_err && win_abort(w) ? 0u : L;  // shards: a window that overflowed is redone
-  if (win_abort(w)) return 0;
-  t0 = w.ctl->t;
-  return w.ctl->L;
+  const CtlView c = ctl_view(w);
+  if (c.err & (kErrCoarse | kErrFine)) return 0;
+  t0 = c.t;
+  return c.L;
 }
 
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
