@@ -69,6 +69,8 @@ def parse():
                     help="at --gpus 1: per-shard device time of G = 1/2/4/8 in-process shards (C4 at N=1e8, "
                          "C5's flood at N=1e9 with G=8)")
     ap.add_argument("--pp-shards", type=int, default=8, help="in-process push-pull shards at --gpus 1")
+    ap.add_argument("--ext-deadline", type=float, default=300.0,
+                    help="seconds the extension legs may take before the line is printed without the rest")
     return ap.parse_args()
 
 
@@ -76,15 +78,67 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+_LEG = ["headline"]  # the leg running now (for the deadline watchdog)
+
+
 def guarded(name, fn):
     """An extension leg that raises is recorded as {"error": ...} so the
     headline line still prints (every rank runs the same legs, so a
     parameter error raises on all of them alike)."""
+    _LEG[0] = name
     try:
         return fn()
     except Exception as e:  # noqa: BLE001 -- reported in the line, not hidden
         log(f"{name} failed: {type(e).__name__}: {e}")
         return {"error": f"{type(e).__name__}: {e}"}
+
+
+class Emitter:
+    """Rank 0 prints the ONE JSON line exactly once.  The extension legs run
+    under a deadline (--ext-deadline s): a leg that blocks -- e.g. a
+    collective of a multi-rank path waiting on a peer that failed -- must not
+    swallow the headline, so when the deadline passes rank 0 prints the line
+    with the unfinished leg marked and every rank exits at once."""
+
+    def __init__(self, rank):
+        import threading
+        self.rank = rank
+        self.lock = threading.Lock()
+        self.done = False
+        self.line = None
+        self.timer = None
+
+    def emit(self):
+        with self.lock:
+            if self.done:
+                return
+            self.done = True
+            if self.rank == 0 and self.line is not None:
+                try:
+                    text = json.dumps(self.line)
+                except RuntimeError:  # a leg changed the extensions dict meanwhile
+                    text = json.dumps(dict(self.line, extensions={"error": "deadline while a leg was writing"}))
+                print(text, flush=True)
+
+    def arm(self, seconds, ext):
+        import threading
+
+        def fire():
+            log(f"extension deadline ({seconds:.0f} s) passed in leg {_LEG[0]}: printing the line and exiting")
+            if ext is not None:
+                ext[_LEG[0]] = {"error": f"deadline: unfinished after {seconds:.0f} s of extension legs"}
+            self.emit()
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
+
+        self.timer = threading.Timer(seconds, fire)
+        self.timer.daemon = True
+        self.timer.start()
+
+    def disarm(self):
+        if self.timer is not None:
+            self.timer.cancel()
 
 
 def main():
@@ -179,9 +233,42 @@ def main():
                 "broadcast_device_ms": round(kern_ms, 3)}
         sim.set_flags(False)
 
-    ext = None
-    if not a.no_extensions:
-        ext = {"flood_failed_1pct": guarded("flood_failed_1pct", lambda: flood_failed(a, sim))}
+    ext = None if a.no_extensions else {}
+    out = Emitter(rank)
+    out.line = {
+        "metric": "gossip messages delivered/sec (node) at N=1e9; rounds-to-coverage parity",
+        "value": round(value, 1),
+        "unit": "msgs/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed * 1e3 / a.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (GPU-built overlay, keyed Philox)",
+        "config": {"workload": "C5-reference-model: single push-flood broadcast per GPU",
+                   "value_counts": "delivered sends (simulator.go:144-145), not TotalMessage (:111)",
+                   "n": a.n, "fanout": a.fanout, "fanin": a.fanin,
+                   "delaylow": a.delaylow, "delayhigh": a.delayhigh,
+                   "droprate": a.droprate, "crashrate": a.crashrate,
+                   # a step ends at the first 10-tick poll with float32 coverage
+                   # >= 99 % (covered) or with no broadcast pending (quiescent:
+                   # with crashrate 0.01 about 1 % of the nodes crash on their
+                   # first receipt, so 99 % can be out of reach)
+                   "ticks": ticks[-1], "status": STATUS[status],
+                   "coverage": round(recv_last / a.n, 6),
+                   "delivered_per_step": sent // a.steps,
+                   "messages_per_step": msgs, "overlay_s": round(overlay_s, 3),
+                   "overlay_stabilised_ms": stab, "parallelism": f"trials{world}"},
+        "roofline": roof,
+        "cpu_baseline": None,
+        "extensions": ext,
+    }
+    if ext is not None:
+        out.arm(a.ext_deadline, ext)
+        ext["flood_failed_1pct"] = guarded("flood_failed_1pct", lambda: flood_failed(a, sim))
     sim.close()
     if not a.no_extensions:
         pp = guarded("pushpull", lambda: pushpull_runs(a, gs, rank, local))
@@ -197,44 +284,13 @@ def main():
                                              lambda: pushpull_sharded(a, gs, rank, world, local, dist))
         if world == 1 and a.shard_scaling:
             ext["c4_shards_inproc"] = guarded("c4_shards_inproc", lambda: shards_inproc(a, gs))
+    out.disarm()
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_n > 0:
         cpu = cpu_baseline(a, gs)
-
-    if rank == 0:
-        line = {
-            "metric": "gossip messages delivered/sec (node) at N=1e9; rounds-to-coverage parity",
-            "value": round(value, 1),
-            "unit": "msgs/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(elapsed * 1e3 / a.steps, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic (GPU-built overlay, keyed Philox)",
-            "config": {"workload": "C5-reference-model: single push-flood broadcast per GPU",
-                       "value_counts": "delivered sends (simulator.go:144-145), not TotalMessage (:111)",
-                       "n": a.n, "fanout": a.fanout, "fanin": a.fanin,
-                       "delaylow": a.delaylow, "delayhigh": a.delayhigh,
-                       "droprate": a.droprate, "crashrate": a.crashrate,
-                       # a step ends at the first 10-tick poll with float32 coverage
-                       # >= 99 % (covered) or with no broadcast pending (quiescent:
-                       # with crashrate 0.01 about 1 % of the nodes crash on their
-                       # first receipt, so 99 % can be out of reach)
-                       "ticks": ticks[-1], "status": STATUS[status],
-                       "coverage": round(recv_last / a.n, 6),
-                       "delivered_per_step": sent // a.steps,
-                       "messages_per_step": msgs, "overlay_s": round(overlay_s, 3),
-                       "overlay_stabilised_ms": stab, "parallelism": f"trials{world}"},
-            "roofline": roof,
-            "cpu_baseline": cpu,
-            "extensions": ext,
-        }
-        print(json.dumps(line), flush=True)
+    out.line["cpu_baseline"] = cpu
+    out.emit()
     if dist is not None:
         dist.destroy_process_group()
 
