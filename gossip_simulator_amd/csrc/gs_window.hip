@@ -1748,9 +1748,10 @@ hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, i
   const uint32_t rs = w.slots;  // rows may be padded past the longest one
   const uint32_t per_round = rs <= 8 ? kExpandBlock * (rs <= 6 ? npt : kExpandNpt) : kExpandBlock;
   const uint64_t rounds = (Tn + per_round - 1) / per_round;
-  // persistent grid: four workgroups per CU (the LDS holds four), whatever the
-  // window's size -- a sparse window then costs one wave of workgroups, not
-  // several (GS_XGRID: A/B knob)
+  // rows <= 8 slots: a persistent grid of four workgroups per CU (the LDS
+  // holds four) whatever the window's size -- a sparse window then costs one
+  // wave of workgroups, not several (GS_XGRID: A/B knob).  Longer rows (the
+  // 20- and 32-slot instances fit more workgroups per CU): up to 8192.
   static const uint64_t cap = [] {
     const char* e = getenv("GS_XGRID");
     if (e) return (uint64_t)std::max(atoi(e), 8);
@@ -1760,7 +1761,7 @@ hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, i
       return (uint64_t)v * 4;
     return (uint64_t)1024;
   }();
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>(rounds, cap);
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>(rounds, rs <= 8 ? cap : 8192);
   const dim3 grid(blocks ? blocks : 1), blk(kExpandBlock);
   const unsigned long long tn = Tn;
   const int st = mode == 1 ? 1 : 0;
