@@ -584,10 +584,10 @@ __device__ __forceinline__ void xcd_rounds(unsigned long long rounds, unsigned l
   }
 }
 
-template <bool WRITE, uint32_t MAXS, uint32_t NPT>
-__global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint32_t t0, uint32_t L,
-                                                         unsigned long long Tn, int add_stats) {
-  __shared__ ExpandLds<kExpandBlock * NPT * MAXS> sm;
+template <bool WRITE, uint32_t MAXS, uint32_t NPT, uint32_t B = kExpandBlock>
+__global__ __launch_bounds__(B) void k_expand(const WinState w, uint32_t t0, uint32_t L,
+                                              unsigned long long Tn, int add_stats) {
+  __shared__ ExpandLds<B * NPT * MAXS> sm;
   const uint32_t tid = threadIdx.x;
   uint32_t Ls = L;  // unit layout stride
   if (w.ctl) {
@@ -597,17 +597,18 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
     Ls = w.lstride;
   }
   const uint32_t units = Ls * w.nfine;
-  constexpr uint32_t per_round = kExpandBlock * NPT;
+  constexpr uint32_t per_round = B * NPT;
   if (tid < kMaxWindow * 2) (&sm.acc[0][0])[tid] = 0;
-  static_assert(kExpandBlock == 256, "thread b owns coarse bin b");
-  const uint32_t reg = tid * kCoarseSub + (blockIdx.x & (kCoarseSub - 1));  // bin tid, this XCD's sub-region
+  static_assert(B % 256 == 0, "thread b < 256 owns coarse bin b");
+  const bool binner = tid < 256;
+  const uint32_t reg = (tid & 255) * kCoarseSub + (blockIdx.x & (kCoarseSub - 1));  // bin tid, this XCD's sub-region
   const unsigned long long cbase = w.ccap[reg], cend = w.ccap[reg + 1];
-  sm.cend[tid] = cend;
+  if (binner) sm.cend[tid] = cend;
   const unsigned long long rounds = (Tn + per_round - 1) / per_round;
   unsigned long long rbeg, rend, rstep;
   xcd_rounds(rounds, rbeg, rend, rstep);
-  // per-tick fired | sent << 16 of this thread's nodes (<= 1024 nodes per
-  // thread per launch): registers, not same-address LDS atomics per node
+  // per-tick fired | sent << 16 of this thread's nodes (<= 1024 rounds per
+  // workgroup, win_expand): registers, not same-address LDS atomics per node
   uint32_t accp[kBitTicks];
 #pragma unroll
   for (uint32_t kx = 0; kx < kBitTicks; ++kx) accp[kx] = 0;
@@ -616,7 +617,7 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
   XSTAMP(0);
 #endif
   for (unsigned long long rd = rbeg; rd < rend; rd += rstep) {
-    sm.cnt[tid] = 0;
+    if (binner) sm.cnt[tid] = 0;
     __syncthreads();
     if (tid == 0) sm.ovf = 0;
     XSTAMP(6);  // the previous round's write-out and this barrier
@@ -624,7 +625,7 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
     uint32_t vv[NPT], kk[NPT];
 #pragma unroll
     for (uint32_t q = 0; q < NPT; ++q) {
-      const unsigned long long g0 = rd * per_round + q * kExpandBlock + __builtin_amdgcn_readfirstlane(tid & ~63u);
+      const unsigned long long g0 = rd * per_round + q * B + __builtin_amdgcn_readfirstlane(tid & ~63u);
       const unsigned long long g = g0 + (tid & 63);
       vv[q] = ~0u;
       kk[q] = 0;
@@ -692,13 +693,13 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
     XSTAMP(3);  // drop / crash draws and LDS ranks
     __syncthreads();
     if (!WRITE) {
-      if (sm.cnt[tid]) atomicAdd(&w.chist[reg], (unsigned long long)sm.cnt[tid]);
+      if (binner && sm.cnt[tid]) atomicAdd(&w.chist[reg], (unsigned long long)sm.cnt[tid]);
       continue;  // the next round's first barrier orders the reuse of sm.cnt
     }
     block_scan256(sm.cnt, sm.off);
     // thread b reserves bin b's run; the atomic's return latency overlaps the
     // LDS scatter below (which needs only off[] from the scan)
-    const uint32_t mycnt = sm.cnt[tid];
+    const uint32_t mycnt = binner ? sm.cnt[tid] : 0u;
     unsigned long long at = 0;
     if (mycnt) at = atomicAdd(&w.cfill[reg], (unsigned long long)mycnt);
     __syncthreads();
@@ -725,9 +726,9 @@ __global__ __launch_bounds__(kExpandBlock) void k_expand(const WinState w, uint3
     // two LDS reads per message; the region bound is checked only in a round
     // whose reservation overflowed (the window is then redone exactly)
     if (!sm.ovf) {
-      for (uint32_t p = tid; p < total; p += kExpandBlock) w.cmsg[sm.gbase[sm.sbin[p]] + p] = sm.sorted[p];
+      for (uint32_t p = tid; p < total; p += B) w.cmsg[sm.gbase[sm.sbin[p]] + p] = sm.sorted[p];
     } else {
-      for (uint32_t p = tid; p < total; p += kExpandBlock) {
+      for (uint32_t p = tid; p < total; p += B) {
         const uint32_t b = sm.sbin[p];
         const unsigned long long pos = sm.gbase[b] + p;
         if (pos < sm.cend[b]) w.cmsg[pos] = sm.sorted[p];
@@ -1746,7 +1747,18 @@ hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, i
   // GS_XNPT=2: two firing nodes per thread (experiment: LDS and VGPRs for 8 workgroups per CU)
   static const uint32_t npt = [] { const char* e = getenv("GS_XNPT"); return e && atoi(e) == 2 ? 2u : kExpandNpt; }();
   const uint32_t rs = w.slots;  // rows may be padded past the longest one
-  const uint32_t per_round = rs <= 8 ? kExpandBlock * (rs <= 6 ? npt : kExpandNpt) : kExpandBlock;
+  // rows <= 6 (C5), 4 nodes per thread: 512-thread workgroups (2048 rows per
+  // round, two per CU by LDS): the per-round scan, reservations and barriers
+  // cost half as much per message and a bin's run per round doubles (~40
+  // messages); 256 (four per CU) and 1024 (one per CU) measured slower
+  // (GS_XBLOCK = 256 / 512 / 1024: A/B knob)
+  static const uint32_t xb = [] {
+    const char* e = getenv("GS_XBLOCK");
+    const int v = e ? atoi(e) : 512;
+    return v == 512 || v == 1024 ? (uint32_t)v : kExpandBlock;
+  }();
+  const uint32_t bsz = rs <= 6 && npt == kExpandNpt ? xb : kExpandBlock;
+  const uint32_t per_round = rs <= 8 ? bsz * (rs <= 6 ? npt : kExpandNpt) : kExpandBlock;
   const uint64_t rounds = (Tn + per_round - 1) / per_round;
   // rows <= 8 slots: a persistent grid of four workgroups per CU (the LDS
   // holds four) whatever the window's size -- a sparse window then costs one
@@ -1761,13 +1773,22 @@ hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, i
       return (uint64_t)v * 4;
     return (uint64_t)1024;
   }();
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>(rounds, rs <= 8 ? cap : 8192);
+  // (a thread counts fired | sent << 16 of its nodes in 16-bit halves: at most
+  // 1024 rounds per workgroup, <= 4096 nodes and 32768 sends per thread)
+  const uint64_t grid_cap = std::max<uint64_t>(rs <= 8 ? cap * kExpandBlock / bsz : 8192, (rounds + 1023) / 1024);
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>(rounds, grid_cap);
   const dim3 grid(blocks ? blocks : 1), blk(kExpandBlock);
   const unsigned long long tn = Tn;
   const int st = mode == 1 ? 1 : 0;
   if (rs <= 6 && npt == 2) {
     if (mode) hipLaunchKernelGGL((k_expand<true, 6, 2>), grid, blk, 0, s, w, t0, L, tn, st);
     else hipLaunchKernelGGL((k_expand<false, 6, 2>), grid, blk, 0, s, w, t0, L, tn, 0);
+  } else if (rs <= 6 && bsz == 1024) {
+    if (mode) hipLaunchKernelGGL((k_expand<true, 6, kExpandNpt, 1024>), grid, dim3(1024), 0, s, w, t0, L, tn, st);
+    else hipLaunchKernelGGL((k_expand<false, 6, kExpandNpt, 1024>), grid, dim3(1024), 0, s, w, t0, L, tn, 0);
+  } else if (rs <= 6 && bsz == 512) {
+    if (mode) hipLaunchKernelGGL((k_expand<true, 6, kExpandNpt, 512>), grid, dim3(512), 0, s, w, t0, L, tn, st);
+    else hipLaunchKernelGGL((k_expand<false, 6, kExpandNpt, 512>), grid, dim3(512), 0, s, w, t0, L, tn, 0);
   } else if (rs <= 6) {
     if (mode) hipLaunchKernelGGL((k_expand<true, 6, kExpandNpt>), grid, blk, 0, s, w, t0, L, tn, st);
     else hipLaunchKernelGGL((k_expand<false, 6, kExpandNpt>), grid, blk, 0, s, w, t0, L, tn, 0);
