@@ -115,7 +115,9 @@ __device__ __forceinline__ void process_chunk(const DevState& st, uint32_t t, ui
       if (j >= st.deg[v]) continue;
       // RandomDrop per friend slot (simulator.go:144, :172)
       const u32x4 r = philox(v, t, j >> 2, c3drop, st.key.k0, st.key.k1);
-      if ((int32_t)uniform(lane_of(r, j & 3), 100u) < st.kd) continue;
+      uint32_t dropd, crashd;  // the drop draw and the message's crash roll (:180)
+      drop_crash(lane_of(r, j & 3), dropd, crashd);
+      if ((int32_t)dropd < st.kd) continue;
       const uint32_t u = st.ids[(size_t)v * S + j];        // GlobalView[id] (:145)
       if (u < st.lo || u >= st.hi) continue;               // another shard's target
       if (MODE == MODE_FLOOD) {
@@ -131,9 +133,8 @@ __device__ __forceinline__ void process_chunk(const DevState& st, uint32_t t, ui
         }
       } else if (MODE == MODE_COUNT) {
         c.v[ST_SENT]++;
-        // the message's crash roll (:180), keyed by its sender's slot
-        const uint32_t roll = (int32_t)uniform(lane_of(philox(v, t, j >> 2, ctr3(K_CRASH, st.key.trial),
-                                                             st.key.k0, st.key.k1), j & 3), 100u) < st.kc;
+        // the message's crash roll (:180), from its drop draw's second base-100 digit
+        const uint32_t roll = (int32_t)crashd < st.kc;
         // receipts | crash rolls << 16: the receipt count is 16 bits, so the
         // 65536th arrival at one node in one tick is an overflow (GS_EOVERFLOW)
         const uint32_t old = atomicAdd(&st.cnt[u], 1u + (roll << 16));

@@ -5,9 +5,9 @@
 // which lane, block, XCD or GPU makes it:
 //   kind SENDER  simulator.go:240   ctr {0, 0, 0, .}            out[0] -> U_n
 //   kind DELAY   simulator.go:167   ctr {v, t, 0, .}            out[0] -> U_(high-low)
-//   kind DROP    simulator.go:172   ctr {v, t, j/4, .}          out[j%4] -> U_100
-//   kind CRASH   simulator.go:180   ctr {v, t, j/4, .}          out[j%4] -> U_100 (the crash roll
-//                                   a message from sender v, fire tick t, slot j carries)
+//   kind DROP    simulator.go:172   ctr {v, t, j/4, .}          out[j%4] = r -> drop = U_100(r)
+//                simulator.go:180   and the crash roll the message from sender v, fire tick t,
+//                                   slot j carries: U_100(100 r mod 2^32) (drop_crash below)
 //   kind PICK    simulator.go:97    ctr {v, 0, j, .}            out[0] -> U_n
 //   kind OVDELAY simulator.go:153,160 ctr {u, t, k, .}          out[0] -> U_(high-low)
 //   kind VICTIM  simulator.go:71    ctr {u, t, k, .}            out[0] -> U_deg
@@ -23,7 +23,7 @@
 namespace gs {
 
 enum Kind : uint32_t {
-  K_SENDER = 1, K_DELAY = 2, K_DROP = 3, K_CRASH = 4,
+  K_SENDER = 1, K_DELAY = 2, K_DROP = 3, K_CRASH = 4,  // K_CRASH: reserved (round 2's crash-roll stream)
   K_PICK = 5, K_OVDELAY = 6, K_VICTIM = 7, K_REPLACE = 8,
   K_PUSHPULL = 9,  // push-pull extension: peer pick + loss per (node, round)
   K_ORDER = 10     // receipt order of a (node, tick): first-crash position
@@ -75,6 +75,19 @@ __host__ __device__ __forceinline__ uint32_t lane_of(const u32x4& v, uint32_t i)
 
 __host__ __device__ __forceinline__ uint32_t uniform(uint32_t r, uint32_t m) {
   return mulhi32(r, m);
+}
+
+// RandomDrop (simulator.go:172) and the message's RandomCrash roll (:180)
+// from ONE 32-bit draw r: the first two base-100 digits of r / 2^32,
+// drop = floor(100 r / 2^32) and crash = floor(100 (100 r mod 2^32) / 2^32)
+// = floor(10^4 r / 2^32) mod 100.  Each of the 10^4 pairs (drop, crash) is
+// taken by floor(2^32 / 10^4) or one more of the 2^32 words, so the two are
+// independent and uniform to within 2.4e-6 relative.
+__host__ __device__ __forceinline__ void drop_crash(uint32_t r, uint32_t& drop, uint32_t& crash) {
+  uint32_t hi, lo;
+  mul64(r, 100u, hi, lo);
+  drop = hi;
+  crash = mulhi32(lo, 100u);
 }
 
 __host__ __device__ __forceinline__ uint32_t ctr3(uint32_t kind, uint32_t trial) {

@@ -656,22 +656,22 @@ __global__ __launch_bounds__(B) void k_expand(const WinState w, uint32_t t0, uin
       const uint32_t v = vv[q], k = kk[q], t = t0 + k;
       uint32_t vn, c3drop;
       node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + v, K_DROP, vn, c3drop);
-      const uint32_t c3crash = (c3drop & 0xFFFFFFu) | (K_CRASH << 24);
       uint32_t sent = 0;
 #pragma unroll
       for (uint32_t jg = 0; jg < (MAXS + 3) / 4; ++jg) {
         if (mm[q][jg * 4] == kEmptyMsg) break;
-        const u32x4 r = philox(vn, t, jg, c3drop, w.key.k0, w.key.k1);   // :144, :172
-        // the messages' crash rolls (:180), keyed by this sender's slots like the drop
-        const u32x4 rc = w.kc > 0 ? philox(vn, t, jg, c3crash, w.key.k0, w.key.k1) : u32x4{~0u, ~0u, ~0u, ~0u};
+        // :144, :172 and the messages' crash rolls (:180): one draw per slot
+        const u32x4 r = philox(vn, t, jg, c3drop, w.key.k0, w.key.k1);
 #pragma unroll
         for (uint32_t jj = 0; jj < 4; ++jj) {
           const uint32_t j = jg * 4 + jj;
           if (j >= MAXS) break;
-          if (mm[q][j] != kEmptyMsg && (int32_t)uniform(lane_of(r, jj), 100u) >= w.kd) {  // kept: :145
+          uint32_t dropd, crashd;
+          drop_crash(lane_of(r, jj), dropd, crashd);
+          if (mm[q][j] != kEmptyMsg && (int32_t)dropd >= w.kd) {  // kept: :145
             uint32_t loc = mm[q][j];
             const uint32_t bin = coarse_bin(w, loc);
-            const uint32_t roll0 = (int32_t)uniform(lane_of(rc, jj), 100u) < w.kc;
+            const uint32_t roll0 = (int32_t)crashd < w.kc;
             mt[q][j] = bin | (atomicAdd(&sm.cnt[bin], 1u) << 8);
             mm[q][j] = loc | (k << kCoarseShift) | (roll0 << kRoll0Coarse);
             ++sent;

@@ -159,16 +159,15 @@ int om_engine_step(om_engine* e, uint32_t ticks, or_tick_stats* out) {
           ++fired;
           const uint32_t d = e->deg[v];
           const uint32_t* row = e->ids + (uint64_t)v * e->stride;
-          uint32_t rnd[4] = {0, 0, 0, 0}, rc[4] = {0, 0, 0, 0};
+          uint32_t rnd[4] = {0, 0, 0, 0};
           for (uint32_t j = 0; j < d; ++j) {
-            if ((j & 3) == 0) {
-              draw4(e->key, v, (uint32_t)t, j >> 2, OR_K_DROP, e->p.trial, rnd);
-              if (e->kc > 0) draw4(e->key, v, (uint32_t)t, j >> 2, OR_K_CRASH, e->p.trial, rc);
-            }
-            if ((int32_t)or_uniform(rnd[j & 3], 100) < e->kd) continue; /* :144, :172 */
+            if ((j & 3) == 0) draw4(e->key, v, (uint32_t)t, j >> 2, OR_K_DROP, e->p.trial, rnd);
+            uint32_t drop, crash;  /* the drop draw and the message's crash roll (:180) */
+            or_drop_crash(rnd[j & 3], &drop, &crash);
+            if ((int32_t)drop < e->kd) continue;                         /* :144, :172 */
             const uint32_t u = row[j];                                   /* :145 */
             ++sent;
-            const uint32_t roll = e->kc > 0 && (int32_t)or_uniform(rc[j & 3], 100) < e->kc;  /* :180 */
+            const uint32_t roll = (int32_t)crash < e->kc;                /* :180 */
             const uint32_t old = __atomic_fetch_add(&e->cnt[u], 1u + (roll << 16), __ATOMIC_RELAXED);
             if ((old & 0xFFFFu) == 0xFFFFu) ovf = 1;  /* 16-bit receipt count: GS_EOVERFLOW */
             if (old == 0) {

@@ -42,6 +42,12 @@ uint32_t or_uniform(uint32_t r, uint32_t m) {
   return (uint32_t)(((uint64_t)r * (uint64_t)m) >> 32);
 }
 
+void or_drop_crash(uint32_t r, uint32_t* drop, uint32_t* crash) {
+  const uint64_t x = (uint64_t)r * 100u;
+  *drop = (uint32_t)(x >> 32);
+  *crash = or_uniform((uint32_t)x, 100);
+}
+
 uint32_t or_first_crash(const uint32_t key[2], uint32_t trial, uint32_t u, uint32_t t, uint32_t k,
                         uint32_t ones) {
   if (k <= 1 || ones >= k) return 1;
@@ -438,21 +444,19 @@ int or_engine_step(or_engine* e, uint32_t ticks, or_tick_stats* out) {
         if (v >= e->lo && v < e->hi) ++fired;
         uint32_t d = e->deg[v];
         const uint32_t* row = e->ids + (uint64_t)v * e->stride;
-        uint32_t rnd[4] = {0, 0, 0, 0}, rc[4] = {0, 0, 0, 0};
+        uint32_t rnd[4] = {0, 0, 0, 0};
         for (uint32_t j = 0; j < d; ++j) {
           if ((j & 3) == 0) {
             uint32_t ctr[4] = {v, (uint32_t)t, j >> 2, c3of(OR_K_DROP, e->p.trial)};
             or_philox(ctr, e->key, rnd);
-            if (e->kc > 0) {  /* the messages' crash rolls (:180), same counter */
-              ctr[3] = c3of(OR_K_CRASH, e->p.trial);
-              or_philox(ctr, e->key, rc);
-            }
           }
-          if ((int32_t)or_uniform(rnd[j & 3], 100) < e->kd) continue; /* :144,:172 */
+          uint32_t drop, crash;  /* the drop draw and the message's crash roll (:180) */
+          or_drop_crash(rnd[j & 3], &drop, &crash);
+          if ((int32_t)drop < e->kd) continue;                         /* :144,:172 */
           uint32_t u = row[j];                                         /* :145 */
           if (u < e->lo || u >= e->hi) continue;  /* another rank's target */
           ++sent;
-          const uint32_t roll = e->kc > 0 && (int32_t)or_uniform(rc[j & 3], 100) < e->kc;
+          const uint32_t roll = (int32_t)crash < e->kc;
           if (e->cnt[u] == 0) e->touched[nt++] = u;
           /* receipts | crash rolls << 16: a 16-bit count, so >= 65536 arrivals at
            * one node in one tick is an overflow (the engine returns GS_EOVERFLOW) */

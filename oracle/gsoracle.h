@@ -39,9 +39,10 @@ extern "C" {
 enum {
   OR_K_SENDER = 1,  /* simulator.go:240  rand.Intn(len(GlobalView))          */
   OR_K_DELAY = 2,   /* simulator.go:167  RandomNetworkDelay, per Broadcast    */
-  OR_K_DROP = 3,    /* simulator.go:172  RandomDrop, per friend slot          */
-  OR_K_CRASH = 4,   /* simulator.go:180  RandomCrash: one roll per message, keyed by its
-                     * sender's (node, fire tick, slot) like the drop           */
+  OR_K_DROP = 3,    /* simulator.go:172  RandomDrop, per friend slot; the same
+                     * draw's second base-100 digit is the message's RandomCrash
+                     * roll (:180), or_drop_crash                               */
+  OR_K_CRASH = 4,   /* reserved (round 2's separate crash-roll stream)          */
   OR_K_PICK = 5,    /* simulator.go:97   new-friend pick                      */
   OR_K_OVDELAY = 6, /* simulator.go:153,160 Breakup/Makeup delay              */
   OR_K_VICTIM = 7,  /* simulator.go:71   victim slot                          */
@@ -104,6 +105,11 @@ uint32_t or_first_crash(const uint32_t key[2], uint32_t trial, uint32_t u, uint3
                         uint32_t ones);
 /* floor(r * m / 2^32): the uniform-in-[0,m) map shared with the HIP engine. */
 uint32_t or_uniform(uint32_t r, uint32_t m);
+/* RandomDrop (simulator.go:172) and the message's RandomCrash roll (:180)
+ * from one draw r: drop = floor(100 r / 2^32), crash = floor(100 (100 r mod
+ * 2^32) / 2^32) -- the first two base-100 digits of r / 2^32 (each of the
+ * 10^4 pairs is taken by floor(2^32 / 10^4) or one more of the 2^32 words). */
+void or_drop_crash(uint32_t r, uint32_t* drop, uint32_t* crash);
 /* Sender chosen as simulator.go:240 does, from the keyed stream. */
 uint64_t or_pick_sender(const or_params* p);
 

@@ -74,6 +74,7 @@ def lib():
         L.or_philox.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
         L.or_uniform.argtypes = [C.c_uint32, C.c_uint32]
         L.or_uniform.restype = C.c_uint32
+        L.or_drop_crash.argtypes = [C.c_uint32, P(C.c_uint32), P(C.c_uint32)]
         L.or_first_crash.argtypes = [P(C.c_uint32), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                      C.c_uint32]
         L.or_first_crash.restype = C.c_uint32

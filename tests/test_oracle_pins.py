@@ -64,6 +64,33 @@ def test_uniform_map(oracle):
     assert oracle.lib().or_uniform(0x80000000, 10) == 5
 
 
+def test_drop_and_crash_are_the_first_two_base100_digits(oracle):
+    """RandomDrop (simulator.go:172) and the message's crash roll (:180) come
+    from one draw r: (drop, crash) = divmod(floor(10^4 r / 2^32), 100), so each
+    of the 10^4 pairs is taken by 429496 or 429497 of the 2^32 words -- the two
+    draws are independent uniforms to within 2.4e-6 relative."""
+    import ctypes as C
+    L = oracle.lib()
+    rng = np.random.default_rng(11)
+    rs = np.concatenate([rng.integers(0, 2**32, 20000, dtype=np.uint64),
+                         np.array([0, 1, 42949672, 42949673, 2**31, 2**32 - 1], np.uint64)])
+    d, c = C.c_uint32(), C.c_uint32()
+    for r in rs.tolist():
+        L.or_drop_crash(r, C.byref(d), C.byref(c))
+        assert divmod((r * 10000) >> 32, 100) == (d.value, c.value)
+    # exact pair counts over all 2^32 words
+    m = np.arange(10000, dtype=np.uint64)
+    first = (m * 2**32 + 9999) // 10000           # smallest r with floor(10^4 r / 2^32) >= m
+    counts = np.diff(np.append(first, 2**32))
+    assert counts.min() == 2**32 // 10000 and counts.max() == 2**32 // 10000 + 1
+    # the law on Philox output: chi-square of the 10^4 pairs over 2e6 draws
+    ws = np.array([oracle.philox([i, 7, 0, 3 << 24], [1, 2]) for i in range(500_000)], np.uint64).ravel()
+    pair = (ws * 10000) >> np.uint64(32)
+    obs = np.bincount(pair.astype(np.int64), minlength=10000)
+    chi2 = float(((obs - len(ws) / 1e4) ** 2 / (len(ws) / 1e4)).sum())
+    assert chi2 < 10000 + 6 * np.sqrt(2 * 10000)  # 9999 dof: mean 9999, sd 141
+
+
 # ---- broadcast known answers -------------------------------------------------
 def ring(n):
     deg = np.full(n, 2, np.uint8)
