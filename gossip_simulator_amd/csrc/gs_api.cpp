@@ -52,6 +52,9 @@ struct gs_ctx {
   uint8_t* d_deg = nullptr;
   uint32_t* d_ids = nullptr;
   uint32_t tab_stride = 0;  // row stride d_ids was allocated for
+  uint32_t* d_pk = nullptr;  // k_expand's packed view of the sealed rows (expand_view)
+  size_t pk_bytes = 0;
+  uint64_t pk_ver = ~0ull;   // table_ver the packed view was built from
   uint32_t row_slots = 0;   // longest row when rows are padded past it (0: the stride)
   void* d_state = nullptr;  // one allocation for recv/crash/ring/cflag/clist/ccount/stats
   uint32_t* d_cnt = nullptr;
@@ -426,6 +429,38 @@ int seal_rows(gs_ctx* c, const uint8_t* deg, uint32_t* ids, uint64_t n) {
   return GS_OK;
 }
 
+// k_expand's packed view of the sealed rows (stride 8, rows <= 6 slots: C5's
+// fanin 6): five 24-B rows per 128-B line instead of four 32-B ones, built
+// once per table version (k_pack_rows, outside any timed step), about 0.8 of
+// the table's bytes beside it.  Other shapes -- and GS_NO_PACK=1, an A/B
+// knob -- read the table itself.  Called before every window run.
+int expand_view(gs_ctx* c) {
+  static const bool off = getenv("GS_NO_PACK") != nullptr;
+  if (!c->win || c->pp || off || c->st.stride != 8 || c->ws.slots > 6 || !c->d_ids) {
+    c->ws.pk = nullptr;
+    return GS_OK;
+  }
+  if (c->pk_ver != c->table_ver || !c->d_pk) {
+    const uint64_t rows = c->ntot, bytes = (rows + 4) / 5 * 128;
+    if (c->pk_bytes < bytes) {
+      if (c->d_pk) (void)hipFree(c->d_pk);
+      c->d_pk = nullptr;
+      c->pk_bytes = 0;
+      if (hipMalloc(&c->d_pk, bytes) != hipSuccess) {  // no room: expand reads the table itself
+        (void)hipGetLastError();
+        c->d_pk = nullptr;
+        c->ws.pk = nullptr;
+        return GS_OK;
+      }
+      c->pk_bytes = bytes;
+    }
+    CK(c, win_pack_rows(c->d_ids, rows, c->d_pk, c->stream));
+    c->pk_ver = c->table_ver;
+  }
+  c->ws.pk = c->d_pk;
+  return GS_OK;
+}
+
 // Shard c keeps the sealed rows of its own nodes [lo, hi) (copied from the
 // full table `deg` / `ids` of stride S on c's device): owner expand reads
 // only the rows of its own firing nodes.
@@ -655,6 +690,7 @@ void destroy_one(gs_ctx* c) {
     if (c->d_gst) (void)hipFree(c->d_gst);
   }
   if (c->h_xbuf) (void)hipHostFree(c->h_xbuf);
+  if (c->d_pk) (void)hipFree(c->d_pk);
   for (void* ptr : {(void*)c->d_deg, (void*)c->d_ids, c->d_state, (void*)c->d_cnt, (void*)c->d_failed, c->d_win,
                     c->d_flist, c->d_rlmsg, (void*)c->d_tstat, (void*)c->d_rtab, (void*)c->d_gcounts,
                     (void*)c->d_glay})
@@ -1980,6 +2016,7 @@ namespace {
 // Window engine: ticks [t0, t0 + n) as windows of <= min(max(delaylow,1),10)
 // ticks (gs_window.hip).  One host sync per window reads its task count.
 int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing, uint64_t tchunk) {
+  RC(expand_view(c));
   WinState& w = c->ws;
   const uint32_t Lmax = std::min<uint32_t>(std::max<int32_t>(c->p.delay_low, 1), kBitTicks);
   uint32_t done = 0, widx = 0;
@@ -2164,6 +2201,7 @@ int run_async(gs_ctx* c, uint64_t tend, uint32_t poll, uint64_t max_ticks, OnTic
   *stop = 0;
   *fallback = false;
   RC(async_setup(c));
+  RC(expand_view(c));
   WinState w = c->ws;
   w.ctl = c->d_ctl;
   w.stage = c->d_stage;
@@ -2792,6 +2830,10 @@ void account_tick(gs_ctx* c, uint64_t tick, const unsigned long long* s, gs_tick
 // Sharded step: `acc` keeps the global counters (the group, or the rank).
 int shard_step(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint32_t ticks, gs_tick_stats* out) {
   const bool timing = (acc->p.flags & GS_FLAG_TIMING) != 0;
+  for (gs_ctx* m : ms) {
+    CK(m, hipSetDevice(m->dev));
+    RC(expand_view(m));
+  }
   std::vector<unsigned long long> sum(kStatFields);
   uint32_t done = 0;
   while (done < ticks) {

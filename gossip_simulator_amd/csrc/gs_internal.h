@@ -138,6 +138,7 @@ struct WinState {
   unsigned long long* unit_off;  // [L*nfine + 1] exclusive scan of usize
   unsigned long long* tfires;    // [kMaxWindow] fires per tick of the window (host-zeroed)
   uint32_t* gmap;                // [ceil(fires/64)] unit of every 64th firing index
+  const uint32_t* pk;            // rows <= 6 slots: the sealed rows packed 5 per 128-B line, or null
   uint32_t* cmsg;                // coarse regions: u_in_coarse | k << 22
   uint32_t* fmsg;                // fine regions:   u_in_fine   | k << 14
   unsigned long long* chist;     // [kRegions] exact coarse region counts (fallback)
@@ -222,6 +223,7 @@ hipError_t win_plan(const WinState& w, bool exact, hipStream_t s);
 hipError_t win_scan_fine(const WinState& w, void* tmp, size_t& tmp_bytes, hipStream_t s);
 hipError_t win_part2(const WinState& w, uint64_t T, bool scatter, hipStream_t s);
 hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
+hipError_t win_pack_rows(const uint32_t* ids, uint64_t n, uint32_t* pk, hipStream_t s);
 hipError_t win_seal_rows(const uint8_t* deg, uint32_t* ids, uint64_t n, uint32_t stride,
                          hipStream_t s);
 hipError_t win_stats_reduce(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);

@@ -497,11 +497,32 @@ __device__ __forceinline__ void tstat_add(uint32_t* tstat, uint32_t key, uint32_
   }
 }
 
+// Packed view (rows <= 6 slots, stride 8): row v is the 24 bytes at byte
+// 24 * (v mod 5) of 128-B line v / 5 (8 bytes of each line unused), so a
+// line holds five rows instead of four and no row straddles two lines.
+__device__ __forceinline__ uint64_t pk_byte(uint32_t v) {
+  const uint32_t line = (uint32_t)(((uint64_t)v * 0xCCCCCCCDull) >> 34);  // v / 5 for every 32-bit v
+  return (uint64_t)line * 128 + (v - line * 5) * 24;
+}
+
 // Friends row of v into registers; slots past the list hold kEmptyMsg (rows
 // are sealed by k_seal_rows, so the length byte is not read).
 template <uint32_t MAXS>
 __device__ __forceinline__ void load_row(const WinState& w, uint32_t v, uint32_t (&mm)[MAXS]) {
   const uint32_t S = w.stride;
+  if (MAXS >= 5 && MAXS <= 6 && w.pk) {  // two 16-B loads from the row's 16-B aligned base
+    const uint64_t b = pk_byte(v);
+    const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(w.pk) + (b & ~15ull));
+    const uint4 x = p[0], y = p[1];
+    const bool odd = (b & 8) != 0;  // the row starts 8 bytes into the first load
+    mm[0] = odd ? x.z : x.x;
+    mm[1] = odd ? x.w : x.y;
+    mm[2] = odd ? y.x : x.z;
+    mm[3] = odd ? y.y : x.w;
+    mm[4 % MAXS] = odd ? y.z : y.x;
+    if (MAXS > 5) mm[5 % MAXS] = odd ? y.w : y.y;
+    return;
+  }
   if ((S & 3) == 0 && S >= 8 && MAXS >= 5 && MAXS <= 8) {  // 16-B aligned rows: uint4 + uint2 / uint4
     const uint4 a = reinterpret_cast<const uint4*>(w.ids + (size_t)v * S)[0];
     mm[0] = a.x; mm[1] = a.y; mm[2] = a.z; mm[3] = a.w;
@@ -753,6 +774,19 @@ __global__ __launch_bounds__(B) void k_expand(const WinState w, uint32_t t0, uin
     if (v) atomicAdd(&row[fld ? ST_SENT : ST_FIRED], v);
     // every delivered send is a receipt; k_resolve subtracts the uncounted ones
     if (v && fld) atomicAdd(&row[ST_MSGS], v);
+  }
+}
+
+// The packed view of sealed stride-8 rows (pk_byte): slots 0..5 of row v.
+__global__ void k_pack_rows(const uint32_t* ids, uint64_t n, uint32_t* pk) {
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n;
+       v += (uint64_t)gridDim.x * blockDim.x) {
+    const uint4 a = reinterpret_cast<const uint4*>(ids + v * 8)[0];
+    const uint2 b = reinterpret_cast<const uint2*>(ids + v * 8)[2];
+    uint2* d = reinterpret_cast<uint2*>(reinterpret_cast<char*>(pk) + pk_byte((uint32_t)v));
+    d[0] = make_uint2(a.x, a.y);
+    d[1] = make_uint2(a.z, a.w);
+    d[2] = b;
   }
 }
 
@@ -1802,6 +1836,12 @@ hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, i
     if (mode) hipLaunchKernelGGL((k_expand<true, kWinMaxStride, 1>), grid, blk, 0, s, w, t0, L, tn, st);
     else hipLaunchKernelGGL((k_expand<false, kWinMaxStride, 1>), grid, blk, 0, s, w, t0, L, tn, 0);
   }
+  return hipGetLastError();
+}
+
+hipError_t win_pack_rows(const uint32_t* ids, uint64_t n, uint32_t* pk, hipStream_t s) {
+  const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_pack_rows, dim3((uint32_t)(blocks ? blocks : 1)), dim3(256), 0, s, ids, n, pk);
   return hipGetLastError();
 }
 
