@@ -2176,7 +2176,8 @@ int async_setup(gs_ctx* c) {
     CK(c, hipMalloc(&c->d_ctl, sizeof(WinCtl)));
     // k_close writes each window's results straight into pinned host memory
     // (no copy launch per window); d_stage is its device address
-    CK(c, hipHostMalloc((void**)&c->h_stage, (size_t)kSlots * kStageWords * 8, hipHostMallocMapped));
+    CK(c, hipHostMalloc((void**)&c->h_stage, (size_t)kSlots * kStageWords * 8,
+                        hipHostMallocMapped | hipHostMallocPortable));
     CK(c, hipHostGetDevicePointer((void**)&c->d_stage, c->h_stage, 0));
     for (uint32_t i = 0; i < kSlots; ++i) {
       hipEvent_t e;
