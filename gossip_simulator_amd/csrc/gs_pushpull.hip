@@ -211,7 +211,10 @@ __global__ __launch_bounds__(kPPRoundBlock) void k_pp_round(const DevState s,
 // dependent-load chain runs for full waves of uninformed nodes however few
 // are left, and the range's newly informed gather in LDS and are stored, not
 // OR'ed (the wave owns its words).
-constexpr uint32_t kPPB = 4;        // words loaded together while streaming
+#ifndef GS_PPB
+#define GS_PPB 8
+#endif
+constexpr uint32_t kPPB = GS_PPB;   // words loaded together while streaming
 constexpr uint32_t kPPRange = 64;   // words per wave range (multiple of kPPB)
 constexpr uint32_t kPPQ = 128;      // queue entries per wave (<= 63 left + 64 appended)
 constexpr uint32_t kPPEdges = 4;    // in-edges loaded per batch
