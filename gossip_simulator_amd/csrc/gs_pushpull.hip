@@ -218,7 +218,12 @@ constexpr uint32_t kPPB = GS_PPB;   // words loaded together while streaming
 constexpr uint32_t kPPRange = 64;   // words per wave range (multiple of kPPB)
 constexpr uint32_t kPPQ = 128;      // queue entries per wave (<= 63 left + 64 appended)
 constexpr uint32_t kPPEdges = 4;    // in-edges loaded per batch
-constexpr uint32_t kPPWaves = kPPRoundBlock / 64;
+#ifndef GS_PPS_BLOCK
+#define GS_PPS_BLOCK 1024
+#endif
+constexpr uint32_t kPPSBlock = GS_PPS_BLOCK;  // k_ppb_round / k_ppa_round workgroup
+constexpr uint32_t kPPWaves = kPPSBlock / 64;
+constexpr uint32_t kPPSGrid = 512 * 1024 / kPPSBlock;  // at most 8192 waves per launch
 
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -271,7 +276,7 @@ __device__ __forceinline__ void ppb_resolve(const DevState& s, const PPSparse& s
   if (pulled || got) atomicOr(&nb[loc >> 6], 1ull << (loc & 63));
 }
 
-__global__ __launch_bounds__(kPPRoundBlock) void k_ppb_round(const DevState s, unsigned long long* __restrict__ next,
+__global__ __launch_bounds__(kPPSBlock) void k_ppb_round(const DevState s, unsigned long long* __restrict__ next,
                                                              const PPSparse sp, uint32_t t) {
   __shared__ uint64_t sh[3 * kPPWaves];
   __shared__ uint32_t s_q[kPPWaves][kPPQ];
@@ -346,7 +351,7 @@ __global__ __launch_bounds__(kPPRoundBlock) void k_ppb_round(const DevState s, u
   }
   const uint64_t v3[3] = {fired, sent, msgs};
   const uint32_t f3[3] = {ST_FIRED, ST_SENT, ST_MSGS};
-  block_add<kPPRoundBlock>(sh, v3, 3, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
+  block_add<kPPSBlock>(sh, v3, 3, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
 }
 
 // Pull-answer round (PP_ANSWER): same draws, outcomes and counters as
@@ -408,7 +413,7 @@ __device__ __forceinline__ void ppa_resolve(const DevState& s, const PPSparse& s
   }
 }
 
-__global__ __launch_bounds__(kPPRoundBlock) void k_ppa_round(const DevState s, unsigned long long* __restrict__ next,
+__global__ __launch_bounds__(kPPSBlock) void k_ppa_round(const DevState s, unsigned long long* __restrict__ next,
                                                              const PPSparse sp, uint32_t t) {
   __shared__ uint64_t sh[3 * kPPWaves];
   __shared__ uint32_t s_q[kPPWaves][kPPQ];
@@ -460,7 +465,7 @@ __global__ __launch_bounds__(kPPRoundBlock) void k_ppa_round(const DevState s, u
   }
   const uint64_t v3[3] = {blockIdx.x == 0 && threadIdx.x == 0 ? c->ncallers : 0ull, sent, msgs};
   const uint32_t f3[3] = {ST_FIRED, ST_SENT, ST_MSGS};
-  block_add<kPPRoundBlock>(sh, v3, 3, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
+  block_add<kPPSBlock>(sh, v3, 3, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
 }
 
 // Shards: the round's mode, chosen by the host from the global informed count
@@ -869,9 +874,9 @@ hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long l
                      sumB, sum2, S2l, t, (const PPCtl*)sp.ctl, sp.fmask);
   if (sp.ctl) {  // no-op unless the round is bottom-up
     const uint64_t nrange = (s.W + kPPRange - 1) / kPPRange;
-    const uint32_t bblocks = (uint32_t)std::min<uint64_t>((nrange + kPPWaves - 1) / kPPWaves, 512);
-    hipLaunchKernelGGL(k_ppb_round, dim3(bblocks), dim3(kPPRoundBlock), 0, st, s, next, sp, t);
-    hipLaunchKernelGGL(k_ppa_round, dim3(bblocks), dim3(kPPRoundBlock), 0, st, s, next, sp, t);
+    const uint32_t bblocks = (uint32_t)std::min<uint64_t>((nrange + kPPWaves - 1) / kPPWaves, kPPSGrid);
+    hipLaunchKernelGGL(k_ppb_round, dim3(bblocks), dim3(kPPSBlock), 0, st, s, next, sp, t);
+    hipLaunchKernelGGL(k_ppa_round, dim3(bblocks), dim3(kPPSBlock), 0, st, s, next, sp, t);
   }
   return hipGetLastError();
 }
@@ -968,11 +973,11 @@ hipError_t pp_round_shard(const DevState& s, unsigned long long* next, unsigned 
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_pp_set_mode, dim3(1), dim3(1), 0, st, sp.ctl, mode);
   const uint64_t nrange = (s.W + kPPRange - 1) / kPPRange;
-  const uint32_t bblocks = (uint32_t)std::min<uint64_t>((nrange + kPPWaves - 1) / kPPWaves, 512);
+  const uint32_t bblocks = (uint32_t)std::min<uint64_t>((nrange + kPPWaves - 1) / kPPWaves, kPPSGrid);
   if (mode == PP_BOTTOM)
-    hipLaunchKernelGGL(k_ppb_round, dim3(bblocks ? bblocks : 1), dim3(kPPRoundBlock), 0, st, s, next, sp, t);
+    hipLaunchKernelGGL(k_ppb_round, dim3(bblocks ? bblocks : 1), dim3(kPPSBlock), 0, st, s, next, sp, t);
   else
-    hipLaunchKernelGGL(k_ppa_round, dim3(bblocks ? bblocks : 1), dim3(kPPRoundBlock), 0, st, s, gnext, sp, t);
+    hipLaunchKernelGGL(k_ppa_round, dim3(bblocks ? bblocks : 1), dim3(kPPSBlock), 0, st, s, gnext, sp, t);
   return hipGetLastError();
 }
 
