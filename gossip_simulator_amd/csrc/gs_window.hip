@@ -809,6 +809,16 @@ __device__ __forceinline__ unsigned long long region_fill(const WinState& w, uin
   return w.cfill[r] < room ? w.cfill[r] : room;
 }
 
+// Unsharded layouts deal k_part2's tiles by XCD: all tiles of coarse bin c
+// go to XCD c & 7, so each fine region is written from one XCD's L2 (the
+// runs of different tiles meet in whole lines there instead of in partial
+// lines from eight L2s).  xcd_bin_pos(c) = the bin's place in that order.
+__device__ __forceinline__ bool tiles_by_xcd(const WinState& w) {
+  return w.csub == kCoarseSub && !w.csrc && !w.noxcd;
+}
+__device__ __forceinline__ uint32_t xcd_bin_pos(uint32_t c) { return (c & 7) * 32 + (c >> 3); }
+__device__ __forceinline__ uint32_t xcd_bin_of(uint32_t pc) { return (pc & 31) * 8 + (pc >> 5); }
+
 // Fine regions inside each coarse region: capacity per fine bucket of coarse
 // c = cfill[c]*1.15/256 + 512 (fast path), or exact counts (fhist != null).
 __global__ void k_plan(const WinState w, bool exact) {
@@ -853,7 +863,25 @@ __global__ void k_plan(const WinState w, bool exact) {
   __syncthreads();
   if (blockIdx.x == 0) {  // every region < kRegions is written (256 * csub >= kRegions)
     uint32_t a = s_tp[tid];
-    if (csub == kCoarseSub) {
+    if (tiles_by_xcd(w)) {
+      // k_part2 deals the tiles of bin c to XCD c & 7: tprefix is in the
+      // order (c & 7, c >> 3, sub-region), so XCD x's tiles are one run
+      __shared__ uint32_t s_pt[256];
+      const uint32_t pc = xcd_bin_pos(tid);
+      s_pt[pc] = live ? ntile : 0u;
+      __syncthreads();
+      const uint32_t mine = s_pt[tid];
+      unsigned long long tot;
+      const uint32_t pre = (uint32_t)block_exscan256_u64(mine, s_x, &tot);
+      s_pt[tid] = pre;
+      __syncthreads();
+      a = s_pt[pc];
+#pragma unroll
+      for (uint32_t x = 0; x < kCoarseSub; ++x) {
+        w.tprefix[pc * kCoarseSub + x] = a;
+        a += live ? (uint32_t)((fl[x] + kPartTile - 1) / kPartTile) : 0u;
+      }
+    } else if (csub == kCoarseSub) {
 #pragma unroll
       for (uint32_t x = 0; x < kCoarseSub; ++x) {
         w.tprefix[tid * kCoarseSub + x] = a;
@@ -911,17 +939,26 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   }
   // a sparse window has few tiles: the workgroups past them leave before
   // staging the 8-KB tile prefix (the grid is sized for the densest window)
-  const uint32_t ntiles = w.tprefix[kRegions];
-  if (blockIdx.x >= ntiles) return;
+  const bool perm = tiles_by_xcd(w);
+  uint32_t g0 = blockIdx.x, g1 = w.tprefix[kRegions], gstep = gridDim.x;
+  if (perm && (gridDim.x & 7) == 0) {  // XCD x = blockIdx & 7 takes its bins' tiles
+    const uint32_t x = blockIdx.x & 7;
+    g0 = w.tprefix[x * 256] + (blockIdx.x >> 3);
+    g1 = w.tprefix[(x + 1) * 256];
+    gstep = gridDim.x >> 3;
+  }
+  if (g0 >= g1) return;
   for (uint32_t i = tid; i <= kRegions; i += kPartBlock) s_tp[i] = w.tprefix[i];
   __syncthreads();
-  for (uint32_t g = blockIdx.x; g < ntiles; g += gridDim.x) {
-    uint32_t lo = 0, hi = kRegions - 1;  // coarse region r: s_tp[r] <= g < s_tp[r+1]
+  for (uint32_t g = g0; g < g1; g += gstep) {
+    uint32_t lo = 0, hi = kRegions - 1;  // tile-order position rho: s_tp[rho] <= g < s_tp[rho+1]
     while (lo < hi) {
       const uint32_t mid = (lo + hi + 1) >> 1;
       if (s_tp[mid] <= g) lo = mid; else hi = mid - 1;
     }
-    const uint32_t r = lo, c = r / w.csub;
+    const uint32_t rho = lo;
+    const uint32_t r = perm ? xcd_bin_of(rho / kCoarseSub) * kCoarseSub + rho % kCoarseSub : rho;
+    const uint32_t c = r / w.csub;
     unsigned long long cb = w.ccap[r];
     const uint32_t* msrc = w.cmsg;  // the region's messages (a receive layout names their buffer)
     if (w.csrc) {
@@ -929,7 +966,7 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8
       cb &= kSrcMask;
     }
     const unsigned long long ce = cb + region_fill(w, r);
-    const unsigned long long base = cb + (unsigned long long)(g - s_tp[r]) * kPartTile;
+    const unsigned long long base = cb + (unsigned long long)(g - s_tp[rho]) * kPartTile;
     if (tid < 256) ts.cnt[tid] = 0;
     __syncthreads();
     if (tid == 0) ts.ovf = 0;
@@ -1861,7 +1898,7 @@ hipError_t win_plan(const WinState& w, bool exact, hipStream_t s) {
 
 hipError_t win_part2(const WinState& w, uint64_t T, bool scatter, hipStream_t s) {
   const uint64_t tiles = (T + kPartTile - 1) / kPartTile + 256;
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>(tiles, 8192);
+  const uint32_t blocks = (uint32_t)(std::min<uint64_t>(tiles, 8192) + 7) & ~7u;  // a multiple of 8: tiles by XCD
   if (scatter) hipLaunchKernelGGL(k_part2<true>, dim3(blocks), dim3(kPartBlock), 0, s, w);
   else hipLaunchKernelGGL(k_part2<false>, dim3(blocks), dim3(kPartBlock), 0, s, w);
   return hipGetLastError();
