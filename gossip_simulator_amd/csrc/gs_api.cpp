@@ -223,7 +223,7 @@ int alloc_window(gs_ctx* c) {
   w.rank = c->rank;
   w.seg_per = (uint32_t)c->seg_per;
   w.csub = kCoarseSub;
-  w.noxcd = getenv("GS_PART2_XCD") ? 0u : 1u;  // A/B knob: k_part2 tiles dealt by XCD (GS_PART2_XCD=1)
+  w.noxcd = getenv("GS_PART2_NOXCD") ? 1u : 0u;  // A/B knob: k_part2 tiles in region order
   w.ccap_end = nullptr;
   w.csrc = nullptr;
   if (c->shard) {  // owner expand (k_expand's coarse_bin)
