@@ -203,6 +203,7 @@ __global__ void k_cut(const WinState w, unsigned long long budget) {
   uint32_t t = 0;
   const uint32_t Lw = win_open(w, t);
   // every load this kernel needs is issued up front (one latency, not a chain)
+  const unsigned long long cap = c->cmsg_cap;
   if (b < kMaxWindow) s_tf[b] = w.tfires[b];
   unsigned long long ts[4][kMaxWindow];  // this thread's tiles' fires per tick
 #pragma unroll
@@ -261,21 +262,13 @@ __global__ void k_cut(const WinState w, unsigned long long budget) {
   const unsigned long long hi = min((unsigned long long)w.n, lo + (1ull << kCoarseShift));
   const unsigned long long sub =
       b < w.ncoarse ? (unsigned long long)((double)s_T * (double)(hi - lo) / (double)w.n / kCoarseSub) + 512 : 0ull;
-  s_sz[b] = sub * kCoarseSub;
-  __syncthreads();
-  for (uint32_t o = 1; o < 256; o <<= 1) {  // inclusive scan over bins
-    const unsigned long long x = b >= o ? s_sz[b - o] : 0ull;
-    __syncthreads();
-    s_sz[b] += x;
-    __syncthreads();
-  }
-  const unsigned long long total = s_sz[255];
-  if (total > c->cmsg_cap) {  // the buffer is too small: no region at all, the host grows and redoes
+  unsigned long long total;
+  const unsigned long long base = block_exscan256_u64(sub * kCoarseSub, &s_sz[0], &total);
+  if (total > cap) {  // the buffer is too small: no region at all, the host grows and redoes
     for (uint32_t x = 0; x < kCoarseSub; ++x) w.ccap[b * kCoarseSub + x] = 0;
     if (b == 0) { w.ccap[kRegions] = 0; atomicOr(w.err, kErrCoarse); }
     return;
   }
-  const unsigned long long base = b ? s_sz[b - 1] : 0ull;
   for (uint32_t x = 0; x < kCoarseSub; ++x) w.ccap[b * kCoarseSub + x] = base + x * sub;
   if (b == 255) w.ccap[kRegions] = total;
 }
