@@ -69,25 +69,25 @@ __device__ __forceinline__ CtlView ctl_view(const WinState& w) {
   const uint32_t e = *w.err;
   return CtlView{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, e};
 }
+// (The tests are selects, not early returns: a branch on the error word would
+// let the compiler sink the control-block load behind it, two latencies.)
 __device__ __forceinline__ uint32_t win_open(const WinState& w, uint32_t& t) {
   const CtlView c = ctl_view(w);
-  if ((c.err & (kErrCoarse | kErrFine)) || c.stop) return 0;
   t = c.tnext;
-  if (t >= c.tend) return 0;
+  const bool dead = (c.err & (kErrCoarse | kErrFine)) || c.stop || t >= c.tend;
   uint32_t Lw = min(c.lmax, c.tend - t);
   if (c.poll) {
     const uint32_t P = c.pbase + c.poll * ((t - c.pbase + c.poll - 1) / c.poll);  // next poll tick
     Lw = min(Lw, P - t + 1);
   }
-  return Lw;
+  return dead ? 0u : Lw;
 }
 // A kernel of an opened window: its start and length (0: skip the window).
 __device__ __forceinline__ uint32_t win_live(const WinState& w, uint32_t& t0, uint32_t L) {
   if (!w.ctl) return w.abort_on_err && win_abort(w) ? 0u : L;  // shards: a window that overflowed is redone
   const CtlView c = ctl_view(w);
-  if (c.err & (kErrCoarse | kErrFine)) return 0;
   t0 = c.t;
-  return c.L;
+  return (c.err & (kErrCoarse | kErrFine)) ? 0u : c.L;
 }
 
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
@@ -127,7 +127,7 @@ __device__ __forceinline__ unsigned long long block_exscan256_u64(unsigned long 
 // the window share are fetched once into the XCD's L2.  usize = fires;
 // tfires[k] = fires per tick (the window cut).  Also zeroes the window's
 // counters (one launch instead of several memsets).
-__global__ void k_units(const WinState w, uint32_t t0, uint32_t L) {
+__global__ __launch_bounds__(256) void k_units(const WinState w, uint32_t t0, uint32_t L) {
   __shared__ uint32_t s_t[kMaxWindow];
   uint32_t Ls = L;
   if (w.ctl) {
@@ -147,16 +147,23 @@ __global__ void k_units(const WinState w, uint32_t t0, uint32_t L) {
   if (tid == 0) w.usize[units] = 0;
   __syncthreads();
   __shared__ uint32_t s_ts[kMaxWindow];  // this tile's fires per tick
+  uint32_t slot[kMaxWindow];  // ring slot of tick t0 + k (uniform)
+#pragma unroll
+  for (uint32_t k = 0; k < kMaxWindow; ++k) slot[k] = k < L ? (t0 + k) % w.R : 0u;
   for (uint32_t f0 = blockIdx.x * 256; f0 < w.nfine; f0 += gridDim.x * 256) {
     const uint32_t f = f0 + threadIdx.x;
     if (threadIdx.x < kMaxWindow) s_ts[threadIdx.x] = 0;
+    // all L loads in flight before the first use (one latency, not L)
+    uint32_t cv[kMaxWindow];
+#pragma unroll
+    for (uint32_t k = 0; k < kMaxWindow; ++k)
+      cv[k] = k < L && k < Ls && f < w.nfine ? w.fcount[(size_t)slot[k] * w.nfine + f] : 0u;
 #pragma unroll
     for (uint32_t k = 0; k < kMaxWindow; ++k) {
-      if (k >= Ls) break;
-      uint32_t c = 0;
-      if (k < L && f < w.nfine) c = w.fcount[(size_t)((t0 + k) % w.R) * w.nfine + f];
-      s_tile[threadIdx.x * (kMaxWindow + 1) + k] = c;
-      acc[k] += c;
+      if (k < Ls) {
+        s_tile[threadIdx.x * (kMaxWindow + 1) + k] = cv[k];
+        acc[k] += cv[k];
+      }
     }
     __syncthreads();
     // per-tile sums for the device-driven unit scan (k_cut, k_unitscan)
@@ -192,7 +199,7 @@ __global__ void k_units(const WinState w, uint32_t t0, uint32_t L) {
 // window holds whole ticks while its friend slots fit `budget`), the coarse
 // region plan of the window's T friend slots, and the window's place in ctl.
 // One block.
-__global__ void k_cut(const WinState w, unsigned long long budget) {
+__global__ __launch_bounds__(256) void k_cut(const WinState w, unsigned long long budget) {
   __shared__ unsigned long long s_sz[256];
   __shared__ unsigned long long s_T;
   __shared__ uint32_t s_go, s_L;
@@ -277,7 +284,7 @@ __global__ void k_cut(const WinState w, unsigned long long budget) {
 // bucket, its Ls units contiguous; ticks >= L count as empty), offset by the
 // tile's start from k_cut, and the group map of those units.  One block per
 // tile.  (Host-driven windows: hipcub scan + k_groupmap.)
-__global__ void k_unitscan(const WinState w) {
+__global__ __launch_bounds__(256) void k_unitscan(const WinState w) {
   __shared__ unsigned long long s_x[4];
   uint32_t t0;
   const uint32_t L = win_live(w, t0, 0);
@@ -285,11 +292,10 @@ __global__ void k_unitscan(const WinState w) {
   const uint32_t Ls = w.lstride, tile = blockIdx.x, f = tile * 256 + threadIdx.x;
   unsigned long long sz[kMaxWindow], sum = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < kMaxWindow; ++k) {
-    sz[k] = 0;
-    if (k < L && f < w.nfine) sz[k] = w.usize[(size_t)f * Ls + k];
-    sum += sz[k];
-  }
+  for (uint32_t k = 0; k < kMaxWindow; ++k)  // all loads in flight, then the sum
+    sz[k] = k < L && f < w.nfine ? w.usize[(size_t)f * Ls + k] : 0ull;
+#pragma unroll
+  for (uint32_t k = 0; k < kMaxWindow; ++k) sum += sz[k];
   unsigned long long tot;
   unsigned long long a = w.toff[tile] + block_exscan256_u64(sum, s_x, &tot);
   if (f >= w.nfine) return;
@@ -1522,13 +1528,11 @@ __global__ __launch_bounds__(ROLLED ? kRolledBlock : kSmallBlock) void k_resolve
   __shared__ uint32_t sk[kWaves][64 * kEmax];      // each wave's sorted keys
   __shared__ uint32_t fcw[kWaves][kWinMaxRing];    // each wave's bucket: fire-list lengths per ring slot
   const uint32_t tid = threadIdx.x, wv = tid >> 6;
-  L = win_live(w, t0, L);
-  if (!L) return;
   static_assert(kWaves * kMaxWindow * 4 == kWaves * 64, "one counter per thread");
   static_assert(kRolledCap == 64 * 16, "the rolled bodies cover 1..kRolledCap");
-  (&st[0][0][0])[tid] = 0;
-  __syncthreads();
   const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
+  // the bucket's size and start are loaded while the window check is in
+  // flight (unused when the window is dead)
   unsigned long long M = 0;
   const uint32_t* gm = nullptr;
   if (f < w.nfine) {
@@ -1540,6 +1544,10 @@ __global__ __launch_bounds__(ROLLED ? kRolledBlock : kSmallBlock) void k_resolve
       gm = w.fmsg + w.fstart[f];
     }
   }
+  L = win_live(w, t0, L);
+  if (!L) return;
+  (&st[0][0][0])[tid] = 0;
+  __syncthreads();
   if (M > 0 && M <= 64) resolve_small_bucket<1, ROLLED>(w, t0, L, f, gm, M, st, sk[wv], fcw[wv]);
   else if (M > 64 && M <= 256) resolve_small_bucket<4, ROLLED>(w, t0, L, f, gm, M, st, sk[wv], fcw[wv]);
   else if (ROLLED && M > 256 && M <= 512)
