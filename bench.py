@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--cpu-n", type=int, default=100_000_000,
                     help="nodes in the bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-cap", type=float, default=40.0, help="seconds the CPU-baseline broadcast may run")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 batched-trials run")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 node-range-sharded run")
@@ -78,6 +79,7 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+DEADLINE_EXIT = 3  # exit status after the extension deadline fired
 _LEG = ["headline"]  # the leg running now (for the deadline watchdog)
 
 
@@ -98,7 +100,9 @@ class Emitter:
     under a deadline (--ext-deadline s): a leg that blocks -- e.g. a
     collective of a multi-rank path waiting on a peer that failed -- must not
     swallow the headline, so when the deadline passes rank 0 prints the line
-    with the unfinished leg marked and every rank exits at once."""
+    with the unfinished leg marked and every rank exits at once, with status
+    DEADLINE_EXIT: the line is there, but the run did not finish, and the
+    exit status says so (torchrun, CI and the evidence scripts see a failure)."""
 
     def __init__(self, rank):
         import threading
@@ -130,7 +134,7 @@ class Emitter:
             self.emit()
             sys.stdout.flush()
             sys.stderr.flush()
-            os._exit(0)
+            os._exit(DEADLINE_EXIT)
 
         self.timer = threading.Timer(seconds, fire)
         self.timer.daemon = True
@@ -669,14 +673,25 @@ def cpu_limits():
     return out
 
 
+def cpu_threads():
+    """The all-core thread count this host allows: the CPUs in the process's
+    affinity mask, capped by the cgroup CPU quota when one is set (the GPU box
+    gives each GPU a 16-CPU quota out of 256 CPUs: more threads than the quota
+    are throttled, not faster)."""
+    lim = cpu_limits()
+    n = lim.get("affinity") or lim.get("nproc") or 1
+    if lim.get("cgroup_cpus"):
+        n = min(n, max(1, int(lim["cgroup_cpus"])))
+    return n, lim
+
+
 def cpu_baseline(a, gs):
     """The all-core OpenMP port of the tick model (oracle/gsomp.c, bit-exact to
     the restatement, checked in tests/test_omp_port.py) on this host: one whole
     broadcast at n = cpu_n with the same parameters, over a table the GPU
     overlay built (copied to the host); times only the port's tick loop,
-    capped at 40 s.  `value` runs one OpenMP thread per host CPU (os.cpu_count());
-    the run at this GPU's CPU share (16 threads, the box's OMP_NUM_THREADS) is
-    reported beside it.  msgs/s as the headline: delivered sends / time
+    capped at --cpu-cap s.  Threads: cpu_threads() (affinity, capped by the
+    cgroup quota).  msgs/s as the headline: delivered sends / time
     (simulator.go:252-253 divides TotalMessage by the broadcast's time)."""
     from oracle import pyoracle as O
     O.build()
@@ -690,45 +705,31 @@ def cpu_baseline(a, gs):
     p = O.make_params(n=n, fanout=a.fanout, fanin=a.fanin, delay_low=a.delaylow,
                       delay_high=a.delayhigh, drop_rate=a.droprate, crash_rate=a.crashrate,
                       seed=a.seed, trial=0)
-
-    def run(threads, cap_s=40):
-        e = O.OmpEngine(p, deg, ids, threads=threads)
-        e.begin(-1)
-        sent = msgs = 0
-        t0 = time.perf_counter()
-        capped = False
-        while True:
-            st = e.step(10)
-            sent += int(st[:, 2].sum())
-            msgs += int(st[:, 3].sum())
-            if O.covered(int(st[-1, 4]), n) or int(st[-1, 6]) == 0:
-                break
-            if time.perf_counter() - t0 > cap_s:
-                capped = True
-                break
-        dt = time.perf_counter() - t0
-        log(f"cpu baseline: {e.threads} threads, n={n}: {sent / dt:.3e} msgs/s ({dt:.1f} s)")
-        return e.threads, sent, msgs, dt, capped
-
-    share = int(os.environ.get("OMP_NUM_THREADS", "0")) or 16
-    allc = os.cpu_count() or share
-    # the all-CPU run is capped at 10 s: under a cgroup quota it is throttled
-    # (r03: 256 threads on a 16-CPU quota ran 18x slower than 16 threads)
-    runs = {allc: run(allc, 10)}
-    if share != allc:
-        runs[share] = run(share)
-    # value: the faster of one thread per host CPU and the GPU's CPU share (a
-    # cgroup quota, when the host sets one, throttles the all-CPU run)
-    best = max(runs, key=lambda k: runs[k][1] / runs[k][3])
-    th, sent, msgs, dt, capped = runs[best]
-    return {"value": round(sent / dt, 1), "unit": "msgs/s", "cores": th, "kind": "port",
-            "messages_per_s": round(msgs / dt, 1), "cpu_model": cpu_model(), **cpu_limits(),
-            "runs": {str(k): {"threads": v[0], "value": round(v[1] / v[3], 1), "s": round(v[3], 3),
-                              "capped": v[4]} for k, v in runs.items()},
+    threads, lim = cpu_threads()
+    e = O.OmpEngine(p, deg, ids, threads=threads)
+    del deg, ids
+    e.begin(-1)
+    sent = msgs = 0
+    t0 = time.perf_counter()
+    capped = False
+    while True:
+        st = e.step(10)
+        sent += int(st[:, 2].sum())
+        msgs += int(st[:, 3].sum())
+        if O.covered(int(st[-1, 4]), n) or int(st[-1, 6]) == 0:
+            break
+        if time.perf_counter() - t0 > a.cpu_cap:
+            capped = True
+            break
+    dt = time.perf_counter() - t0
+    log(f"cpu baseline: {e.threads} threads, n={n}: {sent / dt:.3e} msgs/s ({dt:.1f} s)")
+    return {"value": round(sent / dt, 1), "unit": "msgs/s", "cores": e.threads, "kind": "port",
+            "messages_per_s": round(msgs / dt, 1), "cpu_model": cpu_model(), **lim,
+            "s": round(dt, 3), "capped": capped,
             "sample": f"oracle/gsomp.c (OpenMP port of the tick model), one broadcast at n={n} to "
-                      f"{'the 40 s cap' if capped else '99% / quiescence'} ({sent} delivered sends in {dt:.2f} s) "
-                      f"with {th} threads, same params, GPU-built overlay; runs = one thread per host CPU "
-                      f"({allc}) and this GPU's CPU share ({share}); value = the faster"}
+                      f"{'the %.0f s cap' % a.cpu_cap if capped else '99% / quiescence'} ({sent} delivered sends "
+                      f"in {dt:.2f} s) with {e.threads} threads (the affinity mask capped by the cgroup quota), "
+                      f"same params, GPU-built overlay"}
 
 
 if __name__ == "__main__":

@@ -576,8 +576,11 @@ int ctx_setup(gs_ctx* c, const gs_params* params, int device, bool shard, uint32
     return GS_EINVAL;
   }
   // owner expand: every shard's range fits its 256 / G coarse bins of 2^22 nodes
-  if (shard && !c->pp && (G > 256 || ((c->seg_per + (1ull << kCoarseShift) - 1) >> kCoarseShift) > 256 / G)) {
-    why = "flood node-range shards: each of the G <= 256 shards' ranges must fit 256 / G bins of 2^22 nodes "
+  // and a group's received blocks take source index G of the receive layout's
+  // 8-bit source field (kSrcShift): G <= 255
+  static_assert(kSrcShift + 8 == 64, "8-bit source index in the receive layout");
+  if (shard && !c->pp && (G > 255 || ((c->seg_per + (1ull << kCoarseShift) - 1) >> kCoarseShift) > 256 / G)) {
+    why = "flood node-range shards: each of the G <= 255 shards' ranges must fit 256 / G bins of 2^22 nodes "
           "(n up to about 2^30)";
     return GS_EINVAL;
   }
@@ -3314,8 +3317,11 @@ int gs_reset(gs_ctx* c) {
   for (gs_ctx* m : c->mem) RC(gs_reset(m) ? fail(c, GS_EDEVICE, m->err) : 0);
   if (!c->group) {
     CK(c, hipSetDevice(c->dev));
-    // everything in the state block except the stats ring and error word
+    // everything in the state block except the stats ring, then the error
+    // word (a broadcast that overflowed -- kErrArrivals, or a partition flag
+    // -- leaves the context usable; table validation reports at load time)
     CK(c, hipMemsetAsync(c->d_state, 0, (char*)c->st.stats - (char*)c->d_state, c->stream));
+    if (c->d_err) CK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
     if (c->d_cnt) CK(c, hipMemsetAsync(c->d_cnt, 0, c->st.n * 4, c->stream));
     if (c->win) CK(c, hipMemsetAsync(c->ws.fcount, 0, c->fcount_bytes, c->stream));
     if (c->failed && !c->pp_shard)

@@ -1765,10 +1765,11 @@ __global__ void k_pack(const WinState w, const unsigned long long* poff, uint32_
     dst[i] = src[i];
 }
 
-// Shards: the window's fire lists are consumed (kept if the window overflowed
-// its partition: the host redoes it, and the redo consumes them).
+// Shards: the window's fire lists are consumed right after the expand (and
+// its exact sender redo, which clears the coarse flag first); nothing later
+// reads them -- a receive-side redo (receiver_redo) re-partitions and
+// resolves the received messages only -- so the consume is unconditional.
 __global__ void k_consume_sh(const WinState w, uint32_t t0, uint32_t L) {
-  if (win_abort(w)) return;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < L * w.nfine; i += gridDim.x * blockDim.x) {
     const uint32_t k = i / w.nfine, f = i - k * w.nfine;
     w.fcount[(size_t)((t0 + k) % w.R) * w.nfine + f] = 0;

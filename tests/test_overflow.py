@@ -84,3 +84,9 @@ def test_tick_engine_returns_overflow():
         with pytest.raises(gs.GossipError) as ei:
             sim.step(1)
         assert ei.value.code == -6  # GS_EOVERFLOW
+        # the context stays usable: a reset clears the overflow, and a second
+        # broadcast that stops before the hub's tick runs clean
+        sim.reset()
+        sim.broadcast_begin(0)
+        rows = sim.step(29)
+        assert int(rows[-1][0]) == 29 and int(rows[:, 2].sum()) > 0
