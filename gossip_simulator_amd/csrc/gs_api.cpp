@@ -157,6 +157,19 @@ struct gs_ctx {
   std::vector<unsigned long long*> gig, gfg, ggn;  // push-pull shards: per distinct device, the replicated sets
   std::vector<gs_ctx*> greps;           // push-pull shards: per distinct device, the replica
   OverlayWork ovw;                      // overlay builder buffers, kept between builds
+  // device-driven shard windows (dd_run; the group's or the rank's): gathered
+  // fire counts [G][kMaxWindow] and region rows [G][kDDRow], each member's
+  // window counters [M][kDDWStat] and control block, the pointer tables the
+  // kernels read (region starts [M], sources [M + 1], counters [M], control
+  // blocks [M]); pinned copy of the gathered rows for ranks whose blocks travel
+  void* dd_mem = nullptr;
+  unsigned long long* dd_gcnt = nullptr;
+  unsigned long long* dd_glay = nullptr;
+  unsigned long long* dd_wstat = nullptr;
+  WinCtl* dd_ctl = nullptr;
+  void** dd_ptrs = nullptr;
+  void** h_ddptrs = nullptr;            // pinned staging of dd_ptrs
+  unsigned long long* h_ddlay = nullptr;
 };
 
 namespace {
@@ -197,9 +210,6 @@ bool grow(Buf& b, size_t bytes) {
     if (rc_) return rc_;      \
   } while (0)
 
-// A shard's receive layout (gs_ctx::d_rtab): region starts, ends, fills, its
-// own pack offsets ([kRegions + 1] each), then the source buffers (<= 257).
-constexpr size_t kRtabWords = 4 * (kRegions + 1) + 260;
 
 // Window-engine buffers.  Sizes at n = 1e9, R = 20: flist 40 GB (two bytes
 // per node per ring slot), fcount 4.9 MB; message buffers grow on demand.
@@ -659,6 +669,11 @@ void destroy_one(gs_ctx* c) {
     for (hipEvent_t e : c->gev_c) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->gev_x) (void)hipEventDestroy(e);
     for (gs_ctx* r : c->greps) destroy_one(r);
+    if (!c->gdevs.empty()) (void)hipSetDevice(c->gdevs[0]);
+    if (c->dd_mem) (void)hipFree(c->dd_mem);
+    for (void* ptr : {(void*)c->h_stage, (void*)c->h_ddlay, (void*)c->h_ddptrs})
+      if (ptr) (void)hipHostFree(ptr);
+    for (hipEvent_t e : c->wev) (void)hipEventDestroy(e);
     delete c;
     return;
   }
@@ -706,6 +721,9 @@ void destroy_one(gs_ctx* c) {
                     (void*)c->h_stage, (void*)c->h_rtab, (void*)c->h_glay})
     if (ptr) (void)hipHostFree(ptr);
   if (c->d_ctl) (void)hipFree(c->d_ctl);  // (d_stage maps h_stage)
+  if (c->dd_mem) (void)hipFree(c->dd_mem);
+  for (void* ptr : {(void*)c->h_ddlay, (void*)c->h_ddptrs})
+    if (ptr) (void)hipHostFree(ptr);
   for (hipEvent_t e : c->wev) (void)hipEventDestroy(e);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
@@ -2310,6 +2328,21 @@ int sync_all(const std::vector<gs_ctx*>& ms) {
   return GS_OK;
 }
 
+// A shard that cannot allocate a window buffer marks its error word
+// (kErrNoMem) and keeps taking part in the window's collectives; every rank
+// sees the mark at the next gather (counts, layouts, or the end-of-step
+// check) and returns GS_ENOMEM there, so no rank waits on a peer that left.
+int mark_nomem(gs_ctx* m, const std::string& what) {
+  uint32_t e = 0;
+  CK(m, hipMemcpyAsync(&e, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
+  CK(m, hipStreamSynchronize(m->stream));
+  e |= kErrNoMem;
+  CK(m, hipMemcpyAsync(m->d_err, &e, 4, hipMemcpyHostToDevice, m->stream));
+  CK(m, hipStreamSynchronize(m->stream));
+  m->err = what;
+  return GS_OK;
+}
+
 // Fire counts of the window's units and their scan; with gather, tfires
 // (fires per tick, plus this shard's partition-overflow flag in slot 15) is
 // gathered: every rank's into d_gcounts, or the member's into its h_misc.
@@ -2324,9 +2357,13 @@ int shard_units(gs_ctx* m, uint32_t t, uint32_t Lu, bool gather) {
   CK(m, win_units(w, t, Lu, m->stream));
   size_t need = 0;
   CK(m, win_scan_units(w, Lu, nullptr, need, m->stream));
-  if (!grow(m->tmp, need)) return fail(m, GS_ENOMEM, "cannot allocate scan scratch");
-  need = m->tmp.bytes;
-  CK(m, win_scan_units(w, Lu, m->tmp.p, need, m->stream));
+  if (!grow(m->tmp, need)) {
+    RC(mark_nomem(m, "cannot allocate scan scratch"));
+    CK(m, hipMemcpyAsync(w.tfires + kFlagSlot, m->d_err, 4, hipMemcpyDeviceToDevice, m->stream));
+  } else {
+    need = m->tmp.bytes;
+    CK(m, win_scan_units(w, Lu, m->tmp.p, need, m->stream));
+  }
   if (!gather) return GS_OK;
   if (is_rank(m)) {
     CK(m, hipMemcpyAsync(m->d_gcounts + (size_t)m->rank * kMaxWindow, w.tfires, kMaxWindow * 8,
@@ -2394,7 +2431,7 @@ int shard_expand(gs_ctx* m, uint32_t t, uint32_t L, uint64_t Tn, bool timing) {
   CK(m, hipSetDevice(m->dev));
   plan_coarse_owner(m, Tn * w.slots, nullptr);
   if (!grow(m->cmsg, (m->h_cap[kRegions] + 16) * 4) || !grow(m->gmap, ((Tn + 63) / 64 + 1) * 4))
-    return fail(m, GS_ENOMEM, "cannot allocate " + std::to_string(m->h_cap[kRegions]) + " window messages");
+    return mark_nomem(m, "cannot allocate " + std::to_string(m->h_cap[kRegions]) + " window messages");
   w.cmsg = (uint32_t*)m->cmsg.p;
   w.gmap = (uint32_t*)m->gmap.p;
   w.tofs = 0;
@@ -2463,11 +2500,24 @@ int sender_redo(gs_ctx* m, uint32_t t, uint32_t L, uint64_t Tn) {
   CK(m, hipMemcpyAsync(m->h_misc, w.chist, kRegions * 8, hipMemcpyDeviceToHost, m->stream));
   CK(m, hipStreamSynchronize(m->stream));
   plan_coarse_owner(m, Tn * w.slots, m->h_misc);
-  if (!grow(m->cmsg, (m->h_cap[kRegions] + 16) * 4)) return fail(m, GS_ENOMEM, "cannot allocate the window messages");
+  if (!grow(m->cmsg, (m->h_cap[kRegions] + 16) * 4)) return mark_nomem(m, "cannot allocate the window messages");
   w.cmsg = (uint32_t*)m->cmsg.p;
   CK(m, hipMemcpyAsync(w.ccap, m->h_cap, (kRegions + 1) * 8, hipMemcpyHostToDevice, m->stream));
   CK(m, win_expand(w, t, L, Tn, 2, m->stream));
   ++m->timing.exact_redos;
+  return GS_OK;
+}
+
+// A rank's local allocation result made collective: every rank returns
+// GS_ENOMEM if any rank could not allocate (one u64 all-reduce).
+int agree_ok(gs_ctx* m, bool ok, const char* what) {
+  unsigned long long* d = m->d_gcounts + (size_t)m->G * kMaxWindow;  // scratch
+  m->h_misc[8] = ok ? 0ull : 1ull;
+  CK(m, hipMemcpyAsync(d, &m->h_misc[8], 8, hipMemcpyHostToDevice, m->stream));
+  RC(x_all_reduce(m, d, 1));
+  CK(m, hipMemcpyAsync(&m->h_misc[9], d, 8, hipMemcpyDeviceToHost, m->stream));
+  CK(m, hipStreamSynchronize(m->stream));
+  if (m->h_misc[9]) return fail(m, GS_ENOMEM, ok ? std::string("another rank: ") + what : std::string(what));
   return GS_OK;
 }
 
@@ -2512,8 +2562,9 @@ int shard_exchange(gs_ctx* acc, const std::vector<gs_ctx*>& ms, const std::vecto
     unsigned long long rsum = 0;
     for (uint32_t s = 0; s < G; ++s)
       if (s != me) { in[0][s] = rsum; rsum += bsize(s, me); }
-    if (!grow(m->xsend, (ptot[me] + 16) * 4) || !grow(m->xrecv, (rsum + 16) * 4))
-      return fail(m, GS_ENOMEM, "cannot allocate the exchange buffers");
+    // every rank learns whether every rank has its buffers before any sends
+    const bool ok = grow(m->xsend, (ptot[me] + 16) * 4) && grow(m->xrecv, (rsum + 16) * 4);
+    RC(agree_ok(m, ok, "cannot allocate the exchange buffers"));
     inbuf[0] = (uint32_t*)m->xrecv.p;
     pout[0] = (uint32_t*)m->xsend.p;
   } else {
@@ -2618,7 +2669,7 @@ int shard_exchange(gs_ctx* acc, const std::vector<gs_ctx*>& ms, const std::vecto
           rb[p] = bsize(p, me) * 4;
           rsum += bsize(p, me);
         }
-      if (!grow_pinned(m, (ptot[me] + rsum) * 4 + 16)) return fail(m, GS_ENOMEM, "cannot allocate exchange staging");
+      RC(agree_ok(m, grow_pinned(m, (ptot[me] + rsum) * 4 + 16), "cannot allocate exchange staging"));
       char* hs = m->h_xbuf;
       char* hr = m->h_xbuf + ptot[me] * 4;
       CK(m, hipMemcpyAsync(hs, pout[0], ptot[me] * 4, hipMemcpyDeviceToHost, m->stream));
@@ -2651,7 +2702,8 @@ int shard_receive(gs_ctx* m, const ShardWin& sw, bool timing) {
   CK(m, hipSetDevice(m->dev));
   const uint64_t R = m->rtotal;
   const uint64_t fcap = R + R / 8 + (uint64_t)wr.ncoarse * 256 * 513 + 16;
-  if (!grow(m->fmsg, fcap * 4)) return fail(m, GS_ENOMEM, "cannot allocate " + std::to_string(R) + " received messages");
+  if (!grow(m->fmsg, fcap * 4))  // nothing resolved: every rank stops at the next gather
+    return mark_nomem(m, "cannot allocate " + std::to_string(R) + " received messages");
   wr.fmsg = m->ws.fmsg = (uint32_t*)m->fmsg.p;
   if (timing) CK(m, hipEventRecord(m->ev[4], m->stream));
   CK(m, win_plan(wr, false, m->stream));
@@ -2691,7 +2743,7 @@ int receiver_redo(gs_ctx* m, const ShardWin& sw) {
   CK(m, win_part2(wr, R, false, m->stream));
   size_t need = 0;
   CK(m, win_scan_fine(wr, nullptr, need, m->stream));
-  if (!grow(m->tmp, need)) return fail(m, GS_ENOMEM, "cannot allocate scan scratch");
+  if (!grow(m->tmp, need)) return mark_nomem(m, "cannot allocate scan scratch");
   need = m->tmp.bytes;
   CK(m, win_scan_fine(wr, m->tmp.p, need, m->stream));
   CK(m, hipMemsetAsync(wr.ffill, 0, (size_t)wr.nfine * 8, m->stream));
@@ -2732,6 +2784,9 @@ int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint
     const uint32_t Lw = std::min(Lmax, n - done);
     const uint32_t t = (uint32_t)(t0 + done);
     RC(counts(t, Lw));
+    for (uint32_t r = 0; r < G; ++r)  // a shard could not allocate: every shard stops here
+      if (cnt[(size_t)r * kMaxWindow + kFlagSlot] & kErrNoMem)
+        return fail(acc, GS_ENOMEM, "shard " + std::to_string(r) + " could not allocate a window buffer");
     if (flagged()) {  // a shard's previous window overflowed its receive partition: it redoes it, then all count again
       for (uint32_t r = 0; r < G; ++r) {
         if (!(cnt[(size_t)r * kMaxWindow + kFlagSlot] & (kErrCoarse | kErrFine))) continue;
@@ -2769,6 +2824,12 @@ int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint
       }
       // 3. fills and overflow flags; exact redo of an overflowed expand
       RC(gather_layouts(ms, lay));
+      auto nomem = [&]() {
+        for (uint32_t r = 0; r < G; ++r)
+          if (lay[(size_t)r * K1 + kRegions] & kErrNoMem) return true;
+        return false;
+      };
+      if (nomem()) return fail(acc, GS_ENOMEM, "a shard could not allocate its window messages");
       bool redo = false;
       for (uint32_t r = 0; r < G; ++r)
         if (lay[(size_t)r * K1 + kRegions] & kErrCoarse) {
@@ -2776,7 +2837,10 @@ int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint
           for (gs_ctx* m : ms)
             if (m->rank == r) RC(sender_redo(m, t, L, own[r]));
         }
-      if (redo) RC(gather_layouts(ms, lay));
+      if (redo) {
+        RC(gather_layouts(ms, lay));
+        if (nomem()) return fail(acc, GS_ENOMEM, "a shard could not allocate its window messages");
+      }
       for (gs_ctx* m : ms) {
         CK(m, hipSetDevice(m->dev));
         CK(m, win_consume_sh(m->ws, t, L, m->stream));
@@ -2808,8 +2872,23 @@ int shard_windows(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t t0, uint
       CK(m, hipMemcpyAsync(m->h_err, m->d_err, 4, hipMemcpyDeviceToHost, m->stream));
       CK(m, hipStreamSynchronize(m->stream));
     }
-  for (gs_ctx* m : ms)
-    if (*m->h_err & kErrArrivals) return fail(m, GS_EOVERFLOW, "too many arrivals at one node in one tick");
+  // the errors no gather has carried yet (a receipt count overflow, a shard
+  // that could not allocate its received messages): every rank returns the
+  // same code at the same point (one u64 all-reduce per rank)
+  unsigned long long bad = 0;
+  for (gs_ctx* m : ms) bad |= *m->h_err & (kErrArrivals | kErrNoMem);
+  if (is_rank(m0)) {
+    unsigned long long* d = m0->d_gcounts + (size_t)G * kMaxWindow;  // scratch: [arrivals, nomem]
+    m0->h_misc[8] = (bad & kErrArrivals) ? 1 : 0;
+    m0->h_misc[9] = (bad & kErrNoMem) ? 1 : 0;
+    CK(m0, hipMemcpyAsync(d, &m0->h_misc[8], 16, hipMemcpyHostToDevice, m0->stream));
+    RC(x_all_reduce(m0, d, 2));
+    CK(m0, hipMemcpyAsync(&m0->h_misc[10], d, 16, hipMemcpyDeviceToHost, m0->stream));
+    CK(m0, hipStreamSynchronize(m0->stream));
+    bad = (m0->h_misc[10] ? kErrArrivals : 0u) | (m0->h_misc[11] ? kErrNoMem : 0u);
+  }
+  if (bad & kErrNoMem) return fail(acc, GS_ENOMEM, "a shard could not allocate its received messages");
+  if (bad & kErrArrivals) return fail(acc, GS_EOVERFLOW, "too many arrivals at one node in one tick");
   return GS_OK;
 }
 
@@ -2832,12 +2911,360 @@ void account_tick(gs_ctx* c, uint64_t tick, const unsigned long long* s, gs_tick
   if (o) *o = gs_tick_stats{c->t, s[ST_FIRED], s[ST_SENT], s[ST_MSGS], c->recv, c->crashed, c->pending};
 }
 
+// ---- device-driven shard windows -------------------
+// The shards of one device (a group on one GPU, one stream) or one rank run
+// their windows without a host round trip: every shard's fire counts and
+// region fills are gathered into device buffers (the shards of a device share
+// them; ranks all-gather them with RCCL), k_cut makes the same window cut on
+// every shard, k_rtab lays out each shard's receive side, a fine-region
+// overflow is re-partitioned exactly inside the window, and k_close_dd applies
+// gs_run's poll rule to the global counters.  The host enqueues window i
+// before it reads window i-1's staged counters.  A rank whose blocks travel
+// to other ranks (G > 1) waits once per window: the grouped send / receive
+// needs the block sizes on the host.  A window in which any shard overflowed
+// a region estimate or its buffers is stopped on every shard before anything
+// is consumed or resolved (kErrAbort), and the host redoes it host-driven.
+bool dd_ok(const gs_ctx* acc, const std::vector<gs_ctx*>& ms) {
+  if ((acc->p.flags & GS_FLAG_TIMING) || getenv("GS_SYNC_WINDOWS") || shard_serial()) return false;
+  const gs_ctx* m0 = ms[0];
+  if (m0->pp || !m0->win || !m0->shard) return false;
+  if (acc->group) return !acc->gtrials && acc->gdevs.size() == 1;  // one device: one stream, blocks read in place
+  return is_rank(acc);
+}
+
+int dd_setup(gs_ctx* acc, const std::vector<gs_ctx*>& ms) {
+  gs_ctx* m0 = ms[0];
+  const uint32_t G = m0->G, M = (uint32_t)ms.size();
+  CK(acc, hipSetDevice(m0->dev));
+  if (!acc->dd_mem) {
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t b1 = al((size_t)G * kMaxWindow * 8), b2 = al((size_t)G * kDDRow * 8),
+                 b3 = al((size_t)M * kDDWStat * 8), b4 = al((size_t)M * sizeof(WinCtl)),
+                 b5 = al((size_t)(4 * M + 2) * sizeof(void*));
+    CK(acc, hipMalloc(&acc->dd_mem, b1 + b2 + b3 + b4 + b5));
+    char* q = (char*)acc->dd_mem;
+    acc->dd_gcnt = (unsigned long long*)q; q += b1;
+    acc->dd_glay = (unsigned long long*)q; q += b2;
+    acc->dd_wstat = (unsigned long long*)q; q += b3;
+    acc->dd_ctl = (WinCtl*)q; q += b4;
+    acc->dd_ptrs = (void**)q;
+    CK(acc, hipHostMalloc((void**)&acc->h_ddptrs, (size_t)(4 * M + 2) * sizeof(void*)));
+    if (is_rank(acc) && G > 1) CK(acc, hipHostMalloc((void**)&acc->h_ddlay, (size_t)G * kDDRow * 8));
+  }
+  if (!acc->h_stage) {
+    CK(acc, hipHostMalloc((void**)&acc->h_stage, (size_t)kSlots * kStageWords * 8,
+                          hipHostMallocMapped | hipHostMallocPortable));
+    CK(acc, hipHostGetDevicePointer((void**)&acc->d_stage, acc->h_stage, 0));
+    for (uint32_t i = 0; i < kSlots; ++i) {
+      hipEvent_t e;
+      CK(acc, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      acc->wev.push_back(e);
+    }
+  }
+  return GS_OK;
+}
+
+// Elements a buffer holds for the window kernels (16 of slack, as run_async).
+unsigned long long buf_cap(const Buf& b) { return b.bytes / 4 > 16 ? b.bytes / 4 - 16 : 0; }
+
+// Windows from acc->t + 1 until tend (exclusive), or (poll > 0) until the poll
+// rule stops the run; on_tick(tick, row) sees every tick's global counters in
+// order; *stop = 1 + GS_RUN_* if the poll rule stopped the run; *fallback =
+// true if a window was stopped by an overflow (nothing of it consumed or
+// resolved: the caller redoes it and goes on host-driven from acc->t).
+template <class OnTick>
+int dd_run(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t tend, uint32_t poll, uint64_t max_ticks,
+           OnTick on_tick, uint32_t* stop, bool* fallback) {
+  *stop = 0;
+  *fallback = false;
+  RC(dd_setup(acc, ms));
+  gs_ctx* m0 = ms[0];
+  const uint32_t G = m0->G, M = (uint32_t)ms.size();
+  const bool rank = is_rank(m0), travel = rank && G > 1;
+  const size_t K1 = kRegions + 1;
+  hipStream_t st = m0->stream;
+  CK(acc, hipSetDevice(m0->dev));
+  // the members' own streams (begin, reset, the packed row view) are done
+  // before their windows run on m0's stream
+  for (gs_ctx* m : ms)
+    if (m != m0) CK(acc, hipStreamSynchronize(m->stream));
+  const uint32_t Lmax = std::min<uint32_t>(std::max<int32_t>(m0->p.delay_low, 1), kBitTicks);
+  const uint64_t N = m0->p.n;
+  const unsigned long long budget = ((N + kFineNodes - 1) >> kFineLog) * (unsigned long long)kWinSlotsPerBucket;
+  const uint32_t B8 = m0->ws.obins * kCoarseSub, nreg = G * B8;
+  // the message buffers keep the size the windows so far needed (an overflow
+  // is redone host-driven, which grows them); the group map holds every fire
+  bool ok = true;
+  for (gs_ctx* m : ms)
+    ok = ok && grow(m->gmap, ((m->ntot + 1 + 63) / 64 + 1) * 4) && grow(m->cmsg, 64) && grow(m->fmsg, 64);
+  if (rank) RC(agree_ok(m0, ok, "cannot allocate the window message buffers"));
+  else if (!ok) return fail(acc, GS_ENOMEM, "cannot allocate the window message buffers");
+  // pointer tables: region starts (k_rtab's in-place regions), the receive
+  // layout's sources, the members' counters and control blocks
+  void** hp = acc->h_ddptrs;
+  const uint32_t nsrc = rank ? 2u : M + 1;
+  void** d_ccaps = acc->dd_ptrs;
+  void** d_src = acc->dd_ptrs + M;
+  void** d_wst = acc->dd_ptrs + 2 * M + 1;
+  void** d_ctls = acc->dd_ptrs + 3 * M + 1;
+  for (uint32_t i = 0; i < M; ++i) {
+    hp[i] = ms[i]->ws.ccap;
+    hp[2 * M + 1 + i] = acc->dd_wstat + (size_t)i * kDDWStat;
+    hp[3 * M + 1 + i] = acc->dd_ctl + i;
+  }
+  if (rank) {
+    hp[M] = m0->xrecv.p;
+    hp[M + 1] = m0->cmsg.p;
+  } else {
+    for (uint32_t i = 0; i < M; ++i) hp[M + i] = ms[i]->cmsg.p;
+    hp[2 * M] = nullptr;
+  }
+  CK(acc, hipMemcpyAsync(acc->dd_ptrs, hp, (size_t)(4 * M + 2) * sizeof(void*), hipMemcpyHostToDevice, st));
+  // control blocks: the same window state on every member
+  std::vector<WinCtl> hc(M);
+  for (uint32_t i = 0; i < M; ++i) {
+    WinCtl& h = hc[i];
+    h = WinCtl{};
+    h.tnext = (uint32_t)(acc->t + 1);
+    h.tend = (uint32_t)std::min<uint64_t>(tend, 0xFFFFFFFFull);
+    h.poll = poll;
+    h.pbase = (uint32_t)acc->t;
+    h.lmax = Lmax;
+    h.recv = acc->recv;
+    h.crashed = acc->crashed;
+    h.pending = acc->pending;
+    h.cover = cover_threshold(N);
+    h.max_ticks = max_ticks;
+    h.cmsg_cap = buf_cap(ms[i]->cmsg);
+    h.fmsg_cap = buf_cap(ms[i]->fmsg);
+    h.xs_cap = buf_cap(ms[i]->xsend);
+    h.xr_cap = buf_cap(ms[i]->xrecv);
+  }
+  CK(acc, hipMemcpyAsync(acc->dd_ctl, hc.data(), (size_t)M * sizeof(WinCtl), hipMemcpyHostToDevice, st));
+  CK(acc, hipMemsetAsync(acc->dd_gcnt, 0, (size_t)G * kMaxWindow * 8, st));
+  // the members' window states (send side, and the receive side as
+  // shard_exchange lays it out)
+  std::vector<WinState> ws(M), wr(M);
+  std::vector<uint64_t> tn_bound(M);
+  for (uint32_t i = 0; i < M; ++i) {
+    gs_ctx* m = ms[i];
+    WinState w = m->ws;
+    w.ctl = acc->dd_ctl + i;
+    w.stage = acc->d_stage;
+    w.lstride = Lmax;
+    w.dd = 1;
+    w.guard = 0;
+    w.abort_on_err = 0;
+    w.gcnt = acc->dd_gcnt;
+    w.glay = acc->dd_glay;
+    w.tfires = acc->dd_gcnt + (size_t)m->rank * kMaxWindow;
+    w.cfill = acc->dd_glay + (size_t)m->rank * kDDRow;
+    w.wstat = acc->dd_wstat + (size_t)i * kDDWStat;
+    w.nglob = N;
+    w.gmap = (uint32_t*)m->gmap.p;
+    w.cmsg = (uint32_t*)m->cmsg.p;
+    w.fmsg = (uint32_t*)m->fmsg.p;
+    ws[i] = w;
+    WinState r = w;
+    r.cmsg = nullptr;
+    r.csrc = (const uint32_t* const*)(m->d_rtab + 4 * K1);
+    r.ccap = m->d_rtab;
+    r.ccap_end = m->d_rtab + K1;
+    r.cfill = m->d_rtab + 2 * K1;
+    r.csub = G * kCoarseSub;
+    wr[i] = r;
+    tn_bound[i] = std::min<uint64_t>(m->ntot + 1, 4096ull * 1024);
+  }
+  const uint64_t T_bound = 2048ull * 16384;
+  // ranks whose blocks travel: the block sizes, from the gathered rows
+  auto bsize = [&](uint32_t s, uint32_t d) {
+    unsigned long long a = 0;
+    for (uint32_t r = d * B8; r < (d + 1) * B8; ++r) a += acc->h_ddlay[(size_t)s * kDDRow + r];
+    return a;
+  };
+  // one window: 0 = enqueued up to its close, 1 = stopped at the block
+  // exchange (the window is dead: stopped, or aborted -> *aborted)
+  auto enqueue = [&](uint32_t slot, bool* aborted) -> int {
+    *aborted = false;
+    for (uint32_t i = 0; i < M; ++i) CK(acc, win_units(ws[i], 0, Lmax, st));
+    if (rank) RC(x_all_gather(m0, acc->dd_gcnt, kMaxWindow * 8));
+    for (uint32_t i = 0; i < M; ++i) CK(acc, win_cut(ws[i], budget, st));
+    for (uint32_t i = 0; i < M; ++i) CK(acc, win_unitscan(ws[i], st));
+    for (uint32_t i = 0; i < M; ++i) CK(acc, win_expand(ws[i], 0, Lmax, tn_bound[i], 1, st));
+    if (rank) RC(x_all_gather(m0, acc->dd_glay, kDDRow * 8));
+    for (uint32_t i = 0; i < M; ++i)
+      CK(acc, win_rtab(ws[i], ms[i]->d_rtab, (const unsigned long long* const*)d_ccaps, (const uint32_t* const*)d_src,
+                       nsrc, rank ? 1u : 0u, st));
+    if (travel) {
+      // the window's one host wait: block sizes for the grouped send / receive
+      gs_ctx* m = m0;
+      const uint32_t me = m->rank;
+      CK(acc, hipMemcpyAsync(acc->h_ddlay, acc->dd_glay, (size_t)G * kDDRow * 8, hipMemcpyDeviceToHost, st));
+      CK(acc, hipMemcpyAsync(m->h_err, m->d_err, 4, hipMemcpyDeviceToHost, st));
+      CK(acc, hipMemcpyAsync(m->h_misc, acc->dd_ctl, 32, hipMemcpyDeviceToHost, st));
+      CK(acc, hipStreamSynchronize(st));
+      const uint32_t* hc0 = (const uint32_t*)m->h_misc;  // WinCtl t, L, tnext, tend, poll, pbase, stop, lmax
+      if (*m->h_err & kErrAbort) { *aborted = true; return 1; }
+      if (hc0[1] == 0 || hc0[6]) return 1;  // stopped or past the end: the same on every rank
+      // every rank's send / receive needs against its buffers (their
+      // capacities travel in the gathered rows): a rank that must grow them
+      // does, and then every rank learns whether every rank could
+      std::vector<unsigned long long> ptot(G, 0), rsum(G, 0);
+      for (uint32_t s = 0; s < G; ++s)
+        for (uint32_t d = 0; d < G; ++d)
+          if (s != d) {
+            const unsigned long long b = bsize(s, d);
+            ptot[s] += b;
+            rsum[d] += b;
+          }
+      bool any_grow = false;
+      for (uint32_t s = 0; s < G; ++s) {
+        const unsigned long long* row = acc->h_ddlay + (size_t)s * kDDRow;
+        if (ptot[s] > row[kRegions + 2] || rsum[s] > row[kRegions + 3]) any_grow = true;
+      }
+      if (any_grow) {
+        const void* old_recv = m->xrecv.p;
+        const bool ok = grow(m->xsend, (ptot[me] + 16) * 4) && grow(m->xrecv, (rsum[me] + 16) * 4);
+        unsigned long long* d = m->d_gcounts + (size_t)G * kMaxWindow;  // scratch
+        m->h_misc[8] = ok ? 0ull : 1ull;
+        CK(acc, hipMemcpyAsync(d, &m->h_misc[8], 8, hipMemcpyHostToDevice, st));
+        RC(x_all_reduce(m, d, 1));
+        CK(acc, hipMemcpyAsync(&m->h_misc[9], d, 8, hipMemcpyDeviceToHost, st));
+        CK(acc, hipStreamSynchronize(st));
+        if (m->h_misc[9]) return fail(acc, GS_ENOMEM, "a rank cannot allocate its exchange buffers");
+        WinCtl* c = acc->dd_ctl;
+        m->h_misc[10] = buf_cap(m->xsend);
+        m->h_misc[11] = buf_cap(m->xrecv);
+        CK(acc, hipMemcpyAsync(&c->xs_cap, &m->h_misc[10], 16, hipMemcpyHostToDevice, st));
+        if (m->xrecv.p != old_recv) {  // the receive layout's source 0 (k_rtab wrote the old address)
+          m->h_misc[12] = (unsigned long long)(uintptr_t)m->xrecv.p;
+          CK(acc, hipMemcpyAsync(m->d_rtab + 4 * K1, &m->h_misc[12], 8, hipMemcpyHostToDevice, st));
+          hp[M] = m->xrecv.p;
+          CK(acc, hipMemcpyAsync(&d_src[0], &hp[M], sizeof(void*), hipMemcpyHostToDevice, st));
+        }
+        CK(acc, hipStreamSynchronize(st));  // the pinned words above are reused next window
+      }
+      CK(acc, win_pack(ws[0], m->d_rtab + 3 * K1, nreg, (uint32_t*)m->xsend.p, st));
+      // block of sender s for destination d: after s's blocks for d' < d (its packed output)
+      auto bstart = [&](uint32_t s, uint32_t d) {
+        unsigned long long a = 0;
+        for (uint32_t d2 = 0; d2 < d; ++d2)
+          if (d2 != s) a += bsize(s, d2);
+        return a;
+      };
+      std::vector<unsigned long long> in(G, 0);
+      unsigned long long rs = 0;
+      for (uint32_t s = 0; s < G; ++s)
+        if (s != me) { in[s] = rs; rs += bsize(s, me); }
+      uint32_t* xs = (uint32_t*)m->xsend.p;
+      uint32_t* xr = (uint32_t*)m->xrecv.p;
+      if (m->comm) {
+        const Rccl& r = rccl();
+        NCK(acc, r.group_start());
+        for (uint32_t p = 0; p < G; ++p) {
+          if (p == me) continue;
+          if (bsize(me, p)) NCK(acc, r.send(xs + bstart(me, p), bsize(me, p), ncclUint32, (int)p, m->comm, st));
+          if (bsize(p, me)) NCK(acc, r.recv(xr + in[p], bsize(p, me), ncclUint32, (int)p, m->comm, st));
+        }
+        NCK(acc, r.group_end());
+      } else {
+        std::vector<size_t> sb(G, 0), rb(G, 0);
+        for (uint32_t p = 0; p < G; ++p)
+          if (p != me) { sb[p] = bsize(me, p) * 4; rb[p] = bsize(p, me) * 4; }
+        RC(agree_ok(m, grow_pinned(m, (ptot[me] + rs) * 4 + 16), "cannot allocate exchange staging"));
+        char* hs = m->h_xbuf;
+        char* hr = m->h_xbuf + ptot[me] * 4;
+        CK(acc, hipMemcpyAsync(hs, xs, ptot[me] * 4, hipMemcpyDeviceToHost, st));
+        CK(acc, hipStreamSynchronize(st));
+        if (m->hx.all_to_allv(m->hx.user, hs, sb.data(), hr, rb.data()))
+          return fail(acc, GS_EDEVICE, "the exchange's all_to_allv callback failed");
+        CK(acc, hipMemcpyAsync(xr, hr, rs * 4, hipMemcpyHostToDevice, st));
+        CK(acc, hipStreamSynchronize(st));
+      }
+    }
+    for (uint32_t i = 0; i < M; ++i) {
+      CK(acc, win_plan(wr[i], false, st));
+      CK(acc, win_part2(wr[i], T_bound, true, st));
+      CK(acc, win_fine_redo(wr[i], T_bound, st));
+      CK(acc, win_resolve(wr[i], 0, Lmax, st));
+      CK(acc, win_stats_dd(ws[i], st));
+    }
+    if (rank) RC(x_all_reduce(m0, acc->dd_wstat, kDDWStat));
+    CK(acc, win_close_dd(ws[0], (const unsigned long long* const*)d_wst, (WinCtl* const*)d_ctls, M, slot, st));
+    CK(acc, hipEventRecord(acc->wev[slot], st));
+    return 0;
+  };
+  bool eoverflow = false;
+  // window i-1's results: 0 = go on, 1 = finished
+  auto absorb = [&](uint32_t slot, int* what) -> int {
+    CK(acc, hipEventSynchronize(acc->wev[slot]));
+    const unsigned long long* sg = acc->h_stage + (size_t)slot * kStageWords;
+    const uint32_t t0 = (uint32_t)sg[0], L = (uint32_t)sg[1];
+    *what = 0;
+    if (sg[3] & kErrAbort) {
+      *fallback = true;
+      *what = 1;
+      return GS_OK;
+    }
+    m0->timing.exact_redos += sg[4];
+    for (uint32_t k = 0; k < L; ++k) on_tick((uint64_t)t0 + k, sg + 8 + (size_t)k * kStatFields);
+    if (sg[3] & kErrArrivals) eoverflow = true;
+    if (sg[2]) *stop = (uint32_t)sg[2];
+    if (sg[2] || L == 0 || (uint64_t)t0 + L >= tend || eoverflow) *what = 1;
+    return GS_OK;
+  };
+  bool ab = false;
+  int e0 = 0;
+  RC((e0 = enqueue(0, &ab), e0 < 0 ? e0 : 0));
+  if (e0 == 1) {
+    *fallback = ab;
+  } else {
+    for (uint32_t i = 1;; ++i) {
+      const int e = enqueue(i % kSlots, &ab);
+      if (e < 0) return e;
+      int what = 0;
+      RC(absorb((i - 1) % kSlots, &what));
+      if (what) break;
+      if (e == 1) {  // window i stopped at its exchange (it staged nothing)
+        *fallback = ab;
+        break;
+      }
+    }
+  }
+  CK(acc, hipStreamSynchronize(st));
+  if (*fallback) {  // undo what the stopped window left: its expand's counters, the flags
+    for (gs_ctx* m : ms) {
+      CK(acc, hipMemsetAsync(m->ws.sstats, 0, (size_t)kStatShards * kMaxWindow * kStatFields * 8, st));
+      CK(acc, hipMemcpyAsync(m->h_err, m->d_err, 4, hipMemcpyDeviceToHost, st));
+      CK(acc, hipStreamSynchronize(st));
+      *m->h_err &= ~(kErrCoarse | kErrFine | kErrAbort);
+      CK(acc, hipMemcpyAsync(m->d_err, m->h_err, 4, hipMemcpyHostToDevice, st));
+    }
+    CK(acc, hipStreamSynchronize(st));
+  }
+  if (eoverflow) return fail(acc, GS_EOVERFLOW, "too many arrivals at one node in one tick");
+  return GS_OK;
+}
+
 // Sharded step: `acc` keeps the global counters (the group, or the rank).
 int shard_step(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint32_t ticks, gs_tick_stats* out) {
   const bool timing = (acc->p.flags & GS_FLAG_TIMING) != 0;
   for (gs_ctx* m : ms) {
     CK(m, hipSetDevice(m->dev));
     RC(expand_view(m));
+  }
+  if (dd_ok(acc, ms) && ticks > 0) {  // device-driven windows
+    uint32_t stop = 0, k = 0;
+    bool fallback = false;
+    RC(dd_run(acc, ms, acc->t + ticks + 1, 0, ~0ull,
+              [&](uint64_t tick, const unsigned long long* row) {
+                account_tick(acc, tick, row, out ? &out[k] : nullptr);
+                ++k;
+              },
+              &stop, &fallback));
+    if (!fallback) return GS_OK;
+    ticks -= k;  // a window overflowed: it and the rest host-driven
+    if (out) out += k;
   }
   std::vector<unsigned long long> sum(kStatFields);
   uint32_t done = 0;
@@ -3111,7 +3538,37 @@ int gs_run(gs_ctx* c, uint32_t poll, uint64_t max_ticks, gs_tick_stats* out, siz
   const bool flood = !c->pp;
   const uint64_t pbase = c->t;
   uint64_t f0 = c->fired, s0 = c->sent, m0 = c->msgs;
-  if (async_ok(c)) {  // device-driven windows: the poll rule runs on the device (k_close)
+  if (!c->pp && !c->gtrials && (c->group || c->shard) && dd_ok(c, shards_of(c))) {
+    // device-driven shard windows: the poll rule runs on the device (k_close_dd)
+    if (c->aborted) return fail(c, GS_EDEVICE, "this rank's exchange failed earlier; the run is over");
+    if (!c->begun) return fail(c, GS_EINVAL, "gs_broadcast_begin first");
+    std::vector<gs_ctx*> ms = shards_of(c);
+    for (gs_ctx* m : ms) {
+      CK(m, hipSetDevice(m->dev));
+      RC(expand_view(m));
+    }
+    uint32_t stop = 0;
+    bool fallback = false;
+    const int rc = dd_run(c, ms, ~0ull, poll, max_ticks,
+                          [&](uint64_t tick, const unsigned long long* row) {
+                            account_tick(c, tick, row, nullptr);
+                            if ((tick - pbase) % poll) return;
+                            if (out && k < cap)
+                              out[k] = gs_tick_stats{c->t, c->fired - f0, c->sent - s0, c->msgs - m0, c->recv,
+                                                     c->crashed, c->pending};
+                            ++k;
+                            f0 = c->fired; s0 = c->sent; m0 = c->msgs;
+                          },
+                          &stop, &fallback);
+    if (rc) return c->group ? rc : abort_rank(c, rc);
+    if (!fallback) {
+      st = stop ? (int32_t)stop - 1 : GS_RUN_MAX_TICKS;
+      if (c->tacc.size() == 1) snap_trial(c, 0, st);
+      if (nout) *nout = k;
+      if (status) *status = st;
+      return GS_OK;
+    }
+  } else if (async_ok(c)) {  // device-driven windows: the poll rule runs on the device (k_close)
     uint32_t stop = 0;
     bool fallback = false;
     RC(run_async(c, ~0ull, poll, max_ticks,

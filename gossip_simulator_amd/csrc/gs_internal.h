@@ -119,6 +119,7 @@ struct WinCtl {
   unsigned long long Tn, T;          // broadcasts firing in the window, their friend slots
   unsigned long long recv, crashed, pending, cover, max_ticks;  // poll rule state
   unsigned long long cmsg_cap, fmsg_cap;  // message buffer capacities (elements)
+  unsigned long long xs_cap, xr_cap;      // device-driven shard windows of ranks: send / receive block buffers
 };
 constexpr uint32_t kStageWords = 8 + 16 * 8;  // per-window staging: snapshot + per-tick rows
 
@@ -179,6 +180,20 @@ struct WinState {
   uint32_t abort_on_err;         // host-driven shard windows: an overflowed window's later kernels skip
   uint32_t G, rank;              // shards, this shard's index
   uint32_t seg_per;              // nodes per shard (shard r owns [r*seg_per, ...))
+  // Device-driven shard windows (dd = 1; section 6.6 of DESIGN.md): every
+  // shard's per-tick fire counts are gathered in gcnt ([G][kMaxWindow], this
+  // shard's row is tfires) and its region fills, overflow flags and fine
+  // buffer capacity in glay ([G][kDDRow], this shard's row is cfill), so each
+  // shard cuts the same window and computes its receive layout on the device.
+  // Only kErrAbort (set by k_rtab when any shard overflowed) stops a window;
+  // kErrFine makes the receive side re-partition exactly in the same window
+  // (the guard kernels run only then).
+  uint32_t dd;
+  uint32_t guard;                // 1: this launch runs only if the shard's kErrFine is set
+  unsigned long long* gcnt;
+  unsigned long long* glay;
+  unsigned long long* wstat;     // [kMaxWindow][kStatFields] the window's counters (this shard's, then global)
+  uint64_t nglob;                // nodes of the whole broadcast
   uint64_t n, W;
   uint32_t nfine, ncoarse, R, stride, stride_magic;
   int32_t delay_low;
@@ -210,6 +225,18 @@ __host__ __device__ __forceinline__ void node_key(uint32_t tlog, uint32_t tmask,
 constexpr uint32_t kErrArrivals = 4;  // > 65535 arrivals at one node in one tick (both engines)
 constexpr uint32_t kErrCoarse = 8;    // a coarse region overflowed its estimate
 constexpr uint32_t kErrFine = 16;     // a fine region overflowed its estimate
+constexpr uint32_t kErrAbort = 32;    // device-driven shard windows: a shard's window overflowed, every shard stops
+constexpr uint32_t kErrNoMem = 64;    // host-driven shard windows: a shard could not allocate (every rank returns)
+// device-driven shard windows: a row of glay = kRegions fills, the flag word
+// (kErrCoarse), the capacities (elements) of the shard's fine buffer and, for
+// ranks, of its send / receive block buffers
+constexpr uint32_t kDDRow = kRegions + 4;
+constexpr uint32_t kDDWStat = kMaxWindow * kStatFields + 8;  // wstat words: rows, then flags (kErrArrivals, redos)
+// A shard's receive layout (gs_ctx::d_rtab): region starts, ends, fills, its
+// own pack offsets ([kRegions + 1] each), then the source buffers (<= 257
+// pointers), the window's received messages in the last word.
+constexpr size_t kRtabWords = 4 * (kRegions + 1) + 260;
+constexpr size_t kRtabTotal = kRtabWords - 1;
 
 hipError_t win_units(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
 // device-driven windows (w.ctl set, w.lstride = ctl->lmax)
@@ -230,6 +257,19 @@ hipError_t win_seal_rows(const uint8_t* deg, uint32_t* ids, uint64_t n, uint32_t
 hipError_t win_stats_reduce(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
 // node-range shards
 hipError_t win_consume_sh(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s);
+// device-driven shard windows (w.dd): the receive layout of shard w.rank from
+// the gathered fills (rtab as gs_api.cpp's shard_exchange lays it out;
+// ccaps[s] = sender s's region starts, in place unless `travels`; src[] the
+// layout's source buffers); the exact fine re-partition guarded by kErrFine;
+// the window's counters into w.wstat; the close over the G shards' wstat
+// (wstats / ctls: the group's shards, or this rank's own after the
+// all-reduce) with gs_run's poll rule and the host staging slot.
+hipError_t win_rtab(const WinState& w, unsigned long long* rtab, const unsigned long long* const* ccaps,
+                    const uint32_t* const* src, uint32_t nsrc, uint32_t travels, hipStream_t s);
+hipError_t win_fine_redo(const WinState& w, uint64_t T, hipStream_t s);
+hipError_t win_stats_dd(const WinState& w, hipStream_t s);
+hipError_t win_close_dd(const WinState& w, const unsigned long long* const* wstats, WinCtl* const* ctls,
+                        uint32_t n, uint32_t slot, hipStream_t s);
 // Copies the first min(cfill[r], room) messages of every region r < nreg from
 // w.cmsg to out + poff[r] (the all-to-all's send blocks, back to back);
 // regions with poff[r] = ~0 stay where they are.

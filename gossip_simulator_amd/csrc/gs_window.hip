@@ -53,8 +53,14 @@ constexpr uint32_t kRoll0Fine = kFineLog + 4;
 // ctl->tnext and may hold up to Lw ticks (none once the run has stopped, a
 // partition overflowed -- the host then redoes that window -- or tend is
 // reached; never past the next poll).  0 = nothing to do.
+// Error bits that stop a window: an overflow (the host redoes the window), or
+// in device-driven shard windows only kErrAbort (k_rtab: some shard's window
+// overflowed; a fine overflow is re-partitioned in the window itself).
+__device__ __forceinline__ uint32_t stop_bits(const WinState& w) {
+  return w.dd ? kErrAbort : (kErrCoarse | kErrFine);
+}
 __device__ __forceinline__ bool win_abort(const WinState& w) {
-  return (*w.err & (kErrCoarse | kErrFine)) != 0;
+  return (*w.err & stop_bits(w)) != 0;
 }
 // The window control block's first 32 bytes (t, L, tnext, tend, poll, pbase,
 // stop, lmax) and the error word, all loaded before any is tested: a kernel
@@ -74,7 +80,7 @@ __device__ __forceinline__ CtlView ctl_view(const WinState& w) {
 __device__ __forceinline__ uint32_t win_open(const WinState& w, uint32_t& t) {
   const CtlView c = ctl_view(w);
   t = c.tnext;
-  const bool dead = (c.err & (kErrCoarse | kErrFine)) || c.stop || t >= c.tend;
+  const bool dead = (c.err & stop_bits(w)) || c.stop || t >= c.tend;
   uint32_t Lw = min(c.lmax, c.tend - t);
   if (c.poll) {
     const uint32_t P = c.pbase + c.poll * ((t - c.pbase + c.poll - 1) / c.poll);  // next poll tick
@@ -87,7 +93,9 @@ __device__ __forceinline__ uint32_t win_live(const WinState& w, uint32_t& t0, ui
   if (!w.ctl) return w.abort_on_err && win_abort(w) ? 0u : L;  // shards: a window that overflowed is redone
   const CtlView c = ctl_view(w);
   t0 = c.t;
-  return (c.err & (kErrCoarse | kErrFine)) ? 0u : c.L;
+  // a guarded launch (the exact fine re-partition) runs only after an overflow
+  const bool off = (c.err & stop_bits(w)) || (w.guard && !(c.err & kErrFine));
+  return off ? 0u : c.L;
 }
 
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
@@ -190,6 +198,12 @@ __global__ __launch_bounds__(256) void k_units(const WinState w, uint32_t t0, ui
   if (threadIdx.x < L && s_t[threadIdx.x]) atomicAdd(&w.tfires[threadIdx.x], (unsigned long long)s_t[threadIdx.x]);
   for (uint32_t i = tid; i < kRegions; i += nth) { w.chist[i] = 0; w.cfill[i] = 0; }
   for (uint32_t i = tid; i < w.nfine; i += nth) w.ffill[i] = 0;
+  if (w.dd && tid == 0) {  // this shard's gathered row: flag word, buffer capacities
+    w.cfill[kRegions] = 0;
+    w.cfill[kRegions + 1] = w.ctl->fmsg_cap;
+    w.cfill[kRegions + 2] = w.ctl->xs_cap;
+    w.cfill[kRegions + 3] = w.ctl->xr_cap;
+  }
   // host-driven windows clear the overflow flags here; device-driven and shard
   // windows keep them until the host has redone the window
   if (tid == 0 && !w.ctl && !w.abort_on_err) *w.err &= ~(kErrCoarse | kErrFine);
@@ -211,7 +225,17 @@ __global__ __launch_bounds__(256) void k_cut(const WinState w, unsigned long lon
   const uint32_t Lw = win_open(w, t);
   // every load this kernel needs is issued up front (one latency, not a chain)
   const unsigned long long cap = c->cmsg_cap;
-  if (b < kMaxWindow) s_tf[b] = w.tfires[b];
+  __shared__ unsigned long long s_own[kMaxWindow];  // device-driven shards: this shard's fires per tick
+  if (b < kMaxWindow) {
+    if (w.dd) {  // the cut from every shard's gathered counts: the same window on every shard
+      unsigned long long g = 0;
+      for (uint32_t r = 0; r < w.G; ++r) g += w.gcnt[(size_t)r * kMaxWindow + b];
+      s_tf[b] = g;
+      s_own[b] = w.tfires[b];
+    } else {
+      s_tf[b] = w.tfires[b];
+    }
+  }
   unsigned long long ts[4][kMaxWindow];  // this thread's tiles' fires per tick
 #pragma unroll
   for (uint32_t j = 0; j < 4; ++j)
@@ -228,14 +252,21 @@ __global__ __launch_bounds__(256) void k_cut(const WinState w, unsigned long lon
       uint32_t L = 1;
       unsigned long long Tn = s_tf[0];
       while (L < Lw && (Tn + s_tf[L]) * w.stride <= budget) Tn += s_tf[L++];
-      for (uint32_t k = 0; k < kMaxWindow; ++k) w.tfires[k] = 0;
+      if (w.dd) {  // this shard's own fires (its row is zeroed by k_unitscan, after every shard's cut)
+        Tn = 0;
+        for (uint32_t k = 0; k < L; ++k) Tn += s_own[k];
+      } else {
+        for (uint32_t k = 0; k < kMaxWindow; ++k) w.tfires[k] = 0;
+      }
       c->t = t;
       c->L = L;
       s_L = L;
       c->tnext = t + L;
       c->Tn = Tn;
-      c->T = Tn * w.stride;
-      s_T = Tn * w.stride;
+      // owner expand (shards): the plan of gs_api.cpp's plan_coarse_owner over
+      // the longest row; unsharded: over the stride
+      c->T = Tn * (w.owner ? w.slots : w.stride);
+      s_T = c->T;
     }
   }
   __syncthreads();
@@ -265,15 +296,33 @@ __global__ __launch_bounds__(256) void k_cut(const WinState w, unsigned long lon
   }
   // coarse regions: each sub-region gets 1/8 of its bin's node share of T,
   // plus 512 (plan_coarse on the host)
-  const unsigned long long lo = (unsigned long long)b << kCoarseShift;
-  const unsigned long long hi = min((unsigned long long)w.n, lo + (1ull << kCoarseShift));
-  const unsigned long long sub =
-      b < w.ncoarse ? (unsigned long long)((double)s_T * (double)(hi - lo) / (double)w.n / kCoarseSub) + 512 : 0ull;
+  unsigned long long sub = 0;
+  if (!w.owner) {
+    const unsigned long long lo = (unsigned long long)b << kCoarseShift;
+    const unsigned long long hi = min((unsigned long long)w.n, lo + (1ull << kCoarseShift));
+    sub = b < w.ncoarse ? (unsigned long long)((double)s_T * (double)(hi - lo) / (double)w.n / kCoarseSub) + 512
+                        : 0ull;
+  } else {  // bin b = owner d * obins + 2^22-node chunk of d's range (plan_coarse_owner)
+    const uint32_t d = b / w.obins, k = b % w.obins;
+    unsigned long long cnt = 0;
+    if (d < w.G) {
+      const unsigned long long dlo = (unsigned long long)d * w.seg_per;
+      const unsigned long long dhi = min(dlo + w.seg_per, (unsigned long long)w.nglob);
+      const unsigned long long lo = dlo + ((unsigned long long)k << kCoarseShift);
+      const unsigned long long hi = min(dhi, lo + (1ull << kCoarseShift));
+      cnt = hi > lo ? hi - lo : 0ull;
+    }
+    sub = cnt ? (unsigned long long)((double)s_T * (double)cnt / (double)w.nglob / kCoarseSub) + 512 : 0ull;
+  }
   unsigned long long total;
   const unsigned long long base = block_exscan256_u64(sub * kCoarseSub, &s_sz[0], &total);
   if (total > cap) {  // the buffer is too small: no region at all, the host grows and redoes
     for (uint32_t x = 0; x < kCoarseSub; ++x) w.ccap[b * kCoarseSub + x] = 0;
-    if (b == 0) { w.ccap[kRegions] = 0; atomicOr(w.err, kErrCoarse); }
+    if (b == 0) {
+      w.ccap[kRegions] = 0;
+      atomicOr(w.err, kErrCoarse);
+      if (w.dd) atomicOr(reinterpret_cast<unsigned int*>(&w.cfill[kRegions]), kErrCoarse);  // every shard stops
+    }
     return;
   }
   for (uint32_t x = 0; x < kCoarseSub; ++x) w.ccap[b * kCoarseSub + x] = base + x * sub;
@@ -290,6 +339,9 @@ __global__ __launch_bounds__(256) void k_unitscan(const WinState w) {
   const uint32_t L = win_live(w, t0, 0);
   if (!L) return;
   const uint32_t Ls = w.lstride, tile = blockIdx.x, f = tile * 256 + threadIdx.x;
+  // device-driven shards: every shard's cut has read this shard's gathered
+  // counts; its row restarts at 0 for the next window's k_units
+  if (w.dd && tile == 0 && threadIdx.x < kMaxWindow) w.tfires[threadIdx.x] = 0;
   unsigned long long sz[kMaxWindow], sum = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kMaxWindow; ++k)  // all loads in flight, then the sum
@@ -735,6 +787,7 @@ __global__ __launch_bounds__(B) void k_expand(const WinState w, uint32_t t0, uin
     if (mycnt) {
       if (at + mycnt > cend - cbase) {
         atomicOr(w.err, kErrCoarse);
+        if (w.dd) atomicOr(reinterpret_cast<unsigned int*>(&w.cfill[kRegions]), kErrCoarse);  // every shard stops
         sm.ovf = 1;
       }
       sm.gbase[tid] = cbase + at - sm.off[tid];
@@ -1757,6 +1810,7 @@ __global__ void k_schedule_win(const WinState w, uint32_t node, uint32_t t, uint
 __global__ void k_pack(const WinState w, const unsigned long long* poff, uint32_t nreg, uint32_t* out) {
   const uint32_t r = blockIdx.x;
   if (r >= nreg || poff[r] == ~0ull) return;
+  if (w.dd && (*w.err & kErrAbort)) return;  // device-driven shard window that some shard overflowed
   const unsigned long long f = region_fill(w, r);
   const uint32_t* src = w.cmsg + w.ccap[r];
   uint32_t* dst = out + poff[r];
@@ -1776,7 +1830,296 @@ __global__ void k_consume_sh(const WinState w, uint32_t t0, uint32_t L) {
   }
 }
 
+// Exclusive scan of one u64 per thread over a block of NW waves (s: NW words
+// of LDS); returns the thread's prefix, *total the block's sum.  Block-uniform.
+template <uint32_t NW>
+__device__ __forceinline__ unsigned long long block_exscan_u64(unsigned long long v, unsigned long long* s,
+                                                               unsigned long long* total) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned long long x = v;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s[wv] = x;
+  __syncthreads();
+  unsigned long long before = 0, all = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < NW; ++q) {
+    const unsigned long long t = s[q];
+    if (q < wv) before += t;
+    all += t;
+  }
+  __syncthreads();
+  *total = all;
+  return before + x - v;
+}
+
+// ---- device-driven shard windows ------------------
+// The host-driven shard window (gs_api.cpp shard_windows) reads every shard's
+// fire counts and region fills on the host to cut the window and lay out the
+// receive side.  Here the counts and fills are gathered into device buffers
+// (RCCL all-gathers between ranks; the shards of one device share them), every
+// shard cuts the same window (k_cut over the gathered counts) and computes its
+// own receive layout (k_rtab), so a window needs no host round trip unless
+// its blocks travel between ranks (the host then reads the block sizes for
+// the grouped send / receive).
+
+// Shard w.rank's receive layout from the gathered fills: the region starts,
+// ends and fills of (bin c, sender s, sub-region x) at (c * G + s) * 8 + x, its
+// own pack offsets, the source buffers and the window's received messages --
+// what shard_exchange lays out on the host.  Every shard's row also carries
+// its overflow flag and fine-buffer capacity: if any shard's expand overflowed
+// a region estimate, or any shard would receive more messages than its fine
+// buffer holds, every shard sets kErrAbort (the same decision everywhere,
+// from the same gathered rows) and the host redoes the window host-driven.
+// One block of 256 threads.
+__global__ __launch_bounds__(256) void k_rtab(const WinState w, unsigned long long* rtab,
+                                              const unsigned long long* const* ccaps, const uint32_t* const* src,
+                                              uint32_t nsrc, uint32_t travels) {
+  __shared__ unsigned long long s_x[4];
+  __shared__ unsigned long long s_R[256];
+  __shared__ uint32_t s_abort;
+  const uint32_t tid = threadIdx.x;
+  uint32_t t0;
+  if (!win_live(w, t0, 0)) return;
+  const uint32_t G = w.G, me = w.rank, B8 = w.obins * kCoarseSub, nreg = G * B8;
+  constexpr size_t K1 = kRegions + 1;
+  unsigned long long *rcap = rtab, *rend = rtab + K1, *rfill = rtab + 2 * K1, *mypoff = rtab + 3 * K1;
+  s_R[tid] = 0;
+  if (tid == 0) s_abort = 0;
+  __syncthreads();
+  uint32_t fl = 0;
+  for (uint32_t s = tid; s < G; s += 256) fl |= (uint32_t)w.glay[(size_t)s * kDDRow + kRegions];
+  if (fl & (kErrCoarse | kErrAbort)) atomicOr(&s_abort, 1u);
+  for (uint32_t s = 0; s < G; ++s) {
+    const unsigned long long* row = w.glay + (size_t)s * kDDRow;
+    for (uint32_t r = tid; r < nreg; r += 256) {
+      const unsigned long long f = row[r];
+      if (f) atomicAdd(&s_R[r / B8], f);
+    }
+  }
+  __syncthreads();
+  for (uint32_t d = tid; d < G; d += 256) {  // shard d's fine plan bound (shard_receive's fcap) vs its buffer
+    const unsigned long long lo = (unsigned long long)d * w.seg_per;
+    const unsigned long long nd = min((unsigned long long)w.seg_per, (unsigned long long)w.nglob - lo);
+    const unsigned long long ncd = (((nd + kFineNodes - 1) >> kFineLog) + 255) / 256;
+    const unsigned long long R = s_R[d];
+    if (R + R / 8 + ncd * 256 * 513 + 16 > w.glay[(size_t)d * kDDRow + kRegions + 1]) atomicOr(&s_abort, 2u);
+  }
+  __syncthreads();
+  if (s_abort) {
+    if (tid == 0) atomicOr(w.err, kErrAbort);
+    return;
+  }
+  for (uint32_t rr = tid; rr < K1; rr += 256) {
+    rcap[rr] = rend[rr] = rfill[rr] = 0;
+    mypoff[rr] = ~0ull;
+  }
+  __syncthreads();
+  // region (c, s, x) of the blocks for this shard: in place in sender s's
+  // buffer (its region start), or in the received blocks at the sender's
+  // block offset plus the fills before it inside the block
+  const uint32_t in_src = travels ? 0u : G;
+  const uint32_t per = (B8 + 255) / 256;  // <= 8 (B8 <= kRegions)
+  unsigned long long in_s = 0, tot = 0;
+  for (uint32_t s = 0; s < G; ++s) {
+    const bool tr = travels && s != me;
+    const unsigned long long* row = w.glay + (size_t)s * kDDRow + (size_t)me * B8;
+    const unsigned long long* cc = ccaps[travels ? 0u : s] + (size_t)me * B8;
+    unsigned long long f[8], sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+      const uint32_t i = tid * per + j;
+      f[j] = j < per && i < B8 ? row[i] : 0ull;
+      sum += f[j];
+    }
+    unsigned long long btot;
+    unsigned long long off = block_exscan_u64<4>(sum, s_x, &btot);
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+      const uint32_t i = tid * per + j;
+      if (j >= per || i >= B8) continue;
+      const uint32_t c = i / kCoarseSub, x = i % kCoarseSub;
+      const size_t rr = ((size_t)c * G + s) * kCoarseSub + x;
+      const unsigned long long at = tr ? ((unsigned long long)in_src << kSrcShift) | (in_s + off)
+                                       : ((unsigned long long)(travels ? 1u : s) << kSrcShift) | cc[i];
+      rcap[rr] = at;
+      rend[rr] = at + f[j];
+      rfill[rr] = f[j];
+      off += f[j];
+    }
+    if (tr) in_s += btot;
+    tot += btot;
+  }
+  if (travels) {  // this shard's own blocks that leave, back to back in region order (k_pack)
+    const unsigned long long* row = w.glay + (size_t)me * kDDRow;
+    const uint32_t per2 = (nreg + 255) / 256;
+    unsigned long long f[8], sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+      const uint32_t r = tid * per2 + j;
+      f[j] = j < per2 && r < nreg && r / B8 != me ? row[r] : 0ull;
+      sum += f[j];
+    }
+    unsigned long long btot;
+    unsigned long long off = block_exscan_u64<4>(sum, s_x, &btot);
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+      const uint32_t r = tid * per2 + j;
+      if (j >= per2 || r >= nreg || r / B8 == me) continue;
+      mypoff[r] = off;
+      off += f[j];
+    }
+  }
+  if (tid < nsrc) rtab[4 * K1 + tid] = (unsigned long long)(uintptr_t)src[tid];
+  if (tid == 0) rtab[kRtabTotal] = tot;
+}
+
+// The exact fine re-partition of a device-driven shard window whose fine
+// regions overflowed their estimates (kErrFine): the counts cleared (here),
+// k_plan's tile prefix, k_part2's counting pass, the scan into fstart
+// (k_fine_scan), k_part2's scatter.  Guarded launches (w.guard): they do
+// nothing unless the shard's kErrFine is set; k_stats_dd clears it.
+__global__ void k_fine_zero(const WinState w) {
+  uint32_t t0;
+  if (!win_live(w, t0, 0)) return;
+  const uint32_t nh = w.ncoarse * 256 + 1;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nh; i += gridDim.x * blockDim.x) {
+    w.fhist[i] = 0;
+    if (i < w.nfine) w.ffill[i] = 0;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_fine_scan(const WinState w) {
+  __shared__ unsigned long long s_x[16];
+  uint32_t t0;
+  if (!win_live(w, t0, 0)) return;
+  const uint32_t n = w.nfine + 1, per = (n + 1023) / 1024, tid = threadIdx.x;
+  unsigned long long sum = 0;
+  for (uint32_t j = 0; j < per; ++j) {
+    const uint32_t i = tid * per + j;
+    if (i < n) sum += w.fhist[i];
+  }
+  unsigned long long tot;
+  unsigned long long a = block_exscan_u64<16>(sum, s_x, &tot);
+  for (uint32_t j = 0; j < per; ++j) {
+    const uint32_t i = tid * per + j;
+    if (i >= n) break;
+    w.fstart[i] = a;
+    a += w.fhist[i];
+    if (i < w.nfine) w.ffill[i] = 0;
+  }
+}
+
+// The window's counters of this shard (its stat shards summed into w.wstat,
+// zero rows past the window or in a stopped one) and its flags: kErrArrivals,
+// an exact fine re-partition (kErrFine, cleared here), kErrAbort.
+// kMaxWindow * kStatFields * kCloseLanes threads.
+__global__ void k_stats_dd(const WinState w) {
+  const uint32_t tid = threadIdx.x;
+  const CtlView c = ctl_view(w);
+  const bool dead = (c.err & kErrAbort) != 0;
+  const uint32_t L = dead || c.stop ? 0u : c.L;
+  const uint32_t i = tid / kCloseLanes, part = tid % kCloseLanes, k = i / kStatFields;
+  unsigned long long sum = 0;
+  if (k < L) sum = stat_shard_sum(w, i, part);  // k is uniform over each lane group
+  if (part == 0) w.wstat[i] = sum;
+  if (tid < 8) {
+    constexpr uint32_t F = kMaxWindow * kStatFields;
+    unsigned long long v = 0;
+    if (tid == 0) v = (c.err & kErrArrivals) ? 1 : 0;
+    if (tid == 1) v = (c.err & kErrFine) ? 1 : 0;
+    if (tid == 2) v = dead ? 1 : 0;
+    w.wstat[F + tid] = v;
+  }
+  if (tid == 0 && (c.err & kErrFine)) atomicAnd(w.err, ~kErrFine);
+}
+
+// The close of a device-driven shard window: the window's global counters
+// (the sum of the n shards' wstat: the group's shards, or this rank's own
+// after the all-reduce), gs_run's poll rule (simulator.go:243-248, as
+// k_close) on every shard's control block, and staging slot `slot` for the
+// host.  One block of 128 threads.
+__global__ __launch_bounds__(128) void k_close_dd(const WinState w, const unsigned long long* const* wstats,
+                                                  WinCtl* const* ctls, uint32_t n, uint32_t slot) {
+  __shared__ unsigned long long rows[kDDWStat];
+  const uint32_t tid = threadIdx.x;
+  constexpr uint32_t F = kMaxWindow * kStatFields;
+  for (uint32_t i = tid; i < kDDWStat; i += blockDim.x) {
+    unsigned long long v = 0;
+    for (uint32_t q = 0; q < n; ++q) v += wstats[q][i];
+    rows[i] = v;
+  }
+  __syncthreads();
+  const WinCtl* c0 = ctls[0];
+  const bool dead = rows[F + 2] != 0;
+  const uint32_t t0 = c0->t, L = dead || c0->stop ? 0u : c0->L;
+  unsigned long long* st = w.stage + (size_t)slot * kStageWords;
+  for (uint32_t i = tid; i < F; i += blockDim.x) st[8 + i] = i / kStatFields < L ? rows[i] : 0ull;
+  if (tid != 0) return;
+  uint32_t stop = c0->stop;
+  if (L) {
+    unsigned long long recv = c0->recv, crashed = c0->crashed, pending = c0->pending;
+    for (uint32_t j = 0; j < L; ++j) {
+      recv += rows[j * kStatFields + ST_RECV];
+      crashed += rows[j * kStatFields + ST_CRASH];
+      pending += rows[j * kStatFields + ST_SCHED] - rows[j * kStatFields + ST_FIRED];
+    }
+    const uint32_t tl = t0 + L - 1;  // windows never cross a poll tick
+    if (c0->poll && (tl - c0->pbase) % c0->poll == 0 && !stop) {
+      if (recv >= c0->cover) stop = 1 + GS_RUN_COVERED;
+      else if (pending == 0) stop = 1 + GS_RUN_QUIESCENT;
+      else if (tl >= c0->max_ticks) stop = 1 + GS_RUN_MAX_TICKS;
+    }
+    for (uint32_t q = 0; q < n; ++q) {
+      WinCtl* c = ctls[q];
+      c->recv = recv;
+      c->crashed = crashed;
+      c->pending = pending;
+      c->stop = stop;
+    }
+  }
+  st[0] = t0;
+  st[1] = L;
+  st[2] = stop;
+  st[3] = (dead ? kErrAbort : 0u) | (rows[F] ? kErrArrivals : 0u);
+  st[4] = rows[F + 1];  // exact fine re-partitions in the window
+}
+
 }  // namespace
+
+hipError_t win_rtab(const WinState& w, unsigned long long* rtab, const unsigned long long* const* ccaps,
+                    const uint32_t* const* src, uint32_t nsrc, uint32_t travels, hipStream_t s) {
+  hipLaunchKernelGGL(k_rtab, dim3(1), dim3(256), 0, s, w, rtab, ccaps, src, nsrc, travels);
+  return hipGetLastError();
+}
+
+hipError_t win_fine_redo(const WinState& w, uint64_t T, hipStream_t s) {
+  WinState g = w;
+  g.guard = 1;
+  (void)T;
+  // small persistent grids: when nothing overflowed (nearly always) each launch
+  // only reads the control block and leaves
+  hipLaunchKernelGGL(k_fine_zero, dim3(64), dim3(256), 0, s, g);
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(256), 0, s, g, true);
+  hipLaunchKernelGGL(k_part2<false>, dim3(512), dim3(kPartBlock), 0, s, g);
+  hipLaunchKernelGGL(k_fine_scan, dim3(1), dim3(1024), 0, s, g);
+  hipLaunchKernelGGL(k_part2<true>, dim3(512), dim3(kPartBlock), 0, s, g);
+  return hipGetLastError();
+}
+
+hipError_t win_stats_dd(const WinState& w, hipStream_t s) {
+  hipLaunchKernelGGL(k_stats_dd, dim3(1), dim3(kMaxWindow * kStatFields * kCloseLanes), 0, s, w);
+  return hipGetLastError();
+}
+
+hipError_t win_close_dd(const WinState& w, const unsigned long long* const* wstats, WinCtl* const* ctls,
+                        uint32_t n, uint32_t slot, hipStream_t s) {
+  hipLaunchKernelGGL(k_close_dd, dim3(1), dim3(128), 0, s, w, wstats, ctls, n, slot);
+  return hipGetLastError();
+}
 
 hipError_t win_units(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s) {
   (void)L;

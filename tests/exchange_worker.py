@@ -41,6 +41,27 @@ def main():
         return out.numpy()
 
     z = np.load(os.path.join(d, "table.npz"))
+    if model == "overflow":  # only the rank that owns the hub overflows; every rank must return GS_EOVERFLOW
+        codes = []
+        for mode in ("dd", "host"):
+            if mode == "host":
+                os.environ["GS_SYNC_WINDOWS"] = "1"
+            cfg = gs.Config(n=int(z["n"]), fanout=32, fanin=32, delaylow=10, delayhigh=11, droprate=0.0,
+                            crashrate=0.01, seed=0x5EED, device=0)
+            sim = gs.Simulator.rank_exchange(cfg, world, rank, all_gather, all_reduce, all_to_allv)
+            code = 0
+            try:
+                sim.load_peers(z["deg"], z["ids"])
+                sim.broadcast_begin(0)
+                sim.step(45)
+            except gs.GossipError as e:
+                code = e.code
+            finally:
+                sim.close()
+            codes.append(code)
+        np.savez(os.path.join(d, f"rank{rank}.npz"), codes=np.array(codes))
+        dist.destroy_process_group()
+        return
     kw = {k: (z[k].item()) for k in ("n", "fanout", "fanin", "crashrate", "droprate")}
     cfg = gs.Config(n=int(kw["n"]), fanout=int(kw["fanout"]), fanin=int(kw["fanin"]),
                     crashrate=float(kw["crashrate"]), droprate=float(kw["droprate"]), seed=0x5EED,

@@ -60,8 +60,14 @@ def c4_table(gs):
         return c, deg, ids, rows, sim.received(), sim.crashed()
 
 
-@pytest.mark.parametrize("G", [1, 2, 4, 8])
-def test_shards_match_unsharded_c4_shape(gs, c4_table, G):
+@pytest.mark.parametrize("G,mode", [(1, "dd"), (2, "dd"), (4, "dd"), (8, "dd"), (2, "host"), (8, "host")])
+def test_shards_match_unsharded_c4_shape(gs, c4_table, G, mode, monkeypatch):
+    """mode dd: device-driven shard windows (one device's shards on one
+    stream; the first windows overflow the empty message buffers and are
+    redone host-driven, which grows them); host: GS_SYNC_WINDOWS=1, every
+    window host-driven."""
+    if mode == "host":
+        monkeypatch.setenv("GS_SYNC_WINDOWS", "1")
     c, deg, ids, rows, recv, crash = c4_table
     with gs.Simulator(c, devices=[0] * G) as sim:
         assert len(sim.shard_info()) == G and sim.shard_info()[-1][1] == c.n
@@ -71,6 +77,66 @@ def test_shards_match_unsharded_c4_shape(gs, c4_table, G):
         assert np.array_equal(got, rows)
         assert np.array_equal(sim.received(), recv)
         assert np.array_equal(sim.crashed(), crash)
+
+
+@pytest.mark.parametrize("G", [1, 3, 8])
+def test_shards_run_polls_like_unsharded(gs, c4_table, G):
+    """gs_run over device-driven shard windows (the poll rule on the device,
+    k_close_dd) gives the unsharded run's polls and status, twice (the second
+    broadcast reuses the grown buffers: every window device-driven)."""
+    c, deg, ids, _, recv, crash = c4_table
+    with gs.Simulator(c) as one:
+        one.load_peers(deg, ids)
+        one.broadcast_begin(-1)
+        ref, ref_status = one.run(poll=10)
+    with gs.Simulator(c, devices=[0] * G) as sim:
+        sim.load_peers(deg, ids)
+        for _ in range(2):
+            sim.reset()
+            sim.broadcast_begin(-1)
+            got, status = sim.run(poll=10)
+            assert status == ref_status
+            assert np.array_equal(got, ref)
+            assert np.array_equal(sim.received(), recv) and np.array_equal(sim.crashed(), crash)
+
+
+def skewed_table(n, stride, frac, seed):
+    """Random rows whose targets crowd into the first fine bucket: region
+    estimates overflow (the coarse ones make a device-driven window stop and
+    be redone host-driven; the fine ones are re-partitioned in the window)."""
+    rng = np.random.default_rng(seed)
+    deg = rng.integers(stride // 2, stride + 1, size=n).astype(np.uint8)
+    hot = rng.random((n, stride)) < frac
+    ids = np.where(hot, rng.integers(0, min(n, 16384), size=(n, stride)),
+                   rng.integers(0, n, size=(n, stride))).astype(np.uint32)
+    return deg, ids
+
+
+@pytest.mark.parametrize("G,frac", [(2, 0.8), (3, 0.6)])
+def test_shards_skewed_targets_match_oracle(gs, oracle, G, frac):
+    n, stride = 60000, 6
+    deg, ids = skewed_table(n, stride, frac, seed=G)
+    c = cfg(gs, n=n, crashrate=0.03, droprate=0.05)
+    p = oracle.make_params(n=n, fanout=c.fanout, fanin=c.fanin, delay_low=c.delaylow, delay_high=c.delayhigh,
+                           drop_rate=c.droprate, crash_rate=c.crashrate, seed=c.seed, trial=0)
+    for rep in range(2):  # the second broadcast runs on the grown buffers
+        e = oracle.Engine(p, deg, ids)
+        e.begin(-1)
+        if rep == 0:
+            sim = gs.Simulator(c, devices=[0] * G)
+            sim.load_peers(deg, ids)
+        else:
+            sim.reset()
+        sim.broadcast_begin(-1)
+        for i in range(40):
+            a, b = e.step(10), sim.step(10)
+            assert np.array_equal(a, b), f"rep {rep} poll {i}"
+            if int(a[-1][6]) == 0:
+                break
+        assert np.array_equal(e.received(), sim.received())
+        assert np.array_equal(e.crashed(), sim.crashed())
+    assert sim.timing()["exact_redos"] > 0  # an overflowed estimate was redone exactly
+    sim.close()
 
 
 def test_shard_overlay_matches(gs, c4_table):

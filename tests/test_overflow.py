@@ -90,3 +90,48 @@ def test_tick_engine_returns_overflow():
         sim.broadcast_begin(0)
         rows = sim.step(29)
         assert int(rows[-1][0]) == 29 and int(rows[:, 2].sum()) > 0
+
+
+def star32_table(copies=4):
+    """The same hub overflow within the window engine's 32-slot rows: three
+    levels of 32 relays (32768 leaves), each leaf lists the hub `copies`
+    times.  With crashrate 0.01 the hub holds about 1300 crash-roll receipts,
+    so k_resolve takes its per-node 16-bit counters (the rolled list holds
+    1024) and ~127000 receipts overflow them at tick 40."""
+    L1, L2, L3 = 32, 32 * 32, 32 * 32 * 32
+    n = 1 + L1 + L2 + L3 + 1
+    hub = n - 1
+    deg = np.zeros(n, dtype=np.uint8)
+    ids = np.zeros((n, 32), dtype=np.uint32)
+    deg[0] = 32
+    ids[0] = 1 + np.arange(32)
+    lv1, lv2, lv3 = 1, 1 + L1, 1 + L1 + L2
+    for i in range(L1):
+        deg[lv1 + i] = 32
+        ids[lv1 + i] = lv2 + i * 32 + np.arange(32)
+    for i in range(L2):
+        deg[lv2 + i] = 32
+        ids[lv2 + i] = lv3 + i * 32 + np.arange(32)
+    deg[lv3:hub] = copies
+    ids[lv3:hub, :copies] = hub
+    deg[hub] = 1
+    ids[hub, 0] = 0
+    return n, deg, ids
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [0, 2])
+def test_window_engine_returns_overflow(G):
+    """The window engine (unsharded, device-driven) and in-process shards
+    return GS_EOVERFLOW for the 32-slot star."""
+    import gossip_simulator_amd as gs
+    n, deg, ids = star32_table()
+    cfg = gs.Config(n=n, fanout=32, fanin=32, delaylow=10, delayhigh=11, droprate=0.0, crashrate=0.01,
+                    seed=0x5EED)
+    with (gs.Simulator(cfg, devices=[0] * G) if G else gs.Simulator(cfg)) as sim:
+        sim.load_peers(deg, ids)
+        sim.broadcast_begin(0)
+        with pytest.raises(gs.GossipError) as ei:
+            sim.step(45)
+        assert ei.value.code == -6  # GS_EOVERFLOW
+

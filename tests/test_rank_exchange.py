@@ -83,3 +83,31 @@ def test_two_ranks_match_unsharded(tmp_path, model, n, fanout, fanin, crash, dro
     assert np.array_equal(orr, rec), "the ranks' received words do not make up the unsharded bitset"
     if model == "flood":
         assert np.array_equal(orc, cra)
+
+
+def test_one_rank_overflows_both_return_eoverflow(tmp_path):
+    """a receipt-count overflow on ONE rank (the hub's owner) must
+    end the step with GS_EOVERFLOW on every rank -- device-driven windows and
+    host-driven (GS_SYNC_WINDOWS=1) alike -- instead of leaving the other rank
+    waiting in a collective."""
+    from test_overflow import star32_table
+    n, deg, ids = star32_table()
+    np.savez(tmp_path / "table.npz", deg=deg, ids=ids, n=n)
+    port = free_port()
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "exchange_worker.py"), str(r), "2",
+                               str(port), str(tmp_path), "overflow"], stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT) for r in range(2)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out.decode(errors="replace"))
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} failed:\n{outs[r][-3000:]}"
+        codes = np.load(tmp_path / f"rank{r}.npz")["codes"]
+        assert list(codes) == [-6, -6], f"rank {r}: {list(codes)}"
+
