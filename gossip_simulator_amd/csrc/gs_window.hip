@@ -1114,12 +1114,16 @@ constexpr uint32_t kRolledBlock = GS_ROLLED_BLOCK;  // the rolled replay: 4 wave
 // per-tick large path (resolve_tick), which reuses the same LDS for per-node
 // counters.
 constexpr uint32_t kBitWords = kFineNodes / 32;
+// The staged receipts (k_resolve<true>) take the rest of the union: 48 KB,
+// 12288 receipts per LDS-DMA round trip.
+constexpr uint32_t kResolveStage = (kFineNodes * 4 + 4 * kBitWords * 4 - kBitTicks * kBitWords * 4 - kBitWords * 8) / 4;
 struct ResolveLds {
   union {
     struct {                            // b1 .. dlist, then the infection list
       uint32_t b1[kBitTicks][kBitWords];
       uint2 cr0[kBitWords];             // per word: crashed before the window, a crash-roll
                                         // receipt in the window (from w.rollw)
+      alignas(16) uint32_t stage[kResolveStage];  // STAGE: the bucket's receipts, by LDS-DMA
     };
     struct {                            // large path
       uint32_t cnt[kFineNodes];         // per node at the current tick: arrivals | crash rolls << 16
@@ -1144,6 +1148,7 @@ struct ResolveLds {
   unsigned long long tlast;
 };  // ~72 KB: two workgroups per CU
 static_assert(kBitTicks <= kMaxWindow, "window ticks fit the message format");
+static_assert(kResolveStage % 2048 == 0, "whole batches of 8 receipts per thread");
 static_assert(sizeof(uint32_t) * kFineNodes <= sizeof(((ResolveLds*)0)->cnt), "the infection list fits");
 
 // GS_STAMPS diagnostics: thread 0 adds the cycles since the last stamp to phase i.
@@ -1293,6 +1298,11 @@ __device__ __forceinline__ void flush_counts(const WinState& w, ResolveLds& sm, 
 //            (node, tick) groups in order (rule A6, first_crash); the
 //            infections are Broadcast() (:122, :141)
 // A bucket with more rolled receipts than kRolledCap takes the per-tick large path.
+// STAGE (LDS-DMA staging of the receipts): the bucket's receipts arrive in
+// LDS 12288 at a time -- every wave issues global_load_lds_dwordx4 for its
+// 1-KB chunks, one round trip per stage instead of one per batch of 8
+// receipts per lane -- and are read back 4 per lane with 16-byte LDS reads.
+template <bool STAGE>
 __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
   __shared__ ResolveLds sm;
   const uint32_t tid = threadIdx.x, G = gridDim.x;
@@ -1358,7 +1368,7 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
     p_crash0 = cwg[wc];
     p_roll0 = w.rollw[wc];
     p_fcv = w.fcount[(size_t)(tid < w.R ? tid : 0u) * w.nfine + f];
-    ld(w.fmsg + mb, M, 0, pm);
+    if (!STAGE) ld(w.fmsg + mb, M, 0, pm);
   };
   if (nb > 0) prefetch(fB, MB, mbB);
   for (uint32_t i = 0; i < nb; ++i) {
@@ -1404,56 +1414,89 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
         dhi &= ~(255ull << (8 * b));
       }
     };
-    uint32_t m[kU];
-#pragma unroll
-    for (uint32_t u = 0; u < kU; ++u) m[u] = pm[u];
-    for (uint32_t p0 = 0, nbat = 0; p0 < (sm.err == 3 ? 0u : M); p0 += kBatch, ++nbat) {
-      uint32_t mn[kU];
-      if (p0 + kBatch < M) ld(gm, M, p0 + kBatch, mn);
-      uint2 sp[kU];
-#pragma unroll
-      for (uint32_t u = 0; u < kU; ++u) {
-        sp[u] = make_uint2(0, 0);
-        if (p0 + u * kResolveBlock + tid < M) {
-          const uint32_t loc = msg_loc(m[u]);
-          atomicOr(&sm.b1[msg_tick(m[u])][loc >> 5], 1u << (loc & 31));  // no return
-          sp[u] = sm.cr0[loc >> 5];
-        }
-      }
-      uint32_t dm = 0;  // bit u: receipt u is at a rolled node
-#pragma unroll
-      for (uint32_t u = 0; u < kU; ++u) {
-        const uint32_t sh = msg_loc(m[u]) & 31, k = msg_tick(m[u]);
-        if ((sp[u].x >> sh) & 1u) {  // crashed before the window: not counted (:108)
-          if (k < 8) dlo += 1ull << (8 * k);
-          else dhi += 1ull << (8 * (k - 8));
-        }
-        if ((sp[u].y >> sh) & 1u) dm |= 1u << u;
-      }
-      if (nbat % 31 == 30) flush_dead();
-      const uint32_t nd = __popc(dm);
-      if (__ballot(nd != 0)) {
-        uint32_t pre = 0, tot = 0;  // wave prefix of nd (<= 8)
-#pragma unroll
-        for (uint32_t bb = 0; bb < 4; ++bb) {
-          const unsigned long long bal = __ballot((nd >> bb) & 1u);
-          pre += mbcnt(bal) << bb;
-          tot += (uint32_t)__popcll(bal) << bb;
-        }
-        uint32_t base = 0;
-        if (lane_id() == 0) base = atomicAdd(&sm.ndup, tot);
-        uint32_t at = __builtin_amdgcn_readfirstlane(base) + pre;
-#pragma unroll
-        for (uint32_t u = 0; u < kU; ++u)
-          if ((dm >> u) & 1u) {
-            if (at < kRolledCap) w.rlmsg[(size_t)f * kRolledCap + at] = m[u] & ((1u << 19) - 1);
-            else sm.err = 3;
-            ++at;
-          }
-      }
-#pragma unroll
-      for (uint32_t u = 0; u < kU; ++u) m[u] = mn[u];
+    // one batch: receipts m[u] where valid(u) (a macro body: the host-driven
+    // loop below must compile exactly as it did before the staged variant)
+#define GS_RESOLVE_BATCH(VALID)                                                                   \
+    {                                                                                             \
+      uint2 sp[kU];                                                                               \
+      _Pragma("unroll") for (uint32_t u = 0; u < kU; ++u) {                                       \
+        sp[u] = make_uint2(0, 0);                                                                 \
+        if (VALID) {                                                                              \
+          const uint32_t loc = msg_loc(m[u]);                                                     \
+          atomicOr(&sm.b1[msg_tick(m[u])][loc >> 5], 1u << (loc & 31)); /* no return */         \
+          sp[u] = sm.cr0[loc >> 5];                                                               \
+        }                                                                                         \
+      }                                                                                           \
+      uint32_t dm = 0; /* bit u: receipt u is at a rolled node */                                 \
+      _Pragma("unroll") for (uint32_t u = 0; u < kU; ++u) {                                       \
+        const uint32_t sh = msg_loc(m[u]) & 31, k = msg_tick(m[u]);                               \
+        if ((sp[u].x >> sh) & 1u) { /* crashed before the window: not counted (:108) */           \
+          if (k < 8) dlo += 1ull << (8 * k);                                                      \
+          else dhi += 1ull << (8 * (k - 8));                                                      \
+        }                                                                                         \
+        if ((sp[u].y >> sh) & 1u) dm |= 1u << u;                                                  \
+      }                                                                                           \
+      if (nbat % 31 == 30) flush_dead();                                                          \
+      const uint32_t nd = __popc(dm);                                                             \
+      if (__ballot(nd != 0)) {                                                                    \
+        uint32_t pre = 0, tot = 0; /* wave prefix of nd (<= 8) */                                 \
+        _Pragma("unroll") for (uint32_t bb = 0; bb < 4; ++bb) {                                   \
+          const unsigned long long bal = __ballot((nd >> bb) & 1u);                               \
+          pre += mbcnt(bal) << bb;                                                                \
+          tot += (uint32_t)__popcll(bal) << bb;                                                   \
+        }                                                                                         \
+        uint32_t base = 0;                                                                        \
+        if (lane_id() == 0) base = atomicAdd(&sm.ndup, tot);                                      \
+        uint32_t at = __builtin_amdgcn_readfirstlane(base) + pre;                                 \
+        _Pragma("unroll") for (uint32_t u = 0; u < kU; ++u) if ((dm >> u) & 1u) {                 \
+          if (at < kRolledCap) w.rlmsg[(size_t)f * kRolledCap + at] = m[u] & ((1u << 19) - 1);    \
+          else sm.err = 3;                                                                        \
+          ++at;                                                                                   \
+        }                                                                                         \
+      }                                                                                           \
     }
+    if (!STAGE) {
+      uint32_t m[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) m[u] = pm[u];
+      for (uint32_t p0 = 0, nbat = 0; p0 < (sm.err == 3 ? 0u : M); p0 += kBatch, ++nbat) {
+        uint32_t mn[kU];
+        if (p0 + kBatch < M) ld(gm, M, p0 + kBatch, mn);
+        GS_RESOLVE_BATCH(p0 + u * kResolveBlock + tid < M)
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) m[u] = mn[u];
+      }
+    } else {
+      // stages of up to kResolveStage - 4 receipts: the DMA starts at the
+      // 16-B aligned element below the first one (head = 0..3 leading
+      // elements are not the bucket's)
+      const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+      constexpr uint32_t kStep = kResolveStage - 4;
+      uint32_t nbat = 0;
+      for (uint32_t p0 = 0; p0 < (sm.err == 3 ? 0u : M); p0 += kStep) {
+        const uint32_t cnt = min(kStep, M - p0);
+        const unsigned long long g0 = mb + p0;
+        const uint32_t head = (uint32_t)(g0 & 3), tot = head + cnt;
+        const uint32_t* src = w.fmsg + (g0 - head);
+        const uint32_t nch = (tot + 255) / 256;
+        __syncthreads();  // the previous stage has been read
+        for (uint32_t c = wv; c < nch; c += kResolveBlock / 64) {
+          const uint32_t q = c * 256 + lane * 4;
+          if (q < tot)  // (reads at most 3 elements past the bucket: inside the buffer's slack)
+            __builtin_amdgcn_global_load_lds(src + q,
+                                             (__attribute__((address_space(3))) void*)&sm.stage[c * 256], 16, 0, 0);
+        }
+        __syncthreads();  // every wave's chunks landed (the barrier's fence waits for the DMA)
+        for (uint32_t b0 = 0; b0 < tot; b0 += 8 * kResolveBlock, ++nbat) {
+          const uint32_t q0 = b0 + tid * 4, q1 = q0 + 4 * kResolveBlock;
+          const uint4 a = q0 < tot ? *reinterpret_cast<const uint4*>(&sm.stage[q0]) : make_uint4(0, 0, 0, 0);
+          const uint4 b = q1 < tot ? *reinterpret_cast<const uint4*>(&sm.stage[q1]) : make_uint4(0, 0, 0, 0);
+          const uint32_t m[kU] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+          GS_RESOLVE_BATCH(((u < 4 ? q0 : q1) + (u & 3)) >= head && ((u < 4 ? q0 : q1) + (u & 3)) < tot)
+        }
+      }
+    }
+#undef GS_RESOLVE_BATCH
     flush_dead();
     stamp(w, sm, 2);
     __syncthreads();
@@ -2269,7 +2312,9 @@ hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s
   const uint32_t gs = (w.nfine + kSmallBlock / 64 - 1) / (kSmallBlock / 64);
   hipLaunchKernelGGL(k_resolve_small<false>, dim3(gs), dim3(kSmallBlock), 0, s, w, t0, L);
   static_assert(kSmallMax == 64 * 4, "the two bodies cover 1..kSmallMax");
-  hipLaunchKernelGGL(k_resolve, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
+  static const bool stage = [] { const char* e = getenv("GS_RESOLVE_STAGE"); return e && atoi(e) == 1; }();  // A/B knob
+  if (stage) hipLaunchKernelGGL(k_resolve<true>, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
+  else hipLaunchKernelGGL(k_resolve<false>, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
   // k_resolve_rolled: small blocks (the E = 16 key arrays take 4 KB per wave; blocks finish independently)
   hipLaunchKernelGGL(k_resolve_small<true>, dim3((w.nfine + kRolledBlock / 64 - 1) / (kRolledBlock / 64)),
                      dim3(kRolledBlock), 0, s, w, t0, L);

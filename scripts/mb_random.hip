@@ -38,6 +38,14 @@ __global__ void k_load8(const unsigned long long* b, uint64_t W, uint64_t ops, u
   }
   if (acc == 0x1234567) out[0] = acc;
 }
+// random byte stores into a byte-per-node array (N = 64 * W bytes): the
+// alternative to atomicOr for idempotent "set node u" updates
+__global__ void k_store_byte(unsigned char* a, uint64_t N, uint64_t ops, uint32_t salt) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ops; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t h = mix(i * 0x9E3779B97F4A7C15ull + salt);
+    a[((uint64_t)h * N) >> 32] = 1;
+  }
+}
 __global__ void k_stream(const uint4* a, uint64_t n16, unsigned long long* out) {
   unsigned long long acc = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -59,8 +67,18 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
+  unsigned char* bytes = nullptr;
+  if (hipMalloc(&bytes, W * 64)) return 1;
+  (void)hipMemset(bytes, 0, W * 64);
   for (int rep = 0; rep < 2; ++rep) {
     float ms;
+    (void)hipEventRecord(e0);
+    hipLaunchKernelGGL(k_store_byte, dim3(8192), dim3(256), 0, 0, bytes, W * 64, ops, rep);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    printf("byte store %.3e ops in %7.2f ms = %.3e/s (1 B per node, %.2f GB array)\n", (double)ops, ms,
+           ops / (ms * 1e-3), W * 64 / 1e9);
     (void)hipEventRecord(e0);
     hipLaunchKernelGGL(k_atomic, dim3(8192), dim3(256), 0, 0, b, W, ops, rep);
     (void)hipEventRecord(e1);
