@@ -382,7 +382,13 @@ __device__ __forceinline__ void ppa_resolve(const DevState& s, const PPSparse& s
                                  : (cc && ((s.gcrash[w >> 6] >> (w & 63)) & 1));
       if (!dead) {
         ++msgs;
+#if defined(GS_PP_NOATOMIC)  // timing probe only: the round's sets are not made
+        if (w == 0xFFFFFFFFu) next[0] = 1;
+#elif defined(GS_PP_CHECKFIRST)  // an informed target's bit is set already (next starts as recv)
+        if (!((s.grecv[w >> 6] >> (w & 63)) & 1)) atomicOr(&next[w >> 6], 1ull << (w & 63));
+#else
         atomicOr(&next[w >> 6], 1ull << (w & 63));
+#endif
       }
     }
   }
@@ -406,7 +412,11 @@ __device__ __forceinline__ void ppa_resolve(const DevState& s, const PPSparse& s
         if (!iv && !fv) {  // v's pull from this informed node succeeds
           ++sent;
           ++msgs;
+#if defined(GS_PP_NOATOMIC)
+          if (vb == 0) next[0] = 1;
+#else
           atomicOr(&next[src[k] >> 6], vb);
+#endif
         }
       }
     }
