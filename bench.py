@@ -499,6 +499,8 @@ def flood_sharded(a, gs, rank, world, local, dist, n, fanout, fanin, crashrate, 
         log(f"{name} sharded x{world}: {dt * 1e3 / steps:.1f} ms per broadcast, {tot['sent'] / (dt / steps):.3e} msgs/s")
         return {"value": round(tot["sent"] * steps / dt, 1), "unit": "msgs/s", "shards": world,
                 "ms_per_step": round(dt * 1e3 / steps, 3), "steps": steps, "n": cfg.n, "fanout": fanout,
+                # wall (device-driven windows) over this rank's kernel time (GS_FLAG_TIMING run)
+                "device_ms_per_step": round(kern, 3), "wall_over_device": round(dt * 1e3 / steps / kern, 4) if kern else None,
                 "fanin": fanin, "ticks": tot["tick"], "status": STATUS[status],
                 "coverage": round(tot["received"] / cfg.n, 6),
                 "delivered_per_step": tot["sent"], "messages_per_step": tot["messages"],
@@ -618,8 +620,20 @@ def shards_inproc(a, gs):
                         per.append(round(tm["expand_ms"] + tm["part_ms"] + tm["resolve_ms"], 3))
                     sim.set_flags(False)
                     t0 = sim.shard_timing(0)
+                    # the same broadcast device-driven (one stream, no serial syncs): its wall
+                    os.environ.pop("GS_SHARD_SERIAL", None)
+                    walls = []
+                    for _ in range(2):
+                        sim.reset()
+                        sim.broadcast_begin(-1)
+                        w0 = time.perf_counter()
+                        sim.run(poll=10)
+                        walls.append(time.perf_counter() - w0)
+                    os.environ["GS_SHARD_SERIAL"] = "1"
                     key = f"{name}_G{G}"
                     out[key] = {"n": n, "shard_ms": per, "max_ms": max(per), "sum_ms": round(sum(per), 3),
+                                "dd_wall_ms": round(min(walls) * 1e3, 3),
+                                "dd_wall_over_sum": round(min(walls) * 1e3 / sum(per), 4),
                                 "delivered": tot["sent"], "windows": int(t0["windows"]),
                                 "shard0_phases_ms": {"expand": round(t0["expand_ms"], 3),
                                                      "pack+plan+part2": round(t0["part_ms"], 3),

@@ -75,6 +75,7 @@ struct gs_ctx {
   // mask, round control; rebuilt when the table (table_ver) or the failure
   // mask (fail_ver) changes
   Buf pp_rend, pp_rsrc, pp_rslot, pp_ilist, pp_fmask, pp_scan, pp_ctlb;
+  Buf pp_dset, pp_dcnt;  // deferred sets of the pull-answer rounds (PPSparse::dset)
   uint64_t table_ver = 0, fail_ver = 0, rev_ver = ~0ull, fm_tver = ~0ull, fm_fver = ~0ull;
   PPSparse sp{};
   // window engine (gs_window.hip)
@@ -715,7 +716,7 @@ void destroy_one(gs_ctx* c) {
                     (void*)c->d_glay})
     if (ptr) (void)hipFree(ptr);
   for (Buf* b : {&c->gmap, &c->cmsg, &c->fmsg, &c->tmp, &c->xsend, &c->xrecv, &c->pp_rend, &c->pp_rsrc,
-                 &c->pp_rslot, &c->pp_ilist, &c->pp_fmask, &c->pp_scan, &c->pp_ctlb})
+                 &c->pp_rslot, &c->pp_ilist, &c->pp_fmask, &c->pp_scan, &c->pp_ctlb, &c->pp_dset, &c->pp_dcnt})
     if (b->p) (void)hipFree(b->p);
   for (void* ptr : {(void*)c->h_cap, (void*)c->h_misc, (void*)c->h_err, (void*)c->h_stats, (void*)c->h_tstat,
                     (void*)c->h_stage, (void*)c->h_rtab, (void*)c->h_glay})
@@ -1598,6 +1599,23 @@ int pp_prepare(gs_ctx* c) {
   c->sp.rend = (const unsigned long long*)c->pp_rend.p;
   c->sp.rsrc = (const uint32_t*)c->pp_rsrc.p;
   c->sp.rslot = (const uint8_t*)c->pp_rslot.p;
+  // the pull-answer rounds' deferred sets (n <= 2^30; GS_PP_NODEFER=1: atomics, A/B):
+  // lists, coarse and fine regions for 0.6 n sets each (more fall back to atomicOr)
+  if (!getenv("GS_PP_NODEFER") && n <= (1ull << 30) && pp_rslot_packed(s.stride)) {
+    const uint64_t nfine = (n + 16383) >> 14, want = n * 3 / 5;
+    const uint64_t dcap = std::max<uint64_t>(4096, (want + kPPDLists - 1) / kPPDLists);
+    const uint64_t ccap = std::max<uint64_t>(4096, (want + kPPDRegions - 1) / kPPDRegions), fcap = 16384;
+    const size_t elems = (size_t)kPPDLists * dcap + (size_t)kPPDRegions * ccap + (size_t)nfine * fcap;
+    if (grow(c->pp_dset, elems * 4) && grow(c->pp_dcnt, ((size_t)kPPDLists + kPPDRegions + nfine) * 8)) {
+      c->sp.dset = (uint32_t*)c->pp_dset.p;
+      c->sp.dcnt = (unsigned long long*)c->pp_dcnt.p;
+      c->sp.dcap = dcap;
+      c->sp.ccap = ccap;
+      c->sp.fcap = fcap;
+    } else {
+      (void)hipGetLastError();  // atomics
+    }
+  }
   if (c->failed && s.stride <= 8) {  // the dense rounds read fmask instead of gathering failed words
     if (c->fm_tver != c->table_ver || c->fm_fver != c->fail_ver) {
       if (!grow(c->pp_fmask, (n + 3) & ~3ull)) {

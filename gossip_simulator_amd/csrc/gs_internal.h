@@ -341,7 +341,20 @@ struct PPSparse {
   const uint32_t* rsrc;         // [E] caller v of each in-edge
   const uint8_t* rslot;         // [E] its slot j
   const uint8_t* fmask;         // [n] bit j: friend j is failed (stride <= 8 and a mask set), else null
+  // Deferred sets of the pull-answer rounds (unsharded contexts, n <= 2^30;
+  // null: atomicOr): the round's "x is informed" updates go to per-block
+  // lists ([kPPDLists][dcap]), a coarse LDS partition by x >> 22 into
+  // [kPPDRegions][ccap], a fine one into [nfine][fcap] by x >> 14, then one
+  // workgroup per 16384-node bucket ORs them into `next` from an LDS bitmap:
+  // streamed writes instead of random atomics.  A full list or region falls
+  // back to atomicOr for what does not fit.  dcnt: the fills (lists, coarse
+  // regions, fine regions), zeroed before every round.
+  uint32_t* dset;
+  unsigned long long* dcnt;
+  uint64_t dcap, ccap, fcap;
 };
+constexpr uint32_t kPPDLists = 512;    // = k_ppa_round's grid (kPPSGrid)
+constexpr uint32_t kPPDRegions = 2048; // 256 coarse bins x 8 (XCD) sub-regions
 hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long long* sum, uint32_t t,
                     bool l2_only, const PPSparse& sp, hipStream_t st);
 hipError_t pp_live_edges(const DevState& s, uint32_t* out, hipStream_t st);

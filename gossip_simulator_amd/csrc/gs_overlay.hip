@@ -134,7 +134,7 @@ struct TickCounters {
 };
 
 // One lane per destination node: the makeup / breakup handlers in order.
-__global__ __launch_bounds__(256) void k_process(const OvParams p, uint32_t t, const uint64_t* keys,
+__global__ __launch_bounds__(256) void k_process(const OvParams p, uint32_t t, uint64_t* keys,
                                                  uint64_t m, const int64_t* heads,
                                                  const int64_t* nheads, uint8_t* deg, uint32_t* ids,
                                                  uint64_t* out, uint16_t* oslot,
@@ -148,6 +148,21 @@ __global__ __launch_bounds__(256) void k_process(const OvParams p, uint32_t t, c
     const uint32_t u = (uint32_t)(keys[start] >> (p.B + 1));
     const uint32_t ul = u & p.tmask, tb = u & ~p.tmask;  // node within its trial, trial base
     const uint64_t smask = (1ull << p.B) - 1;
+    // the radix sort ordered the tick's events by destination only (its
+    // passes over the B + 1 low bits are saved); this lane puts its
+    // destination's run in (src, kind) order -- the order the handlers replay
+    // -- by insertion (runs are a few events long in a random overlay)
+    const uint64_t lmask = (2ull << p.B) - 1;
+    for (uint64_t i = start + 1; i < end; ++i) {
+      const uint64_t key = keys[i];
+      uint64_t j = i;
+      for (; j > start; --j) {
+        const uint64_t prev = keys[j - 1];
+        if ((prev & lmask) <= (key & lmask)) break;
+        keys[j] = prev;
+      }
+      keys[j] = key;
+    }
     uint32_t* row = ids + (size_t)u * p.stride;
     uint32_t d = deg[u];
     for (uint64_t i = start; i < end; ++i) {
@@ -363,17 +378,19 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
       OVCHK(grow(oslotb, m * 2));
       OVCHK(grow(heads, m * 8));
       hipcub::DoubleBuffer<uint64_t> db((uint64_t*)bucket[s].p, (uint64_t*)scratch.p);
-      const int end_bit = (int)(2 * p.B + 1);
+      // by destination only (bits B+1 .. 2B): k_process orders each
+      // destination's short run by (src, kind) itself
+      const int begin_bit = (int)(p.B + 1), end_bit = (int)(2 * p.B + 1);
       size_t sort_bytes = 0, sel_bytes = 0;
-      OVCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, db, (int)m, 0, end_bit, stream));
+      OVCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, db, (int)m, begin_bit, end_bit, stream));
       IsHead pred{nullptr, p.B + 1};
       hipcub::CountingInputIterator<int64_t> it(0);
       OVCHK(hipcub::DeviceSelect::If(nullptr, sel_bytes, it, (int64_t*)heads.p, d_nheads, (int)m,
                                      pred, stream));
       OVCHK(grow(cub_tmp, std::max(sort_bytes, sel_bytes)));
       sort_bytes = cub_tmp.bytes;
-      OVCHK(hipcub::DeviceRadixSort::SortKeys(cub_tmp.p, sort_bytes, db, (int)m, 0, end_bit, stream));
-      const uint64_t* keys = db.Current();
+      OVCHK(hipcub::DeviceRadixSort::SortKeys(cub_tmp.p, sort_bytes, db, (int)m, begin_bit, end_bit, stream));
+      uint64_t* keys = db.Current();
       if (db.Current() != (uint64_t*)bucket[s].p) std::swap(bucket[s], scratch);
       pred.keys = keys;
       sel_bytes = cub_tmp.bytes;

@@ -364,33 +364,62 @@ __global__ __launch_bounds__(kPPSBlock) void k_ppb_round(const DevState s, unsig
 // in-edge costs a gather of v's recv / failed words (v must be live and
 // uninformed: its call is a pull from this informed node, counted here).
 // Every live caller is counted as fired from ctl->ncallers.
+// Node x is informed this round: appended to this workgroup's deferred list
+// (the active lanes with `take`, one LDS atomic per wave and call), or, with
+// no deferred buffers or a full list, an atomicOr into next.
+__device__ __forceinline__ void pp_set(const PPSparse& sp, unsigned long long* __restrict__ next, bool take,
+                                       uint32_t x, uint32_t* s_dn) {
+  if (!sp.dset) {
+    if (take) atomicOr(&next[x >> 6], 1ull << (x & 63));
+    return;
+  }
+  const unsigned long long act = __ballot(1), bal = __ballot(take);
+  if (!bal) return;
+  const uint32_t lane = threadIdx.x & 63, leader = (uint32_t)__ffsll((long long)act) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(s_dn, (uint32_t)__popcll(bal));
+  base = __shfl(base, (int)leader, 64);
+  if (take) {
+    const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+    if (pos < sp.dcap) sp.dset[(size_t)blockIdx.x * sp.dcap + pos] = x;
+    else atomicOr(&next[x >> 6], 1ull << (x & 63));
+  }
+}
+
 __device__ __forceinline__ void ppa_resolve(const DevState& s, const PPSparse& sp, uint32_t t, uint32_t c3,
                                             const uint32_t* q, uint32_t cnt, uint64_t base,
-                                            unsigned long long* __restrict__ next, uint64_t& sent, uint64_t& msgs) {
+                                            unsigned long long* __restrict__ next, uint64_t& sent, uint64_t& msgs,
+                                            uint32_t* s_dn) {
   const uint32_t lane = threadIdx.x & 63;
   if (lane >= cnt) return;
   const uint32_t e = q[lane], loc = e & 0xFFFu, d = e >> 16;
   const uint64_t u = base + loc;  // informed (so live)
   const bool cc = s.check_crashed;
-  if (d > 0) {  // u's own call: a push
-    const u32x4 r = philox((uint32_t)(s.gbase + u), t, 0, c3, s.key.k0, s.key.k1);
-    if ((int32_t)uniform(r.y, 100u) >= s.kd) {
-      const uint32_t j = uniform(r.x, d);
-      const uint32_t w = s.ids[u * s.stride + j];
-      ++sent;
-      const bool dead = sp.fmask ? ((sp.fmask[u] >> j) & 1) != 0
-                                 : (cc && ((s.gcrash[w >> 6] >> (w & 63)) & 1));
-      if (!dead) {
-        ++msgs;
-#if defined(GS_PP_NOATOMIC)  // timing probe only: the round's sets are not made
-        if (w == 0xFFFFFFFFu) next[0] = 1;
-#elif defined(GS_PP_CHECKFIRST)  // an informed target's bit is set already (next starts as recv)
-        if (!((s.grecv[w >> 6] >> (w & 63)) & 1)) atomicOr(&next[w >> 6], 1ull << (w & 63));
-#else
-        atomicOr(&next[w >> 6], 1ull << (w & 63));
-#endif
+  {  // u's own call: a push
+    bool take = false;
+    uint32_t w = 0;
+    if (d > 0) {
+      const u32x4 r = philox((uint32_t)(s.gbase + u), t, 0, c3, s.key.k0, s.key.k1);
+      if ((int32_t)uniform(r.y, 100u) >= s.kd) {
+        const uint32_t j = uniform(r.x, d);
+        w = s.ids[u * s.stride + j];
+        ++sent;
+        const bool dead = sp.fmask ? ((sp.fmask[u] >> j) & 1) != 0
+                                   : (cc && ((s.gcrash[w >> 6] >> (w & 63)) & 1));
+        if (!dead) {
+          ++msgs;
+          take = true;
+        }
       }
     }
+#if defined(GS_PP_NOATOMIC)  // timing probe only: the round's sets are not made
+    if (take && w == 0xFFFFFFFFu) next[0] = 1;
+#elif defined(GS_PP_CHECKFIRST)  // an informed target's bit is set already (next starts as recv)
+    if (take && !((s.grecv[w >> 6] >> (w & 63)) & 1)) atomicOr(&next[w >> 6], 1ull << (w & 63));
+#else
+    pp_set(sp, next, take, w, s_dn);
+#endif
   }
   const unsigned long long qb = u ? sp.rend[u - 1] : 0ull, qe = sp.rend[u];
   for (unsigned long long q0 = qb; q0 < qe; q0 += kPPEdges) {
@@ -403,22 +432,25 @@ __device__ __forceinline__ void ppa_resolve(const DevState& s, const PPSparse& s
     }
 #pragma unroll
     for (uint32_t k = 0; k < kPPEdges; ++k) {
-      if (q0 + k >= qe) break;
-      const u32x4 r = philox(src[k], t, 0, c3, s.key.k0, s.key.k1);
-      if (uniform(r.x, (x[k] >> 4) + 1) == (x[k] & 15u) && (int32_t)uniform(r.y, 100u) >= s.kd) {
-        const unsigned long long vb = 1ull << (src[k] & 63);
-        const bool iv = (s.grecv[src[k] >> 6] & vb) != 0;
-        const bool fv = cc && (s.gcrash[src[k] >> 6] & vb) != 0;
-        if (!iv && !fv) {  // v's pull from this informed node succeeds
-          ++sent;
-          ++msgs;
-#if defined(GS_PP_NOATOMIC)
-          if (vb == 0) next[0] = 1;
-#else
-          atomicOr(&next[src[k] >> 6], vb);
-#endif
+      bool take = false;
+      if (q0 + k < qe) {
+        const u32x4 r = philox(src[k], t, 0, c3, s.key.k0, s.key.k1);
+        if (uniform(r.x, (x[k] >> 4) + 1) == (x[k] & 15u) && (int32_t)uniform(r.y, 100u) >= s.kd) {
+          const unsigned long long vb = 1ull << (src[k] & 63);
+          const bool iv = (s.grecv[src[k] >> 6] & vb) != 0;
+          const bool fv = cc && (s.gcrash[src[k] >> 6] & vb) != 0;
+          if (!iv && !fv) {  // v's pull from this informed node succeeds
+            ++sent;
+            ++msgs;
+            take = true;
+          }
         }
       }
+#if defined(GS_PP_NOATOMIC)
+      if (take && src[k] == 0xFFFFFFFFu) next[0] = 1;
+#else
+      pp_set(sp, next, take, src[k], s_dn);
+#endif
     }
   }
 }
@@ -427,8 +459,12 @@ __global__ __launch_bounds__(kPPSBlock) void k_ppa_round(const DevState s, unsig
                                                              const PPSparse sp, uint32_t t) {
   __shared__ uint64_t sh[3 * kPPWaves];
   __shared__ uint32_t s_q[kPPWaves][kPPQ];
+  __shared__ uint32_t s_dn;  // this workgroup's deferred sets
   PPCtl* c = sp.ctl;
   if (c->mode != PP_ANSWER) return;
+  static_assert(kPPSGrid <= kPPDLists, "one deferred list per workgroup");
+  if (threadIdx.x == 0) s_dn = 0;
+  __syncthreads();
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t* q = s_q[wv];
   const uint32_t c3 = ctr3(K_PUSHPULL, s.key.trial);
@@ -460,7 +496,7 @@ __global__ __launch_bounds__(kPPSBlock) void k_ppa_round(const DevState s, unsig
         qn += (uint32_t)__popcll(bal);
         if (qn >= 64) {
           wave_lds_sync();
-          ppa_resolve(s, sp, t, c3, q, 64, base, next, sent, msgs);
+          ppa_resolve(s, sp, t, c3, q, 64, base, next, sent, msgs, &s_dn);
           const uint32_t rest = qn - 64;
           const uint32_t keep = lane < rest ? q[64 + lane] : 0u;
           wave_lds_sync();
@@ -470,12 +506,127 @@ __global__ __launch_bounds__(kPPSBlock) void k_ppa_round(const DevState s, unsig
       }
     }
     wave_lds_sync();
-    if (qn) ppa_resolve(s, sp, t, c3, q, qn, base, next, sent, msgs);
+    if (qn) ppa_resolve(s, sp, t, c3, q, qn, base, next, sent, msgs, &s_dn);
     wave_lds_sync();
+  }
+  if (sp.dset) {
+    __syncthreads();
+    if (threadIdx.x == 0) sp.dcnt[blockIdx.x] = s_dn < sp.dcap ? s_dn : sp.dcap;
   }
   const uint64_t v3[3] = {blockIdx.x == 0 && threadIdx.x == 0 ? c->ncallers : 0ull, sent, msgs};
   const uint32_t f3[3] = {ST_FIRED, ST_SENT, ST_MSGS};
   block_add<kPPSBlock>(sh, v3, 3, s.stats + (size_t)(t % kStatSlots) * kStatFields, f3);
+}
+
+// ---- deferred sets: coarse and fine LDS partitions, then the bitmap OR ----
+constexpr uint32_t kPPDTile = 16384;   // set targets per partition tile
+constexpr uint32_t kPPDBlock = 1024;   // 16 per thread
+
+// Exclusive scan of cnt[0..256) into off[0..257) by the first 256 threads
+// (block-uniform call; every thread passes the barriers).
+__device__ __forceinline__ void ppd_scan256(const uint32_t* cnt, uint32_t* off, uint32_t* s_w) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  uint32_t v = tid < 256 ? cnt[tid] : 0u, x = v;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (tid < 256 && lane == 63) s_w[wv] = x;
+  __syncthreads();
+  if (tid < 256) {
+    uint32_t pre = 0;
+    for (uint32_t q = 0; q < wv; ++q) pre += s_w[q];
+    off[tid] = pre + x - v;
+    if (tid == 255) off[256] = pre + x;
+  }
+  __syncthreads();
+}
+
+// One partition pass: tiles of the `nsrc` input lists (list L holds
+// min(fill[L], cap_in) targets at in + L * cap_in) are counting-sorted in LDS
+// by the 8-bit digit (x >> shift) & 255 and leave as runs: coarse pass (shift
+// 22) into region digit * 8 + (blockIdx & 7) of `out`, fine pass (shift 14)
+// into fine bucket (region's bin) * 256 + digit; one reservation per (tile,
+// digit); what does not fit its region is an atomicOr into next.
+template <bool FINE>
+__global__ __launch_bounds__(kPPDBlock) void k_ppd_part(const PPSparse sp, unsigned long long* __restrict__ next,
+                                                        const uint32_t* in, const unsigned long long* fill,
+                                                        uint32_t nsrc, uint64_t cap_in, uint32_t* out,
+                                                        unsigned long long* ofill, uint64_t cap_out) {
+  if (sp.ctl->mode != PP_ANSWER) return;
+  __shared__ uint32_t buf[kPPDTile];
+  __shared__ uint32_t cnt[256], off[257], s_w[4];
+  __shared__ unsigned long long gb[256], ge[256];
+  constexpr uint32_t kPer = kPPDTile / kPPDBlock;
+  constexpr uint32_t shift = FINE ? 14 : 22;
+  const uint32_t tid = threadIdx.x;
+  const uint64_t nch = (cap_in + kPPDTile - 1) / kPPDTile;
+  for (uint64_t tt = blockIdx.x; tt < nsrc * nch; tt += gridDim.x) {
+    const uint32_t L = (uint32_t)(tt % nsrc);
+    const uint64_t ch = tt / nsrc;
+    const unsigned long long fl = fill[L];
+    const uint64_t n = fl < cap_in ? fl : cap_in, b0 = ch * kPPDTile;
+    if (b0 >= n) continue;  // block-uniform
+    const uint32_t m = (uint32_t)min((uint64_t)kPPDTile, n - b0);
+    if (tid < 256) cnt[tid] = 0;
+    __syncthreads();
+    uint32_t x[kPer], rk[kPer];
+#pragma unroll
+    for (uint32_t r = 0; r < kPer; ++r) {
+      const uint32_t i = r * kPPDBlock + tid;
+      x[r] = i < m ? in[L * cap_in + b0 + i] : ~0u;
+      rk[r] = x[r] != ~0u ? atomicAdd(&cnt[(x[r] >> shift) & 255], 1u) : 0u;
+    }
+    __syncthreads();
+    ppd_scan256(cnt, off, s_w);
+    if (tid < 256 && cnt[tid]) {
+      const uint64_t reg = FINE ? (uint64_t)(L / 8) * 256 + tid : (uint64_t)tid * 8 + (blockIdx.x & 7);
+      const unsigned long long at = atomicAdd(&ofill[reg], (unsigned long long)cnt[tid]);
+      gb[tid] = reg * cap_out + at - off[tid];
+      ge[tid] = reg * cap_out + cap_out;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kPer; ++r)
+      if (x[r] != ~0u) buf[off[(x[r] >> shift) & 255] + rk[r]] = x[r];
+    __syncthreads();
+    for (uint32_t p = tid; p < m; p += kPPDBlock) {
+      const uint32_t v = buf[p], dg = (v >> shift) & 255;
+      const unsigned long long pos = gb[dg] + p;
+      if (pos < ge[dg]) out[pos] = FINE ? (v & ((1u << 14) - 1)) : v;
+      else atomicOr(&next[v >> 6], 1ull << (v & 63));
+    }
+    __syncthreads();
+  }
+}
+
+// One workgroup per 16384-node bucket f: its fine region's targets into an
+// LDS bitmap, ORed into its 256 words of next (this workgroup alone writes
+// them; the fallback atomics ran in the kernels before).
+__global__ __launch_bounds__(256) void k_ppd_apply(const PPSparse sp, unsigned long long* __restrict__ next,
+                                                   uint64_t W, uint32_t nfine) {
+  if (sp.ctl->mode != PP_ANSWER) return;
+  __shared__ uint32_t bm[512];
+  const unsigned long long* ffill = sp.dcnt + kPPDLists + kPPDRegions;
+  const uint32_t* fine = sp.dset + (size_t)kPPDLists * sp.dcap + (size_t)kPPDRegions * sp.ccap;
+  for (uint32_t f = blockIdx.x; f < nfine; f += gridDim.x) {
+    const unsigned long long fl = ffill[f];
+    const uint32_t n = (uint32_t)(fl < sp.fcap ? fl : sp.fcap);
+    if (!n) continue;  // block-uniform
+    bm[threadIdx.x] = 0;
+    bm[threadIdx.x + 256] = 0;
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < n; p += 256) {
+      const uint32_t loc = fine[(size_t)f * sp.fcap + p];
+      atomicOr(&bm[loc >> 5], 1u << (loc & 31));
+    }
+    __syncthreads();
+    const uint64_t w = (uint64_t)f * 256 + threadIdx.x;
+    const unsigned long long v = (unsigned long long)bm[2 * threadIdx.x] |
+                                 ((unsigned long long)bm[2 * threadIdx.x + 1] << 32);
+    if (v && w < W) next[w] |= v;
+    __syncthreads();
+  }
 }
 
 // Shards: the round's mode, chosen by the host from the global informed count
@@ -886,7 +1037,22 @@ hipError_t pp_round(const DevState& s, unsigned long long* next, unsigned long l
     const uint64_t nrange = (s.W + kPPRange - 1) / kPPRange;
     const uint32_t bblocks = (uint32_t)std::min<uint64_t>((nrange + kPPWaves - 1) / kPPWaves, kPPSGrid);
     hipLaunchKernelGGL(k_ppb_round, dim3(bblocks), dim3(kPPSBlock), 0, st, s, next, sp, t);
+    if (sp.dset) {
+      const uint32_t nfine = (uint32_t)((s.n + 16383) >> 14);
+      (void)hipMemsetAsync(sp.dcnt, 0, ((size_t)kPPDLists + kPPDRegions + nfine) * 8, st);
+    }
     hipLaunchKernelGGL(k_ppa_round, dim3(bblocks), dim3(kPPSBlock), 0, st, s, next, sp, t);
+    if (sp.dset) {  // no-ops unless the round is pull-answer
+      const uint32_t nfine = (uint32_t)((s.n + 16383) >> 14);
+      uint32_t* coarse = sp.dset + (size_t)kPPDLists * sp.dcap;
+      uint32_t* fine = coarse + (size_t)kPPDRegions * sp.ccap;
+      unsigned long long* cfill = sp.dcnt + kPPDLists;
+      hipLaunchKernelGGL(k_ppd_part<false>, dim3(1024), dim3(kPPDBlock), 0, st, sp, next, sp.dset, sp.dcnt,
+                         bblocks, sp.dcap, coarse, cfill, sp.ccap);
+      hipLaunchKernelGGL(k_ppd_part<true>, dim3(1024), dim3(kPPDBlock), 0, st, sp, next, coarse, cfill,
+                         kPPDRegions, sp.ccap, fine, cfill + kPPDRegions, sp.fcap);
+      hipLaunchKernelGGL(k_ppd_apply, dim3(std::min<uint32_t>(nfine, 8192)), dim3(256), 0, st, sp, next, s.W, nfine);
+    }
   }
   return hipGetLastError();
 }
