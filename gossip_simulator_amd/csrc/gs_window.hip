@@ -1473,13 +1473,16 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
       const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
       constexpr uint32_t kStep = kResolveStage - 4;
       uint32_t nbat = 0;
-      for (uint32_t p0 = 0; p0 < (sm.err == 3 ? 0u : M); p0 += kStep) {
+      for (uint32_t p0 = 0; p0 < M; p0 += kStep) {
+        __syncthreads();  // the previous stage has been read
+        // block-uniform exit: sm.err is read after the barrier, before any
+        // thread of this stage can set it (the barriers below must be met by all)
+        if (sm.err == 3) break;
         const uint32_t cnt = min(kStep, M - p0);
         const unsigned long long g0 = mb + p0;
         const uint32_t head = (uint32_t)(g0 & 3), tot = head + cnt;
         const uint32_t* src = w.fmsg + (g0 - head);
         const uint32_t nch = (tot + 255) / 256;
-        __syncthreads();  // the previous stage has been read
         for (uint32_t c = wv; c < nch; c += kResolveBlock / 64) {
           const uint32_t q = c * 256 + lane * 4;
           if (q < tot)  // (reads at most 3 elements past the bucket: inside the buffer's slack)
