@@ -112,9 +112,9 @@ def skewed_table(n, stride, frac, seed):
     return deg, ids
 
 
-@pytest.mark.parametrize("G,frac", [(2, 0.8), (3, 0.6)])
-def test_shards_skewed_targets_match_oracle(gs, oracle, G, frac):
-    n, stride = 60000, 6
+@pytest.mark.parametrize("G,frac,n", [(2, 0.8, 60000), (3, 0.6, 100000)])
+def test_shards_skewed_targets_match_oracle(gs, oracle, G, frac, n):
+    stride = 6
     deg, ids = skewed_table(n, stride, frac, seed=G)
     c = cfg(gs, n=n, crashrate=0.03, droprate=0.05)
     p = oracle.make_params(n=n, fanout=c.fanout, fanin=c.fanin, delay_low=c.delaylow, delay_high=c.delayhigh,
