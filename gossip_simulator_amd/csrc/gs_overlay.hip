@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -229,6 +230,127 @@ __global__ __launch_bounds__(256) void k_process(const OvParams p, uint32_t t, u
   }
 }
 
+// Grouped variant (GS_OV_GROUP=1): the tick's events sorted by destination GROUP
+// only (64 consecutive ids: 6 radix bits fewer), one wave per group, a lane per
+// destination.  The group's events are staged in LDS (up to kOvStage; a larger
+// group reads them from global memory), and each lane replays its own events
+// in (src, kind, position) order by repeated minimum search over the group --
+// the order k_process's insertion sort gives, identical keys in position
+// order (they are identical messages, so the order among them is immaterial
+// beyond the ordinal k).  The 64 lanes' rows are consecutive: the row reads
+// and writes of a wave are coalesced instead of one line per destination.
+constexpr uint32_t kOvGroupLog = 6;
+constexpr uint32_t kOvWaves = 4;
+constexpr uint32_t kOvStage = 1024;
+
+__global__ __launch_bounds__(kOvWaves * 64) void k_process_g(const OvParams p, uint32_t t, const uint64_t* keys,
+                                                             uint64_t m, const int64_t* heads,
+                                                             const int64_t* nheads, uint8_t* deg, uint32_t* ids,
+                                                             uint64_t* out, uint16_t* oslot, TickCounters* tc) {
+  __shared__ uint64_t s_ev[kOvWaves][kOvStage];
+  const int64_t H = *nheads;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t h = (int64_t)blockIdx.x * kOvWaves + wv;  // wave-uniform
+  uint32_t mk = 0, bk = 0, err = 0;
+  if (h < H) {
+    const uint64_t start = (uint64_t)heads[h];
+    const uint64_t end = (h + 1 < H) ? (uint64_t)heads[h + 1] : m;
+    const uint32_t E = (uint32_t)(end - start);  // m < 2^31
+    const uint32_t sh = p.B + 1;
+    const uint32_t u = (uint32_t)(keys[start] >> (sh + kOvGroupLog)) << kOvGroupLog | lane;  // this lane's destination
+    const bool staged = E <= kOvStage;
+    uint64_t* ev = s_ev[wv];
+    if (staged) {
+      for (uint32_t i = lane; i < E; i += 64) ev[i] = keys[start + i];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    auto key_at = [&](uint32_t i) { return staged ? ev[i] : keys[start + i]; };
+    uint32_t cnt = 0;
+    for (uint32_t i = 0; i < E; ++i) cnt += (uint32_t)(key_at(i) >> sh) == u;
+    if (cnt) {
+      const uint32_t ul = u & p.tmask, tb = u & ~p.tmask;  // node within its trial, trial base
+      const uint64_t smask = (1ull << p.B) - 1, lmask = (2ull << p.B) - 1;
+      uint32_t* row = ids + (size_t)u * p.stride;
+      uint32_t d = deg[u];
+      uint64_t plow = 0;   // the last replayed event: (low key, position)
+      uint32_t ppos = 0;
+      for (uint32_t k = 0; k < cnt; ++k) {
+        // the next event of u: the least (low key, position) after the last one
+        uint64_t blow = ~0ull;
+        uint32_t bpos = ~0u;
+        for (uint32_t i = 0; i < E; ++i) {
+          const uint64_t key = key_at(i);
+          if ((uint32_t)(key >> sh) != u) continue;
+          const uint64_t lo = key & lmask;
+          const bool after = k == 0 || lo > plow || (lo == plow && i > ppos);
+          if (after && (lo < blow || (lo == blow && i < bpos))) { blow = lo; bpos = i; }
+        }
+        plow = blow;
+        ppos = bpos;
+        const uint64_t i = start + bpos;
+        const uint32_t src = (uint32_t)((blow >> 1) & smask);
+        uint64_t emitted = kEmpty;
+        if (k >= (1u << 26)) { err |= 2; out[i] = kEmpty; continue; }
+        if ((blow & 1) == 0) {                                  // makeUpCh (:66-75)
+          ++mk;
+          if (d < p.fanin) {
+            row[d++] = src;
+          } else {
+            const uint32_t pos = uniform(ov_draw(p, K_VICTIM, u, t, k), d);
+            const uint32_t victim = row[pos];
+            emitted = ev_key(victim, u, 1u, p.B);               // Breakup (:73)
+            row[pos] = src;
+          }
+        } else {                                                // breakUpCh (:76-94)
+          ++bk;
+          uint32_t idx = 0;
+          while (idx < d && row[idx] != src) ++idx;
+          if (idx < d) {
+            if (d > p.fanout) {                                 // removeFriend (:83)
+              for (uint32_t q = idx; q + 1 < d; ++q) row[q] = row[q + 1];
+              --d;
+            } else {                                            // replace (:86-91)
+              uint32_t nf = 0, a = 0, kn, c3;
+              node_key(p.tlog, p.tmask, p.key, u, K_REPLACE, kn, c3);
+              for (; a < 256; ++a) {
+                const u32x4 r = philox(kn, t, (k << 6) | (a >> 2), c3, p.key.k0, p.key.k1);
+                nf = uniform(lane_of(r, a & 3), (uint32_t)p.n);
+                if (nf != (src & p.tmask) && nf != ul) break;
+              }
+              nf |= tb;
+              if (a == 256) {
+                err |= 1;
+              } else {
+                row[idx] = nf;
+                emitted = ev_key(nf, u, 0u, p.B);               // Makeup (:91)
+              }
+            }
+          }
+        }
+        out[i] = emitted;
+        if (emitted != kEmpty)
+          oslot[i] = (uint16_t)((t + fire_offset(p.delay_low, p.delay_span,
+                                                 ov_draw(p, K_OVDELAY, u, t, k))) % p.R);
+      }
+      deg[u] = (uint8_t)d;
+    }
+  }
+  __shared__ uint32_t s_mk, s_bk, s_err;
+  if (threadIdx.x == 0) { s_mk = 0; s_bk = 0; s_err = 0; }
+  __syncthreads();
+  if (mk) atomicAdd(&s_mk, mk);
+  if (bk) atomicAdd(&s_bk, bk);
+  if (err) atomicOr(&s_err, err);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (s_mk) atomicAdd(&tc->makeups, (unsigned long long)s_mk);
+    if (s_bk) atomicAdd(&tc->breakups, (unsigned long long)s_bk);
+    if (s_err) atomicOr(&tc->err, (unsigned long long)s_err);
+  }
+}
+
 #define OVCHK(expr)                                                              \
   do {                                                                           \
     hipError_t e_ = (expr);                                                      \
@@ -302,6 +424,9 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
     return res->rc;
   }
   const uint32_t R = p.R;
+  // GS_OV_GROUP=1: k_process_g (A/B); default one lane per destination (k_process)
+  static const bool group_env = [] { const char* e = getenv("GS_OV_GROUP"); return e && atoi(e) == 1; }();
+  const bool grouped = group_env && p.B >= kOvGroupLog;
   // buffers live in the caller's workspace across builds (batched C3 builds
   // one overlay per batch; reallocating tens of GB per tick was the cost)
   if (ws->bucket.size() < R) ws->bucket.resize(R);
@@ -378,12 +503,14 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
       OVCHK(grow(oslotb, m * 2));
       OVCHK(grow(heads, m * 8));
       hipcub::DoubleBuffer<uint64_t> db((uint64_t*)bucket[s].p, (uint64_t*)scratch.p);
-      // by destination only (bits B+1 .. 2B): k_process orders each
-      // destination's short run by (src, kind) itself
-      const int begin_bit = (int)(p.B + 1), end_bit = (int)(2 * p.B + 1);
+      // by destination group (grouped) or destination only (bits B+1 .. 2B):
+      // the process kernel orders each destination's events by (src, kind)
+      // itself
+      const uint32_t glog = grouped ? kOvGroupLog : 0u;
+      const int begin_bit = (int)(p.B + 1 + glog), end_bit = (int)(2 * p.B + 1);
       size_t sort_bytes = 0, sel_bytes = 0;
       OVCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, db, (int)m, begin_bit, end_bit, stream));
-      IsHead pred{nullptr, p.B + 1};
+      IsHead pred{nullptr, p.B + 1 + glog};
       hipcub::CountingInputIterator<int64_t> it(0);
       OVCHK(hipcub::DeviceSelect::If(nullptr, sel_bytes, it, (int64_t*)heads.p, d_nheads, (int)m,
                                      pred, stream));
@@ -396,9 +523,16 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
       sel_bytes = cub_tmp.bytes;
       OVCHK(hipcub::DeviceSelect::If(cub_tmp.p, sel_bytes, it, (int64_t*)heads.p, d_nheads, (int)m,
                                      pred, stream));
-      hipLaunchKernelGGL(k_process, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, stream, p,
-                         (uint32_t)t, keys, m, (const int64_t*)heads.p, d_nheads, d_deg, d_ids,
-                         (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_tc);
+      if (grouped) {
+        const uint64_t ng = std::min<uint64_t>(m, (ntot >> kOvGroupLog) + 1);  // heads <= groups
+        hipLaunchKernelGGL(k_process_g, dim3((uint32_t)((ng + kOvWaves - 1) / kOvWaves)), dim3(kOvWaves * 64), 0,
+                           stream, p, (uint32_t)t, (const uint64_t*)keys, m, (const int64_t*)heads.p, d_nheads,
+                           d_deg, d_ids, (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_tc);
+      } else {
+        hipLaunchKernelGGL(k_process, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, stream, p,
+                           (uint32_t)t, keys, m, (const int64_t*)heads.p, d_nheads, d_deg, d_ids,
+                           (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_tc);
+      }
       OVCHK(hipGetLastError());
       OutSource osrc{(const uint64_t*)outb.p, (const uint16_t*)oslotb.p};
       const uint64_t per = (uint64_t)kScatterBlock * kScatterIPT;

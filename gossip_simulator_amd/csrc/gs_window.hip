@@ -1114,16 +1114,12 @@ constexpr uint32_t kRolledBlock = GS_ROLLED_BLOCK;  // the rolled replay: 4 wave
 // per-tick large path (resolve_tick), which reuses the same LDS for per-node
 // counters.
 constexpr uint32_t kBitWords = kFineNodes / 32;
-// The staged receipts (k_resolve<true>) take the rest of the union: 48 KB,
-// 12288 receipts per LDS-DMA round trip.
-constexpr uint32_t kResolveStage = (kFineNodes * 4 + 4 * kBitWords * 4 - kBitTicks * kBitWords * 4 - kBitWords * 8) / 4;
 struct ResolveLds {
   union {
     struct {                            // b1 .. dlist, then the infection list
       uint32_t b1[kBitTicks][kBitWords];
       uint2 cr0[kBitWords];             // per word: crashed before the window, a crash-roll
                                         // receipt in the window (from w.rollw)
-      alignas(16) uint32_t stage[kResolveStage];  // STAGE: the bucket's receipts, by LDS-DMA
     };
     struct {                            // large path
       uint32_t cnt[kFineNodes];         // per node at the current tick: arrivals | crash rolls << 16
@@ -1148,7 +1144,6 @@ struct ResolveLds {
   unsigned long long tlast;
 };  // ~72 KB: two workgroups per CU
 static_assert(kBitTicks <= kMaxWindow, "window ticks fit the message format");
-static_assert(kResolveStage % 2048 == 0, "whole batches of 8 receipts per thread");
 static_assert(sizeof(uint32_t) * kFineNodes <= sizeof(((ResolveLds*)0)->cnt), "the infection list fits");
 
 // GS_STAMPS diagnostics: thread 0 adds the cycles since the last stamp to phase i.
@@ -1298,11 +1293,6 @@ __device__ __forceinline__ void flush_counts(const WinState& w, ResolveLds& sm, 
 //            (node, tick) groups in order (rule A6, first_crash); the
 //            infections are Broadcast() (:122, :141)
 // A bucket with more rolled receipts than kRolledCap takes the per-tick large path.
-// STAGE (LDS-DMA staging of the receipts): the bucket's receipts arrive in
-// LDS 12288 at a time -- every wave issues global_load_lds_dwordx4 for its
-// 1-KB chunks, one round trip per stage instead of one per batch of 8
-// receipts per lane -- and are read back 4 per lane with 16-byte LDS reads.
-template <bool STAGE>
 __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
   __shared__ ResolveLds sm;
   const uint32_t tid = threadIdx.x, G = gridDim.x;
@@ -1332,7 +1322,8 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
   stamp(w, sm, 0);
   uint32_t fB = 0, MB = 0;
   unsigned long long mbB = 0;
-  if (nb > 0) { fB = sm.blist[0]; mbB = sm.bstart[0]; MB = sm.bcnt[0]; }
+  auto next_bucket = [&](uint32_t j) { fB = sm.blist[j]; mbB = sm.bstart[j]; MB = sm.bcnt[j]; };
+  if (nb > 0) next_bucket(0);
   uint32_t* rwg = (uint32_t*)w.recv;
   uint32_t* cwg = (uint32_t*)w.crash;
   // this lane's infections per tick over all its buckets
@@ -1368,7 +1359,7 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
     p_crash0 = cwg[wc];
     p_roll0 = w.rollw[wc];
     p_fcv = w.fcount[(size_t)(tid < w.R ? tid : 0u) * w.nfine + f];
-    if (!STAGE) ld(w.fmsg + mb, M, 0, pm);
+    ld(w.fmsg + mb, M, 0, pm);
   };
   if (nb > 0) prefetch(fB, MB, mbB);
   for (uint32_t i = 0; i < nb; ++i) {
@@ -1384,7 +1375,7 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
     const bool in = wi < w.W * 2;
     const uint32_t recv0 = p_in ? p_recv0 : 0u, crash0 = p_in ? p_crash0 : 0u, roll0 = p_in ? p_roll0 : 0u;
     const uint32_t fcv = tid < w.R ? p_fcv : 0u;
-    if (i + 1 < nb) { fB = sm.blist[i + 1]; mbB = sm.bstart[i + 1]; MB = sm.bcnt[i + 1]; }
+    if (i + 1 < nb) next_bucket(i + 1);
     if (roll0) w.rollw[wi] = 0u;  // consumed: the next window starts clear
     const uint32_t rollw = roll0 & ~crash0;
 #pragma unroll
@@ -1414,9 +1405,8 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
         dhi &= ~(255ull << (8 * b));
       }
     };
-    // one batch: receipts m[u] where valid(u) (a macro body: the host-driven
-    // loop below must compile exactly as it did before the staged variant)
-#define GS_RESOLVE_BATCH(VALID)                                                                   \
+    // one batch: receipts m[u] where VALID (a macro body: a lambda spills)
+#define GS_RESOLVE_BATCH(m, VALID)                                                                \
     {                                                                                             \
       uint2 sp[kU];                                                                               \
       _Pragma("unroll") for (uint32_t u = 0; u < kU; ++u) {                                       \
@@ -1455,48 +1445,16 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
         }                                                                                         \
       }                                                                                           \
     }
-    if (!STAGE) {
+    {
       uint32_t m[kU];
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) m[u] = pm[u];
       for (uint32_t p0 = 0, nbat = 0; p0 < (sm.err == 3 ? 0u : M); p0 += kBatch, ++nbat) {
         uint32_t mn[kU];
         if (p0 + kBatch < M) ld(gm, M, p0 + kBatch, mn);
-        GS_RESOLVE_BATCH(p0 + u * kResolveBlock + tid < M)
+        GS_RESOLVE_BATCH(m, p0 + u * kResolveBlock + tid < M)
 #pragma unroll
         for (uint32_t u = 0; u < kU; ++u) m[u] = mn[u];
-      }
-    } else {
-      // stages of up to kResolveStage - 4 receipts: the DMA starts at the
-      // 16-B aligned element below the first one (head = 0..3 leading
-      // elements are not the bucket's)
-      const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-      constexpr uint32_t kStep = kResolveStage - 4;
-      uint32_t nbat = 0;
-      for (uint32_t p0 = 0; p0 < M; p0 += kStep) {
-        __syncthreads();  // the previous stage has been read
-        // block-uniform exit: sm.err is read after the barrier, before any
-        // thread of this stage can set it (the barriers below must be met by all)
-        if (sm.err == 3) break;
-        const uint32_t cnt = min(kStep, M - p0);
-        const unsigned long long g0 = mb + p0;
-        const uint32_t head = (uint32_t)(g0 & 3), tot = head + cnt;
-        const uint32_t* src = w.fmsg + (g0 - head);
-        const uint32_t nch = (tot + 255) / 256;
-        for (uint32_t c = wv; c < nch; c += kResolveBlock / 64) {
-          const uint32_t q = c * 256 + lane * 4;
-          if (q < tot)  // (reads at most 3 elements past the bucket: inside the buffer's slack)
-            __builtin_amdgcn_global_load_lds(src + q,
-                                             (__attribute__((address_space(3))) void*)&sm.stage[c * 256], 16, 0, 0);
-        }
-        __syncthreads();  // every wave's chunks landed (the barrier's fence waits for the DMA)
-        for (uint32_t b0 = 0; b0 < tot; b0 += 8 * kResolveBlock, ++nbat) {
-          const uint32_t q0 = b0 + tid * 4, q1 = q0 + 4 * kResolveBlock;
-          const uint4 a = q0 < tot ? *reinterpret_cast<const uint4*>(&sm.stage[q0]) : make_uint4(0, 0, 0, 0);
-          const uint4 b = q1 < tot ? *reinterpret_cast<const uint4*>(&sm.stage[q1]) : make_uint4(0, 0, 0, 0);
-          const uint32_t m[kU] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-          GS_RESOLVE_BATCH(((u < 4 ? q0 : q1) + (u & 3)) >= head && ((u < 4 ? q0 : q1) + (u & 3)) < tot)
-        }
       }
     }
 #undef GS_RESOLVE_BATCH
@@ -1531,6 +1489,16 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
       stamp(w, sm, 5);
       __syncthreads();
       stamp(w, sm, 6);
+      // Broadcast() of an infected node x = loc | tick << 14 (:122, :141-142):
+      // fire at t + off
+      auto bcast = [&](uint32_t x) {
+        const uint32_t loc = msg_loc(x), t = t0 + msg_tick(x);
+        const uint32_t off = fire_offset(w.delay_low, w.delay_span,
+                                         philox(knode0 + loc, t, 0, c3delay, w.key.k0, w.key.k1).x);
+        const uint32_t slot = (t + off) % w.R;
+        const uint32_t pos = atomicAdd(&sm.fc[slot], 1u);
+        w.flist[((size_t)slot * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
+      };
       // infection list (loc | tick << 14) over the bitmaps, dead from here on
       uint32_t* inf = &sm.cnt[0];
       {
@@ -1551,16 +1519,9 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
       }
       __syncthreads();
       stamp(w, sm, 7);
-      // Broadcast() of each infected node (:122, :141-142): fire at t + off
+      // the listed infections, spread over the block
       const uint32_t ni_all = sm.ninf;
-      for (uint32_t q = tid; q < ni_all; q += kResolveBlock) {
-        const uint32_t x = inf[q], loc = msg_loc(x), t = t0 + msg_tick(x);
-        const uint32_t off = fire_offset(w.delay_low, w.delay_span,
-                                         philox(knode0 + loc, t, 0, c3delay, w.key.k0, w.key.k1).x);
-        const uint32_t slot = (t + off) % w.R;
-        const uint32_t pos = atomicAdd(&sm.fc[slot], 1u);
-        w.flist[((size_t)slot * w.nfine + f) * kFineNodes + pos] = (uint16_t)loc;
-      }
+      for (uint32_t q = tid; q < ni_all; q += kResolveBlock) bcast(inf[q]);
     } else {
       // large path: per-node counters, the messages streamed once per tick
       __syncthreads();
@@ -2315,9 +2276,7 @@ hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s
   const uint32_t gs = (w.nfine + kSmallBlock / 64 - 1) / (kSmallBlock / 64);
   hipLaunchKernelGGL(k_resolve_small<false>, dim3(gs), dim3(kSmallBlock), 0, s, w, t0, L);
   static_assert(kSmallMax == 64 * 4, "the two bodies cover 1..kSmallMax");
-  static const bool stage = [] { const char* e = getenv("GS_RESOLVE_STAGE"); return e && atoi(e) == 1; }();  // A/B knob
-  if (stage) hipLaunchKernelGGL(k_resolve<true>, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
-  else hipLaunchKernelGGL(k_resolve<false>, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
+  hipLaunchKernelGGL(k_resolve, dim3(G), dim3(kResolveBlock), 0, s, w, t0, L);
   // k_resolve_rolled: small blocks (the E = 16 key arrays take 4 KB per wave; blocks finish independently)
   hipLaunchKernelGGL(k_resolve_small<true>, dim3((w.nfine + kRolledBlock / 64 - 1) / (kRolledBlock / 64)),
                      dim3(kRolledBlock), 0, s, w, t0, L);
