@@ -2999,6 +2999,10 @@ int dd_run(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t tend, uint32_t 
   gs_ctx* m0 = ms[0];
   const uint32_t G = m0->G, M = (uint32_t)ms.size();
   const bool rank = is_rank(m0), travel = rank && G > 1;
+  // one in-process shard: its send layout is its receive layout, so the
+  // window runs as the unsharded engine's does (no k_rtab, overflows stop the
+  // window) -- the G = 1 case of bench.py's sharded flood
+  const bool solo = !rank && G == 1 && M == 1;
   const size_t K1 = kRegions + 1;
   hipStream_t st = m0->stream;
   CK(acc, hipSetDevice(m0->dev));
@@ -3079,10 +3083,16 @@ int dd_run(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t tend, uint32_t 
     w.cfill = acc->dd_glay + (size_t)m->rank * kDDRow;
     w.wstat = acc->dd_wstat + (size_t)i * kDDWStat;
     w.nglob = N;
+    w.solo = solo ? 1u : 0u;
     w.gmap = (uint32_t*)m->gmap.p;
     w.cmsg = (uint32_t*)m->cmsg.p;
     w.fmsg = (uint32_t*)m->fmsg.p;
     ws[i] = w;
+    if (solo) {
+      wr[i] = w;
+      tn_bound[i] = std::min<uint64_t>(m->ntot + 1, 4096ull * 1024);
+      continue;
+    }
     WinState r = w;
     r.cmsg = nullptr;
     r.csrc = (const uint32_t* const*)(m->d_rtab + 4 * K1);
@@ -3110,7 +3120,7 @@ int dd_run(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t tend, uint32_t 
     for (uint32_t i = 0; i < M; ++i) CK(acc, win_unitscan(ws[i], st));
     for (uint32_t i = 0; i < M; ++i) CK(acc, win_expand(ws[i], 0, Lmax, tn_bound[i], 1, st));
     if (rank) RC(x_all_gather(m0, acc->dd_glay, kDDRow * 8));
-    for (uint32_t i = 0; i < M; ++i)
+    for (uint32_t i = 0; i < M && !solo; ++i)
       CK(acc, win_rtab(ws[i], ms[i]->d_rtab, (const unsigned long long* const*)d_ccaps, (const uint32_t* const*)d_src,
                        nsrc, rank ? 1u : 0u, st));
     if (travel) {
@@ -3203,12 +3213,13 @@ int dd_run(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t tend, uint32_t 
     for (uint32_t i = 0; i < M; ++i) {
       CK(acc, win_plan(wr[i], false, st));
       CK(acc, win_part2(wr[i], T_bound, true, st));
-      CK(acc, win_fine_redo(wr[i], T_bound, st));
+      if (!solo) CK(acc, win_fine_redo(wr[i], T_bound, st));
       CK(acc, win_resolve(wr[i], 0, Lmax, st));
-      CK(acc, win_stats_dd(ws[i], st));
+      CK(acc, win_stats_dd(ws[i], slot, st));
     }
     if (rank) RC(x_all_reduce(m0, acc->dd_wstat, kDDWStat));
-    CK(acc, win_close_dd(ws[0], (const unsigned long long* const*)d_wst, (WinCtl* const*)d_ctls, M, slot, st));
+    if (!solo)  // (one in-process shard: k_stats_dd closed the window)
+      CK(acc, win_close_dd(ws[0], (const unsigned long long* const*)d_wst, (WinCtl* const*)d_ctls, M, slot, st));
     CK(acc, hipEventRecord(acc->wev[slot], st));
     return 0;
   };

@@ -190,6 +190,9 @@ struct WinState {
   // (the guard kernels run only then).
   uint32_t dd;
   uint32_t guard;                // 1: this launch runs only if the shard's kErrFine is set
+  uint32_t solo;                 // device-driven single in-process shard: its send layout is its
+                                 // receive layout (no k_rtab, no in-window fine redo); any
+                                 // overflow stops the window and the host redoes it
   unsigned long long* gcnt;
   unsigned long long* glay;
   unsigned long long* wstat;     // [kMaxWindow][kStatFields] the window's counters (this shard's, then global)
@@ -267,7 +270,7 @@ hipError_t win_consume_sh(const WinState& w, uint32_t t0, uint32_t L, hipStream_
 hipError_t win_rtab(const WinState& w, unsigned long long* rtab, const unsigned long long* const* ccaps,
                     const uint32_t* const* src, uint32_t nsrc, uint32_t travels, hipStream_t s);
 hipError_t win_fine_redo(const WinState& w, uint64_t T, hipStream_t s);
-hipError_t win_stats_dd(const WinState& w, hipStream_t s);
+hipError_t win_stats_dd(const WinState& w, uint32_t slot, hipStream_t s);  // w.solo: also closes
 hipError_t win_close_dd(const WinState& w, const unsigned long long* const* wstats, WinCtl* const* ctls,
                         uint32_t n, uint32_t slot, hipStream_t s);
 // Copies the first min(cfill[r], room) messages of every region r < nreg from

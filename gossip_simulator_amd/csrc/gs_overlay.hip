@@ -1,21 +1,36 @@
 // gs_overlay.hip -- overlay construction (simulator.go:62-106,127-164,214-235)
-// as a tick-synchronous, sort-bucketed GPU protocol.
+// as a tick-synchronous, sort-bucketed GPU protocol, processed in BLOCKS of
+// ticks.
 //
-// Events are u64 keys  dst << (B+1) | src << 1 | kind  (kind 0 = makeup,
-// 1 = breakup, B = bits of n-1), kept in one bucket per ring slot (arrival tick
-// mod R).  A tick:
-//   1. radix-sort the slot's keys (hipcub) -> each node's events contiguous,
-//      ordered by (src, kind);
-//   2. select segment heads (first event of each dst);
-//   3. one lane per dst replays its events in order -- the makeup / breakup
-//      handler bodies -- with every draw keyed by (dst, tick, ordinal k), so
-//      identical keys (identical messages) commute;
-//   4. each processed event emits at most one event (a breakup on eviction,
-//      a makeup on replacement) into out[i]; a count pass sizes the buckets and
-//      a scatter pass appends them with one global atomic per (block, slot).
+// An event sent at tick t arrives at t + off with off >= delay_low
+// (simulator.go:172-176), so the events of the ticks [t, t + delay_low) are
+// all known before any of them is processed, and a node's events of several
+// such ticks can be replayed in one pass, tick by tick: its friends row is
+// read and written once per block instead of once per tick (the row traffic
+// -- every row of the table is touched in each tick of the burst -- is what
+// bounds the build).  A block holds L ticks, L | 10 (the 10-tick windows of
+// the stabilisation rule, simulator.go:222-234, end on block ends),
+// L <= delay_low, L <= 2^TB.
+//
+// Events are u64 keys  dst << (B+1+TB) | tag << (B+1) | src << 1 | kind
+// (kind 0 = makeup, 1 = breakup, B = bits of the id space, tag = the arrival
+// tick's place in its block, TB = tag bits: 2B + 1 + TB <= 64), kept in one
+// bucket per block of a ring of NB blocks.  A block:
+//   1. radix-sort its bucket by destination (rocprim Onesweep) -> each node's
+//      events contiguous;
+//   2. one lane per destination (the first event of its run) orders the run
+//      by (tag, src, kind) and replays it tick by tick -- the makeup /
+//      breakup handler bodies -- with every draw keyed by (dst, tick,
+//      ordinal k within the tick), so identical keys (identical messages)
+//      commute;
+//   3. each processed event emits at most one event (a breakup on eviction,
+//      a makeup on replacement); a workgroup's emitted events are appended to
+//      a compact list, and a count and a write scatter pass move them into
+//      their arrival blocks' buckets.
 // Tick 0 is the needNewFriendCh burst: every node picks `fanout` friends
 // (self -> id+1, simulator.go:97-101) and sends a makeup to each.
-#include <hipcub/hipcub.hpp>
+// GS_OV_BLOCK=1 forces one tick per block (round 3's per-tick protocol).
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -29,7 +44,6 @@
 namespace gs {
 namespace {
 
-constexpr uint64_t kEmpty = ~0ull;
 constexpr uint32_t kMaxRing = 1024;
 constexpr uint32_t kScatterBlock = 256;
 constexpr uint32_t kScatterIPT = 8;
@@ -42,6 +56,8 @@ struct OvParams {
   Key key;
   // batched trials: trial i's node v has id i << tlog | v (tlog = 32: one trial)
   uint32_t tlog, tmask;
+  // tick blocks: L ticks per block, TB tag bits, NB buckets in the ring
+  uint32_t L, TB, NB;
 };
 
 // Key node and counter word 3 of global id g (per-trial keys, gs_internal.h).
@@ -52,8 +68,14 @@ __device__ __forceinline__ uint32_t ov_draw(const OvParams& p, uint32_t kind, ui
   return philox(node, b, c, c3, p.key.k0, p.key.k1).x;
 }
 
-__device__ __forceinline__ uint64_t ev_key(uint32_t dst, uint32_t src, uint32_t kind, uint32_t B) {
-  return ((uint64_t)dst << (B + 1)) | ((uint64_t)src << 1) | kind;
+// An event arriving at tick a (>= 1): its key and its bucket.
+__device__ __forceinline__ uint64_t ev_key(const OvParams& p, uint32_t dst, uint64_t a, uint32_t src,
+                                           uint32_t kind) {
+  const uint64_t tag = (a - 1) % p.L;
+  return ((uint64_t)dst << (p.B + 1 + p.TB)) | (tag << (p.B + 1)) | ((uint64_t)src << 1) | kind;
+}
+__device__ __forceinline__ uint32_t ev_bucket(const OvParams& p, uint64_t a) {
+  return (uint32_t)(((a - 1) / p.L) % p.NB);
 }
 
 // Item sources for the bucket scatter -------------------------------------
@@ -74,21 +96,23 @@ struct PickSource {  // tick 0: item i = (trial i / (n*fanout), v, j = i % fanou
       ids[(size_t)gv * p.stride + j] = tb | f;                              // :101
       if (j == 0) deg[gv] = (uint8_t)p.fanout;
     }
-    key = ev_key(tb | f, gv, 0u, p.B);                                      // :102 Makeup
-    slot = fire_offset(p.delay_low, p.delay_span, ov_draw(p, K_OVDELAY, gv, 0, j)) % p.R;
+    // :102 Makeup, arriving at tick 0 + off
+    const uint64_t a = fire_offset(p.delay_low, p.delay_span, ov_draw(p, K_OVDELAY, gv, 0, j));
+    key = ev_key(p, tb | f, a, gv, 0u);
+    slot = ev_bucket(p, a);
   }
 };
 
-struct OutSource {  // events emitted by a processing tick
+struct OutSource {  // events emitted by a processing block (a compact list)
   const uint64_t* out;
   const uint16_t* oslot;
   __device__ __forceinline__ void get(uint64_t i, uint64_t& key, uint32_t& slot) const {
     key = out[i];
-    slot = key == kEmpty ? 0xFFFFu : oslot[i];
+    slot = oslot[i];
   }
 };
 
-// COUNT: counts[s] += items bound for s.  WRITE: append them to bucket s.
+// COUNT: counts[s] += items bound for bucket s.  WRITE: append them to bucket s.
 template <bool WRITE, class Src>
 __global__ __launch_bounds__(kScatterBlock) void k_scatter(Src src, uint64_t nitems, uint32_t R,
                                                            unsigned long long* counts,
@@ -122,38 +146,75 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(Src src, uint64_t nit
     if (slot[k] != 0xFFFFu) buckets[slot[k]][s_base[slot[k]] + rank[k]] = key[k];
 }
 
-struct IsHead {
-  const uint64_t* keys;
-  uint32_t shift;
-  __device__ __forceinline__ bool operator()(const int64_t i) const {
-    return i == 0 || (keys[i] >> shift) != (keys[i - 1] >> shift);
-  }
-};
-
 struct TickCounters {
   unsigned long long makeups, breakups, err;
 };
 
-// One lane per destination node: the makeup / breakup handlers in order.
-__global__ __launch_bounds__(256) void k_process(const OvParams p, uint32_t t, uint64_t* keys,
-                                                 uint64_t m, const int64_t* heads,
-                                                 const int64_t* nheads, uint8_t* deg, uint32_t* ids,
-                                                 uint64_t* out, uint16_t* oslot,
-                                                 TickCounters* tc) {
-  const int64_t H = *nheads;
-  const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// The block's sort: rocprim Onesweep, 8-bit digits (gfx950's default for
+// 8-byte keys; 10-bit digits, 3 passes over a 30-bit destination instead of 4,
+// measured no faster: profiles/r04j_overlay_ab.txt).
+using OvRadix = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<512, 12>, rocprim::kernel_config<512, 12>, 8,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+
+// Process a block: each thread takes kProcIPT event positions of the sorted
+// bucket, and the first event of each destination's run (its destination
+// differs from the previous key's) replays the run -- no head list.  The
+// events a workgroup emits are gathered in LDS and appended with one
+// reservation to the compact list (eout, eslot); a workgroup whose runs emit
+// more than kEmitCap appends the rest one by one.
+constexpr uint32_t kProcBlock = 256;
+constexpr uint32_t kProcIPT = 8;
+constexpr uint32_t kEmitCap = 4096;
+
+// Wave-aggregated append among the ACTIVE lanes (divergent call sites).
+__device__ __forceinline__ uint32_t active_append(uint32_t* n) {
+  const unsigned long long act = __ballot(1);
+  const uint32_t lane = threadIdx.x & 63, leader = (uint32_t)__ffsll((long long)act) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(n, (uint32_t)__popcll(act));
+  base = __shfl(base, (int)leader, 64);
+  return base + __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+}
+
+__global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64_t t0, uint64_t* keys, uint64_t m,
+                                                        uint8_t* deg, uint32_t* ids, uint64_t* eout,
+                                                        uint16_t* eslot, unsigned long long* ecount,
+                                                        TickCounters* tc) {
+  __shared__ uint64_t s_ev[kEmitCap];
+  __shared__ uint16_t s_sl[kEmitCap];
+  __shared__ uint32_t s_n, s_mk, s_bk, s_err;
+  __shared__ unsigned long long s_base;
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) { s_n = 0; s_mk = 0; s_bk = 0; s_err = 0; }
+  __syncthreads();
   uint32_t mk = 0, bk = 0, err = 0;
-  if (h < H) {
-    const uint64_t start = (uint64_t)heads[h];
-    const uint64_t end = (h + 1 < H) ? (uint64_t)heads[h + 1] : m;
-    const uint32_t u = (uint32_t)(keys[start] >> (p.B + 1));
+  auto emit = [&](uint64_t key, uint32_t slot) {
+    const uint32_t at = active_append(&s_n);
+    if (at < kEmitCap) {
+      s_ev[at] = key;
+      s_sl[at] = (uint16_t)slot;
+    } else {
+      const unsigned long long q = atomicAdd(ecount, 1ull);
+      eout[q] = key;
+      eslot[q] = (uint16_t)slot;
+    }
+  };
+  const uint32_t sh = p.B + 1 + p.TB;  // destination field
+  const uint64_t smask = (1ull << p.B) - 1, lmask = (1ull << sh) - 1;
+  const uint32_t tagmask = (1u << p.TB) - 1;
+  const uint64_t base = (uint64_t)blockIdx.x * kProcBlock * kProcIPT;
+  for (uint32_t r = 0; r < kProcIPT; ++r) {
+    const uint64_t start = base + (uint64_t)r * kProcBlock + tid;
+    if (start >= m) break;
+    const uint32_t u = (uint32_t)(keys[start] >> sh);
+    if (start > 0 && (uint32_t)(keys[start - 1] >> sh) == u) continue;  // not a run head
+    uint64_t end = start + 1;
+    while (end < m && (uint32_t)(keys[end] >> sh) == u) ++end;
     const uint32_t ul = u & p.tmask, tb = u & ~p.tmask;  // node within its trial, trial base
-    const uint64_t smask = (1ull << p.B) - 1;
-    // the radix sort ordered the tick's events by destination only (its
-    // passes over the B + 1 low bits are saved); this lane puts its
-    // destination's run in (src, kind) order -- the order the handlers replay
-    // -- by insertion (runs are a few events long in a random overlay)
-    const uint64_t lmask = (2ull << p.B) - 1;
+    // the run in (tag, src, kind) order: tick by tick, each tick's events in
+    // the order the handlers replay them (runs are short: insertion)
     for (uint64_t i = start + 1; i < end; ++i) {
       const uint64_t key = keys[i];
       uint64_t j = i;
@@ -166,20 +227,24 @@ __global__ __launch_bounds__(256) void k_process(const OvParams p, uint32_t t, u
     }
     uint32_t* row = ids + (size_t)u * p.stride;
     uint32_t d = deg[u];
+    uint32_t ptag = ~0u, k = 0;
     for (uint64_t i = start; i < end; ++i) {
       const uint64_t key = keys[i];
       const uint32_t src = (uint32_t)((key >> 1) & smask);
-      const uint32_t k = (uint32_t)(i - start);
-      uint64_t emitted = kEmpty;
-      if (k >= (1u << 26)) { err |= 2; out[i] = kEmpty; continue; }
+      const uint32_t tag = (uint32_t)(key >> (p.B + 1)) & tagmask;
+      k = tag == ptag ? k + 1 : 0u;  // the ordinal restarts with each tick
+      ptag = tag;
+      const uint32_t t = (uint32_t)(t0 + tag);
+      uint32_t emitted_dst = ~0u, emitted_kind = 0;
+      if (k >= (1u << 26)) { err |= 2; continue; }
       if ((key & 1) == 0) {                                   // makeUpCh (:66-75)
         ++mk;
         if (d < p.fanin) {
           row[d++] = src;
         } else {
           const uint32_t pos = uniform(ov_draw(p, K_VICTIM, u, t, k), d);
-          const uint32_t victim = row[pos];
-          emitted = ev_key(victim, u, 1u, p.B);               // Breakup (:73)
+          emitted_dst = row[pos];                             // Breakup (:73)
+          emitted_kind = 1;
           row[pos] = src;
         }
       } else {                                                // breakUpCh (:76-94)
@@ -194,8 +259,8 @@ __global__ __launch_bounds__(256) void k_process(const OvParams p, uint32_t t, u
             uint32_t nf = 0, a = 0, kn, c3;
             node_key(p.tlog, p.tmask, p.key, u, K_REPLACE, kn, c3);
             for (; a < 256; ++a) {
-              const u32x4 r = philox(kn, t, (k << 6) | (a >> 2), c3, p.key.k0, p.key.k1);
-              nf = uniform(lane_of(r, a & 3), (uint32_t)p.n);
+              const u32x4 rr = philox(kn, t, (k << 6) | (a >> 2), c3, p.key.k0, p.key.k1);
+              nf = uniform(lane_of(rr, a & 3), (uint32_t)p.n);
               if (nf != (src & p.tmask) && nf != ul) break;
             }
             nf |= tb;
@@ -203,151 +268,34 @@ __global__ __launch_bounds__(256) void k_process(const OvParams p, uint32_t t, u
               err |= 1;
             } else {
               row[idx] = nf;
-              emitted = ev_key(nf, u, 0u, p.B);               // Makeup (:91)
+              emitted_dst = nf;                               // Makeup (:91)
+              emitted_kind = 0;
             }
           }
         }
       }
-      out[i] = emitted;
-      if (emitted != kEmpty)
-        oslot[i] = (uint16_t)((t + fire_offset(p.delay_low, p.delay_span,
-                                               ov_draw(p, K_OVDELAY, u, t, k))) % p.R);
+      if (emitted_dst != ~0u) {
+        const uint64_t a = (uint64_t)t + fire_offset(p.delay_low, p.delay_span, ov_draw(p, K_OVDELAY, u, t, k));
+        emit(ev_key(p, emitted_dst, a, u, emitted_kind), ev_bucket(p, a));
+      }
     }
     deg[u] = (uint8_t)d;
   }
-  // block reduction of the window counters
-  __shared__ uint32_t s_mk, s_bk, s_err;
-  if (threadIdx.x == 0) { s_mk = 0; s_bk = 0; s_err = 0; }
-  __syncthreads();
   if (mk) atomicAdd(&s_mk, mk);
   if (bk) atomicAdd(&s_bk, bk);
   if (err) atomicOr(&s_err, err);
   __syncthreads();
-  if (threadIdx.x == 0) {
+  const uint32_t n = min(s_n, kEmitCap);
+  if (tid == 0) {
+    if (n) s_base = atomicAdd(ecount, (unsigned long long)n);
     if (s_mk) atomicAdd(&tc->makeups, (unsigned long long)s_mk);
     if (s_bk) atomicAdd(&tc->breakups, (unsigned long long)s_bk);
     if (s_err) atomicOr(&tc->err, (unsigned long long)s_err);
   }
-}
-
-// Grouped variant (GS_OV_GROUP=1): the tick's events sorted by destination GROUP
-// only (64 consecutive ids: 6 radix bits fewer), one wave per group, a lane per
-// destination.  The group's events are staged in LDS (up to kOvStage; a larger
-// group reads them from global memory), and each lane replays its own events
-// in (src, kind, position) order by repeated minimum search over the group --
-// the order k_process's insertion sort gives, identical keys in position
-// order (they are identical messages, so the order among them is immaterial
-// beyond the ordinal k).  The 64 lanes' rows are consecutive: the row reads
-// and writes of a wave are coalesced instead of one line per destination.
-constexpr uint32_t kOvGroupLog = 6;
-constexpr uint32_t kOvWaves = 4;
-constexpr uint32_t kOvStage = 1024;
-
-__global__ __launch_bounds__(kOvWaves * 64) void k_process_g(const OvParams p, uint32_t t, const uint64_t* keys,
-                                                             uint64_t m, const int64_t* heads,
-                                                             const int64_t* nheads, uint8_t* deg, uint32_t* ids,
-                                                             uint64_t* out, uint16_t* oslot, TickCounters* tc) {
-  __shared__ uint64_t s_ev[kOvWaves][kOvStage];
-  const int64_t H = *nheads;
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t h = (int64_t)blockIdx.x * kOvWaves + wv;  // wave-uniform
-  uint32_t mk = 0, bk = 0, err = 0;
-  if (h < H) {
-    const uint64_t start = (uint64_t)heads[h];
-    const uint64_t end = (h + 1 < H) ? (uint64_t)heads[h + 1] : m;
-    const uint32_t E = (uint32_t)(end - start);  // m < 2^31
-    const uint32_t sh = p.B + 1;
-    const uint32_t u = (uint32_t)(keys[start] >> (sh + kOvGroupLog)) << kOvGroupLog | lane;  // this lane's destination
-    const bool staged = E <= kOvStage;
-    uint64_t* ev = s_ev[wv];
-    if (staged) {
-      for (uint32_t i = lane; i < E; i += 64) ev[i] = keys[start + i];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    auto key_at = [&](uint32_t i) { return staged ? ev[i] : keys[start + i]; };
-    uint32_t cnt = 0;
-    for (uint32_t i = 0; i < E; ++i) cnt += (uint32_t)(key_at(i) >> sh) == u;
-    if (cnt) {
-      const uint32_t ul = u & p.tmask, tb = u & ~p.tmask;  // node within its trial, trial base
-      const uint64_t smask = (1ull << p.B) - 1, lmask = (2ull << p.B) - 1;
-      uint32_t* row = ids + (size_t)u * p.stride;
-      uint32_t d = deg[u];
-      uint64_t plow = 0;   // the last replayed event: (low key, position)
-      uint32_t ppos = 0;
-      for (uint32_t k = 0; k < cnt; ++k) {
-        // the next event of u: the least (low key, position) after the last one
-        uint64_t blow = ~0ull;
-        uint32_t bpos = ~0u;
-        for (uint32_t i = 0; i < E; ++i) {
-          const uint64_t key = key_at(i);
-          if ((uint32_t)(key >> sh) != u) continue;
-          const uint64_t lo = key & lmask;
-          const bool after = k == 0 || lo > plow || (lo == plow && i > ppos);
-          if (after && (lo < blow || (lo == blow && i < bpos))) { blow = lo; bpos = i; }
-        }
-        plow = blow;
-        ppos = bpos;
-        const uint64_t i = start + bpos;
-        const uint32_t src = (uint32_t)((blow >> 1) & smask);
-        uint64_t emitted = kEmpty;
-        if (k >= (1u << 26)) { err |= 2; out[i] = kEmpty; continue; }
-        if ((blow & 1) == 0) {                                  // makeUpCh (:66-75)
-          ++mk;
-          if (d < p.fanin) {
-            row[d++] = src;
-          } else {
-            const uint32_t pos = uniform(ov_draw(p, K_VICTIM, u, t, k), d);
-            const uint32_t victim = row[pos];
-            emitted = ev_key(victim, u, 1u, p.B);               // Breakup (:73)
-            row[pos] = src;
-          }
-        } else {                                                // breakUpCh (:76-94)
-          ++bk;
-          uint32_t idx = 0;
-          while (idx < d && row[idx] != src) ++idx;
-          if (idx < d) {
-            if (d > p.fanout) {                                 // removeFriend (:83)
-              for (uint32_t q = idx; q + 1 < d; ++q) row[q] = row[q + 1];
-              --d;
-            } else {                                            // replace (:86-91)
-              uint32_t nf = 0, a = 0, kn, c3;
-              node_key(p.tlog, p.tmask, p.key, u, K_REPLACE, kn, c3);
-              for (; a < 256; ++a) {
-                const u32x4 r = philox(kn, t, (k << 6) | (a >> 2), c3, p.key.k0, p.key.k1);
-                nf = uniform(lane_of(r, a & 3), (uint32_t)p.n);
-                if (nf != (src & p.tmask) && nf != ul) break;
-              }
-              nf |= tb;
-              if (a == 256) {
-                err |= 1;
-              } else {
-                row[idx] = nf;
-                emitted = ev_key(nf, u, 0u, p.B);               // Makeup (:91)
-              }
-            }
-          }
-        }
-        out[i] = emitted;
-        if (emitted != kEmpty)
-          oslot[i] = (uint16_t)((t + fire_offset(p.delay_low, p.delay_span,
-                                                 ov_draw(p, K_OVDELAY, u, t, k))) % p.R);
-      }
-      deg[u] = (uint8_t)d;
-    }
-  }
-  __shared__ uint32_t s_mk, s_bk, s_err;
-  if (threadIdx.x == 0) { s_mk = 0; s_bk = 0; s_err = 0; }
   __syncthreads();
-  if (mk) atomicAdd(&s_mk, mk);
-  if (bk) atomicAdd(&s_bk, bk);
-  if (err) atomicOr(&s_err, err);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (s_mk) atomicAdd(&tc->makeups, (unsigned long long)s_mk);
-    if (s_bk) atomicAdd(&tc->breakups, (unsigned long long)s_bk);
-    if (s_err) atomicOr(&tc->err, (unsigned long long)s_err);
+  for (uint32_t j = tid; j < n; j += kProcBlock) {
+    eout[s_base + j] = s_ev[j];
+    eslot[s_base + j] = s_sl[j];
   }
 }
 
@@ -423,34 +371,45 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
              delay_high, kMaxRing);
     return res->rc;
   }
-  const uint32_t R = p.R;
-  // GS_OV_GROUP=1: k_process_g (A/B); default one lane per destination (k_process)
-  static const bool group_env = [] { const char* e = getenv("GS_OV_GROUP"); return e && atoi(e) == 1; }();
-  const bool grouped = group_env && p.B >= kOvGroupLog;
+  {
+    // tick blocks: L | 10, L <= delay_low, L <= 2^TB with 2B + 1 + TB <= 64
+    const char* be = getenv("GS_OV_BLOCK");  // (read per build: tests switch it)
+    const uint32_t lmax = be ? (uint32_t)atoi(be) : 10u;
+    const uint32_t tbmax = std::min<uint32_t>(4u, 63u - 2 * p.B);
+    p.L = 1;
+    for (uint32_t L : {10u, 5u, 2u}) {
+      if (L <= lmax && (int32_t)L <= delay_low && L <= (1u << tbmax)) { p.L = L; break; }
+    }
+    p.TB = 0;
+    while ((1u << p.TB) < p.L) ++p.TB;
+    // the ring: an event arrives at most delay_high - 1 ticks after it is sent
+    p.NB = (p.R + p.L - 1) / p.L + 2;
+  }
+  const uint32_t NB = p.NB;
   // buffers live in the caller's workspace across builds (batched C3 builds
-  // one overlay per batch; reallocating tens of GB per tick was the cost)
-  if (ws->bucket.size() < R) ws->bucket.resize(R);
+  // one overlay per batch; reallocating tens of GB per block was the cost)
+  if (ws->bucket.size() < NB) ws->bucket.resize(NB);
   std::vector<DevBuf>& bucket = ws->bucket;
-  std::vector<uint64_t> fill(R, 0);
-  DevBuf &scratch = ws->scratch, &outb = ws->outb, &oslotb = ws->oslotb, &heads = ws->heads,
-         &cub_tmp = ws->cub_tmp, &meta = ws->meta;
-  // meta layout: counts[R] | fill[R] | ptrs[R] | nheads | TickCounters
+  std::vector<uint64_t> fill(NB, 0);
+  DevBuf &scratch = ws->scratch, &outb = ws->outb, &oslotb = ws->oslotb, &cub_tmp = ws->cub_tmp,
+         &meta = ws->meta;
+  // meta layout: counts[NB] | fill[NB] | ptrs[NB] | nemit (64 B) | TickCounters
   uint64_t pending = 0, wm = 0, wb = 0;
-  std::vector<unsigned long long> h_counts(R), hfill(R);
-  std::vector<uint64_t*> h_ptrs(R, nullptr);
-  unsigned long long *d_counts = nullptr, *d_fill = nullptr;
+  std::vector<unsigned long long> h_counts(NB), hfill(NB);
+  std::vector<uint64_t*> h_ptrs(NB, nullptr);
+  unsigned long long *d_counts = nullptr, *d_fill = nullptr, *d_nemit = nullptr;
+  unsigned long long h_ne = 0;
   uint64_t** d_ptrs = nullptr;
-  int64_t* d_nheads = nullptr;
   TickCounters* d_tc = nullptr;
   TickCounters h_tc;
-  const size_t meta_bytes = R * 8 * 3 + 64 + sizeof(TickCounters);
+  const size_t meta_bytes = NB * 8 * 3 + 64 + sizeof(TickCounters);
 
   OVCHK(grow(meta, meta_bytes));
   d_counts = (unsigned long long*)meta.p;
-  d_fill = d_counts + R;
-  d_ptrs = (uint64_t**)(d_fill + R);
-  d_nheads = (int64_t*)(d_ptrs + R);
-  d_tc = (TickCounters*)((char*)d_nheads + 64);
+  d_fill = d_counts + NB;
+  d_ptrs = (uint64_t**)(d_fill + NB);
+  d_nemit = (unsigned long long*)(d_ptrs + NB);
+  d_tc = (TickCounters*)((char*)d_nemit + 64);
   OVCHK(hipMemsetAsync(meta.p, 0, meta_bytes, stream));
 
   {
@@ -461,138 +420,133 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
       const uint64_t per = (uint64_t)kScatterBlock * kScatterIPT;
       const uint64_t blocks = (items + per - 1) / per;
       hipLaunchKernelGGL((k_scatter<false, PickSource>), dim3((uint32_t)blocks), dim3(kScatterBlock),
-                         0, stream, src, items, R, d_counts, d_fill, (uint64_t* const*)d_ptrs);
+                         0, stream, src, items, NB, d_counts, d_fill, (uint64_t* const*)d_ptrs);
       OVCHK(hipGetLastError());
-      OVCHK(hipMemcpyAsync(h_counts.data(), d_counts, R * 8, hipMemcpyDeviceToHost, stream));
+      OVCHK(hipMemcpyAsync(h_counts.data(), d_counts, NB * 8, hipMemcpyDeviceToHost, stream));
       OVCHK(hipStreamSynchronize(stream));
-      for (uint32_t s = 0; s < R; ++s) {
+      for (uint32_t s = 0; s < NB; ++s) {
         OVCHK(grow(bucket[s], (fill[s] + h_counts[s]) * 8));
         h_ptrs[s] = (uint64_t*)bucket[s].p;
       }
-      OVCHK(hipMemcpyAsync(d_ptrs, h_ptrs.data(), R * 8, hipMemcpyHostToDevice, stream));
+      OVCHK(hipMemcpyAsync(d_ptrs, h_ptrs.data(), NB * 8, hipMemcpyHostToDevice, stream));
       src.write_rows = true;
       hipLaunchKernelGGL((k_scatter<true, PickSource>), dim3((uint32_t)blocks), dim3(kScatterBlock),
-                         0, stream, src, items, R, d_counts, d_fill, (uint64_t* const*)d_ptrs);
+                         0, stream, src, items, NB, d_counts, d_fill, (uint64_t* const*)d_ptrs);
       OVCHK(hipGetLastError());
-      for (uint32_t s = 0; s < R; ++s) { fill[s] += h_counts[s]; pending += h_counts[s]; }
-      OVCHK(hipMemsetAsync(d_counts, 0, R * 8, stream));
+      for (uint32_t s = 0; s < NB; ++s) { fill[s] += h_counts[s]; pending += h_counts[s]; }
+      OVCHK(hipMemsetAsync(d_counts, 0, NB * 8, stream));
     } else if (ntot) {
       OVCHK(hipMemsetAsync(d_deg, 0, ntot, stream));
     }
   }
 
-  for (uint64_t t = 1;; ++t) {
-    if (t > max_ticks) {
+  for (uint64_t blk = 0;; ++blk) {
+    const uint64_t t0 = blk * p.L + 1, tend = t0 + p.L - 1;  // the block's ticks
+    if (t0 > max_ticks) {
       res->rc = GS_ELIVELOCK;
       snprintf(res->msg, sizeof(res->msg),
                "overlay did not stabilise within %llu ticks (fanin <= fanout livelocks, "
                "simulator.go:66-94)", (unsigned long long)max_ticks);
       goto cleanup;
     }
-    const uint32_t s = (uint32_t)(t % R);
+    const uint32_t s = (uint32_t)(blk % NB);
     const uint64_t m = fill[s];
     if (m) {
-      if (m > 0x7FFFFFFFull) {
+      if (m >> 36) {
         res->rc = GS_EOVERFLOW;
-        snprintf(res->msg, sizeof(res->msg), "%llu overlay events in one tick exceed 2^31-1",
+        snprintf(res->msg, sizeof(res->msg), "%llu overlay events in one block exceed 2^36",
                  (unsigned long long)m);
         goto cleanup;
       }
       OVCHK(grow(scratch, m * 8));
       OVCHK(grow(outb, m * 8));
       OVCHK(grow(oslotb, m * 2));
-      OVCHK(grow(heads, m * 8));
-      hipcub::DoubleBuffer<uint64_t> db((uint64_t*)bucket[s].p, (uint64_t*)scratch.p);
-      // by destination group (grouped) or destination only (bits B+1 .. 2B):
-      // the process kernel orders each destination's events by (src, kind)
-      // itself
-      const uint32_t glog = grouped ? kOvGroupLog : 0u;
-      const int begin_bit = (int)(p.B + 1 + glog), end_bit = (int)(2 * p.B + 1);
-      size_t sort_bytes = 0, sel_bytes = 0;
-      OVCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, db, (int)m, begin_bit, end_bit, stream));
-      IsHead pred{nullptr, p.B + 1 + glog};
-      hipcub::CountingInputIterator<int64_t> it(0);
-      OVCHK(hipcub::DeviceSelect::If(nullptr, sel_bytes, it, (int64_t*)heads.p, d_nheads, (int)m,
-                                     pred, stream));
-      OVCHK(grow(cub_tmp, std::max(sort_bytes, sel_bytes)));
-      sort_bytes = cub_tmp.bytes;
-      OVCHK(hipcub::DeviceRadixSort::SortKeys(cub_tmp.p, sort_bytes, db, (int)m, begin_bit, end_bit, stream));
-      uint64_t* keys = db.Current();
-      if (db.Current() != (uint64_t*)bucket[s].p) std::swap(bucket[s], scratch);
-      pred.keys = keys;
-      sel_bytes = cub_tmp.bytes;
-      OVCHK(hipcub::DeviceSelect::If(cub_tmp.p, sel_bytes, it, (int64_t*)heads.p, d_nheads, (int)m,
-                                     pred, stream));
-      if (grouped) {
-        const uint64_t ng = std::min<uint64_t>(m, (ntot >> kOvGroupLog) + 1);  // heads <= groups
-        hipLaunchKernelGGL(k_process_g, dim3((uint32_t)((ng + kOvWaves - 1) / kOvWaves)), dim3(kOvWaves * 64), 0,
-                           stream, p, (uint32_t)t, (const uint64_t*)keys, m, (const int64_t*)heads.p, d_nheads,
-                           d_deg, d_ids, (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_tc);
-      } else {
-        hipLaunchKernelGGL(k_process, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, stream, p,
-                           (uint32_t)t, keys, m, (const int64_t*)heads.p, d_nheads, d_deg, d_ids,
-                           (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_tc);
-      }
-      OVCHK(hipGetLastError());
-      OutSource osrc{(const uint64_t*)outb.p, (const uint16_t*)oslotb.p};
-      const uint64_t per = (uint64_t)kScatterBlock * kScatterIPT;
-      const uint32_t blocks = (uint32_t)((m + per - 1) / per);
-      hipLaunchKernelGGL((k_scatter<false, OutSource>), dim3(blocks), dim3(kScatterBlock), 0, stream,
-                         osrc, m, R, d_counts, d_fill, (uint64_t* const*)d_ptrs);
-      OVCHK(hipGetLastError());
-      OVCHK(hipMemcpyAsync(h_counts.data(), d_counts, R * 8, hipMemcpyDeviceToHost, stream));
-      OVCHK(hipMemcpyAsync(&h_tc, d_tc, sizeof(h_tc), hipMemcpyDeviceToHost, stream));
-      OVCHK(hipStreamSynchronize(stream));
-      if (h_tc.err) {
-        res->rc = (h_tc.err & 1) ? GS_EREJECT : GS_EINVAL;
-        snprintf(res->msg, sizeof(res->msg), (h_tc.err & 1)
-                     ? "replacement-friend rejection exhausted (n too small, simulator.go:87-89)"
-                     : "too many overlay events at one node in one tick");
-        goto cleanup;
-      }
-      // The current slot is consumed; emitted events never land in it.
-      fill[s] = 0;
-      pending -= m;
-      bool moved = false;
-      for (uint32_t q = 0; q < R; ++q) {
-        if (!h_counts[q]) continue;
-        if (bucket[q].bytes < (fill[q] + h_counts[q]) * 8) {
-          DevBuf nb;
-          OVCHK(grow(nb, (fill[q] + h_counts[q]) * 8 * 3 / 2));
-          if (fill[q])
-            OVCHK(hipMemcpyAsync(nb.p, bucket[q].p, fill[q] * 8, hipMemcpyDeviceToDevice, stream));
-          OVCHK(hipStreamSynchronize(stream));
-          (void)hipFree(bucket[q].p);
-          bucket[q] = nb;
-        }
-      }
-      for (uint32_t q = 0; q < R; ++q) {
-        if (h_ptrs[q] != (uint64_t*)bucket[q].p) moved = true;
-        h_ptrs[q] = (uint64_t*)bucket[q].p;
-      }
-      if (moved)
-        OVCHK(hipMemcpyAsync(d_ptrs, h_ptrs.data(), R * 8, hipMemcpyHostToDevice, stream));
       {
-        // hfill is rewritten only after the next tick's count sync, which
-        // orders it after this copy: no host sync after the scatter
-        hfill.assign(fill.begin(), fill.end());
-        OVCHK(hipMemcpyAsync(d_fill, hfill.data(), R * 8, hipMemcpyHostToDevice, stream));
-        hipLaunchKernelGGL((k_scatter<true, OutSource>), dim3(blocks), dim3(kScatterBlock), 0,
-                           stream, osrc, m, R, d_counts, d_fill, (uint64_t* const*)d_ptrs);
+        // by destination only: the process kernel orders each destination's
+        // short run by (tag, src, kind) itself
+        rocprim::double_buffer<uint64_t> db((uint64_t*)bucket[s].p, (uint64_t*)scratch.p);
+        const unsigned begin_bit = p.B + 1 + p.TB, end_bit = 2 * p.B + 1 + p.TB;
+        size_t sort_bytes = 0;
+        OVCHK(rocprim::radix_sort_keys<OvRadix>(nullptr, sort_bytes, db, (size_t)m, begin_bit, end_bit, stream));
+        OVCHK(grow(cub_tmp, sort_bytes));
+        sort_bytes = cub_tmp.bytes;
+        OVCHK(rocprim::radix_sort_keys<OvRadix>(cub_tmp.p, sort_bytes, db, (size_t)m, begin_bit, end_bit, stream));
+        uint64_t* keys = db.current();
+        if (db.current() != (uint64_t*)bucket[s].p) std::swap(bucket[s], scratch);
+        const uint64_t per = (uint64_t)kProcBlock * kProcIPT;
+        hipLaunchKernelGGL(k_process, dim3((uint32_t)((m + per - 1) / per)), dim3(kProcBlock), 0, stream, p, t0,
+                           keys, m, d_deg, d_ids, (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_nemit, d_tc);
         OVCHK(hipGetLastError());
       }
-      for (uint32_t q = 0; q < R; ++q) { fill[q] += h_counts[q]; pending += h_counts[q]; }
-      wm += h_tc.makeups;
-      wb += h_tc.breakups;
-      OVCHK(hipMemsetAsync(d_counts, 0, R * 8, stream));
-      OVCHK(hipMemsetAsync(d_tc, 0, sizeof(TickCounters), stream));
+      OVCHK(hipMemcpyAsync(&h_ne, d_nemit, 8, hipMemcpyDeviceToHost, stream));
+      OVCHK(hipMemsetAsync(d_nemit, 0, 8, stream));
+      OVCHK(hipStreamSynchronize(stream));
+      {
+        // the emitted events: count per bucket, grow, write
+        const uint64_t nitems = h_ne;
+        OutSource osrc{(const uint64_t*)outb.p, (const uint16_t*)oslotb.p};
+        const uint64_t per = (uint64_t)kScatterBlock * kScatterIPT;
+        const uint32_t blocks = (uint32_t)((nitems + per - 1) / per);
+        if (blocks) {
+          hipLaunchKernelGGL((k_scatter<false, OutSource>), dim3(blocks), dim3(kScatterBlock), 0, stream, osrc,
+                             nitems, NB, d_counts, d_fill, (uint64_t* const*)d_ptrs);
+          OVCHK(hipGetLastError());
+        }
+        OVCHK(hipMemcpyAsync(h_counts.data(), d_counts, NB * 8, hipMemcpyDeviceToHost, stream));
+        OVCHK(hipMemcpyAsync(&h_tc, d_tc, sizeof(h_tc), hipMemcpyDeviceToHost, stream));
+        OVCHK(hipStreamSynchronize(stream));
+        if (h_tc.err) {
+          res->rc = (h_tc.err & 1) ? GS_EREJECT : GS_EINVAL;
+          snprintf(res->msg, sizeof(res->msg), (h_tc.err & 1)
+                       ? "replacement-friend rejection exhausted (n too small, simulator.go:87-89)"
+                       : "too many overlay events at one node in one tick");
+          goto cleanup;
+        }
+        // The current bucket is consumed; emitted events never land in it
+        // (they arrive >= delay_low >= L ticks later: a later block).
+        fill[s] = 0;
+        pending -= m;
+        for (uint32_t q = 0; q < NB; ++q) {
+          if (!h_counts[q]) continue;
+          if (bucket[q].bytes < (fill[q] + h_counts[q]) * 8) {
+            DevBuf nb;
+            OVCHK(grow(nb, (fill[q] + h_counts[q]) * 8 * 3 / 2));
+            if (fill[q])
+              OVCHK(hipMemcpyAsync(nb.p, bucket[q].p, fill[q] * 8, hipMemcpyDeviceToDevice, stream));
+            OVCHK(hipStreamSynchronize(stream));
+            (void)hipFree(bucket[q].p);
+            bucket[q] = nb;
+          }
+        }
+        bool moved = false;
+        for (uint32_t q = 0; q < NB; ++q) {
+          if (h_ptrs[q] != (uint64_t*)bucket[q].p) moved = true;
+          h_ptrs[q] = (uint64_t*)bucket[q].p;
+        }
+        if (moved) OVCHK(hipMemcpyAsync(d_ptrs, h_ptrs.data(), NB * 8, hipMemcpyHostToDevice, stream));
+        // hfill is rewritten only after the next block's count sync, which
+        // orders it after this copy: no host sync after the scatter
+        hfill.assign(fill.begin(), fill.end());
+        OVCHK(hipMemcpyAsync(d_fill, hfill.data(), NB * 8, hipMemcpyHostToDevice, stream));
+        if (blocks) {
+          hipLaunchKernelGGL((k_scatter<true, OutSource>), dim3(blocks), dim3(kScatterBlock), 0, stream, osrc,
+                             nitems, NB, d_counts, d_fill, (uint64_t* const*)d_ptrs);
+          OVCHK(hipGetLastError());
+        }
+        for (uint32_t q = 0; q < NB; ++q) { fill[q] += h_counts[q]; pending += h_counts[q]; }
+        wm += h_tc.makeups;
+        wb += h_tc.breakups;
+        OVCHK(hipMemsetAsync(d_counts, 0, NB * 8, stream));
+        OVCHK(hipMemsetAsync(d_tc, 0, sizeof(TickCounters), stream));
+      }
     }
-    if (t % 10 == 0) {                                        // simulator.go:222-234
+    if (tend > max_ticks) continue;  // (the next block reports the livelock)
+    if (tend % 10 == 0) {                                     // simulator.go:222-234
       if (wm == 0 && wb == 0 && pending == 0) {
-        res->final_tick = t;
+        res->final_tick = tend;
         break;
       }
-      if (sink.push) sink.push(sink.self, t, wm, wb);
+      if (sink.push) sink.push(sink.self, tend, wm, wb);
       wm = wb = 0;
     }
   }

@@ -55,9 +55,11 @@ constexpr uint32_t kRoll0Fine = kFineLog + 4;
 // reached; never past the next poll).  0 = nothing to do.
 // Error bits that stop a window: an overflow (the host redoes the window), or
 // in device-driven shard windows only kErrAbort (k_rtab: some shard's window
-// overflowed; a fine overflow is re-partitioned in the window itself).
+// overflowed; a fine overflow is re-partitioned in the window itself) --
+// except a single in-process shard (w.solo), which stops on any overflow as
+// the unsharded engine does.
 __device__ __forceinline__ uint32_t stop_bits(const WinState& w) {
-  return w.dd ? kErrAbort : (kErrCoarse | kErrFine);
+  return w.dd && !w.solo ? kErrAbort : (kErrCoarse | kErrFine | kErrAbort);
 }
 __device__ __forceinline__ bool win_abort(const WinState& w) {
   return (*w.err & stop_bits(w)) != 0;
@@ -2022,44 +2024,49 @@ __global__ __launch_bounds__(1024) void k_fine_scan(const WinState w) {
 
 // The window's counters of this shard (its stat shards summed into w.wstat,
 // zero rows past the window or in a stopped one) and its flags: kErrArrivals,
-// an exact fine re-partition (kErrFine, cleared here), kErrAbort.
+// an exact fine re-partition (kErrFine, cleared here), kErrAbort.  A single
+// in-process shard (w.solo) closes its window here too (close_rows), one
+// launch instead of two.
 // kMaxWindow * kStatFields * kCloseLanes threads.
-__global__ void k_stats_dd(const WinState w) {
+__device__ void close_rows(const WinState& w, const unsigned long long* rows, WinCtl* const* ctls, uint32_t n,
+                           uint32_t slot);
+__global__ void k_stats_dd(const WinState w, uint32_t slot) {
+  __shared__ unsigned long long rows[kDDWStat];  // w.solo: closed here (no k_close_dd)
   const uint32_t tid = threadIdx.x;
   const CtlView c = ctl_view(w);
-  const bool dead = (c.err & kErrAbort) != 0;
+  const bool dead = (c.err & stop_bits(w)) != 0;
   const uint32_t L = dead || c.stop ? 0u : c.L;
   const uint32_t i = tid / kCloseLanes, part = tid % kCloseLanes, k = i / kStatFields;
   unsigned long long sum = 0;
   if (k < L) sum = stat_shard_sum(w, i, part);  // k is uniform over each lane group
-  if (part == 0) w.wstat[i] = sum;
+  if (part == 0) {
+    w.wstat[i] = sum;
+    rows[i] = sum;
+  }
   if (tid < 8) {
     constexpr uint32_t F = kMaxWindow * kStatFields;
     unsigned long long v = 0;
     if (tid == 0) v = (c.err & kErrArrivals) ? 1 : 0;
-    if (tid == 1) v = (c.err & kErrFine) ? 1 : 0;
+    if (tid == 1) v = !w.solo && (c.err & kErrFine) ? 1 : 0;
     if (tid == 2) v = dead ? 1 : 0;
     w.wstat[F + tid] = v;
+    rows[F + tid] = v;
   }
-  if (tid == 0 && (c.err & kErrFine)) atomicAnd(w.err, ~kErrFine);
+  if (tid == 0 && !w.solo && (c.err & kErrFine)) atomicAnd(w.err, ~kErrFine);
+  if (!w.solo) return;
+  __syncthreads();
+  WinCtl* const one[1] = {w.ctl};
+  close_rows(w, rows, one, 1, slot);
 }
 
-// The close of a device-driven shard window: the window's global counters
-// (the sum of the n shards' wstat: the group's shards, or this rank's own
-// after the all-reduce), gs_run's poll rule (simulator.go:243-248, as
-// k_close) on every shard's control block, and staging slot `slot` for the
-// host.  One block of 128 threads.
-__global__ __launch_bounds__(128) void k_close_dd(const WinState w, const unsigned long long* const* wstats,
-                                                  WinCtl* const* ctls, uint32_t n, uint32_t slot) {
-  __shared__ unsigned long long rows[kDDWStat];
+// The close of a device-driven shard window from its summed counter rows
+// (F = kMaxWindow * kStatFields counters, then the flags): gs_run's poll rule
+// (simulator.go:243-248, as k_close) on every shard's control block, and
+// staging slot `slot` for the host.  Block-wide (tid 0 applies the rule).
+__device__ void close_rows(const WinState& w, const unsigned long long* rows, WinCtl* const* ctls, uint32_t n,
+                           uint32_t slot) {
   const uint32_t tid = threadIdx.x;
   constexpr uint32_t F = kMaxWindow * kStatFields;
-  for (uint32_t i = tid; i < kDDWStat; i += blockDim.x) {
-    unsigned long long v = 0;
-    for (uint32_t q = 0; q < n; ++q) v += wstats[q][i];
-    rows[i] = v;
-  }
-  __syncthreads();
   const WinCtl* c0 = ctls[0];
   const bool dead = rows[F + 2] != 0;
   const uint32_t t0 = c0->t, L = dead || c0->stop ? 0u : c0->L;
@@ -2095,6 +2102,22 @@ __global__ __launch_bounds__(128) void k_close_dd(const WinState w, const unsign
   st[4] = rows[F + 1];  // exact fine re-partitions in the window
 }
 
+// The close of a device-driven shard window: the window's global counters
+// (the sum of the n shards' wstat: the group's shards, or this rank's own
+// after the all-reduce), then close_rows.  One block of 128 threads.
+__global__ __launch_bounds__(128) void k_close_dd(const WinState w, const unsigned long long* const* wstats,
+                                                  WinCtl* const* ctls, uint32_t n, uint32_t slot) {
+  __shared__ unsigned long long rows[kDDWStat];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < kDDWStat; i += blockDim.x) {
+    unsigned long long v = 0;
+    for (uint32_t q = 0; q < n; ++q) v += wstats[q][i];
+    rows[i] = v;
+  }
+  __syncthreads();
+  close_rows(w, rows, ctls, n, slot);
+}
+
 }  // namespace
 
 hipError_t win_rtab(const WinState& w, unsigned long long* rtab, const unsigned long long* const* ccaps,
@@ -2117,8 +2140,8 @@ hipError_t win_fine_redo(const WinState& w, uint64_t T, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t win_stats_dd(const WinState& w, hipStream_t s) {
-  hipLaunchKernelGGL(k_stats_dd, dim3(1), dim3(kMaxWindow * kStatFields * kCloseLanes), 0, s, w);
+hipError_t win_stats_dd(const WinState& w, uint32_t slot, hipStream_t s) {
+  hipLaunchKernelGGL(k_stats_dd, dim3(1), dim3(kMaxWindow * kStatFields * kCloseLanes), 0, s, w, slot);
   return hipGetLastError();
 }
 

@@ -29,6 +29,10 @@ def fam(n):
 picks = [i for i, (n, _, _) in enumerate(rows) if "PickSource" in n]
 start = picks[-2] if len(picks) >= 2 else 0
 rows = rows[start:]
+# host-side stalls: the largest idle gaps between consecutive kernels
+gaps = sorted(((rows[i + 1][1] - rows[i][2]) / 1e6, rows[i][0][:60], rows[i + 1][0][:60]) for i in range(len(rows) - 1))[-8:]
+for g, a, b in gaps:
+    print(f"gap {g:.2f} ms after {a} before {b}")
 ticks, cur = [], defaultdict(float)
 span0 = rows[0][1]
 for n, b, e in rows:

@@ -200,6 +200,28 @@ def test_overlay_c2_size_matches_oracle(gs, oracle):
         assert gdeg.min() >= 3 and gdeg.max() <= 6
 
 
+@pytest.mark.parametrize("block,dlow,dhigh", [("1", 10, 20), ("2", 10, 20), ("5", 10, 20), (None, 10, 20),
+                                             (None, 5, 9), (None, 2, 7), (None, 1, 4)])
+def test_overlay_tick_blocks_match_oracle(gs, oracle, monkeypatch, block, dlow, dhigh):
+    """The overlay processes blocks of L ticks at once (L | 10, L <= delaylow;
+    GS_OV_BLOCK caps L): every block length gives the oracle's per-tick
+    overlay -- windows, final tick, rows."""
+    if block is None:
+        monkeypatch.delenv("GS_OV_BLOCK", raising=False)
+    else:
+        monkeypatch.setenv("GS_OV_BLOCK", block)
+    kw = dict(n=50000, fanout=3, fanin=6, delay_low=dlow, delay_high=dhigh, drop_rate=0.1,
+              crash_rate=0.001, seed=7, trial=0)
+    deg, ids, wins, final = oracle.overlay(oracle.make_params(**kw))
+    with gs.Simulator(cfg_from(gs, kw)) as sim:
+        gw, gf = sim.build_overlay()
+        assert gf == final
+        assert [tuple(w) for w in gw] == [tuple(w) for w in wins]
+        gdeg, gids = sim.read_peers()
+        assert np.array_equal(gdeg, deg)
+        assert np.array_equal(masked(gdeg, gids), masked(deg, ids))
+
+
 @pytest.mark.parametrize("mode", ["tick", "hop"])
 def test_c2_full_size_bit_exact(gs, oracle, mode):
     """Config C2: N=1e6, fanout 3 (fanin 6); GPU overlay + broadcast vs oracle, per poll."""
