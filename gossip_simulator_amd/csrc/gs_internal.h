@@ -421,7 +421,7 @@ struct OverlayWindowSink {
 struct OverlayWork {
   struct Buf { void* p = nullptr; size_t bytes = 0; };
   std::vector<Buf> bucket;  // per arrival slot
-  Buf scratch, outb, oslotb, heads, cub_tmp, meta;
+  Buf scratch, outb, oslotb, cub_tmp, meta;
 };
 void overlay_free(OverlayWork* ws);
 // n = nodes per trial; trials > 1 builds every trial's overlay at once in the

@@ -68,14 +68,16 @@ __device__ __forceinline__ uint32_t ov_draw(const OvParams& p, uint32_t kind, ui
   return philox(node, b, c, c3, p.key.k0, p.key.k1).x;
 }
 
-// An event arriving at tick a (>= 1): its key and its bucket.
-__device__ __forceinline__ uint64_t ev_key(const OvParams& p, uint32_t dst, uint64_t a, uint32_t src,
+// An event arriving at tick a (>= 1): its key and its bucket.  (32-bit tick
+// arithmetic: a 64-bit division is a long software sequence on the GPU, and
+// the burst makes one key per friend slot.)
+__device__ __forceinline__ uint64_t ev_key(const OvParams& p, uint32_t dst, uint32_t a, uint32_t src,
                                            uint32_t kind) {
-  const uint64_t tag = (a - 1) % p.L;
-  return ((uint64_t)dst << (p.B + 1 + p.TB)) | (tag << (p.B + 1)) | ((uint64_t)src << 1) | kind;
+  const uint32_t tag = (a - 1) % p.L;
+  return ((uint64_t)dst << (p.B + 1 + p.TB)) | ((uint64_t)tag << (p.B + 1)) | ((uint64_t)src << 1) | kind;
 }
-__device__ __forceinline__ uint32_t ev_bucket(const OvParams& p, uint64_t a) {
-  return (uint32_t)(((a - 1) / p.L) % p.NB);
+__device__ __forceinline__ uint32_t ev_bucket(const OvParams& p, uint32_t a) {
+  return ((a - 1) / p.L) % p.NB;
 }
 
 // Item sources for the bucket scatter -------------------------------------
@@ -97,7 +99,7 @@ struct PickSource {  // tick 0: item i = (trial i / (n*fanout), v, j = i % fanou
       if (j == 0) deg[gv] = (uint8_t)p.fanout;
     }
     // :102 Makeup, arriving at tick 0 + off
-    const uint64_t a = fire_offset(p.delay_low, p.delay_span, ov_draw(p, K_OVDELAY, gv, 0, j));
+    const uint32_t a = fire_offset(p.delay_low, p.delay_span, ov_draw(p, K_OVDELAY, gv, 0, j));
     key = ev_key(p, tb | f, a, gv, 0u);
     slot = ev_bucket(p, a);
   }
@@ -275,7 +277,7 @@ __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64
         }
       }
       if (emitted_dst != ~0u) {
-        const uint64_t a = (uint64_t)t + fire_offset(p.delay_low, p.delay_span, ov_draw(p, K_OVDELAY, u, t, k));
+        const uint32_t a = t + fire_offset(p.delay_low, p.delay_span, ov_draw(p, K_OVDELAY, u, t, k));
         emit(ev_key(p, emitted_dst, a, u, emitted_kind), ev_bucket(p, a));
       }
     }
@@ -338,7 +340,7 @@ void overlay_free(OverlayWork* ws) {
   for (auto& b : ws->bucket)
     if (b.p) (void)hipFree(b.p);
   ws->bucket.clear();
-  for (DevBuf* b : {&ws->scratch, &ws->outb, &ws->oslotb, &ws->heads, &ws->cub_tmp, &ws->meta}) {
+  for (DevBuf* b : {&ws->scratch, &ws->outb, &ws->oslotb, &ws->cub_tmp, &ws->meta}) {
     if (b->p) (void)hipFree(b->p);
     b->p = nullptr;
     b->bytes = 0;
@@ -376,9 +378,16 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
     const char* be = getenv("GS_OV_BLOCK");  // (read per build: tests switch it)
     const uint32_t lmax = be ? (uint32_t)atoi(be) : 10u;
     const uint32_t tbmax = std::min<uint32_t>(4u, 63u - 2 * p.B);
+    // a block's bucket stays below 2^31 events (the sort's item count): the
+    // burst's n * fanout makeups spread over delayhigh - delaylow ticks
+    const double burst = (double)n * p.fanout * (trials > 1 ? trials : 1);
+    const double per_tick = burst / std::max<uint32_t>(p.delay_span, 1u);
     p.L = 1;
     for (uint32_t L : {10u, 5u, 2u}) {
-      if (L <= lmax && (int32_t)L <= delay_low && L <= (1u << tbmax)) { p.L = L; break; }
+      if (L <= lmax && (int32_t)L <= delay_low && L <= (1u << tbmax) && per_tick * L * 1.25 < 2147483647.0) {
+        p.L = L;
+        break;
+      }
     }
     p.TB = 0;
     while ((1u << p.TB) < p.L) ++p.TB;
@@ -452,9 +461,9 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
     const uint32_t s = (uint32_t)(blk % NB);
     const uint64_t m = fill[s];
     if (m) {
-      if (m >> 36) {
+      if (m > 0x7FFFFFFFull) {
         res->rc = GS_EOVERFLOW;
-        snprintf(res->msg, sizeof(res->msg), "%llu overlay events in one block exceed 2^36",
+        snprintf(res->msg, sizeof(res->msg), "%llu overlay events in one block exceed 2^31-1",
                  (unsigned long long)m);
         goto cleanup;
       }
