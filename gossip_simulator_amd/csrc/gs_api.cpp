@@ -702,7 +702,7 @@ void destroy_one(gs_ctx* c) {
     (void)hipFree(c->ws.dbg);
   }
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
-  overlay_free(&c->ovw);
+  overlay_free(&c->ovw, c->stream);
   if (c->own_ig) {
     if (c->d_ig) (void)hipFree(c->d_ig);
     if (c->d_fg) (void)hipFree(c->d_fg);
@@ -1424,7 +1424,7 @@ int overlay_into(gs_ctx* c, uint64_t max_ticks, gs_window* win, size_t cap, size
   if (nwin) *nwin = ws.n;
   if (final_tick) *final_tick = res.final_tick;
   // batched contexts rebuild per batch (gs_set_trial): keep the workspace
-  if (c->trials <= 1) overlay_free(&c->ovw);
+  if (c->trials <= 1) overlay_free(&c->ovw, c->stream);
   if (rc) return fail(c, rc, res.msg);
   return seal_rows(c, c->d_deg, c->d_ids, n);
 }
@@ -1560,6 +1560,8 @@ int begin_one(gs_ctx* c, uint64_t s, uint32_t* sched) {
 // not fit, leave the dense rounds only (same results).
 int pp_prepare(gs_ctx* c) {
   c->sp = PPSparse{};
+  static const bool load_deg = [] { const char* e = getenv("GS_PP_NODEG"); return e && atoi(e) == 0; }();  // A/B
+  c->sp.nodeg = load_deg ? 0u : 1u;
   if (c->pp_shard) {  // bottom-up rounds only: the partition built the reverse table
     c->sp.ctl = (PPCtl*)c->pp_ctlb.p;
     c->sp.rend = (const unsigned long long*)c->pp_rend.p;

@@ -326,6 +326,7 @@ struct PPCtl {
   unsigned long long bthr;      // dense rounds bottom-up once ninf >= bthr (0: always, ~0: never)
   unsigned long long athr;      // other dense rounds pull-answer once ninf >= athr (~0: never, top-down)
   unsigned long long ncallers;  // live nodes with a non-empty row: calls per round
+  unsigned long long nlive0;    // live nodes with an empty row (0: every live node calls)
   unsigned long long seg_cap;   // entries per segment
   uint32_t nseg;                // segments in use (<= kPPSegs)
   uint32_t mode;                // PPMode of the current round
@@ -355,6 +356,9 @@ struct PPSparse {
   uint32_t* dset;
   unsigned long long* dcnt;
   uint64_t dcap, ccap, fcap;
+  // bottom-up rounds: an informed caller's degree byte is not loaded when
+  // every live node calls and no failed-slot mask is set (GS_PP_NODEG=0: load)
+  uint32_t nodeg;
 };
 constexpr uint32_t kPPDLists = 512;    // = k_ppa_round's grid (kPPSGrid)
 constexpr uint32_t kPPDRegions = 2048; // 256 coarse bins x 8 (XCD) sub-regions
@@ -423,7 +427,7 @@ struct OverlayWork {
   std::vector<Buf> bucket;  // per arrival slot
   Buf scratch, outb, oslotb, cub_tmp, meta;
 };
-void overlay_free(OverlayWork* ws);
+void overlay_free(OverlayWork* ws, hipStream_t st);
 // n = nodes per trial; trials > 1 builds every trial's overlay at once in the
 // id space trial << tlog | node (tlog = 32 for one trial).
 int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, int32_t fanin,

@@ -25,11 +25,13 @@
 //      commute;
 //   3. each processed event emits at most one event (a breakup on eviction,
 //      a makeup on replacement); a workgroup's emitted events are appended to
-//      a compact list, and a count and a write scatter pass move them into
-//      their arrival blocks' buckets.
+//      a compact list and counted per bucket, and a write scatter pass moves
+//      them into their arrival blocks' buckets.
 // Tick 0 is the needNewFriendCh burst: every node picks `fanout` friends
 // (self -> id+1, simulator.go:97-101) and sends a makeup to each.
-// GS_OV_BLOCK=1 forces one tick per block (round 3's per-tick protocol).
+// Blocks of several ticks measured SLOWER than one tick per block (the row
+// traffic halves, but the longer runs and fuller buckets cost more), so the
+// default is L = 1; GS_OV_BLOCK=2|5|10 enables them (tests check every L).
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
@@ -167,8 +169,8 @@ using OvRadix = rocprim::radix_sort_config<
 // reservation to the compact list (eout, eslot); a workgroup whose runs emit
 // more than kEmitCap appends the rest one by one.
 constexpr uint32_t kProcBlock = 256;
-constexpr uint32_t kProcIPT = 8;
-constexpr uint32_t kEmitCap = 4096;
+constexpr uint32_t kProcIPT = 4;
+constexpr uint32_t kEmitCap = 1024;  // (10 KB of LDS: eight waves per SIMD, as the VGPRs allow)
 
 // Wave-aggregated append among the ACTIVE lanes (divergent call sites).
 __device__ __forceinline__ uint32_t active_append(uint32_t* n) {
@@ -183,13 +185,15 @@ __device__ __forceinline__ uint32_t active_append(uint32_t* n) {
 __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64_t t0, uint64_t* keys, uint64_t m,
                                                         uint8_t* deg, uint32_t* ids, uint64_t* eout,
                                                         uint16_t* eslot, unsigned long long* ecount,
-                                                        TickCounters* tc) {
+                                                        unsigned long long* counts, TickCounters* tc) {
   __shared__ uint64_t s_ev[kEmitCap];
   __shared__ uint16_t s_sl[kEmitCap];
+  __shared__ uint32_t s_hist[kMaxRing];  // the workgroup's emitted events per bucket
   __shared__ uint32_t s_n, s_mk, s_bk, s_err;
   __shared__ unsigned long long s_base;
   const uint32_t tid = threadIdx.x;
   if (tid == 0) { s_n = 0; s_mk = 0; s_bk = 0; s_err = 0; }
+  for (uint32_t q = tid; q < p.NB; q += kProcBlock) s_hist[q] = 0;
   __syncthreads();
   uint32_t mk = 0, bk = 0, err = 0;
   auto emit = [&](uint64_t key, uint32_t slot) {
@@ -201,6 +205,7 @@ __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64
       const unsigned long long q = atomicAdd(ecount, 1ull);
       eout[q] = key;
       eslot[q] = (uint16_t)slot;
+      atomicAdd(&counts[slot], 1ull);
     }
   };
   const uint32_t sh = p.B + 1 + p.TB;  // destination field
@@ -295,10 +300,16 @@ __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64
     if (s_err) atomicOr(&tc->err, (unsigned long long)s_err);
   }
   __syncthreads();
+  // the list, and the per-bucket counts the host sizes the buckets by (no
+  // separate count pass over the list)
   for (uint32_t j = tid; j < n; j += kProcBlock) {
     eout[s_base + j] = s_ev[j];
     eslot[s_base + j] = s_sl[j];
+    atomicAdd(&s_hist[s_sl[j]], 1u);
   }
+  __syncthreads();
+  for (uint32_t q = tid; q < p.NB; q += kProcBlock)
+    if (s_hist[q]) atomicAdd(&counts[q], (unsigned long long)s_hist[q]);
 }
 
 #define OVCHK(expr)                                                              \
@@ -316,7 +327,10 @@ using DevBuf = OverlayWork::Buf;
 // Grown with 25 % headroom: a batched context rebuilds overlays batch after
 // batch, and a regrow (hipFree + hipMalloc of GB-sized buckets) cost up to
 // 1.7 s where the next batch's events outnumbered the first's by a little.
-static hipError_t grow(DevBuf& b, size_t bytes) {
+// (The stream-ordered pool allocator instead corrupted the N = 1e9 build:
+// profiles/r04s_overlay_pool.txt.)
+static hipError_t grow(DevBuf& b, size_t bytes, hipStream_t st) {
+  (void)st;
   if (b.bytes >= bytes) return hipSuccess;
   const size_t nb = std::max(bytes + bytes / 4, b.bytes * 3 / 2);
   if (b.p) (void)hipFree(b.p);
@@ -335,7 +349,8 @@ static uint32_t node_bits(uint64_t n) {
 
 }  // namespace
 
-void overlay_free(OverlayWork* ws) {
+void overlay_free(OverlayWork* ws, hipStream_t st) {
+  (void)st;
   if (!ws) return;
   for (auto& b : ws->bucket)
     if (b.p) (void)hipFree(b.p);
@@ -375,8 +390,11 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
   }
   {
     // tick blocks: L | 10, L <= delay_low, L <= 2^TB with 2B + 1 + TB <= 64
-    const char* be = getenv("GS_OV_BLOCK");  // (read per build: tests switch it)
-    const uint32_t lmax = be ? (uint32_t)atoi(be) : 10u;
+    // default one tick per block: blocks of 2, 5 or 10 ticks measured slower
+    // (profiles/r04q_overlay_blocks.txt); GS_OV_BLOCK raises the cap (read per
+    // build: the tests switch it)
+    const char* be = getenv("GS_OV_BLOCK");
+    const uint32_t lmax = be ? (uint32_t)atoi(be) : 1u;
     const uint32_t tbmax = std::min<uint32_t>(4u, 63u - 2 * p.B);
     // a block's bucket stays below 2^31 events (the sort's item count): the
     // burst's n * fanout makeups spread over delayhigh - delaylow ticks
@@ -413,7 +431,7 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
   TickCounters h_tc;
   const size_t meta_bytes = NB * 8 * 3 + 64 + sizeof(TickCounters);
 
-  OVCHK(grow(meta, meta_bytes));
+  OVCHK(grow(meta, meta_bytes, stream));
   d_counts = (unsigned long long*)meta.p;
   d_fill = d_counts + NB;
   d_ptrs = (uint64_t**)(d_fill + NB);
@@ -434,7 +452,7 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
       OVCHK(hipMemcpyAsync(h_counts.data(), d_counts, NB * 8, hipMemcpyDeviceToHost, stream));
       OVCHK(hipStreamSynchronize(stream));
       for (uint32_t s = 0; s < NB; ++s) {
-        OVCHK(grow(bucket[s], (fill[s] + h_counts[s]) * 8));
+        OVCHK(grow(bucket[s], (fill[s] + h_counts[s]) * 8, stream));
         h_ptrs[s] = (uint64_t*)bucket[s].p;
       }
       OVCHK(hipMemcpyAsync(d_ptrs, h_ptrs.data(), NB * 8, hipMemcpyHostToDevice, stream));
@@ -467,43 +485,41 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
                  (unsigned long long)m);
         goto cleanup;
       }
-      OVCHK(grow(scratch, m * 8));
-      OVCHK(grow(outb, m * 8));
-      OVCHK(grow(oslotb, m * 2));
+      OVCHK(grow(scratch, m * 8, stream));
+      OVCHK(grow(outb, m * 8, stream));
+      OVCHK(grow(oslotb, m * 2, stream));
       {
-        // by destination only: the process kernel orders each destination's
-        // short run by (tag, src, kind) itself
+        // by (destination, tag): each destination's run comes out tick by
+        // tick, and the process kernel orders each tick's few events by
+        // (src, kind) itself (sorting by destination only left runs of L
+        // ticks to the insertion sort, in global memory: slower than the
+        // TB extra radix bits)
         rocprim::double_buffer<uint64_t> db((uint64_t*)bucket[s].p, (uint64_t*)scratch.p);
-        const unsigned begin_bit = p.B + 1 + p.TB, end_bit = 2 * p.B + 1 + p.TB;
+        const unsigned begin_bit = p.B + 1, end_bit = 2 * p.B + 1 + p.TB;
         size_t sort_bytes = 0;
         OVCHK(rocprim::radix_sort_keys<OvRadix>(nullptr, sort_bytes, db, (size_t)m, begin_bit, end_bit, stream));
-        OVCHK(grow(cub_tmp, sort_bytes));
+        OVCHK(grow(cub_tmp, sort_bytes, stream));
         sort_bytes = cub_tmp.bytes;
         OVCHK(rocprim::radix_sort_keys<OvRadix>(cub_tmp.p, sort_bytes, db, (size_t)m, begin_bit, end_bit, stream));
         uint64_t* keys = db.current();
         if (db.current() != (uint64_t*)bucket[s].p) std::swap(bucket[s], scratch);
         const uint64_t per = (uint64_t)kProcBlock * kProcIPT;
         hipLaunchKernelGGL(k_process, dim3((uint32_t)((m + per - 1) / per)), dim3(kProcBlock), 0, stream, p, t0,
-                           keys, m, d_deg, d_ids, (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_nemit, d_tc);
+                           keys, m, d_deg, d_ids, (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_nemit, d_counts,
+                           d_tc);
         OVCHK(hipGetLastError());
       }
       OVCHK(hipMemcpyAsync(&h_ne, d_nemit, 8, hipMemcpyDeviceToHost, stream));
+      OVCHK(hipMemcpyAsync(h_counts.data(), d_counts, NB * 8, hipMemcpyDeviceToHost, stream));
+      OVCHK(hipMemcpyAsync(&h_tc, d_tc, sizeof(h_tc), hipMemcpyDeviceToHost, stream));
       OVCHK(hipMemsetAsync(d_nemit, 0, 8, stream));
       OVCHK(hipStreamSynchronize(stream));
       {
-        // the emitted events: count per bucket, grow, write
+        // the emitted events (k_process counted them per bucket): grow, write
         const uint64_t nitems = h_ne;
         OutSource osrc{(const uint64_t*)outb.p, (const uint16_t*)oslotb.p};
         const uint64_t per = (uint64_t)kScatterBlock * kScatterIPT;
         const uint32_t blocks = (uint32_t)((nitems + per - 1) / per);
-        if (blocks) {
-          hipLaunchKernelGGL((k_scatter<false, OutSource>), dim3(blocks), dim3(kScatterBlock), 0, stream, osrc,
-                             nitems, NB, d_counts, d_fill, (uint64_t* const*)d_ptrs);
-          OVCHK(hipGetLastError());
-        }
-        OVCHK(hipMemcpyAsync(h_counts.data(), d_counts, NB * 8, hipMemcpyDeviceToHost, stream));
-        OVCHK(hipMemcpyAsync(&h_tc, d_tc, sizeof(h_tc), hipMemcpyDeviceToHost, stream));
-        OVCHK(hipStreamSynchronize(stream));
         if (h_tc.err) {
           res->rc = (h_tc.err & 1) ? GS_EREJECT : GS_EINVAL;
           snprintf(res->msg, sizeof(res->msg), (h_tc.err & 1)
@@ -519,7 +535,7 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
           if (!h_counts[q]) continue;
           if (bucket[q].bytes < (fill[q] + h_counts[q]) * 8) {
             DevBuf nb;
-            OVCHK(grow(nb, (fill[q] + h_counts[q]) * 8 * 3 / 2));
+            OVCHK(grow(nb, (fill[q] + h_counts[q]) * 8 * 3 / 2, stream));
             if (fill[q])
               OVCHK(hipMemcpyAsync(nb.p, bucket[q].p, fill[q] * 8, hipMemcpyDeviceToDevice, stream));
             OVCHK(hipStreamSynchronize(stream));

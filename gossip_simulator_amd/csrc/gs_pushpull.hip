@@ -290,6 +290,10 @@ __global__ __launch_bounds__(kPPSBlock) void k_ppb_round(const DevState s, unsig
   uint64_t fired = 0, sent = 0, msgs = 0;
   const uint64_t W = (s.n + 63) >> 6;
   const uint64_t nrange = (W + kPPRange - 1) / kPPRange;
+  // every live node calls (no empty rows) and no failed-slot mask: an
+  // informed caller's push needs only its loss draw (sent = delivered), so
+  // its degree byte is not loaded -- in the late rounds, nearly every node's
+  const bool nodeg = sp.ctl->nlive0 == 0 && !fmask && sp.nodeg;
   for (uint64_t rg = (uint64_t)blockIdx.x * kPPWaves + wv; rg < nrange; rg += (uint64_t)gridDim.x * kPPWaves) {
     const uint64_t w0 = rg * kPPRange, base = w0 << 6;
     nb[lane] = 0;
@@ -305,7 +309,7 @@ __global__ __launch_bounds__(kPPSBlock) void k_ppb_round(const DevState s, unsig
         Iw[i] = inb ? s.recv[word] : ~0ull;
         const unsigned long long Fw = inb ? s.crash[word] : ~0ull;
         live[i] = v < s.n && !((Fw >> lane) & 1);
-        d[i] = live[i] ? s.deg[v] : 0u;
+        d[i] = live[i] && !(nodeg && ((Iw[i] >> lane) & 1)) ? s.deg[v] : (live[i] ? 1u : 0u);
         fm[i] = fmask && live[i] ? fmask[v] : 0u;
       }
 #pragma unroll
@@ -866,11 +870,16 @@ __global__ __launch_bounds__(kPPBlock) void k_ppe_commit(const DevState s, const
 
 // Live nodes with a non-empty row (each calls once per round).
 __global__ __launch_bounds__(kPPBlock) void k_pp_callers(const DevState s, PPCtl* c) {
-  uint64_t k = 0;
-  for (uint64_t v = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; v < s.n; v += (uint64_t)gridDim.x * kPPBlock)
-    k += s.deg[v] > 0 && !((s.crash[v >> 6] >> (v & 63)) & 1);
+  uint64_t k = 0, z = 0;
+  for (uint64_t v = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; v < s.n; v += (uint64_t)gridDim.x * kPPBlock) {
+    const bool live = !((s.crash[v >> 6] >> (v & 63)) & 1);
+    k += live && s.deg[v] > 0;
+    z += live && s.deg[v] == 0;
+  }
   k = wave_sum64(k);
+  z = wave_sum64(z);
   if ((threadIdx.x & 63) == 0 && k) atomicAdd(&c->ncallers, (unsigned long long)k);
+  if ((threadIdx.x & 63) == 0 && z) atomicAdd(&c->nlive0, (unsigned long long)z);
 }
 
 // ---- reverse table ------------------------------------------------------------

@@ -200,12 +200,12 @@ def test_overlay_c2_size_matches_oracle(gs, oracle):
         assert gdeg.min() >= 3 and gdeg.max() <= 6
 
 
-@pytest.mark.parametrize("block,dlow,dhigh", [("1", 10, 20), ("2", 10, 20), ("5", 10, 20), (None, 10, 20),
-                                             (None, 5, 9), (None, 2, 7), (None, 1, 4)])
+@pytest.mark.parametrize("block,dlow,dhigh", [("1", 10, 20), ("2", 10, 20), ("5", 10, 20), ("10", 10, 20),
+                                             (None, 10, 20), ("10", 5, 9), ("10", 2, 7), ("10", 1, 4)])
 def test_overlay_tick_blocks_match_oracle(gs, oracle, monkeypatch, block, dlow, dhigh):
-    """The overlay processes blocks of L ticks at once (L | 10, L <= delaylow;
-    GS_OV_BLOCK caps L): every block length gives the oracle's per-tick
-    overlay -- windows, final tick, rows."""
+    """The overlay can process blocks of L ticks at once (L | 10, L <=
+    delaylow; GS_OV_BLOCK caps L, default 1): every block length gives the
+    oracle's per-tick overlay -- windows, final tick, rows."""
     if block is None:
         monkeypatch.delenv("GS_OV_BLOCK", raising=False)
     else:
