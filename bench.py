@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 batched-trials run")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 node-range-sharded run")
     ap.add_argument("--c3-trials", type=int, default=10_000)
-    ap.add_argument("--c3-batch", type=int, default=2500, help="trials per batched context")
+    ap.add_argument("--c3-batch", type=int, default=5000, help="trials per batched context")
     ap.add_argument("--no-extensions", action="store_true",
                     help="skip the C5 extension runs (1%% failed mask, push-pull)")
     ap.add_argument("--shard-scaling", action="store_true",
