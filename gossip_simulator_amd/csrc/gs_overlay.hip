@@ -105,6 +105,15 @@ struct PickSource {  // tick 0: item i = (trial i / (n*fanout), v, j = i % fanou
     key = ev_key(p, tb | f, a, gv, 0u);
     slot = ev_bucket(p, a);
   }
+  // the counting pass needs the bucket only: the delay draw, not the pick
+  __device__ __forceinline__ uint32_t bucket_of(uint64_t i) const {
+    const uint64_t per = p.n * p.fanout;
+    const uint32_t tr = (uint32_t)(i / per);
+    const uint64_t rem = i - (uint64_t)tr * per;
+    const uint32_t v = (uint32_t)(rem / p.fanout), j = (uint32_t)(rem % p.fanout);
+    const uint32_t gv = (uint32_t)((uint64_t)tr << p.tlog) | v;
+    return ev_bucket(p, fire_offset(p.delay_low, p.delay_span, ov_draw(p, K_OVDELAY, gv, 0, j)));
+  }
 };
 
 struct OutSource {  // events emitted by a processing block (a compact list)
@@ -114,6 +123,7 @@ struct OutSource {  // events emitted by a processing block (a compact list)
     key = out[i];
     slot = oslot[i];
   }
+  __device__ __forceinline__ uint32_t bucket_of(uint64_t i) const { return oslot[i]; }
 };
 
 // COUNT: counts[s] += items bound for bucket s.  WRITE: append them to bucket s.
@@ -133,7 +143,10 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(Src src, uint64_t nit
   for (uint32_t k = 0; k < kScatterIPT; ++k) {
     const uint64_t i = base + (uint64_t)k * kScatterBlock + threadIdx.x;
     slot[k] = 0xFFFFu;
-    if (i < nitems) src.get(i, key[k], slot[k]);
+    if (i < nitems) {
+      if (WRITE) src.get(i, key[k], slot[k]);
+      else slot[k] = src.bucket_of(i);
+    }
     if (slot[k] != 0xFFFFu) rank[k] = atomicAdd(&s_hist[slot[k]], 1u);
   }
   __syncthreads();
