@@ -170,6 +170,7 @@ struct gs_ctx {
   WinCtl* dd_ctl = nullptr;
   void** dd_ptrs = nullptr;
   void** h_ddptrs = nullptr;            // pinned staging of dd_ptrs
+  WinState* dd_wsm = nullptr;           // in-process group: the members' window states [3][M] (WinGroup)
   unsigned long long* h_ddlay = nullptr;
 };
 
@@ -2093,7 +2094,7 @@ int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing, uint64_t tchunk
     plan_coarse(c, T, nullptr);
     const uint64_t fcap = T + T / 8 + (uint64_t)w.ncoarse * 256 * 513 + 16;
     if (!grow(c->gmap, ((Tn + 63) / 64 + 1) * 4) || !grow(c->cmsg, (c->h_cap[kRegions] + 16) * 4) ||
-        !grow(c->fmsg, fcap * 4))
+        !grow(c->fmsg, (fcap + 16) * 4))  // buf_cap(fmsg) >= fcap (the device-driven windows' bound)
       return fail(c, GS_ENOMEM, "cannot allocate " + std::to_string(T) + " window messages");
     w.gmap = (uint32_t*)c->gmap.p;
     w.cmsg = (uint32_t*)c->cmsg.p;
@@ -2722,7 +2723,9 @@ int shard_receive(gs_ctx* m, const ShardWin& sw, bool timing) {
   CK(m, hipSetDevice(m->dev));
   const uint64_t R = m->rtotal;
   const uint64_t fcap = R + R / 8 + (uint64_t)wr.ncoarse * 256 * 513 + 16;
-  if (!grow(m->fmsg, fcap * 4))  // nothing resolved: every rank stops at the next gather
+  // (+16: buf_cap's slack -- k_rtab checks the next device-driven window's
+  // bound against buf_cap, so a buffer grown to exactly fcap aborted it)
+  if (!grow(m->fmsg, (fcap + 16) * 4))  // nothing resolved: every rank stops at the next gather
     return mark_nomem(m, "cannot allocate " + std::to_string(R) + " received messages");
   wr.fmsg = m->ws.fmsg = (uint32_t*)m->fmsg.p;
   if (timing) CK(m, hipEventRecord(m->ev[4], m->stream));
@@ -2952,6 +2955,12 @@ bool dd_ok(const gs_ctx* acc, const std::vector<gs_ctx*>& ms) {
   return is_rank(acc);
 }
 
+// GS_WINLOG=1: one stderr line per device-driven shard window (and its aborts)
+bool dd_log() {
+  static const bool on = getenv("GS_WINLOG") != nullptr;
+  return on;
+}
+
 int dd_setup(gs_ctx* acc, const std::vector<gs_ctx*>& ms) {
   gs_ctx* m0 = ms[0];
   const uint32_t G = m0->G, M = (uint32_t)ms.size();
@@ -2960,14 +2969,15 @@ int dd_setup(gs_ctx* acc, const std::vector<gs_ctx*>& ms) {
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t b1 = al((size_t)G * kMaxWindow * 8), b2 = al((size_t)G * kDDRow * 8),
                  b3 = al((size_t)M * kDDWStat * 8), b4 = al((size_t)M * sizeof(WinCtl)),
-                 b5 = al((size_t)(4 * M + 2) * sizeof(void*));
-    CK(acc, hipMalloc(&acc->dd_mem, b1 + b2 + b3 + b4 + b5));
+                 b5 = al((size_t)(4 * M + 2) * sizeof(void*)), b6 = al((size_t)3 * M * sizeof(WinState));
+    CK(acc, hipMalloc(&acc->dd_mem, b1 + b2 + b3 + b4 + b5 + b6));
     char* q = (char*)acc->dd_mem;
     acc->dd_gcnt = (unsigned long long*)q; q += b1;
     acc->dd_glay = (unsigned long long*)q; q += b2;
     acc->dd_wstat = (unsigned long long*)q; q += b3;
     acc->dd_ctl = (WinCtl*)q; q += b4;
-    acc->dd_ptrs = (void**)q;
+    acc->dd_ptrs = (void**)q; q += b5;
+    acc->dd_wsm = (WinState*)q;
     CK(acc, hipHostMalloc((void**)&acc->h_ddptrs, (size_t)(4 * M + 2) * sizeof(void*)));
     if (is_rank(acc) && G > 1) CK(acc, hipHostMalloc((void**)&acc->h_ddlay, (size_t)G * kDDRow * 8));
   }
@@ -3106,6 +3116,31 @@ int dd_run(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t tend, uint32_t 
     tn_bound[i] = std::min<uint64_t>(m->ntot + 1, 4096ull * 1024);
   }
   const uint64_t T_bound = 2048ull * 16384;
+  // an in-process group launches each small per-shard kernel once for all its
+  // shards (WinGroup; GS_DD_GROUP=0: one launch per shard, the A/B baseline)
+  static const bool group_env = [] { const char* e = getenv("GS_DD_GROUP"); return !(e && atoi(e) == 0); }();
+  const bool grouped = !rank && M > 1 && group_env;
+  std::vector<WinState> wall;
+  WinGroup grp{};
+  if (grouped) {
+    wall.reserve(3 * M);
+    wall.insert(wall.end(), ws.begin(), ws.end());
+    wall.insert(wall.end(), wr.begin(), wr.end());
+    for (uint32_t i = 0; i < M; ++i) {
+      wall.push_back(wr[i]);
+      wall.back().guard = 1;
+    }
+    CK(acc, hipMemcpyAsync(acc->dd_wsm, wall.data(), wall.size() * sizeof(WinState), hipMemcpyHostToDevice, st));
+    grp.ws = acc->dd_wsm;
+    grp.wr = acc->dd_wsm + M;
+    grp.wg = acc->dd_wsm + 2 * M;
+    grp.M = M;
+    for (uint32_t i = 0; i < M; ++i) {
+      grp.nfine_max = std::max(grp.nfine_max, ws[i].nfine);
+      grp.ncoarse_max = std::max(grp.ncoarse_max, ws[i].ncoarse);
+      grp.slots_max = std::max(grp.slots_max, ws[i].slots);
+    }
+  }
   // ranks whose blocks travel: the block sizes, from the gathered rows
   auto bsize = [&](uint32_t s, uint32_t d) {
     unsigned long long a = 0;
@@ -3116,13 +3151,22 @@ int dd_run(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t tend, uint32_t 
   // exchange (the window is dead: stopped, or aborted -> *aborted)
   auto enqueue = [&](uint32_t slot, bool* aborted) -> int {
     *aborted = false;
-    for (uint32_t i = 0; i < M; ++i) CK(acc, win_units(ws[i], 0, Lmax, st));
-    if (rank) RC(x_all_gather(m0, acc->dd_gcnt, kMaxWindow * 8));
-    for (uint32_t i = 0; i < M; ++i) CK(acc, win_cut(ws[i], budget, st));
-    for (uint32_t i = 0; i < M; ++i) CK(acc, win_unitscan(ws[i], st));
-    for (uint32_t i = 0; i < M; ++i) CK(acc, win_expand(ws[i], 0, Lmax, tn_bound[i], 1, st));
+    if (grouped) {
+      CK(acc, win_units_g(grp, Lmax, st));
+      CK(acc, win_cut_g(grp, budget, st));
+      CK(acc, win_unitscan_g(grp, st));
+    } else {
+      for (uint32_t i = 0; i < M; ++i) CK(acc, win_units(ws[i], 0, Lmax, st));
+      if (rank) RC(x_all_gather(m0, acc->dd_gcnt, kMaxWindow * 8));
+      for (uint32_t i = 0; i < M; ++i) CK(acc, win_cut(ws[i], budget, st));
+      for (uint32_t i = 0; i < M; ++i) CK(acc, win_unitscan(ws[i], st));
+    }
+    if (grouped) CK(acc, win_expand_g(grp, Lmax, st));
+    for (uint32_t i = 0; i < M && !grouped; ++i) CK(acc, win_expand(ws[i], 0, Lmax, tn_bound[i], 1, st));
     if (rank) RC(x_all_gather(m0, acc->dd_glay, kDDRow * 8));
-    for (uint32_t i = 0; i < M && !solo; ++i)
+    if (grouped)
+      CK(acc, win_rtab_g(grp, (const unsigned long long* const*)d_ccaps, (const uint32_t* const*)d_src, nsrc, st));
+    for (uint32_t i = 0; i < M && !solo && !grouped; ++i)
       CK(acc, win_rtab(ws[i], ms[i]->d_rtab, (const unsigned long long* const*)d_ccaps, (const uint32_t* const*)d_src,
                        nsrc, rank ? 1u : 0u, st));
     if (travel) {
@@ -3212,12 +3256,18 @@ int dd_run(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t tend, uint32_t 
         CK(acc, hipStreamSynchronize(st));
       }
     }
-    for (uint32_t i = 0; i < M; ++i) {
-      CK(acc, win_plan(wr[i], false, st));
-      CK(acc, win_part2(wr[i], T_bound, true, st));
-      if (!solo) CK(acc, win_fine_redo(wr[i], T_bound, st));
-      CK(acc, win_resolve(wr[i], 0, Lmax, st));
-      CK(acc, win_stats_dd(ws[i], slot, st));
+    if (grouped) {
+      CK(acc, win_recv_g(grp, T_bound, st));
+      CK(acc, win_resolve_g(grp, Lmax, st));
+      CK(acc, win_stats_dd_g(grp, slot, st));
+    } else {
+      for (uint32_t i = 0; i < M; ++i) {
+        CK(acc, win_plan(wr[i], false, st));
+        CK(acc, win_part2(wr[i], T_bound, true, st));
+        if (!solo) CK(acc, win_fine_redo(wr[i], T_bound, st));
+        CK(acc, win_resolve(wr[i], 0, Lmax, st));
+        CK(acc, win_stats_dd(ws[i], slot, st));
+      }
     }
     if (rank) RC(x_all_reduce(m0, acc->dd_wstat, kDDWStat));
     if (!solo)  // (one in-process shard: k_stats_dd closed the window)
@@ -3233,10 +3283,12 @@ int dd_run(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t tend, uint32_t 
     const uint32_t t0 = (uint32_t)sg[0], L = (uint32_t)sg[1];
     *what = 0;
     if (sg[3] & kErrAbort) {
+      if (dd_log()) fprintf(stderr, "[dd] window at t0=%u aborted: redone host-driven\n", t0);
       *fallback = true;
       *what = 1;
       return GS_OK;
     }
+    if (dd_log()) fprintf(stderr, "[dd] t0=%u L=%u stop=%llu redos=%llu\n", t0, L, sg[2], sg[4]);
     m0->timing.exact_redos += sg[4];
     for (uint32_t k = 0; k < L; ++k) on_tick((uint64_t)t0 + k, sg + 8 + (size_t)k * kStatFields);
     if (sg[3] & kErrArrivals) eoverflow = true;
@@ -3268,6 +3320,15 @@ int dd_run(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t tend, uint32_t 
       CK(acc, hipMemsetAsync(m->ws.sstats, 0, (size_t)kStatShards * kMaxWindow * kStatFields * 8, st));
       CK(acc, hipMemcpyAsync(m->h_err, m->d_err, 4, hipMemcpyDeviceToHost, st));
       CK(acc, hipStreamSynchronize(st));
+      if (dd_log()) {  // the window's cut and coarse plan (plan 0: k_cut found the buffer too small)
+        const size_t i = (size_t)(std::find(ms.begin(), ms.end(), m) - ms.begin());
+        WinCtl h1{};
+        unsigned long long plan = 0;
+        CK(acc, hipMemcpy(&h1, acc->dd_ctl + i, sizeof(WinCtl), hipMemcpyDeviceToHost));
+        CK(acc, hipMemcpy(&plan, m->ws.ccap + kRegions, 8, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[dd] shard %u flags %#x t=%u L=%u Tn=%llu T=%llu cmsg_cap=%llu plan=%llu\n", m->rank,
+                *m->h_err, h1.t, h1.L, h1.Tn, h1.T, h1.cmsg_cap, plan);
+      }
       *m->h_err &= ~(kErrCoarse | kErrFine | kErrAbort);
       CK(acc, hipMemcpyAsync(m->d_err, m->h_err, 4, hipMemcpyHostToDevice, st));
     }

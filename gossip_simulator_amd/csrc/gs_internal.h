@@ -271,6 +271,31 @@ hipError_t win_rtab(const WinState& w, unsigned long long* rtab, const unsigned 
                     const uint32_t* const* src, uint32_t nsrc, uint32_t travels, hipStream_t s);
 hipError_t win_fine_redo(const WinState& w, uint64_t T, hipStream_t s);
 hipError_t win_stats_dd(const WinState& w, uint32_t slot, hipStream_t s);  // w.solo: also closes
+// The M device-driven shard windows of an in-process group (one device): each
+// small per-shard kernel is one launch for all M (the window states in device
+// memory: send side ws, receive side wr, wr with guard = 1 for the fine redo)
+struct WinGroup {
+  const WinState* ws;
+  const WinState* wr;
+  const WinState* wg;
+  uint32_t M;
+  uint32_t nfine_max;
+  uint32_t ncoarse_max;
+  uint32_t slots_max;  // the longest row (k_expand's variant)
+};
+hipError_t win_units_g(const WinGroup& g, uint32_t L, hipStream_t s);
+hipError_t win_cut_g(const WinGroup& g, unsigned long long budget, hipStream_t s);
+hipError_t win_unitscan_g(const WinGroup& g, hipStream_t s);
+hipError_t win_rtab_g(const WinGroup& g, const unsigned long long* const* ccaps, const uint32_t* const* src,
+                      uint32_t nsrc, hipStream_t s);
+// k_plan + k_part2 scatter of every shard's receive side, then the guarded
+// exact fine redo (win_fine_redo)
+hipError_t win_recv_g(const WinGroup& g, uint64_t T, hipStream_t s);
+hipError_t win_stats_dd_g(const WinGroup& g, uint32_t slot, hipStream_t s);
+// k_expand (mode 1: write + per-tick stats) and the resolve of every shard,
+// each shard on a 1/M slice of the persistent grid
+hipError_t win_expand_g(const WinGroup& g, uint32_t L, hipStream_t s);
+hipError_t win_resolve_g(const WinGroup& g, uint32_t L, hipStream_t s);
 hipError_t win_close_dd(const WinState& w, const unsigned long long* const* wstats, WinCtl* const* ctls,
                         uint32_t n, uint32_t slot, hipStream_t s);
 // Copies the first min(cfill[r], room) messages of every region r < nreg from

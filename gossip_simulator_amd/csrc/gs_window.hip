@@ -137,7 +137,7 @@ __device__ __forceinline__ unsigned long long block_exscan256_u64(unsigned long 
 // the window share are fetched once into the XCD's L2.  usize = fires;
 // tfires[k] = fires per tick (the window cut).  Also zeroes the window's
 // counters (one launch instead of several memsets).
-__global__ __launch_bounds__(256) void k_units(const WinState w, uint32_t t0, uint32_t L) {
+__device__ __forceinline__ void units_body(const WinState& w, uint32_t t0, uint32_t L) {
   __shared__ uint32_t s_t[kMaxWindow];
   uint32_t Ls = L;
   if (w.ctl) {
@@ -210,12 +210,20 @@ __global__ __launch_bounds__(256) void k_units(const WinState w, uint32_t t0, ui
   // windows keep them until the host has redone the window
   if (tid == 0 && !w.ctl && !w.abort_on_err) *w.err &= ~(kErrCoarse | kErrFine);
 }
+__global__ __launch_bounds__(256) void k_units(const WinState w, uint32_t t0, uint32_t L) { units_body(w, t0, L); }
+
+// The device-driven shard windows of an in-process group launch each small
+// per-shard kernel once for all M shards: shard blockIdx.y (or blockIdx.x for
+// the one-block kernels) reads its window state from a device array.
+__global__ __launch_bounds__(256) void k_units_m(const WinState* __restrict__ ws, uint32_t t0, uint32_t L) {
+  units_body(ws[blockIdx.y], t0, L);
+}
 
 // Device-driven windows: the cut (as the host-driven engine makes it: a
 // window holds whole ticks while its friend slots fit `budget`), the coarse
 // region plan of the window's T friend slots, and the window's place in ctl.
 // One block.
-__global__ __launch_bounds__(256) void k_cut(const WinState w, unsigned long long budget) {
+__device__ __forceinline__ void cut_body(const WinState& w, unsigned long long budget) {
   __shared__ unsigned long long s_sz[256];
   __shared__ unsigned long long s_T;
   __shared__ uint32_t s_go, s_L;
@@ -330,13 +338,18 @@ __global__ __launch_bounds__(256) void k_cut(const WinState w, unsigned long lon
   for (uint32_t x = 0; x < kCoarseSub; ++x) w.ccap[b * kCoarseSub + x] = base + x * sub;
   if (b == 255) w.ccap[kRegions] = total;
 }
+__global__ __launch_bounds__(256) void k_cut(const WinState w, unsigned long long budget) { cut_body(w, budget); }
+__global__ __launch_bounds__(256) void k_cut_m(const WinState* __restrict__ ws, unsigned long long budget) {
+  cut_body(ws[blockIdx.x], budget);
+}
 
 // Device-driven windows: the unit scan inside each 256-bucket tile (thread =
 // bucket, its Ls units contiguous; ticks >= L count as empty), offset by the
 // tile's start from k_cut, and the group map of those units.  One block per
 // tile.  (Host-driven windows: hipcub scan + k_groupmap.)
-__global__ __launch_bounds__(256) void k_unitscan(const WinState w) {
+__device__ __forceinline__ void unitscan_body(const WinState& w) {
   __shared__ unsigned long long s_x[4];
+  if (blockIdx.x >= w.ncoarse) return;  // shards of a group: the grid covers the largest
   uint32_t t0;
   const uint32_t L = win_live(w, t0, 0);
   if (!L) return;
@@ -364,6 +377,8 @@ __global__ __launch_bounds__(256) void k_unitscan(const WinState w) {
   }
   if (f == w.nfine - 1) w.unit_off[(size_t)w.nfine * Ls] = a;
 }
+__global__ __launch_bounds__(256) void k_unitscan(const WinState w) { unitscan_body(w); }
+__global__ __launch_bounds__(256) void k_unitscan_m(const WinState* __restrict__ ws) { unitscan_body(ws[blockIdx.y]); }
 
 // gmap[q] = unit holding firing index 64*q.
 __global__ void k_groupmap(const WinState w, uint32_t L) {
@@ -658,9 +673,9 @@ __device__ __forceinline__ void xcd_rounds(unsigned long long rounds, unsigned l
   }
 }
 
-template <bool WRITE, uint32_t MAXS, uint32_t NPT, uint32_t B = kExpandBlock>
-__global__ __launch_bounds__(B) void k_expand(const WinState w, uint32_t t0, uint32_t L,
-                                              unsigned long long Tn, int add_stats) {
+template <bool WRITE, uint32_t MAXS, uint32_t NPT, uint32_t B>
+__device__ __forceinline__ void expand_body(const WinState& w, uint32_t t0, uint32_t L, unsigned long long Tn,
+                                            int add_stats) {
   __shared__ ExpandLds<B * NPT * MAXS> sm;
   const uint32_t tid = threadIdx.x;
   uint32_t Ls = L;  // unit layout stride
@@ -830,6 +845,17 @@ __global__ __launch_bounds__(B) void k_expand(const WinState w, uint32_t t0, uin
     if (v && fld) atomicAdd(&row[ST_MSGS], v);
   }
 }
+template <bool WRITE, uint32_t MAXS, uint32_t NPT, uint32_t B = kExpandBlock>
+__global__ __launch_bounds__(B) void k_expand(const WinState w, uint32_t t0, uint32_t L, unsigned long long Tn,
+                                              int add_stats) {
+  expand_body<WRITE, MAXS, NPT, B>(w, t0, L, Tn, add_stats);
+}
+// the shards of an in-process group (device-driven: each reads its Tn from its
+// control block), a slice of the persistent grid each
+template <bool WRITE, uint32_t MAXS, uint32_t NPT, uint32_t B = kExpandBlock>
+__global__ __launch_bounds__(B) void k_expand_m(const WinState* __restrict__ ws, uint32_t L, int add_stats) {
+  expand_body<WRITE, MAXS, NPT, B>(ws[blockIdx.y], 0u, L, 0ull, add_stats);
+}
 
 // The packed view of sealed stride-8 rows (pk_byte): slots 0..5 of row v.
 __global__ void k_pack_rows(const uint32_t* ids, uint64_t n, uint32_t* pk) {
@@ -875,7 +901,7 @@ __device__ __forceinline__ uint32_t xcd_bin_of(uint32_t pc) { return (pc & 31) *
 
 // Fine regions inside each coarse region: capacity per fine bucket of coarse
 // c = cfill[c]*1.15/256 + 512 (fast path), or exact counts (fhist != null).
-__global__ void k_plan(const WinState w, bool exact) {
+__device__ __forceinline__ void plan_body(const WinState& w, bool exact) {
   __shared__ unsigned long long s_base[257];
   __shared__ unsigned long long s_cap[256];
   __shared__ uint32_t s_tp[257];
@@ -961,6 +987,8 @@ __global__ void k_plan(const WinState w, bool exact) {
     w.fstart[f] = x < cap ? x : cap;
   }
 }
+__global__ void k_plan(const WinState w, bool exact) { plan_body(w, exact); }
+__global__ void k_plan_m(const WinState* __restrict__ ws, bool exact) { plan_body(ws[blockIdx.y], exact); }
 
 // LDS counting sort of one tile by an 8-bit digit, then coalesced runs out.
 #ifndef GS_PART_BLOCK
@@ -983,7 +1011,7 @@ struct TileSort {
 // part2: coarse tiles -> fine regions; message = u_in_fine | k << 14.
 // SCATTER=false counts per fine bucket (exact fallback).
 template <bool SCATTER>
-__global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_part2(const WinState w) {
+__device__ __forceinline__ void part2_body(const WinState& w) {
   __shared__ TileSort ts;
   __shared__ uint32_t s_tp[kRegions + 1];
   const uint32_t tid = threadIdx.x;
@@ -1090,6 +1118,15 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8
     }
     __syncthreads();
   }
+}
+template <bool SCATTER>
+__global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_part2(const WinState w) {
+  part2_body<SCATTER>(w);
+}
+template <bool SCATTER>
+__global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_part2_m(
+    const WinState* __restrict__ ws) {
+  part2_body<SCATTER>(ws[blockIdx.y]);
 }
 
 constexpr uint32_t kResolveMaxBuckets = 256;  // buckets one persistent workgroup may own
@@ -1295,7 +1332,7 @@ __device__ __forceinline__ void flush_counts(const WinState& w, ResolveLds& sm, 
 //            (node, tick) groups in order (rule A6, first_crash); the
 //            infections are Broadcast() (:122, :141)
 // A bucket with more rolled receipts than kRolledCap takes the per-tick large path.
-__global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
+__device__ __forceinline__ void resolve_body(const WinState& w, uint32_t t0, uint32_t L) {
   __shared__ ResolveLds sm;
   const uint32_t tid = threadIdx.x, G = gridDim.x;
   L = win_live(w, t0, L);
@@ -1555,6 +1592,13 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(con
   if (w.dbg && tid < 2 * kStampPhases) atomicAdd(&w.dbg[tid], (&sm.stamp[0][0])[tid]);
   if (!w.tstat) flush_counts(w, sm, acc_ni, L, ~0u);
 }
+__global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve(const WinState w, uint32_t t0, uint32_t L) {
+  resolve_body(w, t0, L);
+}
+__global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve_m(const WinState* __restrict__ ws,
+                                                                                uint32_t L) {
+  resolve_body(ws[blockIdx.y], 0u, L);
+}
 
 // Small buckets (1..kSmallMax receipts in the window): one wave per bucket.
 // In the sparse windows at the start and end of a broadcast nearly every
@@ -1582,8 +1626,7 @@ __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t
 // One launch for all sizes: each wave takes one bucket and the body by its
 // receipt count (wave-uniform).
 template <bool ROLLED>
-__global__ __launch_bounds__(ROLLED ? kRolledBlock : kSmallBlock) void k_resolve_small(const WinState w, uint32_t t0,
-                                                                                       uint32_t L) {
+__device__ __forceinline__ void resolve_small_body(const WinState& w, uint32_t t0, uint32_t L) {
   constexpr uint32_t kWaves = (ROLLED ? kRolledBlock : kSmallBlock) / 64;
   constexpr uint32_t kEmax = ROLLED ? 16 : 4;
   __shared__ uint32_t st[kWaves][kMaxWindow][4];  // per wave: dead (not counted), recv, crash per tick
@@ -1635,6 +1678,16 @@ __global__ __launch_bounds__(ROLLED ? kRolledBlock : kSmallBlock) void k_resolve
     }
     if (v && fld == 2) atomicAdd(&row[ST_CRASH], (unsigned long long)v);
   }
+}
+template <bool ROLLED>
+__global__ __launch_bounds__(ROLLED ? kRolledBlock : kSmallBlock) void k_resolve_small(const WinState w, uint32_t t0,
+                                                                                       uint32_t L) {
+  resolve_small_body<ROLLED>(w, t0, L);
+}
+template <bool ROLLED>
+__global__ __launch_bounds__(ROLLED ? kRolledBlock : kSmallBlock) void k_resolve_small_m(
+    const WinState* __restrict__ ws, uint32_t L) {
+  resolve_small_body<ROLLED>(ws[blockIdx.y], 0u, L);
 }
 
 template <uint32_t E, bool ROLLED>
@@ -1884,9 +1937,9 @@ __device__ __forceinline__ unsigned long long block_exscan_u64(unsigned long lon
 // buffer holds, every shard sets kErrAbort (the same decision everywhere,
 // from the same gathered rows) and the host redoes the window host-driven.
 // One block of 256 threads.
-__global__ __launch_bounds__(256) void k_rtab(const WinState w, unsigned long long* rtab,
-                                              const unsigned long long* const* ccaps, const uint32_t* const* src,
-                                              uint32_t nsrc, uint32_t travels) {
+__device__ __forceinline__ void rtab_body(const WinState& w, unsigned long long* rtab,
+                                          const unsigned long long* const* ccaps, const uint32_t* const* src,
+                                          uint32_t nsrc, uint32_t travels) {
   __shared__ unsigned long long s_x[4];
   __shared__ unsigned long long s_R[256];
   __shared__ uint32_t s_abort;
@@ -1985,13 +2038,24 @@ __global__ __launch_bounds__(256) void k_rtab(const WinState w, unsigned long lo
   if (tid < nsrc) rtab[4 * K1 + tid] = (unsigned long long)(uintptr_t)src[tid];
   if (tid == 0) rtab[kRtabTotal] = tot;
 }
+__global__ __launch_bounds__(256) void k_rtab(const WinState w, unsigned long long* rtab,
+                                              const unsigned long long* const* ccaps, const uint32_t* const* src,
+                                              uint32_t nsrc, uint32_t travels) {
+  rtab_body(w, rtab, ccaps, src, nsrc, travels);
+}
+// shard blockIdx.x's layout goes to its receive state's region table (wr.ccap)
+__global__ __launch_bounds__(256) void k_rtab_m(const WinState* __restrict__ ws, const WinState* __restrict__ wr,
+                                                const unsigned long long* const* ccaps, const uint32_t* const* src,
+                                                uint32_t nsrc) {
+  rtab_body(ws[blockIdx.x], const_cast<unsigned long long*>(wr[blockIdx.x].ccap), ccaps, src, nsrc, 0u);
+}
 
 // The exact fine re-partition of a device-driven shard window whose fine
 // regions overflowed their estimates (kErrFine): the counts cleared (here),
 // k_plan's tile prefix, k_part2's counting pass, the scan into fstart
 // (k_fine_scan), k_part2's scatter.  Guarded launches (w.guard): they do
 // nothing unless the shard's kErrFine is set; k_stats_dd clears it.
-__global__ void k_fine_zero(const WinState w) {
+__device__ __forceinline__ void fine_zero_body(const WinState& w) {
   uint32_t t0;
   if (!win_live(w, t0, 0)) return;
   const uint32_t nh = w.ncoarse * 256 + 1;
@@ -2000,8 +2064,10 @@ __global__ void k_fine_zero(const WinState w) {
     if (i < w.nfine) w.ffill[i] = 0;
   }
 }
+__global__ void k_fine_zero(const WinState w) { fine_zero_body(w); }
+__global__ void k_fine_zero_m(const WinState* __restrict__ ws) { fine_zero_body(ws[blockIdx.y]); }
 
-__global__ __launch_bounds__(1024) void k_fine_scan(const WinState w) {
+__device__ __forceinline__ void fine_scan_body(const WinState& w) {
   __shared__ unsigned long long s_x[16];
   uint32_t t0;
   if (!win_live(w, t0, 0)) return;
@@ -2021,6 +2087,10 @@ __global__ __launch_bounds__(1024) void k_fine_scan(const WinState w) {
     if (i < w.nfine) w.ffill[i] = 0;
   }
 }
+__global__ __launch_bounds__(1024) void k_fine_scan(const WinState w) { fine_scan_body(w); }
+__global__ __launch_bounds__(1024) void k_fine_scan_m(const WinState* __restrict__ ws) {
+  fine_scan_body(ws[blockIdx.x]);
+}
 
 // The window's counters of this shard (its stat shards summed into w.wstat,
 // zero rows past the window or in a stopped one) and its flags: kErrArrivals,
@@ -2030,7 +2100,7 @@ __global__ __launch_bounds__(1024) void k_fine_scan(const WinState w) {
 // kMaxWindow * kStatFields * kCloseLanes threads.
 __device__ void close_rows(const WinState& w, const unsigned long long* rows, WinCtl* const* ctls, uint32_t n,
                            uint32_t slot);
-__global__ void k_stats_dd(const WinState w, uint32_t slot) {
+__device__ __forceinline__ void stats_dd_body(const WinState& w, uint32_t slot) {
   __shared__ unsigned long long rows[kDDWStat];  // w.solo: closed here (no k_close_dd)
   const uint32_t tid = threadIdx.x;
   const CtlView c = ctl_view(w);
@@ -2058,6 +2128,8 @@ __global__ void k_stats_dd(const WinState w, uint32_t slot) {
   WinCtl* const one[1] = {w.ctl};
   close_rows(w, rows, one, 1, slot);
 }
+__global__ void k_stats_dd(const WinState w, uint32_t slot) { stats_dd_body(w, slot); }
+__global__ void k_stats_dd_m(const WinState* __restrict__ ws, uint32_t slot) { stats_dd_body(ws[blockIdx.x], slot); }
 
 // The close of a device-driven shard window from its summed counter rows
 // (F = kMaxWindow * kStatFields counters, then the flags): gs_run's poll rule
@@ -2148,6 +2220,49 @@ hipError_t win_stats_dd(const WinState& w, uint32_t slot, hipStream_t s) {
 hipError_t win_close_dd(const WinState& w, const unsigned long long* const* wstats, WinCtl* const* ctls,
                         uint32_t n, uint32_t slot, hipStream_t s) {
   hipLaunchKernelGGL(k_close_dd, dim3(1), dim3(128), 0, s, w, wstats, ctls, n, slot);
+  return hipGetLastError();
+}
+
+hipError_t win_units_g(const WinGroup& g, uint32_t L, hipStream_t s) {
+  const uint32_t blocks = std::max<uint32_t>(std::min<uint32_t>((g.nfine_max + 255) / 256, 4096), 1);
+  hipLaunchKernelGGL(k_units_m, dim3(blocks, g.M), dim3(256), 0, s, g.ws, 0u, L);
+  return hipGetLastError();
+}
+
+hipError_t win_cut_g(const WinGroup& g, unsigned long long budget, hipStream_t s) {
+  hipLaunchKernelGGL(k_cut_m, dim3(g.M), dim3(256), 0, s, g.ws, budget);
+  return hipGetLastError();
+}
+
+hipError_t win_unitscan_g(const WinGroup& g, hipStream_t s) {
+  hipLaunchKernelGGL(k_unitscan_m, dim3(std::max<uint32_t>(g.ncoarse_max, 1), g.M), dim3(256), 0, s, g.ws);
+  return hipGetLastError();
+}
+
+hipError_t win_rtab_g(const WinGroup& g, const unsigned long long* const* ccaps, const uint32_t* const* src,
+                      uint32_t nsrc, hipStream_t s) {
+  hipLaunchKernelGGL(k_rtab_m, dim3(g.M), dim3(256), 0, s, g.ws, g.wr, ccaps, src, nsrc);
+  return hipGetLastError();
+}
+
+hipError_t win_recv_g(const WinGroup& g, uint64_t T, hipStream_t s) {
+  const uint32_t pblocks = std::min<uint32_t>((g.nfine_max + 1 + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_plan_m, dim3(pblocks, g.M), dim3(256), 0, s, g.wr, false);
+  const uint64_t tiles = (T + kPartTile - 1) / kPartTile + 256;
+  const uint32_t blocks = (uint32_t)(std::min<uint64_t>(tiles, 8192) + 7) & ~7u;
+  hipLaunchKernelGGL(k_part2_m<true>, dim3(blocks, g.M), dim3(kPartBlock), 0, s, g.wr);
+  // the guarded exact redo (win_fine_redo): each launch leaves at once unless
+  // its shard's fine regions overflowed
+  hipLaunchKernelGGL(k_fine_zero_m, dim3(64, g.M), dim3(256), 0, s, g.wg);
+  hipLaunchKernelGGL(k_plan_m, dim3(1, g.M), dim3(256), 0, s, g.wg, true);
+  hipLaunchKernelGGL(k_part2_m<false>, dim3(512, g.M), dim3(kPartBlock), 0, s, g.wg);
+  hipLaunchKernelGGL(k_fine_scan_m, dim3(g.M), dim3(1024), 0, s, g.wg);
+  hipLaunchKernelGGL(k_part2_m<true>, dim3(512, g.M), dim3(kPartBlock), 0, s, g.wg);
+  return hipGetLastError();
+}
+
+hipError_t win_stats_dd_g(const WinGroup& g, uint32_t slot, hipStream_t s) {
+  hipLaunchKernelGGL(k_stats_dd_m, dim3(g.M), dim3(kMaxWindow * kStatFields * kCloseLanes), 0, s, g.ws, slot);
   return hipGetLastError();
 }
 
@@ -2251,6 +2366,29 @@ hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, i
   return hipGetLastError();
 }
 
+hipError_t win_expand_g(const WinGroup& g, uint32_t L, hipStream_t s) {
+  static const uint32_t cus = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      return (uint32_t)v;
+    return 256u;
+  }();
+  const uint32_t rs = g.slots_max;
+  // win_expand's persistent grid (rows <= 8: four 256-thread workgroups per
+  // CU, or two of 512 for rows <= 6) split over the shards, a multiple of 8
+  // per shard (blockIdx.x & 7 is the XCD); longer rows: 8192 per shard
+  const uint32_t bsz = rs <= 6 ? 512u : kExpandBlock;
+  const uint32_t total = rs <= 8 ? cus * 4 * kExpandBlock / bsz : 8192u * g.M;
+  const uint32_t bx = std::max<uint32_t>(8, ((total + g.M - 1) / g.M + 7) & ~7u);
+  const dim3 grid(bx, g.M);
+  if (rs <= 6) hipLaunchKernelGGL((k_expand_m<true, 6, kExpandNpt, 512>), grid, dim3(512), 0, s, g.ws, L, 1);
+  else if (rs <= 8) hipLaunchKernelGGL((k_expand_m<true, 8, kExpandNpt>), grid, dim3(kExpandBlock), 0, s, g.ws, L, 1);
+  else if (rs <= 20) hipLaunchKernelGGL((k_expand_m<true, 20, 1>), grid, dim3(kExpandBlock), 0, s, g.ws, L, 1);
+  else hipLaunchKernelGGL((k_expand_m<true, kWinMaxStride, 1>), grid, dim3(kExpandBlock), 0, s, g.ws, L, 1);
+  return hipGetLastError();
+}
+
 hipError_t win_pack_rows(const uint32_t* ids, uint64_t n, uint32_t* pk, hipStream_t s) {
   const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
   hipLaunchKernelGGL(k_pack_rows, dim3((uint32_t)(blocks ? blocks : 1)), dim3(256), 0, s, ids, n, pk);
@@ -2303,6 +2441,26 @@ hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s
   // k_resolve_rolled: small blocks (the E = 16 key arrays take 4 KB per wave; blocks finish independently)
   hipLaunchKernelGGL(k_resolve_small<true>, dim3((w.nfine + kRolledBlock / 64 - 1) / (kRolledBlock / 64)),
                      dim3(kRolledBlock), 0, s, w, t0, L);
+  return hipGetLastError();
+}
+
+hipError_t win_resolve_g(const WinGroup& g, uint32_t L, hipStream_t s) {
+  static const uint32_t cus = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      return (uint32_t)v;
+    return 256u;
+  }();
+  // k_resolve's two workgroups per CU split over the shards (each still owns
+  // <= kResolveMaxBuckets buckets of its shard)
+  uint32_t G = std::min<uint32_t>(g.nfine_max, (2 * cus + g.M - 1) / g.M);
+  G = std::max<uint32_t>(G, (g.nfine_max + kResolveMaxBuckets - 1) / kResolveMaxBuckets);
+  const uint32_t gs = (g.nfine_max + kSmallBlock / 64 - 1) / (kSmallBlock / 64);
+  hipLaunchKernelGGL(k_resolve_small_m<false>, dim3(gs, g.M), dim3(kSmallBlock), 0, s, g.wr, L);
+  hipLaunchKernelGGL(k_resolve_m, dim3(G, g.M), dim3(kResolveBlock), 0, s, g.wr, L);
+  hipLaunchKernelGGL(k_resolve_small_m<true>, dim3((g.nfine_max + kRolledBlock / 64 - 1) / (kRolledBlock / 64), g.M),
+                     dim3(kRolledBlock), 0, s, g.wr, L);
   return hipGetLastError();
 }
 
