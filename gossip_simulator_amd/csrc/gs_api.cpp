@@ -1563,6 +1563,12 @@ int pp_prepare(gs_ctx* c) {
   c->sp = PPSparse{};
   static const bool load_deg = [] { const char* e = getenv("GS_PP_NODEG"); return e && atoi(e) == 0; }();  // A/B
   c->sp.nodeg = load_deg ? 0u : 1u;
+  // k_ppb_round's ranges: 2 = a lane per word where few nodes are uninformed
+  // (default), 1 = always, 0 = never (GS_PPB_WORDS, A/B)
+  static const uint32_t words = [] { const char* e = getenv("GS_PPB_WORDS"); return e ? (uint32_t)std::min(std::max(atoi(e), 0), 2) : 2u; }();
+  c->sp.words = words;
+  static const uint32_t maxu = [] { const char* e = getenv("GS_PPB_WORD_MAXU"); return e ? (uint32_t)std::max(atoi(e), 0) : 4u; }();
+  c->sp.word_maxu = maxu;
   if (c->pp_shard) {  // bottom-up rounds only: the partition built the reverse table
     c->sp.ctl = (PPCtl*)c->pp_ctlb.p;
     c->sp.rend = (const unsigned long long*)c->pp_rend.p;

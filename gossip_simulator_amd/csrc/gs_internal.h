@@ -384,6 +384,8 @@ struct PPSparse {
   // bottom-up rounds: an informed caller's degree byte is not loaded when
   // every live node calls and no failed-slot mask is set (GS_PP_NODEG=0: load)
   uint32_t nodeg;
+  uint32_t word_maxu;  // words == 2: a range goes by word if no word holds more live uninformed nodes
+  uint32_t words;  // k_ppb_round with nodeg: 2 a lane per bitset word in ranges with few uninformed nodes, 1 always, 0 never
 };
 constexpr uint32_t kPPDLists = 512;    // = k_ppa_round's grid (kPPSGrid)
 constexpr uint32_t kPPDRegions = 2048; // 256 coarse bins x 8 (XCD) sub-regions

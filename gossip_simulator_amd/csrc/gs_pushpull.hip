@@ -294,11 +294,73 @@ __global__ __launch_bounds__(kPPSBlock) void k_ppb_round(const DevState s, unsig
   // informed caller's push needs only its loss draw (sent = delivered), so
   // its degree byte is not loaded -- in the late rounds, nearly every node's
   const bool nodeg = sp.ctl->nlive0 == 0 && !fmask && sp.nodeg;
+  const uint32_t ppb_words = sp.words;  // GS_PPB_WORDS: 0 a lane per node throughout, 1 a lane per word (A/B)
   for (uint64_t rg = (uint64_t)blockIdx.x * kPPWaves + wv; rg < nrange; rg += (uint64_t)gridDim.x * kPPWaves) {
     const uint64_t w0 = rg * kPPRange, base = w0 << 6;
     nb[lane] = 0;
     uint32_t qn = 0;  // wave-uniform
-    for (uint32_t wi = 0; wi < kPPRange; wi += kPPB) {
+    bool by_word = false;
+    const uint64_t word = w0 + lane;
+    unsigned long long mi = 0, mu = 0;
+    if (nodeg && ppb_words) {
+      if (word < W) {
+        const uint64_t left = s.n - (word << 6);
+        const unsigned long long valid = left >= 64 ? ~0ull : ((1ull << left) - 1);
+        const unsigned long long Iw = s.recv[word], Fw = s.crash[word];
+        mi = Iw & ~Fw & valid;
+        mu = ~Iw & ~Fw & valid;
+      }
+      uint32_t mx = (uint32_t)__popcll(mu);  // the most live uninformed nodes of one word
+#pragma unroll
+      for (uint32_t o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o, 64));
+      by_word = ppb_words == 1 || mx <= sp.word_maxu;
+    }
+    if (by_word) {
+      // a lane per WORD of the range: an informed caller costs its loss draw
+      // and a bit scan, no per-node load, ballot or queue step (the late
+      // rounds, where nearly every caller is informed, are VALU-bound); the
+      // live uninformed nodes of the word (few: sp.word_maxu at most, else the
+      // range takes the lane-per-node loop below) join the queue one per lane
+      // and step
+      fired += (uint64_t)(__popcll(mi) + __popcll(mu));  // nodeg: every live node calls
+      const uint32_t vb = (uint32_t)(s.gbase + (word << 6));
+      uint32_t pushed = 0;
+      while (mi) {
+        const uint32_t b = (uint32_t)__builtin_ctzll(mi);
+        mi &= mi - 1;
+        const u32x4 r = philox(vb + b, t, 0, c3, s.key.k0, s.key.k1);
+        pushed += (int32_t)uniform(r.y, 100u) >= s.kd ? 1u : 0u;
+      }
+      sent += pushed;
+      msgs += pushed;  // no fmask: every push that is not lost is delivered
+      while (__ballot(mu != 0)) {  // wave-uniform trip count
+        const bool has = mu != 0;
+        uint32_t e = 0;
+        if (has) {
+          const uint32_t b = (uint32_t)__builtin_ctzll(mu);
+          mu &= mu - 1;
+          const uint64_t v = (word << 6) + b;
+          e = (uint32_t)(v - base) | (uint32_t)s.deg[v] << 16;
+        }
+        const unsigned long long bal = __ballot(has);
+        if (has) {
+          const uint32_t at = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          q[at] = e;
+        }
+        qn += (uint32_t)__popcll(bal);
+        if (qn >= 64) {
+          wave_lds_sync();
+          ppb_resolve(s, sp, t, c3, q, 64, base, nb, sent, msgs);
+          const uint32_t rest = qn - 64;
+          const uint32_t keep = lane < rest ? q[64 + lane] : 0u;
+          wave_lds_sync();
+          if (lane < rest) q[lane] = keep;
+          qn = rest;
+        }
+      }
+    }
+    for (uint32_t wi = 0; wi < kPPRange && !by_word; wi += kPPB) {
       unsigned long long Iw[kPPB];
       uint32_t d[kPPB], fm[kPPB];
       bool live[kPPB];
@@ -348,7 +410,6 @@ __global__ __launch_bounds__(kPPSBlock) void k_ppb_round(const DevState s, unsig
     wave_lds_sync();
     if (qn) ppb_resolve(s, sp, t, c3, q, qn, base, nb, sent, msgs);
     wave_lds_sync();
-    const uint64_t word = w0 + lane;
     const unsigned long long x = nb[lane];
     if (x && word < W) next[word] = s.recv[word] | x;
     wave_lds_sync();  // nb and q are reused by the next range
