@@ -1559,6 +1559,13 @@ int begin_one(gs_ctx* c, uint64_t s, uint32_t* sched) {
 // once per peer table, the failed-slot mask once per (table, failure mask),
 // the informed list and round control.  GS_FLAG_PP_DENSE, or buffers that do
 // not fit, leave the dense rounds only (same results).
+// The failed-slot mask buffer: fmask bytes [n] (8-aligned), then the fany
+// bitset [ceil(n / 64)] (pp_fmask_any).
+size_t fmask_bytes(uint64_t n) { return ((n + 7) & ~7ull) + ((n + 63) >> 6) * 8; }
+unsigned long long* fmask_any(gs_ctx* c) {
+  return (unsigned long long*)((char*)c->pp_fmask.p + ((c->st.n + 7) & ~7ull));
+}
+
 int pp_prepare(gs_ctx* c) {
   c->sp = PPSparse{};
   static const bool load_deg = [] { const char* e = getenv("GS_PP_NODEG"); return e && atoi(e) == 0; }();  // A/B
@@ -1567,8 +1574,10 @@ int pp_prepare(gs_ctx* c) {
   // (default), 1 = always, 0 = never (GS_PPB_WORDS, A/B)
   static const uint32_t words = [] { const char* e = getenv("GS_PPB_WORDS"); return e ? (uint32_t)std::min(std::max(atoi(e), 0), 2) : 2u; }();
   c->sp.words = words;
-  static const uint32_t maxu = [] { const char* e = getenv("GS_PPB_WORD_MAXU"); return e ? (uint32_t)std::max(atoi(e), 0) : 4u; }();
+  static const uint32_t maxu = [] { const char* e = getenv("GS_PPB_WORD_MAXU"); return e ? (uint32_t)std::max(atoi(e), 0) : 64u; }();
   c->sp.word_maxu = maxu;
+  static const uint32_t maxi = [] { const char* e = getenv("GS_PPA_WORD_MAXI"); return e ? (uint32_t)std::max(atoi(e), 0) : 64u; }();
+  c->sp.word_maxi = maxi;
   if (c->pp_shard) {  // bottom-up rounds only: the partition built the reverse table
     c->sp.ctl = (PPCtl*)c->pp_ctlb.p;
     c->sp.rend = (const unsigned long long*)c->pp_rend.p;
@@ -1576,12 +1585,14 @@ int pp_prepare(gs_ctx* c) {
     c->sp.rslot = (const uint8_t*)c->pp_rslot.p;
     if (c->failed) {
       if (c->fm_tver != c->table_ver || c->fm_fver != c->fail_ver) {
-        if (!grow(c->pp_fmask, (c->st.n + 3) & ~3ull)) return fail(c, GS_ENOMEM, "cannot allocate the failed-slot mask");
+        if (!grow(c->pp_fmask, fmask_bytes(c->st.n))) return fail(c, GS_ENOMEM, "cannot allocate the failed-slot mask");
         CK(c, pp_fmask_rows(c->st, (uint8_t*)c->pp_fmask.p, c->stream));
+        CK(c, pp_fmask_any((const uint8_t*)c->pp_fmask.p, c->st.n, fmask_any(c), c->stream));
         c->fm_tver = c->table_ver;
         c->fm_fver = c->fail_ver;
       }
       c->sp.fmask = (const uint8_t*)c->pp_fmask.p;
+      c->sp.fany = fmask_any(c);
     }
     return GS_OK;
   }
@@ -1627,16 +1638,18 @@ int pp_prepare(gs_ctx* c) {
   }
   if (c->failed && s.stride <= 8) {  // the dense rounds read fmask instead of gathering failed words
     if (c->fm_tver != c->table_ver || c->fm_fver != c->fail_ver) {
-      if (!grow(c->pp_fmask, (n + 3) & ~3ull)) {
+      if (!grow(c->pp_fmask, fmask_bytes(n))) {
         (void)hipGetLastError();
         return GS_OK;
       }
       CK(c, pp_fmask_build(s, c->sp.rend, c->sp.rsrc, c->sp.rslot, (uint8_t*)c->pp_fmask.p, c->stream));
+      CK(c, pp_fmask_any((const uint8_t*)c->pp_fmask.p, n, fmask_any(c), c->stream));
       c->fm_tver = c->table_ver;
       c->fm_fver = c->fail_ver;
       built = true;
     }
     c->sp.fmask = (const uint8_t*)c->pp_fmask.p;
+    c->sp.fany = fmask_any(c);
   }
   if (built) {
     CK(c, hipStreamSynchronize(c->stream));

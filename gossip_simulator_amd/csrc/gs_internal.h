@@ -370,6 +370,7 @@ struct PPSparse {
   const uint32_t* rsrc;         // [E] caller v of each in-edge
   const uint8_t* rslot;         // [E] its slot j
   const uint8_t* fmask;         // [n] bit j: friend j is failed (stride <= 8 and a mask set), else null
+  const unsigned long long* fany;  // [W] bit v: fmask[v] != 0 (with fmask), else null
   // Deferred sets of the pull-answer rounds (unsharded contexts, n <= 2^30;
   // null: atomicOr): the round's "x is informed" updates go to per-block
   // lists ([kPPDLists][dcap]), a coarse LDS partition by x >> 22 into
@@ -384,6 +385,7 @@ struct PPSparse {
   // bottom-up rounds: an informed caller's degree byte is not loaded when
   // every live node calls and no failed-slot mask is set (GS_PP_NODEG=0: load)
   uint32_t nodeg;
+  uint32_t word_maxi;  // k_ppa_round (words != 0): a range goes by word if no word holds more informed nodes
   uint32_t word_maxu;  // words == 2: a range goes by word if no word holds more live uninformed nodes
   uint32_t words;  // k_ppb_round with nodeg: 2 a lane per bitset word in ranges with few uninformed nodes, 1 always, 0 never
 };
@@ -421,6 +423,8 @@ hipError_t pp_rev_fill_range(const uint8_t* deg, const uint32_t* ids, uint64_t n
                              uint64_t hi, unsigned long long* rend, uint32_t* rsrc, uint8_t* rslot, hipStream_t st);
 // fmask of the shard's own callers from their rows and the replicated failed set.
 hipError_t pp_fmask_rows(const DevState& s, uint8_t* fmask, hipStream_t st);
+// fany bit v = (fmask[v] != 0), W = ceil(n / 64) words.
+hipError_t pp_fmask_any(const uint8_t* fmask, uint64_t n, unsigned long long* fany, hipStream_t st);
 // One sharded round in `mode` (PP_BOTTOM: k_ppb_round into next, the shard's
 // own words; PP_ANSWER: k_ppa_round into gnext, a bitset by global id whose
 // bits in other shards' ranges go to their owners); commit with pp_commit.

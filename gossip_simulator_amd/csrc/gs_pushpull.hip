@@ -231,6 +231,58 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Position of the k-th set bit of m (k < popc(m)).
+__device__ __forceinline__ uint32_t nth_bit(unsigned long long m, uint32_t k) {
+  uint32_t pos = 0, x = (uint32_t)m, c = (uint32_t)__popc(x);
+  if (k >= c) { k -= c; x = (uint32_t)(m >> 32); pos = 32; }
+  c = (uint32_t)__popc(x & 0xFFFFu);
+  if (k >= c) { k -= c; x >>= 16; pos += 16; }
+  c = (uint32_t)__popc(x & 0xFFu);
+  if (k >= c) { k -= c; x >>= 8; pos += 8; }
+  c = (uint32_t)__popc(x & 0xFu);
+  if (k >= c) { k -= c; x >>= 4; pos += 4; }
+  c = (uint32_t)__popc(x & 0x3u);
+  if (k >= c) { k -= c; x >>= 2; pos += 2; }
+  return pos + (k >= (x & 1u) ? 1u : 0u);
+}
+
+// The set bits of a wave's 64 words (lane l holds the mask of word l of the
+// range), in node order, 64 at a time: f(cnt, off) runs wave-wide with lane
+// j < cnt holding the node offset (word * 64 + bit) of the next bit.  A wave
+// scan of the popcounts, then a binary search of the lane's word in LDS (pre:
+// 64 u32, msk: 64 u64 of the wave) and the bit's rank inside it: the queue of
+// a range is its nodes in order, so a 64-node batch touches few lines of the
+// in-edge lists and of the degree bytes.
+template <class F>
+__device__ __forceinline__ void for_each_bit(unsigned long long m, uint32_t* pre, unsigned long long* msk, F&& f) {
+  const uint32_t lane = threadIdx.x & 63, c = (uint32_t)__popcll(m);
+  uint32_t x = c;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+    if (lane >= o) x += y;
+  }
+  const uint32_t total = (uint32_t)__shfl((int)x, 63, 64);
+  if (!total) return;
+  pre[lane] = x - c;
+  msk[lane] = m;
+  wave_lds_sync();
+  for (uint32_t p0 = 0; p0 < total; p0 += 64) {
+    const uint32_t p = p0 + lane;
+    uint32_t off = 0;
+    if (p < total) {
+      uint32_t lo = 0, hi = 63;  // the last word whose first bit ranks <= p
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= p) lo = mid; else hi = mid - 1;
+      }
+      off = (lo << 6) + nth_bit(msk[lo], p - pre[lo]);
+    }
+    f(min(64u, total - p0), off);
+  }
+  wave_lds_sync();  // pre / msk are reused by the next range
+}
+
 // Resolves queue entries [0, cnt) (cnt <= 64), one per lane.  Entry = node
 // offset in the range (12 bits) | deg << 16.
 __device__ __forceinline__ void ppb_resolve(const DevState& s, const PPSparse& sp, uint32_t t, uint32_t c3,
@@ -281,6 +333,8 @@ __global__ __launch_bounds__(kPPSBlock) void k_ppb_round(const DevState s, unsig
   __shared__ uint64_t sh[3 * kPPWaves];
   __shared__ uint32_t s_q[kPPWaves][kPPQ];
   __shared__ unsigned long long s_nb[kPPWaves][kPPRange];
+  __shared__ uint32_t s_pre[kPPWaves][64];
+  __shared__ unsigned long long s_msk[kPPWaves][64];
   if (sp.ctl->mode != PP_BOTTOM) return;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t* q = s_q[wv];
@@ -295,6 +349,9 @@ __global__ __launch_bounds__(kPPSBlock) void k_ppb_round(const DevState s, unsig
   // its degree byte is not loaded -- in the late rounds, nearly every node's
   const bool nodeg = sp.ctl->nlive0 == 0 && !fmask && sp.nodeg;
   const uint32_t ppb_words = sp.words;  // GS_PPB_WORDS: 0 a lane per node throughout, 1 a lane per word (A/B)
+  // lane-per-word ranges: every live node calls, and a failed-slot mask (if
+  // any) has its has-a-failed-friend bits
+  const bool wordok = sp.ctl->nlive0 == 0 && sp.nodeg && (!fmask || sp.fany);
   for (uint64_t rg = (uint64_t)blockIdx.x * kPPWaves + wv; rg < nrange; rg += (uint64_t)gridDim.x * kPPWaves) {
     const uint64_t w0 = rg * kPPRange, base = w0 << 6;
     nb[lane] = 0;
@@ -302,7 +359,7 @@ __global__ __launch_bounds__(kPPSBlock) void k_ppb_round(const DevState s, unsig
     bool by_word = false;
     const uint64_t word = w0 + lane;
     unsigned long long mi = 0, mu = 0;
-    if (nodeg && ppb_words) {
+    if (wordok && ppb_words) {
       if (word < W) {
         const uint64_t left = s.n - (word << 6);
         const unsigned long long valid = left >= 64 ? ~0ull : ((1ull << left) - 1);
@@ -319,46 +376,32 @@ __global__ __launch_bounds__(kPPSBlock) void k_ppb_round(const DevState s, unsig
       // a lane per WORD of the range: an informed caller costs its loss draw
       // and a bit scan, no per-node load, ballot or queue step (the late
       // rounds, where nearly every caller is informed, are VALU-bound); the
-      // live uninformed nodes of the word (few: sp.word_maxu at most, else the
-      // range takes the lane-per-node loop below) join the queue one per lane
-      // and step
+      // range's live uninformed nodes are resolved 64 at a time in node order
+      // (for_each_bit)
       fired += (uint64_t)(__popcll(mi) + __popcll(mu));  // nodeg: every live node calls
       const uint32_t vb = (uint32_t)(s.gbase + (word << 6));
-      uint32_t pushed = 0;
+      const unsigned long long fa = fmask && word < W ? sp.fany[word] : 0ull;
+      uint32_t pushed = 0, dead = 0;
       while (mi) {
         const uint32_t b = (uint32_t)__builtin_ctzll(mi);
         mi &= mi - 1;
         const u32x4 r = philox(vb + b, t, 0, c3, s.key.k0, s.key.k1);
-        pushed += (int32_t)uniform(r.y, 100u) >= s.kd ? 1u : 0u;
+        if ((int32_t)uniform(r.y, 100u) >= s.kd) {
+          ++pushed;
+          if ((fa >> b) & 1) {  // a push to a failed friend is sent, not delivered
+            const uint64_t v = (word << 6) + b;
+            dead += (fmask[v] >> uniform(r.x, s.deg[v])) & 1;
+          }
+        }
       }
       sent += pushed;
-      msgs += pushed;  // no fmask: every push that is not lost is delivered
-      while (__ballot(mu != 0)) {  // wave-uniform trip count
-        const bool has = mu != 0;
-        uint32_t e = 0;
-        if (has) {
-          const uint32_t b = (uint32_t)__builtin_ctzll(mu);
-          mu &= mu - 1;
-          const uint64_t v = (word << 6) + b;
-          e = (uint32_t)(v - base) | (uint32_t)s.deg[v] << 16;
-        }
-        const unsigned long long bal = __ballot(has);
-        if (has) {
-          const uint32_t at = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-          q[at] = e;
-        }
-        qn += (uint32_t)__popcll(bal);
-        if (qn >= 64) {
-          wave_lds_sync();
-          ppb_resolve(s, sp, t, c3, q, 64, base, nb, sent, msgs);
-          const uint32_t rest = qn - 64;
-          const uint32_t keep = lane < rest ? q[64 + lane] : 0u;
-          wave_lds_sync();
-          if (lane < rest) q[lane] = keep;
-          qn = rest;
-        }
-      }
+      msgs += pushed - dead;
+      for_each_bit(mu, s_pre[wv], s_msk[wv], [&](uint32_t cnt, uint32_t off) {
+        q[lane] = lane < cnt ? off | (uint32_t)s.deg[base + off] << 16 : 0u;
+        wave_lds_sync();
+        ppb_resolve(s, sp, t, c3, q, cnt, base, nb, sent, msgs);
+        wave_lds_sync();
+      });
     }
     for (uint32_t wi = 0; wi < kPPRange && !by_word; wi += kPPB) {
       unsigned long long Iw[kPPB];
@@ -525,6 +568,8 @@ __global__ __launch_bounds__(kPPSBlock) void k_ppa_round(const DevState s, unsig
   __shared__ uint64_t sh[3 * kPPWaves];
   __shared__ uint32_t s_q[kPPWaves][kPPQ];
   __shared__ uint32_t s_dn;  // this workgroup's deferred sets
+  __shared__ uint32_t s_pre[kPPWaves][64];
+  __shared__ unsigned long long s_msk[kPPWaves][64];
   PPCtl* c = sp.ctl;
   if (c->mode != PP_ANSWER) return;
   static_assert(kPPSGrid <= kPPDLists, "one deferred list per workgroup");
@@ -539,7 +584,28 @@ __global__ __launch_bounds__(kPPSBlock) void k_ppa_round(const DevState s, unsig
   for (uint64_t rg = (uint64_t)blockIdx.x * kPPWaves + wv; rg < nrange; rg += (uint64_t)gridDim.x * kPPWaves) {
     const uint64_t w0 = rg * kPPRange, base = w0 << 6;
     uint32_t qn = 0;  // wave-uniform
-    for (uint32_t wi = 0; wi < kPPRange; wi += kPPB) {
+    // a lane per WORD of the range where no word holds more than
+    // sp.word_maxi informed nodes: the range's informed nodes are resolved 64
+    // at a time in node order (for_each_bit), so a sparse range costs its
+    // informed nodes / 64 batches instead of 64 word steps
+    bool by_word = false;
+    const uint64_t word = w0 + lane;
+    unsigned long long mi = 0;
+    if (sp.words) {
+      mi = word < W ? s.recv[word] : 0ull;  // informed => live and in range
+      uint32_t mx = (uint32_t)__popcll(mi);
+#pragma unroll
+      for (uint32_t o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o, 64));
+      by_word = sp.words == 1 || mx <= sp.word_maxi;
+    }
+    if (by_word)
+      for_each_bit(mi, s_pre[wv], s_msk[wv], [&](uint32_t cnt, uint32_t off) {
+        q[lane] = lane < cnt ? off | (uint32_t)s.deg[base + off] << 16 : 0u;
+        wave_lds_sync();
+        ppa_resolve(s, sp, t, c3, q, cnt, base, next, sent, msgs, &s_dn);
+        wave_lds_sync();
+      });
+    for (uint32_t wi = 0; wi < kPPRange && !by_word; wi += kPPB) {
       unsigned long long Iw[kPPB];
       uint32_t d[kPPB];
 #pragma unroll
@@ -1032,6 +1098,22 @@ __global__ __launch_bounds__(kPPBlock) void k_rev_fill_range(const uint8_t* deg,
 }
 
 // fmask[v] bit j = friend j of own caller v is failed (replicated failed set).
+// fany bit v: node v has a failed friend (fmask[v] != 0): the lane-per-word
+// bottom-up ranges read a node's degree and mask byte only then.  A thread
+// per 64-node word.
+__global__ __launch_bounds__(kPPBlock) void k_pp_fmask_any(const uint8_t* __restrict__ fmask, uint64_t n,
+                                                           unsigned long long* __restrict__ fany) {
+  const uint64_t W = (n + 63) >> 6;
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < W; w += (uint64_t)gridDim.x * blockDim.x) {
+    unsigned long long bits = 0;
+    for (uint32_t b = 0; b < 64; ++b) {
+      const uint64_t v = (w << 6) + b;
+      if (v < n && fmask[v]) bits |= 1ull << b;
+    }
+    fany[w] = bits;
+  }
+}
+
 __global__ __launch_bounds__(kPPBlock) void k_pp_fmask_rows(const DevState s, uint8_t* fmask) {
   for (uint64_t v = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; v < s.n; v += (uint64_t)gridDim.x * kPPBlock) {
     const uint32_t d = s.deg[v];
@@ -1202,6 +1284,13 @@ hipError_t pp_rev_fill_range(const uint8_t* deg, const uint32_t* ids, uint64_t n
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((nfull + kPPBlock - 1) / kPPBlock, 8192);
   hipLaunchKernelGGL(k_rev_fill_range, dim3(blocks), dim3(kPPBlock), 0, st, deg, ids, nfull, stride, lo, hi, rend,
                      rsrc, rslot);
+  return hipGetLastError();
+}
+
+hipError_t pp_fmask_any(const uint8_t* fmask, uint64_t n, unsigned long long* fany, hipStream_t st) {
+  const uint64_t W = (n + 63) >> 6;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((W + kPPBlock - 1) / kPPBlock, 8192);
+  hipLaunchKernelGGL(k_pp_fmask_any, dim3(blocks), dim3(kPPBlock), 0, st, fmask, n, fany);
   return hipGetLastError();
 }
 
