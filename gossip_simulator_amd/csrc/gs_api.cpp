@@ -1578,6 +1578,8 @@ int pp_prepare(gs_ctx* c) {
   c->sp.word_maxu = maxu;
   static const uint32_t maxi = [] { const char* e = getenv("GS_PPA_WORD_MAXI"); return e ? (uint32_t)std::max(atoi(e), 0) : 64u; }();
   c->sp.word_maxi = maxi;
+  static const uint32_t pullfirst = [] { const char* e = getenv("GS_PPB_PULLFIRST"); return e && !atoi(e) ? 0u : 1u; }();
+  c->sp.pullfirst = pullfirst;
   if (c->pp_shard) {  // bottom-up rounds only: the partition built the reverse table
     c->sp.ctl = (PPCtl*)c->pp_ctlb.p;
     c->sp.rend = (const unsigned long long*)c->pp_rend.p;

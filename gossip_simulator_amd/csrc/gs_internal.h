@@ -385,6 +385,7 @@ struct PPSparse {
   // bottom-up rounds: an informed caller's degree byte is not loaded when
   // every live node calls and no failed-slot mask is set (GS_PP_NODEG=0: load)
   uint32_t nodeg;
+  uint32_t pullfirst;  // bottom-up: skip the in-edge scan of a node whose own pull succeeded (GS_PPB_PULLFIRST=0: scan, A/B)
   uint32_t word_maxi;  // k_ppa_round (words != 0): a range goes by word if no word holds more informed nodes
   uint32_t word_maxu;  // words == 2: a range goes by word if no word holds more live uninformed nodes
   uint32_t words;  // k_ppb_round with nodeg: 2 a lane per bitset word in ranges with few uninformed nodes, 1 always, 0 never

@@ -303,7 +303,10 @@ __device__ __forceinline__ void ppb_resolve(const DevState& s, const PPSparse& s
     }
   }
   const unsigned long long Iu = pull ? s.grecv[u >> 6] : 0ull;  // u is a global id
-  bool got = false;
+  const bool pulled = pull && ((Iu >> (u & 63)) & 1);  // u informed => u live
+  // a node its own pull informs needs no push receipt (sp.pullfirst: the
+  // in-edge scan waits for the pull's two dependent loads, and skips)
+  bool got = sp.pullfirst && pulled;
   for (unsigned long long q0 = qb; q0 < qe && !got; q0 += kPPEdges) {
     uint32_t src[kPPEdges], x[kPPEdges];
 #pragma unroll
@@ -320,7 +323,6 @@ __device__ __forceinline__ void ppb_resolve(const DevState& s, const PPSparse& s
         got |= ((s.grecv[src[k] >> 6] >> (src[k] & 63)) & 1) != 0;
     }
   }
-  const bool pulled = pull && ((Iu >> (u & 63)) & 1);  // u informed => u live
   if (pulled) {
     ++sent;
     ++msgs;
