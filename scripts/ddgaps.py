@@ -1,6 +1,7 @@
 """The last broadcast of a rocprofv3 kernel-trace .db (from its k_schedule_win
-on): kernel time by kernel, the idle time before each kernel by kernel (the
-gap a launch waited for), span and busy time.  Usage: python ddgaps.py <db>"""
+on, or from the last kernel named <mark>): kernel time by kernel, the idle
+time before each kernel by kernel (the gap a launch waited for), span and
+busy time.  Usage: python ddgaps.py <db> [mark]"""
 import re
 import sqlite3
 import sys
@@ -8,7 +9,8 @@ from collections import defaultdict
 
 db = sqlite3.connect(sys.argv[1])
 rows = db.execute("select name, start, end from kernels order by start").fetchall()
-starts = [i for i, (n, _, _) in enumerate(rows) if "k_schedule" in n]
+mark = sys.argv[2] if len(sys.argv) > 2 else "k_schedule"  # the kernel that starts a broadcast
+starts = [i for i, (n, _, _) in enumerate(rows) if mark in n]
 rows = rows[starts[-1]:] if starts else rows
 
 
