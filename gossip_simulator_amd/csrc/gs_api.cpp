@@ -313,8 +313,10 @@ void plan_coarse(gs_ctx* c, uint64_t T, const unsigned long long* exact) {
   for (uint32_t b = 0; b < 256; ++b) {
     const uint64_t lo = (uint64_t)b << kCoarseShift;
     const uint64_t hi = std::min<uint64_t>(w.n, lo + (1ull << kCoarseShift));
+    const double xr = (double)kXRoundNodes * w.stride;  // one expand round's slots (gs_internal.h)
     const unsigned long long sub =
-        b < w.ncoarse ? (unsigned long long)((double)T * (double)(hi - lo) / (double)w.n / kCoarseSub) + 512 : 0ull;
+        b < w.ncoarse ? (unsigned long long)(((double)T / kCoarseSub + xr) * (double)(hi - lo) / (double)w.n) + 512
+                      : 0ull;
     for (uint32_t x = 0; x < kCoarseSub; ++x) {
       const uint32_t r = b * kCoarseSub + x;
       c->h_cap[r] = a;
@@ -2448,7 +2450,9 @@ void plan_coarse_owner(gs_ctx* c, uint64_t T, const unsigned long long* exact) {
       const uint64_t hi = std::min<uint64_t>(dhi, lo + (1ull << kCoarseShift));
       cnt = hi > lo ? hi - lo : 0;
     }
-    const unsigned long long sub = cnt ? (unsigned long long)((double)T * (double)cnt / (double)N / kCoarseSub) + 512 : 0;
+    const double xr = (double)kXRoundNodes * w.slots;  // one expand round's slots (gs_internal.h)
+    const unsigned long long sub =
+        cnt ? (unsigned long long)(((double)T / kCoarseSub + xr) * (double)cnt / (double)N) + 512 : 0;
     for (uint32_t x = 0; x < kCoarseSub; ++x) {
       const uint32_t r = b * kCoarseSub + x;
       c->h_cap[r] = a;
@@ -3305,6 +3309,7 @@ int dd_run(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t tend, uint32_t 
     *what = 0;
     if (sg[3] & kErrAbort) {
       if (dd_log()) fprintf(stderr, "[dd] window at t0=%u aborted: redone host-driven\n", t0);
+      ++m0->timing.dd_fallbacks;
       *fallback = true;
       *what = 1;
       return GS_OK;

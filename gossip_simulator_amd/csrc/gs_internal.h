@@ -107,6 +107,12 @@ constexpr unsigned long long kSrcMask = (1ull << kSrcShift) - 1;
 constexpr uint32_t kPartTile = GS_PART_TILE;    // messages per partition tile (runs of ~64 per fine bucket)
 constexpr uint32_t kRolledCap = 1024;           // rolled receipts per bucket k_resolve lists (more: its large path)
 constexpr uint32_t kBitTicks = 10;              // window length k_resolve's per-tick bitmaps hold
+// Coarse sub-region estimates: k_expand deals its rounds to the XCDs in 8
+// contiguous runs of ceil(rounds / 8), so one XCD's sub-region of a bin can
+// hold one round more than an eighth of the bin's share: at most this many
+// firing nodes per round (512 threads x 4) times the row length, times the
+// bin's node share, is added to every sub-region (small windows, small N)
+constexpr uint32_t kXRoundNodes = 2048;
 constexpr uint32_t kWinSlotsPerBucket = 1u << 16;  // window cut: friend slots per fine bucket
                                                 // (bounds the message buffers, not LDS)
 

@@ -310,8 +310,10 @@ __device__ __forceinline__ void cut_body(const WinState& w, unsigned long long b
   if (!w.owner) {
     const unsigned long long lo = (unsigned long long)b << kCoarseShift;
     const unsigned long long hi = min((unsigned long long)w.n, lo + (1ull << kCoarseShift));
-    sub = b < w.ncoarse ? (unsigned long long)((double)s_T * (double)(hi - lo) / (double)w.n / kCoarseSub) + 512
-                        : 0ull;
+    const double xr = (double)kXRoundNodes * w.stride;  // one expand round's slots (kXRoundNodes)
+    sub = b < w.ncoarse
+              ? (unsigned long long)(((double)s_T / kCoarseSub + xr) * (double)(hi - lo) / (double)w.n) + 512
+              : 0ull;
   } else {  // bin b = owner d * obins + 2^22-node chunk of d's range (plan_coarse_owner)
     const uint32_t d = b / w.obins, k = b % w.obins;
     unsigned long long cnt = 0;
@@ -322,7 +324,8 @@ __device__ __forceinline__ void cut_body(const WinState& w, unsigned long long b
       const unsigned long long hi = min(dhi, lo + (1ull << kCoarseShift));
       cnt = hi > lo ? hi - lo : 0ull;
     }
-    sub = cnt ? (unsigned long long)((double)s_T * (double)cnt / (double)w.nglob / kCoarseSub) + 512 : 0ull;
+    const double xr = (double)kXRoundNodes * w.slots;
+    sub = cnt ? (unsigned long long)(((double)s_T / kCoarseSub + xr) * (double)cnt / (double)w.nglob) + 512 : 0ull;
   }
   unsigned long long total;
   const unsigned long long base = block_exscan256_u64(sub * kCoarseSub, &s_sz[0], &total);
@@ -937,7 +940,11 @@ __device__ __forceinline__ void plan_body(const WinState& w, bool exact) {
   __shared__ unsigned long long s_x[4];
   s_cap[tid] = live ? (cnt + cnt / 8 + nf - 1) / nf + 512 : 0;
   unsigned long long tb, tt;
-  s_base[tid] = block_exscan256_u64(s_cap[tid] * 256, s_x, &tb);
+  // the bucket's nf fine regions (a partial last bucket's were counted as
+  // 256 before: its plan outgrew the host's bound R + R/8 + 513 * 256 per
+  // coarse bucket, and a shard window whose fine buffer was sized by that
+  // bound overflowed every time -- r04aj)
+  s_base[tid] = block_exscan256_u64(s_cap[tid] * nf, s_x, &tb);
   s_tp[tid] = (uint32_t)block_exscan256_u64(live ? ntile : 0u, s_x, &tt);
   if (tid == 0) { s_base[256] = tb; s_tp[256] = (uint32_t)tt; }
   __syncthreads();

@@ -126,6 +126,8 @@ typedef struct gs_timing {
   uint64_t pp_early_rounds;  /* push-pull: rounds of this broadcast run sparse (informed list)   */
   uint64_t pp_bottom_rounds; /* push-pull: dense rounds of this broadcast run bottom-up          */
   uint64_t pp_answer_rounds; /* push-pull: dense rounds of this broadcast run pull-answer        */
+  uint64_t dd_fallbacks;     /* device-driven shard windows stopped by an overflow and redone
+                              * host-driven (cumulative; a buffer that fits makes it stop growing) */
 } gs_timing;
 
 /* gs_run status */
