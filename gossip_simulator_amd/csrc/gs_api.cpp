@@ -77,6 +77,9 @@ struct gs_ctx {
   Buf pp_rend, pp_rsrc, pp_rslot, pp_ilist, pp_fmask, pp_scan, pp_ctlb;
   Buf pp_dset, pp_dcnt;  // deferred sets of the pull-answer rounds (PPSparse::dset)
   uint64_t table_ver = 0, fail_ver = 0, rev_ver = ~0ull, fm_tver = ~0ull, fm_fver = ~0ull;
+  // push-pull: live callers and live empty rows of (cl_tver, cl_fver) (pp_seed_ctx)
+  uint64_t cl_tver = ~0ull, cl_fver = ~0ull;
+  unsigned long long cl_counts[2] = {0, 0};
   PPSparse sp{};
   // window engine (gs_window.hip)
   bool win = false;
@@ -1568,6 +1571,25 @@ unsigned long long* fmask_any(gs_ctx* c) {
   return (unsigned long long*)((char*)c->pp_fmask.p + ((c->st.n + 7) & ~7ull));
 }
 
+// pp_seed on context c's state and stream: the live callers are counted
+// once per (table, failure mask) version and reused after (a pass over the
+// 1e9 degree bytes was 0.76 ms of every push-pull broadcast_begin).  Leaves
+// the stream synchronized.
+int pp_seed_ctx(gs_ctx* c, unsigned long long* next, uint32_t node, unsigned long long thr, unsigned long long bthr,
+                unsigned long long athr) {
+  const bool known = c->sp.ctl && c->cl_tver == c->table_ver && c->cl_fver == c->fail_ver;
+  CK(c, pp_seed(c->st, next, node, c->d_flag, c->sp, thr, bthr, athr, known ? c->cl_counts : nullptr, c->stream));
+  if (c->sp.ctl && !known) {
+    CK(c, hipMemcpyAsync(&c->cl_counts[0], &c->sp.ctl->ncallers, 8, hipMemcpyDeviceToHost, c->stream));
+    CK(c, hipMemcpyAsync(&c->cl_counts[1], &c->sp.ctl->nlive0, 8, hipMemcpyDeviceToHost, c->stream));
+    CK(c, hipStreamSynchronize(c->stream));
+    c->cl_tver = c->table_ver;
+    c->cl_fver = c->fail_ver;
+  }
+  CK(c, hipStreamSynchronize(c->stream));
+  return GS_OK;
+}
+
 int pp_prepare(gs_ctx* c) {
   c->sp = PPSparse{};
   static const bool load_deg = [] { const char* e = getenv("GS_PP_NODEG"); return e && atoi(e) == 0; }();  // A/B
@@ -1826,9 +1848,7 @@ int pp_shard_begin(gs_ctx* acc, uint64_t sender) {
     for (gs_ctx* r : reps) {
       CK(r, hipSetDevice(r->dev));
       CK(r, hipMemsetAsync(r->d_next, 0, r->st.W * 8, r->stream));
-      CK(r, pp_seed(r->st, r->d_next, (uint32_t)sender, r->d_flag, r->sp, r->st.n >> pp_shift(), ~0ull, ~0ull,
-                    r->stream));
-      CK(r, hipStreamSynchronize(r->stream));
+      RC(pp_seed_ctx(r, r->d_next, (uint32_t)sender, r->st.n >> pp_shift(), ~0ull, ~0ull));
     }
   acc->rep_live = sparse;
   acc->pp_gn_ok = false;
@@ -1843,7 +1863,7 @@ int pp_shard_begin(gs_ctx* acc, uint64_t sender) {
     CK(m, hipSetDevice(m->dev));
     if (int rc = pp_prepare(m)) return fail(acc, rc, m->err);
     const uint32_t node = sender >= m->lo && sender < m->hi ? (uint32_t)(sender - m->lo) : ~0u;
-    CK(m, pp_seed(m->st, m->d_next, node, m->d_flag, m->sp, 0ull, 0ull, ~0ull, m->stream));
+    RC(pp_seed_ctx(m, m->d_next, node, 0ull, 0ull, ~0ull));
     uint32_t ok = 0;
     CK(m, hipMemcpyAsync(&ok, m->d_flag, 4, hipMemcpyDeviceToHost, m->stream));
     CK(m, hipStreamSynchronize(m->stream));
@@ -2028,8 +2048,7 @@ int gs_broadcast_begin(gs_ctx* c, int64_t sender) {
     RC(pp_prepare(c));
     const uint64_t n = c->st.n;
     const unsigned long long thr = (c->p.flags & GS_FLAG_PP_EARLY) ? n : (n >> pp_shift());
-    CK(c, pp_seed(c->st, c->d_next, (uint32_t)s, c->d_flag, c->sp, thr, pp_bottom_thr(c), pp_answer_thr(c),
-                  c->stream));
+    RC(pp_seed_ctx(c, c->d_next, (uint32_t)s, thr, pp_bottom_thr(c), pp_answer_thr(c)));
     uint32_t ok = 0;
     CK(c, hipMemcpyAsync(&ok, c->d_flag, 4, hipMemcpyDeviceToHost, c->stream));
     CK(c, hipStreamSynchronize(c->stream));

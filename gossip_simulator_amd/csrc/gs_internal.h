@@ -404,10 +404,12 @@ hipError_t pp_live_edges(const DevState& s, uint32_t* out, hipStream_t st);
 hipError_t pp_commit(const DevState& s, const unsigned long long* next, uint32_t t, const PPSparse& sp,
                      hipStream_t st);
 // Sender informed unless failed; flag = 1 if informed.  Also initialises ctl
-// (counts live callers: a pass over deg and the failed mask).
+// with the live callers and the live nodes with an empty row: counted (a pass
+// over deg and the failed mask) when callers is null, else callers[0..1] as
+// counted before for the same table and mask.
 hipError_t pp_seed(const DevState& s, unsigned long long* next, uint32_t node, uint32_t* flag,
                    const PPSparse& sp, unsigned long long thr, unsigned long long bthr, unsigned long long athr,
-                   hipStream_t st);
+                   const unsigned long long* callers, hipStream_t st);
 // Reverse table: rend must hold n + 1 words of scratch-free u64 space; tmp /
 // tmp_bytes the hipcub scan workspace (pp_rev_scan_bytes).
 size_t pp_rev_scan_bytes(uint64_t n);

@@ -997,6 +997,12 @@ __global__ __launch_bounds__(kPPBlock) void k_ppe_commit(const DevState s, const
   }
 }
 
+// The counts of k_pp_callers, from an earlier count of the same table and mask.
+__global__ void k_pp_set_callers(PPCtl* c, unsigned long long ncallers, unsigned long long nlive0) {
+  c->ncallers = ncallers;
+  c->nlive0 = nlive0;
+}
+
 // Live nodes with a non-empty row (each calls once per round).
 __global__ __launch_bounds__(kPPBlock) void k_pp_callers(const DevState s, PPCtl* c) {
   uint64_t k = 0, z = 0;
@@ -1230,12 +1236,16 @@ hipError_t pp_live_edges(const DevState& s, uint32_t* out, hipStream_t st) {
 
 hipError_t pp_seed(const DevState& s, unsigned long long* next, uint32_t node, uint32_t* flag,
                    const PPSparse& sp, unsigned long long thr, unsigned long long bthr, unsigned long long athr,
-                   hipStream_t st) {
+                   const unsigned long long* callers, hipStream_t st) {
   if (sp.ctl) {
     hipError_t e = hipMemsetAsync(sp.ctl, 0, sizeof(PPCtl), st);
     if (e != hipSuccess) return e;
-    const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.n + kPPBlock - 1) / kPPBlock, 4096);
-    hipLaunchKernelGGL(k_pp_callers, dim3(blocks), dim3(kPPBlock), 0, st, s, sp.ctl);
+    if (callers) {
+      hipLaunchKernelGGL(k_pp_set_callers, dim3(1), dim3(1), 0, st, sp.ctl, callers[0], callers[1]);
+    } else {
+      const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.n + kPPBlock - 1) / kPPBlock, 4096);
+      hipLaunchKernelGGL(k_pp_callers, dim3(blocks), dim3(kPPBlock), 0, st, s, sp.ctl);
+    }
   }
   hipLaunchKernelGGL(k_pp_seed, dim3(1), dim3(1), 0, st, s, next, node, flag, sp, thr, bthr, athr);
   return hipGetLastError();
