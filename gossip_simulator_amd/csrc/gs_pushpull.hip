@@ -963,11 +963,21 @@ __global__ __launch_bounds__(kPPBlock) void k_ppe_round(const DevState s, unsign
 __global__ __launch_bounds__(kPPBlock) void k_ppe_commit(const DevState s, const unsigned long long* __restrict__ next,
                                                          PPSparse sp, uint32_t t) {
   __shared__ uint64_t sh[kPPBlock / 64];
+  __shared__ unsigned long long s_b[kPPSegs], s_e[kPPSegs];
   PPCtl* c = sp.ctl;
   if (c->mode != PP_EARLY) return;
   const uint64_t G = (uint64_t)gridDim.x * kPPBlock, gid = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x;
   uint64_t newly = 0;
-  if (c->ovf) {
+  const bool ovf = c->ovf != 0;
+  const uint32_t nseg = c->nseg;
+  if (!ovf) {  // the segments' bounds staged once per block (a chain of 2 * nseg loads per thread before)
+    for (uint32_t sg = threadIdx.x; sg < nseg; sg += kPPBlock) {
+      s_b[sg] = c->seglen[sg];
+      s_e[sg] = c->segcnt[sg];
+    }
+    __syncthreads();
+  }
+  if (ovf) {
     for (uint64_t w = gid; w < s.W; w += G) {
       const unsigned long long nx = next[w], old = s.recv[w];
       newly += (uint64_t)__popcll(nx & ~old);
@@ -975,8 +985,8 @@ __global__ __launch_bounds__(kPPBlock) void k_ppe_commit(const DevState s, const
     }
   } else {
     const unsigned long long cap = c->seg_cap;
-    for (uint32_t sg = 0; sg < c->nseg; ++sg) {
-      const unsigned long long b = c->seglen[sg], e = c->segcnt[sg];
+    for (uint32_t sg = 0; sg < nseg; ++sg) {
+      const unsigned long long b = s_b[sg], e = s_e[sg];
       for (uint64_t k = b + gid; k < e; k += G) {
         const uint32_t v = sp.ilist[(size_t)sg * cap + k];
         atomicOr(&s.recv[v >> 6], 1ull << (v & 63));
