@@ -350,7 +350,10 @@ __global__ __launch_bounds__(kPPSBlock) void k_ppb_round(const DevState s, unsig
   // informed caller's push needs only its loss draw (sent = delivered), so
   // its degree byte is not loaded -- in the late rounds, nearly every node's
   const bool nodeg = sp.ctl->nlive0 == 0 && !fmask && sp.nodeg;
-  const uint32_t ppb_words = sp.words;  // GS_PPB_WORDS: 0 a lane per node throughout, 1 a lane per word (A/B)
+  // GS_PPB_WORDS (A/B): 0 a lane per node throughout, 1 a lane per word, 2 a
+  // lane per word where no word holds more than sp.word_maxu live uninformed
+  // nodes (default; 64, i.e. always)
+  const uint32_t ppb_words = sp.words;
   // lane-per-word ranges: every live node calls, and a failed-slot mask (if
   // any) has its has-a-failed-friend bits
   const bool wordok = sp.ctl->nlive0 == 0 && sp.nodeg && (!fmask || sp.fany);
