@@ -385,19 +385,25 @@ __global__ __launch_bounds__(kPPSBlock) void k_ppb_round(const DevState s, unsig
       // (for_each_bit)
       fired += (uint64_t)(__popcll(mi) + __popcll(mu));  // nodeg: every live node calls
       const uint32_t vb = (uint32_t)(s.gbase + (word << 6));
-      const unsigned long long fa = fmask && word < W ? sp.fany[word] : 0ull;
+      unsigned long long mf = fmask && word < W ? sp.fany[word] & mi : 0ull;
       uint32_t pushed = 0, dead = 0;
       while (mi) {
         const uint32_t b = (uint32_t)__builtin_ctzll(mi);
         mi &= mi - 1;
         const u32x4 r = philox(vb + b, t, 0, c3, s.key.k0, s.key.k1);
-        if ((int32_t)uniform(r.y, 100u) >= s.kd) {
-          ++pushed;
-          if ((fa >> b) & 1) {  // a push to a failed friend is sent, not delivered
-            const uint64_t v = (word << 6) + b;
-            dead += (fmask[v] >> uniform(r.x, s.deg[v])) & 1;
-          }
-        }
+        pushed += (int32_t)uniform(r.y, 100u) >= s.kd ? 1u : 0u;
+      }
+      // callers with a failed friend (a push to it is sent, not delivered): a
+      // second pass with their draws made again, so the loop above never waits
+      // for a degree or mask byte (one of ~17 callers at 1 % failed, but in
+      // nearly every step of a 64-lane wave)
+      while (mf) {
+        const uint32_t b = (uint32_t)__builtin_ctzll(mf);
+        mf &= mf - 1;
+        const uint64_t v = (word << 6) + b;
+        const uint32_t fm = fmask[v], d = s.deg[v];
+        const u32x4 r = philox(vb + b, t, 0, c3, s.key.k0, s.key.k1);
+        if ((int32_t)uniform(r.y, 100u) >= s.kd) dead += (fm >> uniform(r.x, d)) & 1;
       }
       sent += pushed;
       msgs += pushed - dead;
