@@ -75,6 +75,7 @@ struct gs_ctx {
   // mask, round control; rebuilt when the table (table_ver) or the failure
   // mask (fail_ver) changes
   Buf pp_rend, pp_rsrc, pp_rslot, pp_ilist, pp_fmask, pp_scan, pp_ctlb;
+  Buf pp_rfail;  // push-pull: failed-caller bit per in-edge (with pp_fmask)
   Buf pp_dset, pp_dcnt;  // deferred sets of the pull-answer rounds (PPSparse::dset)
   uint64_t table_ver = 0, fail_ver = 0, rev_ver = ~0ull, fm_tver = ~0ull, fm_fver = ~0ull;
   // push-pull: live callers and live empty rows of (cl_tver, cl_fver) (pp_seed_ctx)
@@ -722,7 +723,7 @@ void destroy_one(gs_ctx* c) {
                     (void*)c->d_glay})
     if (ptr) (void)hipFree(ptr);
   for (Buf* b : {&c->gmap, &c->cmsg, &c->fmsg, &c->tmp, &c->xsend, &c->xrecv, &c->pp_rend, &c->pp_rsrc,
-                 &c->pp_rslot, &c->pp_ilist, &c->pp_fmask, &c->pp_scan, &c->pp_ctlb, &c->pp_dset, &c->pp_dcnt})
+                 &c->pp_rslot, &c->pp_ilist, &c->pp_fmask, &c->pp_scan, &c->pp_ctlb, &c->pp_dset, &c->pp_dcnt, &c->pp_rfail})
     if (b->p) (void)hipFree(b->p);
   for (void* ptr : {(void*)c->h_cap, (void*)c->h_misc, (void*)c->h_err, (void*)c->h_stats, (void*)c->h_tstat,
                     (void*)c->h_stage, (void*)c->h_rtab, (void*)c->h_glay})
@@ -1670,12 +1671,18 @@ int pp_prepare(gs_ctx* c) {
       }
       CK(c, pp_fmask_build(s, c->sp.rend, c->sp.rsrc, c->sp.rslot, (uint8_t*)c->pp_fmask.p, c->stream));
       CK(c, pp_fmask_any((const uint8_t*)c->pp_fmask.p, n, fmask_any(c), c->stream));
+      // (optional: without it the answer test gathers the caller's failed word)
+      if (grow(c->pp_rfail, ((n * s.stride + 31) >> 5) * 4 + 4))
+        CK(c, pp_rfail_build(s, c->sp.rend, c->sp.rsrc, (uint32_t*)c->pp_rfail.p, c->stream));
+      else
+        (void)hipGetLastError();
       c->fm_tver = c->table_ver;
       c->fm_fver = c->fail_ver;
       built = true;
     }
     c->sp.fmask = (const uint8_t*)c->pp_fmask.p;
     c->sp.fany = fmask_any(c);
+    c->sp.rfail = c->pp_rfail.p && !getenv("GS_PP_NORFAIL") ? (const uint32_t*)c->pp_rfail.p : nullptr;
   }
   if (built) {
     CK(c, hipStreamSynchronize(c->stream));

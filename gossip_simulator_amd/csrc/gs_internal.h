@@ -377,6 +377,7 @@ struct PPSparse {
   const uint8_t* rslot;         // [E] its slot j
   const uint8_t* fmask;         // [n] bit j: friend j is failed (stride <= 8 and a mask set), else null
   const unsigned long long* fany;  // [W] bit v: fmask[v] != 0 (with fmask), else null
+  const uint32_t* rfail;        // [ceil(E / 32)] bit q: in-edge q's caller is failed (with fmask, unsharded), else null
   // Deferred sets of the pull-answer rounds (unsharded contexts, n <= 2^30;
   // null: atomicOr): the round's "x is informed" updates go to per-block
   // lists ([kPPDLists][dcap]), a coarse LDS partition by x >> 22 into
@@ -434,6 +435,9 @@ hipError_t pp_rev_fill_range(const uint8_t* deg, const uint32_t* ids, uint64_t n
 hipError_t pp_fmask_rows(const DevState& s, uint8_t* fmask, hipStream_t st);
 // fany bit v = (fmask[v] != 0), W = ceil(n / 64) words.
 hipError_t pp_fmask_any(const uint8_t* fmask, uint64_t n, unsigned long long* fany, hipStream_t st);
+// rfail bit q = (rsrc[q] is failed), q < rend[n - 1].
+hipError_t pp_rfail_build(const DevState& s, const unsigned long long* rend, const uint32_t* rsrc, uint32_t* rfail,
+                          hipStream_t st);
 // One sharded round in `mode` (PP_BOTTOM: k_ppb_round into next, the shard's
 // own words; PP_ANSWER: k_ppa_round into gnext, a bitset by global id whose
 // bits in other shards' ranges go to their owners); commit with pp_commit.

@@ -557,7 +557,11 @@ __device__ __forceinline__ void ppa_resolve(const DevState& s, const PPSparse& s
         if (uniform(r.x, (x[k] >> 4) + 1) == (x[k] & 15u) && (int32_t)uniform(r.y, 100u) >= s.kd) {
           const unsigned long long vb = 1ull << (src[k] & 63);
           const bool iv = (s.grecv[src[k] >> 6] & vb) != 0;
-          const bool fv = cc && (s.gcrash[src[k] >> 6] & vb) != 0;
+          // v failed: its in-edge's bit (sp.rfail: a line the in-edge scan
+          // reads anyway) instead of a gather of v's failed word
+          const uint64_t q = q0 + k;
+          const bool fv = cc && (sp.rfail ? ((sp.rfail[q >> 5] >> (q & 31)) & 1u) != 0
+                                          : (s.gcrash[src[k] >> 6] & vb) != 0);
           if (!iv && !fv) {  // v's pull from this informed node succeeds
             ++sent;
             ++msgs;
@@ -1125,6 +1129,23 @@ __global__ __launch_bounds__(kPPBlock) void k_rev_fill_range(const uint8_t* deg,
 }
 
 // fmask[v] bit j = friend j of own caller v is failed (replicated failed set).
+// rfail bit q: in-edge q's caller rsrc[q] is failed (the pull-answer rounds'
+// answer test).  A thread per 32 in-edges; E = rend[n - 1] in-edges.
+__global__ __launch_bounds__(kPPBlock) void k_pp_rfail(const DevState s, const unsigned long long* __restrict__ rend,
+                                                       const uint32_t* __restrict__ rsrc, uint32_t* __restrict__ rfail) {
+  const uint64_t E = s.n ? rend[s.n - 1] : 0ull, NW = (E + 31) >> 5;
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < NW; w += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t bits = 0;
+    for (uint32_t b = 0; b < 32; ++b) {
+      const uint64_t q = (w << 5) + b;
+      if (q >= E) break;
+      const uint32_t v = rsrc[q];
+      if ((s.gcrash[v >> 6] >> (v & 63)) & 1) bits |= 1u << b;
+    }
+    rfail[w] = bits;
+  }
+}
+
 // fany bit v: node v has a failed friend (fmask[v] != 0): the lane-per-word
 // bottom-up ranges read a node's degree and mask byte only then.  A thread
 // per 64-node word.
@@ -1315,6 +1336,14 @@ hipError_t pp_rev_fill_range(const uint8_t* deg, const uint32_t* ids, uint64_t n
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((nfull + kPPBlock - 1) / kPPBlock, 8192);
   hipLaunchKernelGGL(k_rev_fill_range, dim3(blocks), dim3(kPPBlock), 0, st, deg, ids, nfull, stride, lo, hi, rend,
                      rsrc, rslot);
+  return hipGetLastError();
+}
+
+hipError_t pp_rfail_build(const DevState& s, const unsigned long long* rend, const uint32_t* rsrc, uint32_t* rfail,
+                          hipStream_t st) {
+  const uint64_t NW = (s.n * s.stride + 31) >> 5;  // at most
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((NW + kPPBlock - 1) / kPPBlock, 8192);
+  hipLaunchKernelGGL(k_pp_rfail, dim3(blocks ? blocks : 1), dim3(kPPBlock), 0, st, s, rend, rsrc, rfail);
   return hipGetLastError();
 }
 
