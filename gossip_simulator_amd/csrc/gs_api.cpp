@@ -1673,7 +1673,7 @@ int pp_prepare(gs_ctx* c) {
       CK(c, pp_fmask_any((const uint8_t*)c->pp_fmask.p, n, fmask_any(c), c->stream));
       // (optional: without it the answer test gathers the caller's failed word)
       if (grow(c->pp_rfail, ((n * s.stride + 31) >> 5) * 4 + 4))
-        CK(c, pp_rfail_build(s, c->sp.rend, c->sp.rsrc, (uint32_t*)c->pp_rfail.p, c->stream));
+        CK(c, pp_rfail_build(s, c->sp.rend, c->sp.rsrc, c->sp.rslot, (uint32_t*)c->pp_rfail.p, c->stream));
       else
         (void)hipGetLastError();
       c->fm_tver = c->table_ver;

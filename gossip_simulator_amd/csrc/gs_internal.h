@@ -436,8 +436,8 @@ hipError_t pp_fmask_rows(const DevState& s, uint8_t* fmask, hipStream_t st);
 // fany bit v = (fmask[v] != 0), W = ceil(n / 64) words.
 hipError_t pp_fmask_any(const uint8_t* fmask, uint64_t n, unsigned long long* fany, hipStream_t st);
 // rfail bit q = (rsrc[q] is failed), q < rend[n - 1].
-hipError_t pp_rfail_build(const DevState& s, const unsigned long long* rend, const uint32_t* rsrc, uint32_t* rfail,
-                          hipStream_t st);
+hipError_t pp_rfail_build(const DevState& s, const unsigned long long* rend, const uint32_t* rsrc,
+                          const uint8_t* rslot, uint32_t* rfail, hipStream_t st);
 // One sharded round in `mode` (PP_BOTTOM: k_ppb_round into next, the shard's
 // own words; PP_ANSWER: k_ppa_round into gnext, a bitset by global id whose
 // bits in other shards' ranges go to their owners); commit with pp_commit.

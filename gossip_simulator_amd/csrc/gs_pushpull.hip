@@ -1130,19 +1130,29 @@ __global__ __launch_bounds__(kPPBlock) void k_rev_fill_range(const uint8_t* deg,
 
 // fmask[v] bit j = friend j of own caller v is failed (replicated failed set).
 // rfail bit q: in-edge q's caller rsrc[q] is failed (the pull-answer rounds'
-// answer test).  A thread per 32 in-edges; E = rend[n - 1] in-edges.
+// answer test; rfail zeroed before).  Built from the failed callers' side: a
+// thread per failed-set word, and for each failed caller v and slot j the
+// in-edge (v, j) is found in friend w's short in-list (a pass over every
+// in-edge with a gather of its caller's failed word took 175 ms at N = 1e9).
 __global__ __launch_bounds__(kPPBlock) void k_pp_rfail(const DevState s, const unsigned long long* __restrict__ rend,
-                                                       const uint32_t* __restrict__ rsrc, uint32_t* __restrict__ rfail) {
-  const uint64_t E = s.n ? rend[s.n - 1] : 0ull, NW = (E + 31) >> 5;
-  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < NW; w += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t bits = 0;
-    for (uint32_t b = 0; b < 32; ++b) {
-      const uint64_t q = (w << 5) + b;
-      if (q >= E) break;
-      const uint32_t v = rsrc[q];
-      if ((s.gcrash[v >> 6] >> (v & 63)) & 1) bits |= 1u << b;
+                                                       const uint32_t* __restrict__ rsrc,
+                                                       const uint8_t* __restrict__ rslot, uint32_t* __restrict__ rfail) {
+  for (uint64_t wd = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; wd < s.W;
+       wd += (uint64_t)gridDim.x * blockDim.x) {
+    for (unsigned long long m = s.crash[wd]; m; m &= m - 1) {
+      const uint64_t v = (wd << 6) + (uint64_t)__builtin_ctzll(m);
+      if (v >= s.n) break;
+      const uint32_t d = s.deg[v];
+      for (uint32_t j = 0; j < d; ++j) {
+        const uint32_t w = s.ids[v * s.stride + j];
+        const unsigned long long qb = w ? rend[w - 1] : 0ull, qe = rend[w];
+        for (unsigned long long q = qb; q < qe; ++q)
+          if (rsrc[q] == (uint32_t)v && (rslot[q] & 15u) == j) {
+            atomicOr(&rfail[q >> 5], 1u << (q & 31));
+            break;
+          }
+      }
     }
-    rfail[w] = bits;
   }
 }
 
@@ -1339,11 +1349,13 @@ hipError_t pp_rev_fill_range(const uint8_t* deg, const uint32_t* ids, uint64_t n
   return hipGetLastError();
 }
 
-hipError_t pp_rfail_build(const DevState& s, const unsigned long long* rend, const uint32_t* rsrc, uint32_t* rfail,
-                          hipStream_t st) {
+hipError_t pp_rfail_build(const DevState& s, const unsigned long long* rend, const uint32_t* rsrc,
+                          const uint8_t* rslot, uint32_t* rfail, hipStream_t st) {
   const uint64_t NW = (s.n * s.stride + 31) >> 5;  // at most
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((NW + kPPBlock - 1) / kPPBlock, 8192);
-  hipLaunchKernelGGL(k_pp_rfail, dim3(blocks ? blocks : 1), dim3(kPPBlock), 0, st, s, rend, rsrc, rfail);
+  hipError_t e = hipMemsetAsync(rfail, 0, NW * 4, st);
+  if (e != hipSuccess) return e;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.W + kPPBlock - 1) / kPPBlock, 8192);
+  hipLaunchKernelGGL(k_pp_rfail, dim3(blocks ? blocks : 1), dim3(kPPBlock), 0, st, s, rend, rsrc, rslot, rfail);
   return hipGetLastError();
 }
 
