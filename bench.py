@@ -13,7 +13,12 @@ in HBM before the timed region; the overlay build is timed separately.
 Multi-GPU: one process per GPU; each rank runs an independent trial (its own
 overlay, trial = rank) -- batched Monte Carlo trials with no data-path
 collective, so "scaling" is weak and value = all ranks' delivered sends / the
-slowest rank's time.  `value` counts delivered sends (friend slots not
+slowest rank's time.  BASELINE.json's 8-GPU target is ONE N = 1e9 run across
+the GPUs: the line's top-level `strong_scaling` block reports exactly that --
+the C5 flood and the C5 push-pull broadcast node-range sharded over the ranks
+(one run, total work fixed), with every rank's device time beside the wall;
+at --gpus 1 the block holds the same workloads on the one GPU (the headline
+broadcast and the unsharded push-pull), so the 1 -> N ratio is explicit.  `value` counts delivered sends (friend slots not
 dropped, simulator.go:144-145); the reference's TotalMessage (:111) also leaves
 out receipts at crashed nodes and is reported as config.messages_per_step.
 
@@ -288,6 +293,7 @@ def main():
                                              lambda: pushpull_sharded(a, gs, rank, world, local, dist))
         if world == 1 and a.shard_scaling:
             ext["c4_shards_inproc"] = guarded("c4_shards_inproc", lambda: shards_inproc(a, gs))
+        out.line["strong_scaling"] = strong_scaling_block(world, out.line, ext)
     out.disarm()
 
     cpu = None
@@ -297,6 +303,35 @@ def main():
     out.emit()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def strong_scaling_block(world, line, ext):
+    """BASELINE.json's multi-GPU target as measured: ONE N = 1e9 broadcast over
+    `world` GPUs (total work fixed), beside the weak-scaling headline.  At
+    world > 1: the flood and the push-pull runs node-range sharded over the
+    ranks (c5_flood_sharded, c5_pushpull_sharded: wall time = the slowest
+    rank's, device time of every rank from its GS_FLAG_TIMING run); at
+    world == 1 the same workloads on the one GPU (the headline broadcast and
+    the unsharded push-pull) -- the 1-GPU end of the curve."""
+    ext = ext or {}
+    out = {"n_gpus": world, "scaling": "strong",
+           "workload": "one N=1e9 broadcast (C5 parameters) node-range sharded over the GPUs"}
+    if world > 1:
+        fl, pp = ext.get("c5_flood_sharded") or {}, ext.get("c5_pushpull_sharded") or {}
+        out["flood"] = {k: fl.get(k) for k in ("value", "unit", "ms_per_step", "device_ms_per_step",
+                                               "device_ms_per_rank", "wall_over_device", "status", "error")
+                        if k in fl}
+        out["pushpull"] = {k: pp.get(k) for k in ("value", "unit", "ms_per_step", "rounds_to_99", "status",
+                                                  "placement", "error") if k in pp}
+    else:
+        roof = line.get("roofline") or {}
+        out["flood"] = {"value": line.get("value"), "unit": line.get("unit"), "ms_per_step": line.get("ms_per_step"),
+                        "device_ms_per_step": roof.get("broadcast_device_ms"),
+                        "device_ms_per_rank": [roof.get("broadcast_device_ms")], "status": line["config"].get("status")}
+        pp = ext.get("pushpull") or {}
+        out["pushpull"] = {k: pp.get(k) for k in ("value", "unit", "ms_per_step", "rounds_to_99", "status", "error")
+                           if k in pp}
+    return out
 
 
 def failed_mask(n, frac, seed):
@@ -494,6 +529,12 @@ def flood_sharded(a, gs, rank, world, local, dist, n, fanout, fanin, crashrate, 
         sim.set_flags(False)
         kern = tm["deliver_ms"] + tm["resolve_ms"]
         launches = max(int(tm["resolve_launches"]), 1)
+        per_rank = [round(kern, 3)]
+        if dist is not None:
+            kt = torch.zeros(world, dtype=torch.float64, device="cuda")
+            kt[rank] = kern
+            dist.all_reduce(kt, op=dist.ReduceOp.SUM)
+            per_rank = [round(float(x), 3) for x in kt.cpu()]
         shard_sent = tot["sent"] / world  # a shard's share of the deliveries (balanced ranges)
         ach = BYTES_PER_SEND * shard_sent / (kern * 1e-3) / 1e9 if kern > 0 else 0.0
         log(f"{name} sharded x{world}: {dt * 1e3 / steps:.1f} ms per broadcast, {tot['sent'] / (dt / steps):.3e} msgs/s")
@@ -501,6 +542,7 @@ def flood_sharded(a, gs, rank, world, local, dist, n, fanout, fanin, crashrate, 
                 "ms_per_step": round(dt * 1e3 / steps, 3), "steps": steps, "n": cfg.n, "fanout": fanout,
                 # wall (device-driven windows) over this rank's kernel time (GS_FLAG_TIMING run)
                 "device_ms_per_step": round(kern, 3), "wall_over_device": round(dt * 1e3 / steps / kern, 4) if kern else None,
+                "device_ms_per_rank": per_rank,
                 "fanin": fanin, "ticks": tot["tick"], "status": STATUS[status],
                 "coverage": round(tot["received"] / cfg.n, 6),
                 "delivered_per_step": tot["sent"], "messages_per_step": tot["messages"],

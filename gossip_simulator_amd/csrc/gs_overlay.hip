@@ -46,7 +46,10 @@
 namespace gs {
 namespace {
 
-constexpr uint32_t kMaxRing = 1024;
+// Buckets in the overlay's ring of blocks: NB = ceil(R / L) + 2 <= kMaxRing
+// (the scatter's and the process kernel's LDS histograms hold kMaxRing), so
+// delayhigh <= kMaxRing - 2 at one tick per block
+constexpr uint32_t kMaxRing = 1026;
 constexpr uint32_t kScatterBlock = 256;
 constexpr uint32_t kScatterIPT = 8;
 
@@ -395,10 +398,10 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
   p.delay_low = delay_low;
   p.delay_span = (uint32_t)(delay_high - delay_low);
   p.key = key;
-  if (p.R > kMaxRing) {
+  if (p.R + 2 > kMaxRing) {
     res->rc = GS_EINVAL;
     snprintf(res->msg, sizeof(res->msg), "delayhigh %d exceeds the overlay ring limit %u",
-             delay_high, kMaxRing);
+             delay_high, kMaxRing - 2);
     return res->rc;
   }
   {
@@ -423,7 +426,7 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
     p.TB = 0;
     while ((1u << p.TB) < p.L) ++p.TB;
     // the ring: an event arrives at most delay_high - 1 ticks after it is sent
-    p.NB = (p.R + p.L - 1) / p.L + 2;
+    p.NB = (p.R + p.L - 1) / p.L + 2;  // <= R + 2 <= kMaxRing (checked above)
   }
   const uint32_t NB = p.NB;
   // buffers live in the caller's workspace across builds (batched C3 builds

@@ -25,6 +25,7 @@
 // in front of them, so the early and late rounds, where almost every call is
 // decided by the summaries, cost the table stream only.
 #include <algorithm>
+#include <vector>
 
 #include <hipcub/hipcub.hpp>
 
@@ -1134,6 +1135,11 @@ __global__ __launch_bounds__(kPPBlock) void k_rev_fill_range(const uint8_t* deg,
 // thread per failed-set word, and for each failed caller v and slot j the
 // in-edge (v, j) is found in friend w's short in-list (a pass over every
 // in-edge with a gather of its caller's failed word took 175 ms at N = 1e9).
+// In-lists longer than this are not scanned per failed caller (the scan is
+// the friend's whole in-list, so a hub listed by many failed callers would
+// cost quadratically): k_pp_rfail_hubs walks them once instead.
+constexpr uint32_t kRfailScan = 64;
+
 __global__ __launch_bounds__(kPPBlock) void k_pp_rfail(const DevState s, const unsigned long long* __restrict__ rend,
                                                        const uint32_t* __restrict__ rsrc,
                                                        const uint8_t* __restrict__ rslot, uint32_t* __restrict__ rfail) {
@@ -1146,11 +1152,36 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_rfail(const DevState s, const u
       for (uint32_t j = 0; j < d; ++j) {
         const uint32_t w = s.ids[v * s.stride + j];
         const unsigned long long qb = w ? rend[w - 1] : 0ull, qe = rend[w];
+        if (qe - qb > kRfailScan) continue;  // a hub: k_pp_rfail_hubs
         for (unsigned long long q = qb; q < qe; ++q)
           if (rsrc[q] == (uint32_t)v && (rslot[q] & 15u) == j) {
             atomicOr(&rfail[q >> 5], 1u << (q & 31));
             break;
           }
+      }
+    }
+  }
+}
+
+// The in-edges of every node with more than kRfailScan of them: one wave per
+// such node walks its in-list once and marks the edges whose caller failed
+// (linear in the hubs' in-degrees).
+__global__ __launch_bounds__(kPPBlock) void k_pp_rfail_hubs(const DevState s, const unsigned long long* __restrict__ rend,
+                                                            const uint32_t* __restrict__ rsrc,
+                                                            uint32_t* __restrict__ rfail) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  for (uint64_t w0 = wave * 64; w0 < s.n; w0 += nwaves * 64) {
+    // the wave's 64 candidate nodes, one per lane; then each hub among them in turn
+    const uint64_t w = w0 + lane;
+    const unsigned long long qe = w < s.n ? rend[w] : 0ull, qb = w < s.n && w ? rend[w - 1] : 0ull;
+    for (unsigned long long hubs = __ballot(w < s.n && qe - qb > kRfailScan); hubs; hubs &= hubs - 1) {
+      const uint32_t h = (uint32_t)__builtin_ctzll(hubs);
+      const unsigned long long hb = __shfl(qb, h, 64), he = __shfl(qe, h, 64);
+      for (unsigned long long q = hb + lane; q < he; q += 64) {
+        const uint32_t v = rsrc[q];
+        if ((s.crash[v >> 6] >> (v & 63)) & 1ull) atomicOr(&rfail[q >> 5], 1u << (q & 31));
       }
     }
   }
@@ -1211,6 +1242,179 @@ __global__ void k_pp_seed(const DevState s, unsigned long long* next, uint32_t n
   }
 }
 
+
+// ---- reverse table by partitioning (pp_rev_build_part) ----------------------
+// The in-edges (v, j) -> u of the whole table, without a random atomic per
+// edge (k_rev_count + k_rev_fill make two, 0.85 s at N = 1e9): a histogram of
+// the targets' 2^22-node coarse bins (exact coarse regions), a coarse
+// partition of the edges as 8-byte records (u mod 2^22 | v << 22 | slot byte
+// << 53), a fine partition of each coarse region by the 16384-node bucket,
+// and one workgroup per bucket that counts its targets' in-edges in LDS, writes
+// their rend and places rsrc / rslot.  The order of a node's in-list is free
+// (every use of the reverse table is order-independent, as with the atomic
+// fill).
+constexpr uint32_t kRvShift = 22;            // coarse bin = u >> 22
+constexpr uint32_t kRvBins = 512;            // n < 2^31
+constexpr uint32_t kRvBlock = 1024;
+constexpr uint32_t kRvRows = 2 * kRvBlock;   // rows per coarse-pass round
+constexpr uint32_t kRvTile = 16 * kRvBlock;  // records per fine-pass tile
+
+__device__ __forceinline__ uint8_t rv_slot_byte(uint32_t stride, uint32_t j, uint32_t d) {
+  return (uint8_t)(pp_rslot_packed(stride) ? j | (d - 1) << 4 : j);
+}
+
+__global__ __launch_bounds__(kRvBlock) void k_rv_hist(const DevState s, unsigned long long* chist) {
+  __shared__ uint32_t h[kRvBins];
+  for (uint32_t b = threadIdx.x; b < kRvBins; b += kRvBlock) h[b] = 0;
+  __syncthreads();
+  for (uint64_t v = (uint64_t)blockIdx.x * kRvBlock + threadIdx.x; v < s.n; v += (uint64_t)gridDim.x * kRvBlock) {
+    const uint32_t d = s.deg[v];
+    for (uint32_t j = 0; j < d; ++j) atomicAdd(&h[s.ids[v * s.stride + j] >> kRvShift], 1u);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < kRvBins; b += kRvBlock)
+    if (h[b]) atomicAdd(&chist[b], (unsigned long long)h[b]);
+}
+
+// Rounds of kRvRows rows: count per coarse bin in LDS, one reservation per
+// (round, bin), then every record to its bin's run (the rows re-read from L2).
+__global__ __launch_bounds__(kRvBlock) void k_rv_coarse(const DevState s, const unsigned long long* __restrict__ cstart,
+                                                        unsigned long long* __restrict__ cfill,
+                                                        unsigned long long* __restrict__ rec) {
+  __shared__ uint32_t cnt[kRvBins], off[kRvBins];
+  __shared__ unsigned long long gb[kRvBins];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t rounds = (s.n + kRvRows - 1) / kRvRows;
+  for (uint64_t r = blockIdx.x; r < rounds; r += gridDim.x) {
+    for (uint32_t b = tid; b < kRvBins; b += kRvBlock) { cnt[b] = 0; off[b] = 0; }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+      const uint64_t v = r * kRvRows + k * kRvBlock + tid;
+      if (v >= s.n) continue;
+      const uint32_t d = s.deg[v];
+      for (uint32_t j = 0; j < d; ++j) atomicAdd(&cnt[s.ids[v * s.stride + j] >> kRvShift], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = tid; b < kRvBins; b += kRvBlock)
+      if (cnt[b]) gb[b] = cstart[b] + atomicAdd(&cfill[b], (unsigned long long)cnt[b]);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+      const uint64_t v = r * kRvRows + k * kRvBlock + tid;
+      if (v >= s.n) continue;
+      const uint32_t d = s.deg[v];
+      for (uint32_t j = 0; j < d; ++j) {
+        const uint32_t u = s.ids[v * s.stride + j], b = u >> kRvShift;
+        const unsigned long long pos = gb[b] + atomicAdd(&off[b], 1u);
+        rec[pos] = (u & ((1u << kRvShift) - 1)) | (v << kRvShift) |
+                   ((unsigned long long)rv_slot_byte(s.stride, j, d) << 53);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Tiles of a coarse region -> its fine regions (bits 14..21 of u): LDS counts,
+// one reservation per (tile, bucket), records placed by offset atomics.  A
+// fine region past its planned capacity sets *ovf (the build falls back).
+__global__ __launch_bounds__(kRvBlock) void k_rv_fine(const unsigned long long* __restrict__ rec,
+                                                      const unsigned long long* __restrict__ cstart,
+                                                      const unsigned long long* __restrict__ cend,
+                                                      const uint32_t* __restrict__ tpre, uint32_t nbins,
+                                                      const unsigned long long* __restrict__ fstart,
+                                                      unsigned long long* __restrict__ ffill,
+                                                      unsigned long long* __restrict__ frec, uint32_t* ovf) {
+  __shared__ uint32_t cnt[256], off[256];
+  __shared__ unsigned long long gb[256], ge[256];
+  __shared__ uint32_t s_tp[kRvBins + 1];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i <= nbins; i += kRvBlock) s_tp[i] = tpre[i];
+  __syncthreads();
+  const uint32_t ntiles = s_tp[nbins];
+  for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    uint32_t lo = 0, hi = nbins - 1;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (s_tp[mid] <= t) lo = mid; else hi = mid - 1;
+    }
+    const uint32_t c = lo;
+    const unsigned long long b0 = cstart[c] + (unsigned long long)(t - s_tp[c]) * kRvTile, be = cend[c];
+    if (tid < 256) { cnt[tid] = 0; off[tid] = 0; }
+    __syncthreads();
+    unsigned long long r[kRvTile / kRvBlock];
+#pragma unroll
+    for (uint32_t k = 0; k < kRvTile / kRvBlock; ++k) {
+      const unsigned long long i = b0 + k * kRvBlock + tid;
+      r[k] = i < be ? rec[i] : ~0ull;
+      if (r[k] != ~0ull) atomicAdd(&cnt[(r[k] >> 14) & 255], 1u);
+    }
+    __syncthreads();
+    if (tid < 256 && cnt[tid]) {
+      const size_t fb = (size_t)c * 256 + tid;
+      gb[tid] = fstart[fb] + atomicAdd(&ffill[fb], (unsigned long long)cnt[tid]);
+      ge[tid] = fstart[fb + 1];
+      if (gb[tid] + cnt[tid] > ge[tid]) atomicOr(ovf, 1u);
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kRvTile / kRvBlock; ++k)
+      if (r[k] != ~0ull) {
+        const uint32_t d = (r[k] >> 14) & 255;
+        const unsigned long long pos = gb[d] + atomicAdd(&off[d], 1u);
+        if (pos < ge[d]) frec[pos] = r[k];
+      }
+    __syncthreads();
+  }
+}
+
+// One workgroup per 16384-node bucket: in-degree counts in LDS, the bucket's
+// rend (end of each node's in-edges), then rsrc / rslot in place.
+__global__ __launch_bounds__(kRvBlock) void k_rv_final(const unsigned long long* __restrict__ frec,
+                                                       const unsigned long long* __restrict__ fstart,
+                                                       const unsigned long long* __restrict__ ffill,
+                                                       const unsigned long long* __restrict__ bbase, uint64_t n,
+                                                       unsigned long long* __restrict__ rend, uint32_t* __restrict__ rsrc,
+                                                       uint8_t* __restrict__ rslot) {
+  __shared__ uint32_t cnt[16384];
+  __shared__ unsigned long long s_x[kRvBlock / 64];
+  const uint32_t tid = threadIdx.x, b = blockIdx.x;
+  const unsigned long long M = ffill[b], f0 = fstart[b], ob = bbase[b];
+  for (uint32_t i = tid; i < 16384; i += kRvBlock) cnt[i] = 0;
+  __syncthreads();
+  for (unsigned long long i = tid; i < M; i += kRvBlock) atomicAdd(&cnt[frec[f0 + i] & 16383], 1u);
+  __syncthreads();
+  // exclusive offsets: 16 consecutive counters per thread
+  uint32_t loc[16], sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k) { loc[k] = cnt[tid * 16 + k]; sum += loc[k]; }
+  const uint32_t lane = tid & 63, wv = tid >> 6;
+  uint32_t x = sum;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_x[wv] = x;
+  __syncthreads();
+  uint32_t before = 0;
+  for (uint32_t q = 0; q < wv; ++q) before += (uint32_t)s_x[q];
+  uint32_t a = before + x - sum;
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k) {
+    const uint64_t u = (uint64_t)b * 16384 + tid * 16 + k;
+    cnt[tid * 16 + k] = a;
+    a += loc[k];
+    if (u < n) rend[u] = ob + a;  // the end of u's in-edges
+  }
+  __syncthreads();
+  for (unsigned long long i = tid; i < M; i += kRvBlock) {
+    const unsigned long long rc = frec[f0 + i];
+    const unsigned long long at = ob + atomicAdd(&cnt[rc & 16383], 1u);
+    rsrc[at] = (uint32_t)((rc >> kRvShift) & 0x7FFFFFFFull);
+    rslot[at] = (uint8_t)(rc >> 53);
+  }
+}
 }  // namespace
 
 // Every context sets grecv / gcrash (ctx_setup: = recv / crash; push-pull
@@ -1320,6 +1524,100 @@ hipError_t pp_rev_build(const DevState& s, unsigned long long* rend, uint32_t* r
   return hipGetLastError();
 }
 
+// The reverse table by partitioning (the k_rv_* kernels above): host-paced
+// (three small read-backs), temporaries allocated here and freed before
+// return.  An error (no memory for the ~17 B per edge of temporaries, or a
+// fine region past its planned size on a skewed table) leaves the outputs
+// unspecified: the caller then builds with pp_rev_build.
+hipError_t pp_rev_build_part(const DevState& s, unsigned long long* rend, uint32_t* rsrc, uint8_t* rslot,
+                             hipStream_t st) {
+  if (!s.n || s.n >= (1ull << 31)) return hipErrorInvalidValue;
+  const uint64_t n = s.n, nbins = (n + (1ull << kRvShift) - 1) >> kRvShift, nbf = (n + 16383) >> 14;
+  // small device arrays: chist[512] | cstart[513] | cend[512] | fstart[nbf+1] | ffill[nbf] | bbase[nbf] | tpre[513] | ovf
+  const size_t small = 8 * (512 + 513 + 512 + (nbf + 1) + nbf + nbf) + 4 * 513 + 64;
+  char* sm = nullptr;
+  hipError_t e = hipMalloc(&sm, small);
+  if (e != hipSuccess) return e;
+  unsigned long long* d_chist = (unsigned long long*)sm;
+  unsigned long long* d_cstart = d_chist + 512;
+  unsigned long long* d_cend = d_cstart + 513;
+  unsigned long long* d_fstart = d_cend + 512;
+  unsigned long long* d_ffill = d_fstart + nbf + 1;
+  unsigned long long* d_bbase = d_ffill + nbf;
+  uint32_t* d_tpre = (uint32_t*)(d_bbase + nbf);
+  uint32_t* d_ovf = d_tpre + 513;
+  unsigned long long *rec = nullptr, *frec = nullptr;
+  std::vector<unsigned long long> h(512, 0), cs(513, 0), ce(512, 0), fs(nbf + 1, 0), ff(nbf, 0), bb(nbf, 0);
+  std::vector<uint32_t> tp(513, 0);
+  uint32_t ovf = 0;
+  unsigned long long E = 0, F = 0;
+  const uint32_t grid = 512;
+  auto done = [&](hipError_t r) {
+    (void)hipStreamSynchronize(st);
+    if (rec) (void)hipFree(rec);
+    if (frec) (void)hipFree(frec);
+    (void)hipFree(sm);
+    return r;
+  };
+#define RV(x)                          \
+  do {                                 \
+    hipError_t e_ = (x);               \
+    if (e_ != hipSuccess) return done(e_); \
+  } while (0)
+  RV(hipMemsetAsync(sm, 0, small, st));
+  hipLaunchKernelGGL(k_rv_hist, dim3(grid), dim3(kRvBlock), 0, st, s, d_chist);
+  RV(hipGetLastError());
+  RV(hipMemcpyAsync(h.data(), d_chist, 512 * 8, hipMemcpyDeviceToHost, st));
+  RV(hipStreamSynchronize(st));
+  // exact coarse regions; a fine region planned at 1.125 x its node share of
+  // its coarse region + 1024
+  for (uint64_t c = 0; c < nbins; ++c) {
+    cs[c + 1] = cs[c] + h[c];
+    ce[c] = cs[c] + h[c];
+    tp[c + 1] = tp[c] + (uint32_t)((h[c] + kRvTile - 1) / kRvTile);
+    const uint64_t nf = std::min<uint64_t>(256, nbf - c * 256);
+    const uint64_t nodes_c = std::min<uint64_t>(1ull << kRvShift, n - (c << kRvShift));
+    for (uint64_t d = 0; d < nf; ++d) {
+      const uint64_t fb = c * 256 + d, nodes_b = std::min<uint64_t>(16384, n - fb * 16384);
+      const unsigned long long share = (unsigned long long)((double)h[c] * nodes_b / nodes_c);
+      fs[fb + 1] = fs[fb] + share + share / 8 + 1024;
+    }
+  }
+  E = cs[nbins];
+  F = fs[nbf];
+  RV(hipMemcpyAsync(d_cstart, cs.data(), 513 * 8, hipMemcpyHostToDevice, st));
+  RV(hipMemcpyAsync(d_cend, ce.data(), 512 * 8, hipMemcpyHostToDevice, st));
+  RV(hipMemcpyAsync(d_fstart, fs.data(), (nbf + 1) * 8, hipMemcpyHostToDevice, st));
+  RV(hipMemcpyAsync(d_tpre, tp.data(), 513 * 4, hipMemcpyHostToDevice, st));
+  RV(hipMalloc(&rec, std::max<unsigned long long>(E, 1) * 8));
+  RV(hipMalloc(&frec, std::max<unsigned long long>(F, 1) * 8));
+  {
+    unsigned long long* d_cfill = d_chist;  // reused: the fills of the coarse pass
+    RV(hipMemsetAsync(d_cfill, 0, 512 * 8, st));
+    const uint64_t rounds = (n + kRvRows - 1) / kRvRows;
+    hipLaunchKernelGGL(k_rv_coarse, dim3((uint32_t)std::min<uint64_t>(rounds, grid)), dim3(kRvBlock), 0, st, s,
+                       d_cstart, d_cfill, rec);
+    RV(hipGetLastError());
+  }
+  if (tp[nbins]) {
+    hipLaunchKernelGGL(k_rv_fine, dim3(std::min<uint32_t>(tp[nbins], grid)), dim3(kRvBlock), 0, st, rec, d_cstart,
+                       d_cend, d_tpre, (uint32_t)nbins, d_fstart, d_ffill, frec, d_ovf);
+    RV(hipGetLastError());
+  }
+  RV(hipMemcpyAsync(ff.data(), d_ffill, nbf * 8, hipMemcpyDeviceToHost, st));
+  RV(hipMemcpyAsync(&ovf, d_ovf, 4, hipMemcpyDeviceToHost, st));
+  RV(hipStreamSynchronize(st));
+  if (ovf) return done(hipErrorInvalidValue);  // a skewed table: the atomic build
+  for (uint64_t b = 1; b < nbf; ++b) bb[b] = bb[b - 1] + ff[b - 1];
+  RV(hipMemcpyAsync(d_bbase, bb.data(), nbf * 8, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_rv_final, dim3((uint32_t)nbf), dim3(kRvBlock), 0, st, frec, d_fstart, d_ffill, d_bbase, n, rend,
+                     rsrc, rslot);
+  RV(hipGetLastError());
+  RV(hipMemcpyAsync(rend + n, &E, 8, hipMemcpyHostToDevice, st));
+#undef RV
+  return done(hipSuccess);
+}
+
 hipError_t pp_fmask_build(const DevState& s, const unsigned long long* rend, const uint32_t* rsrc,
                           const uint8_t* rslot, uint8_t* fmask, hipStream_t st) {
   hipError_t e = hipMemsetAsync(fmask, 0, (s.n + 3) & ~3ull, st);
@@ -1356,6 +1654,8 @@ hipError_t pp_rfail_build(const DevState& s, const unsigned long long* rend, con
   if (e != hipSuccess) return e;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.W + kPPBlock - 1) / kPPBlock, 8192);
   hipLaunchKernelGGL(k_pp_rfail, dim3(blocks ? blocks : 1), dim3(kPPBlock), 0, st, s, rend, rsrc, rslot, rfail);
+  const uint32_t hblocks = (uint32_t)std::min<uint64_t>((s.n + 64 * (kPPBlock / 64) - 1) / (64 * (kPPBlock / 64)), 4096);
+  hipLaunchKernelGGL(k_pp_rfail_hubs, dim3(hblocks ? hblocks : 1), dim3(kPPBlock), 0, st, s, rend, rsrc, rfail);
   return hipGetLastError();
 }
 

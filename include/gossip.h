@@ -128,6 +128,8 @@ typedef struct gs_timing {
   uint64_t pp_answer_rounds; /* push-pull: dense rounds of this broadcast run pull-answer        */
   uint64_t dd_fallbacks;     /* device-driven shard windows stopped by an overflow and redone
                               * host-driven (cumulative; a buffer that fits makes it stop growing) */
+  uint64_t pp_rev_part;      /* push-pull: 1 if the last reverse table was built by partitioning the
+                              * edges, 0 by the atomic count + fill (GS_PP_REV_ATOMIC, or a fallback) */
 } gs_timing;
 
 /* gs_run status */

@@ -222,6 +222,29 @@ def test_overlay_tick_blocks_match_oracle(gs, oracle, monkeypatch, block, dlow, 
         assert np.array_equal(masked(gdeg, gids), masked(deg, ids))
 
 
+def test_overlay_longest_ring_and_its_limit(gs, oracle):
+    """the overlay's ring of blocks holds ceil(R / L) + 2 buckets,
+    and its LDS histograms kMaxRing = 1026 of them.  delayhigh = 1024 (the
+    longest ring, 1026 buckets) must build the oracle's overlay; 1025 must be
+    refused (GS_EINVAL) instead of overrunning the histograms."""
+    from gossip_simulator_amd import _lib
+    kw = dict(n=3000, fanout=3, fanin=6, delay_low=10, delay_high=1024, drop_rate=0.1,
+              crash_rate=0.001, seed=11, trial=0)
+    deg, ids, wins, final = oracle.overlay(oracle.make_params(**kw))
+    with gs.Simulator(cfg_from(gs, kw)) as sim:
+        gw, gf = sim.build_overlay()
+        assert gf == final
+        assert [tuple(w) for w in gw] == [tuple(w) for w in wins]
+        gdeg, gids = sim.read_peers()
+        assert np.array_equal(gdeg, deg)
+        assert np.array_equal(masked(gdeg, gids), masked(deg, ids))
+    kw["delay_high"] = 1025
+    with gs.Simulator(cfg_from(gs, kw)) as sim:
+        with pytest.raises(_lib.GossipError) as e:
+            sim.build_overlay()
+        assert e.value.code == _lib.GS_EINVAL and "ring limit" in str(e.value)
+
+
 @pytest.mark.parametrize("mode", ["tick", "hop"])
 def test_c2_full_size_bit_exact(gs, oracle, mode):
     """Config C2: N=1e6, fanout 3 (fanin 6); GPU overlay + broadcast vs oracle, per poll."""

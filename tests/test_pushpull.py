@@ -178,6 +178,52 @@ def test_gpu_pushpull_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac, rounds,
             assert tm["pp_answer_rounds"] + tm["pp_bottom_rounds"] == r + 1 - tm["pp_early_rounds"]
         if rounds == "early":
             assert tm["pp_early_rounds"] >= 1
+        if rounds != "dense" and n > 100:
+            # the reverse table came from the edge partition (k_rv_*), not the atomic fill
+            assert tm["pp_rev_part"] == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rounds", ["answer", "bottom", "auto"])
+def test_gpu_pushpull_new_mask_and_table_on_one_context(oracle, rounds):
+    """the per-(table, failure mask) caches (live-caller counts,
+    the has-failed-friend bits, the failed-caller bit per in-edge) must follow
+    a new mask and a new table on the SAME context: three broadcasts -- mask A,
+    then mask B, then a new table with mask B -- each bit-exact per round.
+    Both tables carry a hub (friend 0 of every node) whose in-list is longer
+    than the per-caller scan bound, so the failed-caller bits of its in-edges
+    come from the hub pass (a quadratic scan before)."""
+    import gossip_simulator_amd as gs
+    gs.load()
+    kw = dict(PP, n=20000)
+    n = kw["n"]
+    rng = np.random.default_rng(9)
+    tables = []
+    for seed, hub in ((3, 0), (4, 5)):
+        deg, ids = random_table(n, 6, 5, 6, seed=seed)
+        ids = ids.copy()
+        ids[np.arange(n) != hub, 0] = hub
+        tables.append((deg, ids))
+    masks = [words_of(rng.random(n) < 0.01), words_of(rng.random(n) < 0.03)]
+    cfg = gs.Config(n=n, fanout=kw["fanout"], fanin=kw["fanin"], delaylow=kw["delay_low"],
+                    delayhigh=kw["delay_high"], droprate=kw["drop_rate"], crashrate=kw["crash_rate"],
+                    seed=kw["seed"], trial=kw["trial"], model="pushpull", pp_rounds=rounds)
+    with gs.Simulator(cfg) as sim:
+        for case, (ti, mi) in enumerate(((0, 0), (0, 1), (1, 1))):
+            deg, ids = tables[ti]
+            if case == 0 or ti != 0:
+                sim.load_peers(deg, ids)
+            sim.set_failed(masks[mi])
+            e = oracle.Engine(oracle.make_params(**kw), deg, ids)
+            e.set_failed(masks[mi])
+            e.begin(-1)
+            sim.broadcast_begin(-1)
+            for r in range(80):
+                a, b = e.step(1), sim.step(1)
+                assert np.array_equal(a, b), f"broadcast {case}, round {r + 1}:\n{a}\n{b}"
+                if oracle.covered(int(a[0, 4]), n) or int(a[0, 4]) == 0:
+                    break
+            assert sha(e.received()) == sha(sim.received()), f"broadcast {case}"
 
 
 @pytest.mark.gpu
