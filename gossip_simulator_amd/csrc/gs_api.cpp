@@ -196,9 +196,6 @@ bool grow(Buf& b, size_t bytes) {
   return true;
 }
 
-// u16 units the fine-message buffer holds for the window kernels (32 of slack)
-unsigned long long buf_cap16(const Buf& b) { return b.bytes / 2 > 32 ? b.bytes / 2 - 32 : 0; }
-
 #define CK(c, expr)                                                                   \
   do {                                                                                \
     hipError_t e_ = (expr);                                                           \
@@ -258,8 +255,8 @@ int alloc_window(gs_ctx* c) {
   const size_t units = (size_t)kMaxWindow * w.nfine + 1;
   const size_t b_fc = al((size_t)w.R * w.nfine * 4), b_units = al(units * 8),
                b_small = al(kRegions * 8) * 2 + al((kRegions + 1) * 8) + al((kRegions + 1) * 4) + al(kMaxWindow * 8),
-               b_fhist = al(((size_t)w.ncoarse * kDigits + 1) * 8),
-               b_fbase = al(((size_t)w.ncoarse * kDigits + 1) * 8), b_ffill = al((size_t)w.ncoarse * kDigits * 8),
+               b_fhist = al(((size_t)w.ncoarse * 256 + 1) * 8), b_fbase = al(((size_t)w.nfine + 1) * 8),
+               b_ffill = al((size_t)w.nfine * 8),
                b_sst = al((size_t)kStatShards * kMaxWindow * kStatFields * 8),
                b_rlcnt = al((size_t)w.nfine * 4),
                b_tsum = al((size_t)w.ncoarse * kMaxWindow * 8) + al(((size_t)w.ncoarse + 1) * 8);
@@ -340,6 +337,7 @@ void refresh_window(gs_ctx* c) {
   w.ids = c->st.ids;
   w.recv = c->st.recv;
   w.crash = c->st.crash;
+  w.rollw = c->st.rollw;
   w.stats = c->st.stats;
   w.err = c->d_err;
   w.stride = c->st.stride;
@@ -614,7 +612,8 @@ int ctx_setup(gs_ctx* c, const gs_params* params, int device, bool shard, uint32
                b_clist = tick ? al((size_t)s.R * kShards * s.CS * 4) : 0,
                b_ccount = tick ? al((size_t)s.R * kShards * kCounterStride * 4) : 0,
                b_stats = al((size_t)kStatSlots * kStatFields * 8);
-  const size_t total = 2 * b_bits + b_next + b_ring + b_cflag + b_clist + b_ccount + b_stats + 256;
+  const size_t b_roll = c->win ? b_bits : 0;
+  const size_t total = 2 * b_bits + b_roll + b_next + b_ring + b_cflag + b_clist + b_ccount + b_stats + 256;
   c->state_bytes = total;
   if (hipMalloc(&c->d_state, total) != hipSuccess) {
     why = "cannot allocate " + std::to_string(total) + " bytes of device state";
@@ -623,6 +622,7 @@ int ctx_setup(gs_ctx* c, const gs_params* params, int device, bool shard, uint32
   char* q = (char*)c->d_state;
   s.recv = (unsigned long long*)q; q += b_bits;
   s.crash = (unsigned long long*)q; q += b_bits;
+  s.rollw = b_roll ? (uint32_t*)q : nullptr; q += b_roll;
   c->d_next = b_next ? (unsigned long long*)q : nullptr;
   c->d_ppsum = b_next ? (unsigned long long*)(q + al(s.W * 8)) : nullptr;
   q += b_next;
@@ -2152,13 +2152,13 @@ int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing, uint64_t tchunk
     if (L < Lw) RC(units(L));
     const unsigned long long T = Tn * w.stride;  // friend slots of the firing nodes
     plan_coarse(c, T, nullptr);
-    const uint64_t fcap = fine_units_bound(T, w.ncoarse, w.kc);  // u16 units
+    const uint64_t fcap = T + T / 8 + (uint64_t)w.ncoarse * 256 * 513 + 16;
     if (!grow(c->gmap, ((Tn + 63) / 64 + 1) * 4) || !grow(c->cmsg, (c->h_cap[kRegions] + 16) * 4) ||
-        !grow(c->fmsg, (fcap + 32) * 2))  // buf_cap16(fmsg) >= fcap (the device-driven windows' bound)
+        !grow(c->fmsg, (fcap + 16) * 4))  // buf_cap(fmsg) >= fcap (the device-driven windows' bound)
       return fail(c, GS_ENOMEM, "cannot allocate " + std::to_string(T) + " window messages");
     w.gmap = (uint32_t*)c->gmap.p;
     w.cmsg = (uint32_t*)c->cmsg.p;
-    w.fmsg = (uint16_t*)c->fmsg.p;
+    w.fmsg = (uint32_t*)c->fmsg.p;
     if (timing)
       while (c->ev.size() < (size_t)(widx + 1) * 5) {
         hipEvent_t ev;
@@ -2192,7 +2192,7 @@ int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing, uint64_t tchunk
         err = kErrFine;  // the fine regions must be redone as well
       }
       if (err & kErrFine) {
-        CK(c, hipMemsetAsync(w.fhist, 0, ((size_t)w.ncoarse * kDigits + 1) * 8, c->stream));
+        CK(c, hipMemsetAsync(w.fhist, 0, ((size_t)w.ncoarse * 256 + 1) * 8, c->stream));
         CK(c, win_plan(w, true, c->stream));
         CK(c, win_part2(w, T, false, c->stream));
         size_t need2 = 0;
@@ -2200,7 +2200,7 @@ int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing, uint64_t tchunk
         if (!grow(c->tmp, need2)) return fail(c, GS_ENOMEM, "cannot allocate scan scratch");
         need2 = c->tmp.bytes;
         CK(c, win_scan_fine(w, c->tmp.p, need2, c->stream));
-        CK(c, hipMemsetAsync(w.ffill, 0, (size_t)w.ncoarse * kDigits * 8, c->stream));
+        CK(c, hipMemsetAsync(w.ffill, 0, (size_t)w.nfine * 8, c->stream));
         CK(c, win_part2(w, T, true, c->stream));
         ++c->timing.exact_redos;
       }
@@ -2312,7 +2312,7 @@ int run_async(gs_ctx* c, uint64_t tend, uint32_t poll, uint64_t max_ticks, OnTic
   w.lstride = std::min<uint32_t>(std::max<int32_t>(c->p.delay_low, 1), kBitTicks);
   w.gmap = (uint32_t*)c->gmap.p;
   w.cmsg = (uint32_t*)c->cmsg.p;
-  w.fmsg = (uint16_t*)c->fmsg.p;
+  w.fmsg = (uint32_t*)c->fmsg.p;
   WinCtl h{};
   h.tnext = (uint32_t)(c->t + 1);
   h.tend = (uint32_t)std::min<uint64_t>(tend, 0xFFFFFFFFull);
@@ -2325,7 +2325,7 @@ int run_async(gs_ctx* c, uint64_t tend, uint32_t poll, uint64_t max_ticks, OnTic
   h.cover = cover_threshold(c->p.n);
   h.max_ticks = max_ticks;
   h.cmsg_cap = c->cmsg.bytes / 4 > 16 ? c->cmsg.bytes / 4 - 16 : 0;
-  h.fmsg_cap = buf_cap16(c->fmsg);
+  h.fmsg_cap = c->fmsg.bytes / 4 > 16 ? c->fmsg.bytes / 4 - 16 : 0;
   CK(c, hipMemcpyAsync(c->d_ctl, &h, sizeof h, hipMemcpyHostToDevice, c->stream));
   CK(c, hipMemsetAsync(w.tfires, 0, kMaxWindow * 8, c->stream));
   const uint64_t budget = (uint64_t)w.nfine * kWinSlotsPerBucket;
@@ -2784,12 +2784,12 @@ int shard_receive(gs_ctx* m, const ShardWin& sw, bool timing) {
   WinState& wr = m->wr;
   CK(m, hipSetDevice(m->dev));
   const uint64_t R = m->rtotal;
-  const uint64_t fcap = fine_units_bound(R, wr.ncoarse, wr.kc);  // u16 units
-  // (+32: buf_cap16's slack -- k_rtab checks the next device-driven window's
-  // bound against buf_cap16, so a buffer grown to exactly fcap aborted it)
-  if (!grow(m->fmsg, (fcap + 32) * 2))  // nothing resolved: every rank stops at the next gather
+  const uint64_t fcap = R + R / 8 + (uint64_t)wr.ncoarse * 256 * 513 + 16;
+  // (+16: buf_cap's slack -- k_rtab checks the next device-driven window's
+  // bound against buf_cap, so a buffer grown to exactly fcap aborted it)
+  if (!grow(m->fmsg, (fcap + 16) * 4))  // nothing resolved: every rank stops at the next gather
     return mark_nomem(m, "cannot allocate " + std::to_string(R) + " received messages");
-  wr.fmsg = m->ws.fmsg = (uint16_t*)m->fmsg.p;
+  wr.fmsg = m->ws.fmsg = (uint32_t*)m->fmsg.p;
   if (timing) CK(m, hipEventRecord(m->ev[4], m->stream));
   CK(m, win_plan(wr, false, m->stream));
   CK(m, win_part2(wr, R, true, m->stream));
@@ -2822,8 +2822,8 @@ int receiver_redo(gs_ctx* m, const ShardWin& sw) {
   CK(m, hipSetDevice(m->dev));
   RC(clear_part_flags(m));
   const uint64_t R = m->rtotal;
-  CK(m, hipMemsetAsync(wr.ffill, 0, (size_t)wr.ncoarse * kDigits * 8, m->stream));
-  CK(m, hipMemsetAsync(wr.fhist, 0, ((size_t)wr.ncoarse * kDigits + 1) * 8, m->stream));
+  CK(m, hipMemsetAsync(wr.ffill, 0, (size_t)wr.nfine * 8, m->stream));
+  CK(m, hipMemsetAsync(wr.fhist, 0, ((size_t)wr.ncoarse * 256 + 1) * 8, m->stream));
   CK(m, win_plan(wr, true, m->stream));
   CK(m, win_part2(wr, R, false, m->stream));
   size_t need = 0;
@@ -2831,7 +2831,7 @@ int receiver_redo(gs_ctx* m, const ShardWin& sw) {
   if (!grow(m->tmp, need)) return mark_nomem(m, "cannot allocate scan scratch");
   need = m->tmp.bytes;
   CK(m, win_scan_fine(wr, m->tmp.p, need, m->stream));
-  CK(m, hipMemsetAsync(wr.ffill, 0, (size_t)wr.ncoarse * kDigits * 8, m->stream));
+  CK(m, hipMemsetAsync(wr.ffill, 0, (size_t)wr.nfine * 8, m->stream));
   CK(m, win_part2(wr, R, true, m->stream));
   CK(m, win_resolve(wr, sw.t, sw.L, m->stream));
   CK(m, win_stats_reduce(wr, sw.t, sw.L, m->stream));
@@ -3132,7 +3132,7 @@ int dd_run(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t tend, uint32_t 
     h.cover = cover_threshold(N);
     h.max_ticks = max_ticks;
     h.cmsg_cap = buf_cap(ms[i]->cmsg);
-    h.fmsg_cap = buf_cap16(ms[i]->fmsg);
+    h.fmsg_cap = buf_cap(ms[i]->fmsg);
     h.xs_cap = buf_cap(ms[i]->xsend);
     h.xr_cap = buf_cap(ms[i]->xrecv);
   }
@@ -3160,7 +3160,7 @@ int dd_run(gs_ctx* acc, const std::vector<gs_ctx*>& ms, uint64_t tend, uint32_t 
     w.solo = solo ? 1u : 0u;
     w.gmap = (uint32_t*)m->gmap.p;
     w.cmsg = (uint32_t*)m->cmsg.p;
-    w.fmsg = (uint16_t*)m->fmsg.p;
+    w.fmsg = (uint32_t*)m->fmsg.p;
     ws[i] = w;
     if (solo) {
       wr[i] = w;

@@ -53,6 +53,7 @@ struct DevState {
   const uint32_t* ids;
   unsigned long long* recv;
   unsigned long long* crash;
+  uint32_t* rollw;         // window engine: crash-roll marks of the window (cleared by k_resolve)
   uint32_t* cnt;
   unsigned long long* ring;
   uint32_t* cflag;
@@ -89,30 +90,6 @@ constexpr uint32_t kFineLog = 14;               // 16384 nodes per fine bucket
 constexpr uint32_t kFineNodes = 1u << kFineLog;
 constexpr uint32_t kCoarseShift = kFineLog + 8; // 256 fine buckets per coarse bucket
 constexpr uint32_t kMaxWindow = 16;             // tick offset in 4 bits
-// Fine regions (k_part2 -> the resolve kernels): five per fine bucket f.
-// q = 0..3: the receipts at the bucket's quarter q (nodes q * 4096 .. + 4095)
-// that carry no crash roll, as u16 messages loc12 | k << 12; q = 4: the
-// receipts that carry a crash roll, as u32 messages loc14 | k << 14 | 1 << 18
-// (two u16 units each, at an even unit index).  Offsets, fills and counts are
-// in u16 units.  A coarse bucket's 1280 regions are q-major: region
-// (f >> 8) * kDigits + q * 256 + (f & 255) -- k_part2's digit of a message is
-// its region inside the coarse bucket.
-constexpr uint32_t kQuarterLog = 12;
-constexpr uint32_t kFineRegs = 5;
-constexpr uint32_t kRollReg = 4;
-constexpr uint32_t kDigits = 256 * kFineRegs;   // k_part2's digits (fine regions) per coarse bucket
-__host__ __device__ inline uint32_t fine_reg(uint32_t f, uint32_t q) { return (f >> 8) * kDigits + q * 256 + (f & 255); }
-// An upper bound (u16 units) on the fine plan of R messages over ncoarse
-// coarse buckets: k_plan's estimate gives each of a coarse bucket's fine
-// buckets 4 quarter regions of ceil(1.125 * cnt / (4 * nf)) + 128 (even) and a
-// roll region of 2 * (ceil(1.5 * cnt * kc / (100 * nf)) + 64), and an exact
-// plan needs at most R plain units + 2 per roll message + one unit of padding
-// per region.  Host and device (k_rtab) size and check the buffer with it.
-__host__ __device__ inline unsigned long long fine_units_bound(unsigned long long R, unsigned long long ncoarse,
-                                                               int32_t kc) {
-  const unsigned long long rolls = kc > 0 ? R * (unsigned long long)(kc > 100 ? 100 : kc) / 100 : 0;
-  return 2 * R + R / 4 + 3 * rolls + ncoarse * 256 * (4 * 131 + 2 * 66 + 8) + 64;
-}
 // Coarse regions: each of the 256 coarse bins has kCoarseSub sub-regions, one
 // per XCD (a block writes the sub-region of blockIdx % 8): the reservation
 // atomics of a bin spread over 8 addresses, and the runs written into one
@@ -147,7 +124,7 @@ struct WinCtl {
   uint32_t poll, pbase, stop, lmax;  // polls at pbase + k*poll (0: none); 1 + GS_RUN_* once stopped
   unsigned long long Tn, T;          // broadcasts firing in the window, their friend slots
   unsigned long long recv, crashed, pending, cover, max_ticks;  // poll rule state
-  unsigned long long cmsg_cap, fmsg_cap;  // message buffer capacities (u32 / u16 elements)
+  unsigned long long cmsg_cap, fmsg_cap;  // message buffer capacities (elements)
   unsigned long long xs_cap, xr_cap;      // device-driven shard windows of ranks: send / receive block buffers
 };
 constexpr uint32_t kStageWords = 8 + 16 * 8;  // per-window staging: snapshot + per-tick rows
@@ -157,6 +134,7 @@ struct WinState {
   const uint32_t* ids;
   unsigned long long* recv;
   unsigned long long* crash;
+  uint32_t* rollw;               // [2W] nodes with a crash-roll receipt in the window (k_part2 -> k_resolve)
   uint32_t* rlmsg;               // [nfine][kRolledCap] receipts at rolled nodes (k_resolve -> k_resolve_rolled)
   uint32_t* rlcnt;               // [nfine] their counts (zeroed by the consumer)
   unsigned long long* stats;
@@ -170,15 +148,15 @@ struct WinState {
   const uint32_t* pk;            // rows <= 6 slots: the sealed rows packed 5 per 128-B line, or null
   uint32_t noxcd;                // 1: k_part2 tiles in region order (GS_PART2_NOXCD=1, A/B); else dealt by XCD
   uint32_t* cmsg;                // coarse regions: u_in_coarse | k << 22
-  uint16_t* fmsg;                // fine regions (kFineRegs per fine bucket, u16 units; see kQuarterLog)
+  uint32_t* fmsg;                // fine regions:   u_in_fine   | k << 14
   unsigned long long* chist;     // [kRegions] exact coarse region counts (fallback)
   unsigned long long* ccap;      // [kRegions + 1] coarse region starts, region = bin * csub + sub
   const unsigned long long* ccap_end;  // [kRegions] region ends (null: ccap[r + 1])
   unsigned long long* cfill;     // [kRegions] coarse region fill
   uint32_t* tprefix;             // [kRegions + 1] part2 tiles per coarse region (prefix)
-  unsigned long long* fhist;     // [ncoarse*kDigits + 1] exact fine region sizes, u16 units (fallback)
-  unsigned long long* fstart;    // [ncoarse*kDigits + 1] fine region starts (fine_reg; u16 units, even)
-  unsigned long long* ffill;     // [ncoarse*kDigits] fine region fills (u16 units)
+  unsigned long long* fhist;     // [ncoarse*256 + 1] exact fine counts (fallback)
+  unsigned long long* fstart;    // [nfine + 1] fine region starts
+  unsigned long long* ffill;     // [nfine] fine region fill
   unsigned long long* tsum;      // [ncoarse][kMaxWindow] fires per (256-bucket tile, tick) (k_units)
   unsigned long long* toff;      // [ncoarse + 1] device-driven windows: firing index of each tile's first unit (k_cut)
   unsigned long long* sstats;    // [kStatShards][kMaxWindow][kStatFields] per-window partial counters
@@ -258,7 +236,6 @@ constexpr uint32_t kErrCoarse = 8;    // a coarse region overflowed its estimate
 constexpr uint32_t kErrFine = 16;     // a fine region overflowed its estimate
 constexpr uint32_t kErrAbort = 32;    // device-driven shard windows: a shard's window overflowed, every shard stops
 constexpr uint32_t kErrNoMem = 64;    // host-driven shard windows: a shard could not allocate (every rank returns)
-constexpr uint32_t kErrWide = 128;    // a coarse bucket's fine regions span >= 2^31 u16 units in one window (k_part2)
 // device-driven shard windows: a row of glay = kRegions fills, the flag word
 // (kErrCoarse), the capacities (elements) of the shard's fine buffer and, for
 // ranks, of its send / receive block buffers

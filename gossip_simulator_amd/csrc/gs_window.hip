@@ -131,32 +131,6 @@ __device__ __forceinline__ unsigned long long block_exscan256_u64(unsigned long 
   return before + x - v;
 }
 
-// Exclusive scan of one u64 per thread over a block of NW waves (s: NW words
-// of LDS); returns the thread's prefix, *total the block's sum.  Block-uniform.
-template <uint32_t NW>
-__device__ __forceinline__ unsigned long long block_exscan_u64(unsigned long long v, unsigned long long* s,
-                                                               unsigned long long* total) {
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  unsigned long long x = v;
-#pragma unroll
-  for (uint32_t o = 1; o < 64; o <<= 1) {
-    const unsigned long long y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) s[wv] = x;
-  __syncthreads();
-  unsigned long long before = 0, all = 0;
-#pragma unroll
-  for (uint32_t q = 0; q < NW; ++q) {
-    const unsigned long long t = s[q];
-    if (q < wv) before += t;
-    all += t;
-  }
-  __syncthreads();
-  *total = all;
-  return before + x - v;
-}
-
 // Units = (fine bucket f, tick k), bucket-major (u = f*Ls + k, Ls = the layout
 // stride: L, or lmax for device-driven windows): the L fire lists of one
 // bucket are expanded back to back, so friends-row lines that several ticks of
@@ -225,7 +199,7 @@ __device__ __forceinline__ void units_body(const WinState& w, uint32_t t0, uint3
   __syncthreads();
   if (threadIdx.x < L && s_t[threadIdx.x]) atomicAdd(&w.tfires[threadIdx.x], (unsigned long long)s_t[threadIdx.x]);
   for (uint32_t i = tid; i < kRegions; i += nth) { w.chist[i] = 0; w.cfill[i] = 0; }
-  for (uint32_t i = tid; i < w.ncoarse * kDigits; i += nth) w.ffill[i] = 0;  // every fine region (fine_reg)
+  for (uint32_t i = tid; i < w.nfine; i += nth) w.ffill[i] = 0;
   if (w.dd && tid == 0) {  // this shard's gathered row: flag word, buffer capacities
     w.cfill[kRegions] = 0;
     w.cfill[kRegions + 1] = w.ctl->fmsg_cap;
@@ -928,18 +902,11 @@ __device__ __forceinline__ bool tiles_by_xcd(const WinState& w) {
 __device__ __forceinline__ uint32_t xcd_bin_pos(uint32_t c) { return (c & 7) * 32 + (c >> 3); }
 __device__ __forceinline__ uint32_t xcd_bin_of(uint32_t pc) { return (pc & 31) * 8 + (pc >> 5); }
 
-// Fine regions inside each coarse region (kFineRegs per fine bucket: four
-// quarter regions of u16 messages and the roll region, q-major, gs_internal.h
-// fine_reg), in u16 units.  Fast path: a coarse bucket with cnt messages over nf fine buckets
-// gives every quarter region ceil(1.125 * cnt / (4 * nf)) + 128 units and the
-// roll region 2 * (ceil(1.5 * cnt * kc / (100 * nf)) + 64) (none when kc = 0),
-// every capacity even so every region starts at an even unit (the roll
-// region's u32 messages are aligned).  exact: only the tile prefix (fstart
-// comes from the exact count + scan instead).
+// Fine regions inside each coarse region: capacity per fine bucket of coarse
+// c = cfill[c]*1.15/256 + 512 (fast path), or exact counts (fhist != null).
 __device__ __forceinline__ void plan_body(const WinState& w, bool exact) {
   __shared__ unsigned long long s_base[257];
-  __shared__ unsigned long long s_cap[256];   // u16 units per fine bucket of coarse bucket c
-  __shared__ unsigned long long s_qcap[256];  // units per quarter region
+  __shared__ unsigned long long s_cap[256];
   __shared__ uint32_t s_tp[257];
   const uint32_t tid = threadIdx.x;  // 256 threads per block: thread c plans coarse bucket c
   if (w.ctl) {
@@ -971,19 +938,12 @@ __device__ __forceinline__ void plan_body(const WinState& w, bool exact) {
   // the last coarse bucket may hold fewer than 256 fine buckets
   const uint32_t nf = live ? min(256u, w.nfine - tid * 256) : 1u;
   __shared__ unsigned long long s_x[4];
-  {
-    const unsigned long long q = (cnt + cnt / 8 + 4 * nf - 1) / (4 * nf);
-    const unsigned long long qcap = ((q + 128) + 1) & ~1ull;
-    const unsigned long long kc = w.kc > 0 ? (unsigned long long)min(w.kc, 100) : 0ull;
-    const unsigned long long rr = kc ? (cnt * 3 * kc + 200 * nf - 1) / (200 * nf) : 0ull;
-    const unsigned long long rcap = kc ? 2 * (rr + 64) : 0ull;
-    s_qcap[tid] = live ? qcap : 0;
-    s_cap[tid] = live ? 4 * qcap + rcap : 0;
-  }
+  s_cap[tid] = live ? (cnt + cnt / 8 + nf - 1) / nf + 512 : 0;
   unsigned long long tb, tt;
-  // the bucket's nf fine buckets (a partial last bucket's were counted as
-  // 256 before: its plan outgrew the host's bound and a shard window whose
-  // fine buffer was sized by that bound overflowed every time -- r04aj)
+  // the bucket's nf fine regions (a partial last bucket's were counted as
+  // 256 before: its plan outgrew the host's bound R + R/8 + 513 * 256 per
+  // coarse bucket, and a shard window whose fine buffer was sized by that
+  // bound overflowed every time -- r04aj)
   s_base[tid] = block_exscan256_u64(s_cap[tid] * nf, s_x, &tb);
   s_tp[tid] = (uint32_t)block_exscan256_u64(live ? ntile : 0u, s_x, &tt);
   if (tid == 0) { s_base[256] = tb; s_tp[256] = (uint32_t)tt; }
@@ -1028,18 +988,10 @@ __device__ __forceinline__ void plan_body(const WinState& w, bool exact) {
   // is flagged for the host to grow the buffer and redo it
   const unsigned long long cap = w.ctl ? w.ctl->fmsg_cap : ~0ull;
   if (w.ctl && blockIdx.x == 0 && tid == 0 && s_base[w.ncoarse] > cap) atomicOr(w.err, kErrFine);
-  // coarse bucket c's regions, q-major: quarter q of its nf fine buckets at
-  // s_base[c] + q * nf * qcap, then the roll regions
-  const uint32_t nreg = w.ncoarse * kDigits;
-  for (uint32_t r = blockIdx.x * blockDim.x + tid; r <= nreg; r += gridDim.x * blockDim.x) {
-    const uint32_t c = r / kDigits, rem = r - c * kDigits, q = rem >> 8, d = rem & 255;
-    unsigned long long x = s_base[w.ncoarse];
-    if (r < nreg) {
-      const unsigned long long nf = min(256u, w.nfine - c * 256), qc = s_qcap[c];
-      const unsigned long long rc = s_cap[c] - 4 * qc;
-      x = s_base[c] + q * nf * qc + min((unsigned long long)d, nf) * (q < kRollReg ? qc : rc);
-    }
-    w.fstart[r] = x < cap ? x : cap & ~1ull;
+  for (uint32_t f = blockIdx.x * blockDim.x + tid; f <= w.nfine; f += gridDim.x * blockDim.x) {
+    const uint32_t c = f >> 8, d = f & 255;
+    const unsigned long long x = f == w.nfine ? s_base[w.ncoarse] : s_base[c] + d * s_cap[c];
+    w.fstart[f] = x < cap ? x : cap;
   }
 }
 __global__ void k_plan(const WinState w, bool exact) { plan_body(w, exact); }
@@ -1052,60 +1004,30 @@ __global__ void k_plan_m(const WinState* __restrict__ ws, bool exact) { plan_bod
 constexpr uint32_t kPartBlock = GS_PART_BLOCK;  // threads per partition tile (16 messages each)
 static_assert(kPartTile % kPartBlock == 0, "whole messages per thread");
 
-// The tile holds coarse messages as they came.  The digit of a message is its
-// fine region inside the coarse bucket: fine bucket fd = bits 14..21 of the
-// coarse message, region q = its quarter (bits 12..13), or kRollReg if it
-// carries a crash roll (bit 26); digit = q * 256 + fd (fine_reg).  The
-// counters become the digits' exclusive offsets in place.  ~77 KB: two tiles
-// per CU.
+// The tile holds coarse messages as they came: the fine digit (bits 14..21) is
+// re-read at write-out, so there is no per-slot bin byte (64 KB: two tiles/CU).
 struct TileSort {
   uint32_t buf[kPartTile];
-  uint32_t cnt[kDigits];   // counts, then (in place) the exclusive offsets
-  int32_t gdelta[kDigits];  // digit d's message at tile position p goes to unit cbase + gdelta[d] + p * width(d)
-  unsigned long long cbase;  // the coarse bucket's first region start (fstart)
-  uint32_t ovf;              // a fine region of this tile overflowed
-  uint32_t total;
+  uint32_t cnt[256];
+  uint32_t off[257];
+  unsigned long long gbase[256];  // digit b's message p goes to gbase[b] + p
+  unsigned long long gend[256];  // end of fine region b (fstart[c*256 + b + 1])
+  uint32_t ovf;                  // a fine region of this tile overflowed
 };
 
-__device__ __forceinline__ uint32_t part2_digit(uint32_t m) {
-  const uint32_t q = (m >> kRoll0Coarse) & 1u ? kRollReg : (m >> kQuarterLog) & 3u;
-  return (q << 8) | ((m >> kFineLog) & 255u);
-}
-// The digit again, from a value the compiler may not reuse: the rank and
-// scatter passes recompute it instead of keeping 16 digits live across the
-// barrier (which spilled)
-__device__ __forceinline__ uint32_t part2_digit_again(uint32_t m) {
-  asm volatile("" : "+v"(m));
-  return part2_digit(m);
-}
-// u16 units a message of digit d takes (roll-region messages are u32)
-__device__ __forceinline__ uint32_t digit_width(uint32_t d) { return d >= kRollReg * 256 ? 2u : 1u; }
-// The fine message of coarse message m at unit `at`: quarter regions get
-// loc12 | k << 12 (u16), the roll region loc14 | k << 14 | 1 << 18 (u32).
-__device__ __forceinline__ void fine_store(uint16_t* fm, unsigned long long at, uint32_t m) {
-  const uint32_t k = (m >> kCoarseShift) & (kMaxWindow - 1);
-  if ((m >> kRoll0Coarse) & 1u)
-    *reinterpret_cast<uint32_t*>(fm + at) = (m & (kFineNodes - 1)) | (k << kFineLog) | (1u << kRoll0Fine);
-  else
-    fm[at] = (uint16_t)((m & ((1u << kQuarterLog) - 1)) | (k << kQuarterLog));
-}
-
-// part2: coarse tiles -> the fine regions of their coarse bucket.
-// SCATTER=false counts units per fine region into fhist (exact fallback).
-// A coarse bucket's fine regions must span < 2^31 units in one window (32-bit
-// deltas in LDS): a wider one sets kErrWide and the window fails.
+// part2: coarse tiles -> fine regions; message = u_in_fine | k << 14.
+// SCATTER=false counts per fine bucket (exact fallback).
 template <bool SCATTER>
 __device__ __forceinline__ void part2_body(const WinState& w) {
   __shared__ TileSort ts;
-  __shared__ uint32_t s_tb[257];  // the tile prefix at every 8th region (the search's first level)
-  __shared__ unsigned long long s_x[kPartBlock / 64];
+  __shared__ uint32_t s_tp[kRegions + 1];
   const uint32_t tid = threadIdx.x;
   if (w.ctl) {
     uint32_t t0;
     if (!win_live(w, t0, 0)) return;
   }
   // a sparse window has few tiles: the workgroups past them leave before
-  // staging the tile prefix (the grid is sized for the densest window)
+  // staging the 8-KB tile prefix (the grid is sized for the densest window)
   const bool perm = tiles_by_xcd(w);
   uint32_t g0 = blockIdx.x, g1 = w.tprefix[kRegions], gstep = gridDim.x;
   if (perm && (gridDim.x & 7) == 0) {  // XCD x = blockIdx & 7 takes its bins' tiles
@@ -1115,25 +1037,15 @@ __device__ __forceinline__ void part2_body(const WinState& w) {
     gstep = gridDim.x >> 3;
   }
   if (g0 >= g1) return;
-  static_assert(kRegions == 256 * 8, "two-level tile search");
-  for (uint32_t i = tid; i <= 256; i += kPartBlock) s_tb[i] = w.tprefix[i * 8];
+  for (uint32_t i = tid; i <= kRegions; i += kPartBlock) s_tp[i] = w.tprefix[i];
   __syncthreads();
   for (uint32_t g = g0; g < g1; g += gstep) {
-    // tile-order position rho: tprefix[rho] <= g < tprefix[rho + 1] (the last
-    // such rho where empty regions repeat a prefix): the group of 8 in LDS,
-    // then the 8 entries of the group (one line, the same for every lane)
-    uint32_t lo = 0, hi = 255;
+    uint32_t lo = 0, hi = kRegions - 1;  // tile-order position rho: s_tp[rho] <= g < s_tp[rho+1]
     while (lo < hi) {
       const uint32_t mid = (lo + hi + 1) >> 1;
-      if (s_tb[mid] <= g) lo = mid; else hi = mid - 1;
+      if (s_tp[mid] <= g) lo = mid; else hi = mid - 1;
     }
-    const uint4* tp4 = reinterpret_cast<const uint4*>(w.tprefix + lo * 8);
-    const uint4 ta = tp4[0], tbv = tp4[1];
-    const uint32_t xs = (ta.y <= g) + (ta.z <= g) + (ta.w <= g) + (tbv.x <= g) + (tbv.y <= g) + (tbv.z <= g) +
-                        (tbv.w <= g);
-    const uint32_t tstart = xs == 0 ? ta.x : xs == 1 ? ta.y : xs == 2 ? ta.z : xs == 3 ? ta.w
-                          : xs == 4 ? tbv.x : xs == 5 ? tbv.y : xs == 6 ? tbv.z : tbv.w;
-    const uint32_t rho = lo * 8 + xs;
+    const uint32_t rho = lo;
     const uint32_t r = perm ? xcd_bin_of(rho / kCoarseSub) * kCoarseSub + rho % kCoarseSub : rho;
     const uint32_t c = r / w.csub;
     unsigned long long cb = w.ccap[r];
@@ -1143,15 +1055,13 @@ __device__ __forceinline__ void part2_body(const WinState& w) {
       cb &= kSrcMask;
     }
     const unsigned long long ce = cb + region_fill(w, r);
-    const unsigned long long base = cb + (unsigned long long)(g - tstart) * kPartTile;
-    for (uint32_t i = tid; i < kDigits; i += kPartBlock) ts.cnt[i] = 0;
-    if (tid == 0) {
-      ts.ovf = 0;
-      if (SCATTER) ts.cbase = w.fstart[(size_t)c * kDigits];
-    }
+    const unsigned long long base = cb + (unsigned long long)(g - s_tp[rho]) * kPartTile;
+    if (tid < 256) ts.cnt[tid] = 0;
     __syncthreads();
+    if (tid == 0) ts.ovf = 0;
     constexpr uint32_t kPer = kPartTile / kPartBlock;
-    uint32_t m[kPer];
+    static_assert(kPartTile <= 65536 && kPer % 2 == 0, "two 16-bit ranks per register");
+    uint32_t m[kPer], rank[kPer / 2] = {};
 #pragma unroll
     for (uint32_t r = 0; r < kPer; ++r) {
       const unsigned long long x = base + r * kPartBlock + tid;
@@ -1159,80 +1069,58 @@ __device__ __forceinline__ void part2_body(const WinState& w) {
       const uint32_t m1 = msrc[x < ce ? x : ce - 1];
       m[r] = x < ce ? m1 : kEmptyMsg;
     }
-    // counts (no-return LDS atomics); the scatter below takes each message's
-    // place with a second atomic on the offsets, so no rank is kept in a
-    // register (the order inside a digit's run is free: the resolve kernels
-    // do not depend on receipt order, rule A6)
 #pragma unroll
     for (uint32_t r = 0; r < kPer; ++r)
-      if (m[r] != kEmptyMsg) atomicAdd(&ts.cnt[part2_digit(m[r])], 1u);
+      if (m[r] != kEmptyMsg) rank[r / 2] |= atomicAdd(&ts.cnt[(m[r] >> kFineLog) & 255], 1u) << (16 * (r & 1));
     __syncthreads();
     if (!SCATTER) {
-      for (uint32_t d = tid; d < kDigits; d += kPartBlock)
-        if (ts.cnt[d]) atomicAdd(&w.fhist[(size_t)c * kDigits + d], (unsigned long long)ts.cnt[d] * digit_width(d));
+      if (tid < 256 && ts.cnt[tid]) atomicAdd(&w.fhist[c * 256 + tid], (unsigned long long)ts.cnt[tid]);
       __syncthreads();
       continue;
     }
-    // digits d = tid and tid + 1024 (< kDigits) of this thread
-    constexpr uint32_t kD2 = kDigits - kPartBlock;
-    static_assert(kDigits > kPartBlock && kDigits <= 2 * kPartBlock, "two digits per thread at most");
-    const uint32_t n0 = ts.cnt[tid], n1 = tid < kD2 ? ts.cnt[kPartBlock + tid] : 0u;
-    unsigned long long tot;
-    // the scan runs over (digit tid, digit tid + 1024) pairs: offsets of the
-    // first kPartBlock digits, then the rest
-    const uint32_t ex0 = (uint32_t)block_exscan_u64<kPartBlock / 64>(n0, s_x, &tot);
-    unsigned long long tot1;
-    const uint32_t ex1 = (uint32_t)tot + (uint32_t)block_exscan_u64<kPartBlock / 64>(n1, s_x, &tot1);
-    ts.cnt[tid] = ex0;
-    if (tid < kD2) ts.cnt[kPartBlock + tid] = ex1;
-    // the runs' reservations; the atomics' return latency overlaps the LDS
-    // scatter below (which needs only the offsets)
-    unsigned long long at0 = 0, at1 = 0;
-    if (n0) at0 = atomicAdd(&w.ffill[(size_t)c * kDigits + tid], (unsigned long long)n0 * digit_width(tid));
-    if (n1)
-      at1 = atomicAdd(&w.ffill[(size_t)c * kDigits + kPartBlock + tid],
-                      (unsigned long long)n1 * digit_width(kPartBlock + tid));
-    if (tid == 0) ts.total = (uint32_t)(tot + tot1);
+    block_scan256(ts.cnt, ts.off);
+    // thread b < 256 reserves fine bucket c*256+b's run; the atomic's return
+    // latency overlaps the LDS scatter (which needs only off[] from the scan)
+    const uint32_t mycnt = tid < 256 ? ts.cnt[tid] : 0u;
+    const uint32_t myf = c * 256 + (tid & 255);
+    unsigned long long at = 0, fb = 0, fe = 0;
+    if (mycnt) {
+      at = atomicAdd(&w.ffill[myf], (unsigned long long)mycnt);
+      fb = w.fstart[myf];
+      fe = w.fstart[myf + 1];
+    }
     __syncthreads();
 #pragma unroll
     for (uint32_t r = 0; r < kPer; ++r)
-      if (m[r] != kEmptyMsg) ts.buf[atomicAdd(&ts.cnt[part2_digit_again(m[r])], 1u)] = m[r];
-    {
-      const unsigned long long cbase = ts.cbase;
-#pragma unroll
-      for (uint32_t j = 0; j < 2; ++j) {
-        const uint32_t d = j ? kPartBlock + tid : tid, n = j ? n1 : n0, off = j ? ex1 : ex0;
-        if (!n) continue;
-        const uint32_t wd = digit_width(d);
-        const size_t rg = (size_t)c * kDigits + d;
-        const unsigned long long fb = w.fstart[rg], fe = w.fstart[rg + 1], at = j ? at1 : at0;
-        if (at + (unsigned long long)n * wd > fe - fb) {
-          atomicOr(w.err, kErrFine);
-          ts.ovf = 1;
+      if (m[r] != kEmptyMsg) {
+        ts.buf[ts.off[(m[r] >> kFineLog) & 255] + ((rank[r / 2] >> (16 * (r & 1))) & 0xFFFFu)] = m[r];
+        if ((m[r] >> kRoll0Coarse) & 1u) {  // a crash roll: its node is special in k_resolve
+          const uint32_t v = (c << kCoarseShift) | (m[r] & ((1u << kCoarseShift) - 1));
+          atomicOr(&w.rollw[v >> 5], 1u << (v & 31));
         }
-        const long long dl = (long long)(fb + at - cbase) - (long long)off * wd;
-        if (dl >= (1ll << 31) - kPartTile * 2) {
-          atomicOr(w.err, kErrWide | kErrFine);  // the window stops; an exact redo fails the same way
-          ts.ovf = 1;
-        }
-        ts.gdelta[d] = (int32_t)dl;
       }
+    if (mycnt) {
+      if (at + mycnt > fe - fb) {
+        atomicOr(w.err, kErrFine);
+        ts.ovf = 1;
+      }
+      ts.gbase[tid] = fb + at - ts.off[tid];
+      ts.gend[tid] = fe;
     }
     __syncthreads();
-    const uint32_t total = ts.total;
-    const unsigned long long cbase = ts.cbase;
+    const uint32_t total = ts.off[256];
     // two LDS reads per message; the region bound is checked only in a tile
     // whose reservation overflowed (the window is then redone exactly)
     if (!ts.ovf) {
       for (uint32_t p = tid; p < total; p += kPartBlock) {
-        const uint32_t x = ts.buf[p], d = part2_digit(x);
-        fine_store(w.fmsg, cbase + (unsigned long long)(ts.gdelta[d] + (long long)p * digit_width(d)), x);
+        const uint32_t m1 = ts.buf[p];
+        w.fmsg[ts.gbase[(m1 >> kFineLog) & 255] + p] = (m1 & (kFineNodes - 1)) | ((m1 >> kCoarseShift) << kFineLog);
       }
-    } else if (!(*w.err & kErrWide)) {
+    } else {
       for (uint32_t p = tid; p < total; p += kPartBlock) {
-        const uint32_t x = ts.buf[p], d = part2_digit(x), wd = digit_width(d);
-        const unsigned long long pos = cbase + (unsigned long long)(ts.gdelta[d] + (long long)p * wd);
-        if (pos + wd <= w.fstart[(size_t)c * kDigits + d + 1]) fine_store(w.fmsg, pos, x);
+        const uint32_t m1 = ts.buf[p], b = (m1 >> kFineLog) & 255;
+        const unsigned long long pos = ts.gbase[b] + p;
+        if (pos < ts.gend[b]) w.fmsg[pos] = (m1 & (kFineNodes - 1)) | ((m1 >> kCoarseShift) << kFineLog);
       }
     }
     __syncthreads();
@@ -1248,7 +1136,7 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   part2_body<SCATTER>(ws[blockIdx.y]);
 }
 
-constexpr uint32_t kResolveMaxBuckets = 128;  // buckets one persistent workgroup may own
+constexpr uint32_t kResolveMaxBuckets = 256;  // buckets one persistent workgroup may own
 constexpr uint32_t kSmallMax = 256;           // buckets with <= this many receipts: k_resolve_small
 #ifndef GS_SMALL_BLOCK
 #define GS_SMALL_BLOCK 512
@@ -1262,7 +1150,7 @@ constexpr uint32_t kRolledBlock = GS_ROLLED_BLOCK;  // the rolled replay: 4 wave
 // Bit-parallel resolve (k_resolve).  Three kinds of node in a window:
 //   crashed before it: every receipt is uncounted (simulator.go:108), by tick;
 //   ROLLED: live, and a receipt in the window carries a crash roll (k_part2
-//     writes those receipts to the bucket's roll region): the receipts are written to the bucket's
+//     marks those nodes in w.rollw): the receipts are written to the bucket's
 //     rolled list (w.rlmsg, w.rlcnt) and replayed exactly (rule A6) by
 //     k_resolve_rolled after this kernel, sorted per wave like k_resolve_small;
 //   plain: every receipt is counted and the first one informs the node
@@ -1277,7 +1165,7 @@ struct ResolveLds {
     struct {                            // b1 .. dlist, then the infection list
       uint32_t b1[kBitTicks][kBitWords];
       uint2 cr0[kBitWords];             // per word: crashed before the window, a crash-roll
-                                        // receipt in the window (from the roll region)
+                                        // receipt in the window (from w.rollw)
     };
     struct {                            // large path
       uint32_t cnt[kFineNodes];         // per node at the current tick: arrivals | crash rolls << 16
@@ -1291,10 +1179,8 @@ struct ResolveLds {
   uint32_t st[kMaxWindow][4];       // dead (not counted), recv, crash per tick: whole launch
   uint32_t dead[kMaxWindow];        // this bucket's receipts at nodes crashed before the window
   uint32_t blist[kResolveMaxBuckets];  // this workgroup's non-empty buckets
-  unsigned long long bbase[kResolveMaxBuckets];  // their quarter-0 region starts (fstart, u16 units)
-  uint4 bq[kResolveMaxBuckets];        // starts of quarters 1..3 and of the roll region, relative to bbase
-  uint4 bc[kResolveMaxBuckets];        // messages in quarters 0..3
-  uint32_t br[kResolveMaxBuckets];     // messages in the roll region
+  unsigned long long bstart[kResolveMaxBuckets];  // their message region starts (fstart)
+  uint32_t bcnt[kResolveMaxBuckets];   // their message counts (ffill)
   uint32_t ndup;
   uint32_t ninf;
   uint32_t err;
@@ -1315,50 +1201,7 @@ __device__ __forceinline__ void stamp(const WinState& w, ResolveLds& sm, uint32_
   }
 }
 
-// receipt (k_resolve's register form, and the roll region's and the rolled
-// list's stored form): loc | k << 14 | roll0 << 18; a quarter region's u16
-// message m of quarter q is (q << 12 | m & 4095) | (m >> 12) << 14
-__device__ __forceinline__ uint32_t quarter_msg(uint32_t q, uint32_t m) {
-  return (q << kQuarterLog) | (m & ((1u << kQuarterLog) - 1)) | ((m >> kQuarterLog) << kFineLog);
-}
-// The receipts of fine bucket f in one index space: quarters 0..3, then the
-// roll region (the large path and k_resolve_small; 64-bit starts).  Named
-// members, not arrays: a selected array element becomes an indexed scratch
-// load.
-struct FineSrc {
-  const uint16_t* fm;
-  unsigned long long s0, s1, s2, s3, s4;  // region starts
-  uint32_t p1, p2, p3, p4, total;         // messages before region q; all of them
-  __device__ __forceinline__ uint32_t operator[](uint32_t p) const {
-    const bool a1 = p >= p1, a2 = p >= p2, a3 = p >= p3, a4 = p >= p4;
-    if (a4) return *reinterpret_cast<const uint32_t*>(fm + s4 + 2ull * (p - p4));
-    const uint32_t q = (uint32_t)a1 + (uint32_t)a2 + (uint32_t)a3;
-    // masked sums, not a select chain (which the compiler turns into a table)
-    const unsigned long long m1 = 0ull - (unsigned long long)a1, m2 = 0ull - (unsigned long long)a2,
-                             m3 = 0ull - (unsigned long long)a3;
-    const unsigned long long sq = s0 + ((s1 - s0) & m1) + ((s2 - s1) & m2) + ((s3 - s2) & m3);
-    const uint32_t pq = (p1 & (uint32_t)m1) + ((p2 - p1) & (uint32_t)m2) + ((p3 - p2) & (uint32_t)m3);
-    return quarter_msg(q, fm[sq + (p - pq)]);
-  }
-};
-__device__ __forceinline__ FineSrc fine_src(const WinState& w, uint32_t f) {
-  FineSrc r;
-  r.fm = w.fmsg;
-  r.s0 = w.fstart[fine_reg(f, 0)];
-  r.s1 = w.fstart[fine_reg(f, 1)];
-  r.s2 = w.fstart[fine_reg(f, 2)];
-  r.s3 = w.fstart[fine_reg(f, 3)];
-  r.s4 = w.fstart[fine_reg(f, kRollReg)];
-  const unsigned long long c0 = w.ffill[fine_reg(f, 0)], c1 = w.ffill[fine_reg(f, 1)],
-                           c2 = w.ffill[fine_reg(f, 2)], c3 = w.ffill[fine_reg(f, 3)],
-                           c4 = w.ffill[fine_reg(f, kRollReg)] / 2;
-  r.p1 = (uint32_t)c0;
-  r.p2 = (uint32_t)(c0 + c1);
-  r.p3 = (uint32_t)(c0 + c1 + c2);
-  r.p4 = (uint32_t)(c0 + c1 + c2 + c3);
-  r.total = (uint32_t)(c0 + c1 + c2 + c3 + c4);
-  return r;
-}
+// receipt (fine message): loc | k << 14 | roll0 << 18
 
 __device__ __forceinline__ uint32_t msg_loc(uint32_t m) { return m & (kFineNodes - 1); }
 __device__ __forceinline__ uint32_t msg_tick(uint32_t m) { return (m >> kFineLog) & (kMaxWindow - 1); }
@@ -1487,7 +1330,7 @@ __device__ __forceinline__ void flush_counts(const WinState& w, ResolveLds& sm, 
 // resolves its non-empty ones in turn, and adds its per-tick counters once at
 // the end.  Per bucket:
 //   stage    thread w owns bit word w (32 nodes): its recv/crash words in
-//            registers, spec = crashed | marked by a roll-region receipt, its
+//            registers, spec = crashed | marked in rollw (cleared here), its
 //            b1 words and chain head zeroed
 //   receipts every receipt sets its (tick, node) bit in b1; receipts at
 //            special nodes are listed, then chained under their word
@@ -1509,49 +1352,23 @@ __device__ __forceinline__ void resolve_body(const WinState& w, uint32_t t0, uin
   __syncthreads();
   {
     const uint32_t f = blockIdx.x + tid * G;
-    const bool mine = tid < kResolveMaxBuckets && f < w.nfine;
-    unsigned long long fs[kFineRegs], fc[kFineRegs];
-#pragma unroll
-    for (uint32_t q = 0; q < kFineRegs; ++q) {
-      fs[q] = mine ? w.fstart[fine_reg(f, q)] : 0ull;
-      fc[q] = mine ? w.ffill[fine_reg(f, q)] : 0ull;
-    }
-    const unsigned long long M = fc[0] + fc[1] + fc[2] + fc[3] + fc[kRollReg] / 2;
-    const bool ne = M > kSmallMax;  // small: k_resolve_small
+    const unsigned long long fl = tid < kResolveMaxBuckets && f < w.nfine ? w.ffill[f] : 0ull;
+    const bool ne = fl > kSmallMax;  // small: k_resolve_small
     const uint32_t at = wave_append(&sm.nb, ne);
     if (ne) {
       // the bucket descriptors come from LDS later: a wait for them never waits
-      // for the vector loads in flight (the next bucket's prefetch).  (A
-      // bucket past 2^28 receipts takes the large path, which reads its
-      // regions from fstart / ffill.)
-      const bool huge = M >= (1ull << 28);  // no 32-bit offsets; loads stay at the bucket's first units
+      // for the vector loads in flight (the next bucket's prefetch)
       sm.blist[at] = f;
-      sm.bbase[at] = fs[0];
-      sm.bq[at] = huge ? make_uint4(0, 0, 0, 0)
-                       : make_uint4((uint32_t)(fs[1] - fs[0]), (uint32_t)(fs[2] - fs[0]), (uint32_t)(fs[3] - fs[0]),
-                                    (uint32_t)(fs[kRollReg] - fs[0]));
-      sm.bc[at] = huge ? make_uint4(0, 0, 0, 0)
-                       : make_uint4((uint32_t)fc[0], (uint32_t)fc[1], (uint32_t)fc[2], (uint32_t)fc[3]);
-      sm.br[at] = huge ? ~0u : (uint32_t)(fc[kRollReg] / 2);  // ~0u > kRolledCap: the large path
+      sm.bstart[at] = w.fstart[f];
+      sm.bcnt[at] = (uint32_t)fl;
     }
   }
   __syncthreads();
   const uint32_t nb = sm.nb;
   stamp(w, sm, 0);
-  uint32_t fB = 0, rB = 0;
-  uint4 qB = make_uint4(0, 0, 0, 0), cB = make_uint4(0, 0, 0, 0);
+  uint32_t fB = 0, MB = 0;
   unsigned long long mbB = 0;
-  // (wave-uniform: scalar registers)
-  auto next_bucket = [&](uint32_t j) {
-    auto u = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); };
-    fB = u(sm.blist[j]);
-    const unsigned long long b = sm.bbase[j];
-    mbB = ((unsigned long long)u((uint32_t)(b >> 32)) << 32) | u((uint32_t)b);
-    const uint4 q = sm.bq[j], cc = sm.bc[j];
-    qB = make_uint4(u(q.x), u(q.y), u(q.z), u(q.w));
-    cB = make_uint4(u(cc.x), u(cc.y), u(cc.z), u(cc.w));
-    rB = u(sm.br[j]);
-  };
+  auto next_bucket = [&](uint32_t j) { fB = sm.blist[j]; mbB = sm.bstart[j]; MB = sm.bcnt[j]; };
   if (nb > 0) next_bucket(0);
   uint32_t* rwg = (uint32_t*)w.recv;
   uint32_t* cwg = (uint32_t*)w.crash;
@@ -1561,27 +1378,22 @@ __device__ __forceinline__ void resolve_body(const WinState& w, uint32_t t0, uin
   for (uint32_t k = 0; k < kBitTicks / 2; ++k) acc_ni[k] = 0;
   static_assert(kBitTicks % 2 == 0 && 32 * kResolveMaxBuckets < 65536, "two 16-bit counts per register");
   constexpr uint32_t kU = 8;  // loads in flight per lane
-  constexpr uint32_t kBatch = kResolveBlock * 2;  // receipts of each quarter per batch
-  // messages p0 + (u & 1) * kResolveBlock + tid of quarter u >> 1 of a bucket
-  // (two loads per quarter and batch): raw u16 loads, valid iff the index is
-  // below the quarter's count (clamped into the region otherwise)
-  auto ld = [&](unsigned long long mb, uint4 rq, uint4 cq, uint32_t p0, uint32_t (&m)[kU]) {
-    static_assert(kU == 8, "two loads per quarter");
-    const uint16_t* gm = w.fmsg + mb;
+  constexpr uint32_t kBatch = kResolveBlock * kU;
+  // messages p0 + u * kResolveBlock + tid of a bucket (gm, M): raw loads, valid
+  // iff the index is < M (M >= 1); 32-bit byte offsets from the uniform base
+  // (M < 2^28)
+  auto ld = [&](const uint32_t* gm, uint32_t M, uint32_t p0, uint32_t (&m)[kU]) {
 #pragma unroll
     for (uint32_t u = 0; u < kU; ++u) {
-      const uint32_t q = u >> 1;
-      const uint32_t rel = q == 0 ? 0u : q == 1 ? rq.x : q == 2 ? rq.y : rq.z;
-      const uint32_t c = q == 0 ? cq.x : q == 1 ? cq.y : q == 2 ? cq.z : cq.w;
-      const uint32_t p = p0 + (u & 1) * kResolveBlock + tid;
-      m[u] = gm[rel + (p < c ? p : (c ? c - 1 : 0u))];
+      const uint32_t p = p0 + u * kResolveBlock + tid;
+      m[u] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(gm) + ((p < M ? p : M - 1) << 2));
     }
   };
   // the next bucket's state words and first batch of messages are loaded
   // while this bucket finishes (from the end of its receipts)
-  uint32_t pm[kU], p_recv0 = 0, p_crash0 = 0, p_fcv = 0, p_rm = 0;
+  uint32_t pm[kU], p_recv0 = 0, p_crash0 = 0, p_roll0 = 0, p_fcv = 0;
   bool p_in = false;
-  auto prefetch = [&](uint32_t f, unsigned long long mb, uint4 rq, uint4 cq, uint32_t nr) {
+  auto prefetch = [&](uint32_t f, uint32_t M, unsigned long long mb) {
     const uint64_t wi = ((uint64_t)(f << kFineLog) >> 5) + tid;
     const bool in = wi < w.W * 2;
     // branch-free (clamped) loads, masked where they are used: a load in a
@@ -1591,19 +1403,14 @@ __device__ __forceinline__ void resolve_body(const WinState& w, uint32_t t0, uin
     p_in = in;
     p_recv0 = rwg[wc];
     p_crash0 = cwg[wc];
+    p_roll0 = w.rollw[wc];
     p_fcv = w.fcount[(size_t)(tid < w.R ? tid : 0u) * w.nfine + f];
-    ld(mb, rq, cq, 0, pm);
-    // the roll region's receipts, one per thread (the rest are loaded at staging)
-    p_rm = *reinterpret_cast<const uint32_t*>(w.fmsg + mb + rq.w + 2 * (tid < nr && nr <= kRolledCap ? tid : 0u));
+    ld(w.fmsg + mb, M, 0, pm);
   };
-  if (nb > 0) prefetch(fB, mbB, qB, cB, rB);
+  if (nb > 0) prefetch(fB, MB, mbB);
   for (uint32_t i = 0; i < nb; ++i) {
-    const uint32_t f = fB, nr = rB;
-    const uint4 rq = qB, cq = cB;
+    const uint32_t f = fB, M = MB;
     const unsigned long long mb = mbB;
-    const unsigned long long Mfull = (unsigned long long)cq.x + cq.y + cq.z + cq.w + (nr > kRolledCap ? 1024 : nr);
-    const uint32_t cmax = max(max(cq.x, cq.y), max(cq.z, cq.w));
-    const uint32_t rm0 = p_rm;
     const uint32_t node0 = f << kFineLog;
     const uint64_t wi = ((uint64_t)node0 >> 5) + tid;
     // Philox keys of the bucket's nodes: key node knode0 + local offset (a
@@ -1612,44 +1419,25 @@ __device__ __forceinline__ void resolve_body(const WinState& w, uint32_t t0, uin
     node_key(w.tlog, w.tmask, w.key, (uint64_t)w.base + node0, K_ORDER, knode0, c3order);
     const uint32_t c3delay = (c3order & 0xFFFFFFu) | (K_DELAY << 24);
     const bool in = wi < w.W * 2;
-    const uint32_t recv0 = p_in ? p_recv0 : 0u, crash0 = p_in ? p_crash0 : 0u;
+    const uint32_t recv0 = p_in ? p_recv0 : 0u, crash0 = p_in ? p_crash0 : 0u, roll0 = p_in ? p_roll0 : 0u;
     const uint32_t fcv = tid < w.R ? p_fcv : 0u;
     if (i + 1 < nb) next_bucket(i + 1);
+    if (roll0) w.rollw[wi] = 0u;  // consumed: the next window starts clear
+    const uint32_t rollw = roll0 & ~crash0;
 #pragma unroll
     for (uint32_t k = 0; k < kBitTicks; ++k)
       if (k < L) sm.b1[k][tid] = 0;
-    sm.cr0[tid] = make_uint2(crash0, 0u);
+    sm.cr0[tid] = make_uint2(crash0, rollw);
     if (tid < w.R) sm.fc[tid] = fcv;
     if (tid < kMaxWindow) sm.dead[tid] = 0;
-    if (tid == 0) {
-      sm.ndup = 0;
-      sm.ninf = 0;
-      sm.err = Mfull >= (1u << 28) || nr > kRolledCap ? 3 : 0;
-      sm.cls = Mfull >= 1024 ? 1 : 0;
-    }
+    if (tid == 0) { sm.ndup = 0; sm.ninf = 0; sm.err = M >= (1u << 28) ? 3 : 0; sm.cls = M >= 1024 ? 1 : 0; }
     __syncthreads();
-    // the receipts that carry a crash roll (the roll region): a node crashed
-    // before the window does not count them (:108); any other is ROLLED, and
-    // they open its list for k_resolve_rolled
-    if (sm.err != 3) {
-      for (uint32_t e = tid; e < nr; e += kResolveBlock) {
-        const uint32_t me = e == tid ? rm0 : *reinterpret_cast<const uint32_t*>(w.fmsg + mb + rq.w + 2ull * e);
-        const uint32_t loc = msg_loc(me), bit = 1u << (loc & 31);
-        if (sm.cr0[loc >> 5].x & bit) {
-          atomicAdd(&sm.dead[msg_tick(me)], 1u);
-        } else {
-          atomicOr(&sm.cr0[loc >> 5].y, bit);
-          w.rlmsg[(size_t)f * kRolledCap + atomicAdd(&sm.ndup, 1u)] = me;  // nr <= kRolledCap
-        }
-      }
-    }
-    __syncthreads();
-    const uint32_t rollw = sm.cr0[tid].y;
     stamp(w, sm, 1);
     // receipts: (tick, node) bits; uncounted receipts at crashed nodes by
     // tick (8-bit fields per lane, flushed every 31 batches); receipts at
     // rolled nodes listed.  The next batch's loads are issued before this
     // batch's LDS work.
+    const uint32_t* gm = w.fmsg + mb;
     unsigned long long dlo = 0, dhi = 0;  // uncounted receipts, ticks 0..7 / 8..15
     auto flush_dead = [&]() {
       while (dlo) {
@@ -1707,14 +1495,10 @@ __device__ __forceinline__ void resolve_body(const WinState& w, uint32_t t0, uin
       uint32_t m[kU];
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) m[u] = pm[u];
-      const uint32_t cnt4[4] = {cq.x, cq.y, cq.z, cq.w};
-      for (uint32_t p0 = 0, nbat = 0; p0 < (sm.err == 3 ? 0u : cmax); p0 += kBatch, ++nbat) {
+      for (uint32_t p0 = 0, nbat = 0; p0 < (sm.err == 3 ? 0u : M); p0 += kBatch, ++nbat) {
         uint32_t mn[kU];
-        if (p0 + kBatch < cmax) ld(mb, rq, cq, p0 + kBatch, mn);
-        uint32_t mc[kU];
-#pragma unroll
-        for (uint32_t u = 0; u < kU; ++u) mc[u] = quarter_msg(u >> 1, m[u]);
-        GS_RESOLVE_BATCH(mc, p0 + (u & 1) * kResolveBlock + tid < cnt4[u >> 1])
+        if (p0 + kBatch < M) ld(gm, M, p0 + kBatch, mn);
+        GS_RESOLVE_BATCH(m, p0 + u * kResolveBlock + tid < M)
 #pragma unroll
         for (uint32_t u = 0; u < kU; ++u) m[u] = mn[u];
       }
@@ -1723,7 +1507,7 @@ __device__ __forceinline__ void resolve_body(const WinState& w, uint32_t t0, uin
     flush_dead();
     stamp(w, sm, 2);
     __syncthreads();
-    if (i + 1 < nb) prefetch(fB, mbB, qB, cB, rB);
+    if (i + 1 < nb) prefetch(fB, MB, mbB);
     // the rolled list goes to k_resolve_rolled (none on the large path)
     if (tid == 0) w.rlcnt[f] = sm.err == 3 ? 0u : min(sm.ndup, kRolledCap);
     stamp(w, sm, 3);
@@ -1794,8 +1578,7 @@ __device__ __forceinline__ void resolve_body(const WinState& w, uint32_t t0, uin
       sm.nrecv[tid] = 0;
       sm.ncrash[tid] = 0;
       __syncthreads();
-      const FineSrc src = fine_src(w, f);
-      for (uint32_t k = 0; k < L; ++k) resolve_tick(w, sm, f, src, 0, src.total, k, t0 + k);
+      for (uint32_t k = 0; k < L; ++k) resolve_tick(w, sm, f, gm, 0, M, k, t0 + k);
       rw = sm.recv[tid] | sm.nrecv[tid];
       cw = sm.crash[tid] | sm.ncrash[tid];
       if (tid == 0 && sm.err == 1) atomicOr(w.err, kErrArrivals);
@@ -1841,9 +1624,9 @@ __global__ __launch_bounds__(kResolveBlock, GS_RESOLVE_WAVES) void k_resolve_m(c
 // kRolledCap, E = 1, 4, 8 or 16); a rolled node is live when the window starts,
 // and its recv/crash bits are untouched by k_resolve, so the replay is the
 // same receive case from the same state.
-template <uint32_t E, bool ROLLED, class Src>
+template <uint32_t E, bool ROLLED>
 __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t t0, uint32_t L, uint32_t f,
-                                                     const Src gm, unsigned long long M,
+                                                     const uint32_t* gm, unsigned long long M,
                                                      uint32_t (*st)[kMaxWindow][4], uint32_t* skw,
                                                      uint32_t* fcw);
 
@@ -1862,23 +1645,27 @@ __device__ __forceinline__ void resolve_small_body(const WinState& w, uint32_t t
   const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
   // the bucket's size and start are loaded while the window check is in
   // flight (unused when the window is dead)
-  const bool has = f < w.nfine;
-  const uint32_t* rl = w.rlmsg + (size_t)(has ? f : 0u) * kRolledCap;
-  const FineSrc fsrc = fine_src(w, has ? f : 0u);  // (unused for ROLLED)
-  const unsigned long long M = !has ? 0ull : ROLLED ? (unsigned long long)w.rlcnt[f] : fsrc.total;
+  unsigned long long M = 0;
+  const uint32_t* gm = nullptr;
+  if (f < w.nfine) {
+    if (ROLLED) {
+      M = w.rlcnt[f];
+      gm = w.rlmsg + (size_t)f * kRolledCap;
+    } else {
+      M = w.ffill[f];
+      gm = w.fmsg + w.fstart[f];
+    }
+  }
   L = win_live(w, t0, L);
   if (!L) return;
   (&st[0][0][0])[tid] = 0;
   __syncthreads();
-  if (ROLLED) {
-    if (M > 0 && M <= 64) resolve_small_bucket<1, true>(w, t0, L, f, rl, M, st, sk[wv], fcw[wv]);
-    else if (M > 64 && M <= 256) resolve_small_bucket<4, true>(w, t0, L, f, rl, M, st, sk[wv], fcw[wv]);
-    else if (M > 256 && M <= 512) resolve_small_bucket<8, true>(w, t0, L, f, rl, M, st, sk[wv], fcw[wv]);
-    else if (M > 512 && M <= kRolledCap) resolve_small_bucket<16, true>(w, t0, L, f, rl, M, st, sk[wv], fcw[wv]);
-  } else {
-    if (M > 0 && M <= 64) resolve_small_bucket<1, false>(w, t0, L, f, fsrc, M, st, sk[wv], fcw[wv]);
-    else if (M > 64 && M <= 256) resolve_small_bucket<4, false>(w, t0, L, f, fsrc, M, st, sk[wv], fcw[wv]);
-  }
+  if (M > 0 && M <= 64) resolve_small_bucket<1, ROLLED>(w, t0, L, f, gm, M, st, sk[wv], fcw[wv]);
+  else if (M > 64 && M <= 256) resolve_small_bucket<4, ROLLED>(w, t0, L, f, gm, M, st, sk[wv], fcw[wv]);
+  else if (ROLLED && M > 256 && M <= 512)
+    resolve_small_bucket<ROLLED ? 8 : 1, ROLLED>(w, t0, L, f, gm, M, st, sk[wv], fcw[wv]);
+  else if (ROLLED && M > 512 && M <= kRolledCap)
+    resolve_small_bucket<ROLLED ? 16 : 1, ROLLED>(w, t0, L, f, gm, M, st, sk[wv], fcw[wv]);
   if (ROLLED && M && (threadIdx.x & 63) == 0) w.rlcnt[f] = 0;  // consumed
   // device-driven windows: the window's fire lists of the buckets the body
   // did not take are consumed here (see resolve_small_bucket); k_resolve and
@@ -1910,9 +1697,9 @@ __global__ __launch_bounds__(ROLLED ? kRolledBlock : kSmallBlock) void k_resolve
   resolve_small_body<ROLLED>(ws[blockIdx.y], 0u, L);
 }
 
-template <uint32_t E, bool ROLLED, class Src>
+template <uint32_t E, bool ROLLED>
 __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t t0, uint32_t L, uint32_t f,
-                                                     const Src gm, unsigned long long M,
+                                                     const uint32_t* gm, unsigned long long M,
                                                      uint32_t (*st)[kMaxWindow][4], uint32_t* skw,
                                                      uint32_t* fcw) {
   constexpr uint32_t N = 64 * E;
@@ -1943,6 +1730,8 @@ __device__ __forceinline__ void resolve_small_bucket(const WinState& w, uint32_t
       if (i < M) {
         const uint32_t m = gm[i];
         key[r] = (msg_loc(m) << 5) | (msg_tick(m) << 1) | ((m >> kRoll0Fine) & 1u);
+        // k_part2 marked the node of a crash roll for k_resolve: clear it here
+        if (!ROLLED && ((m >> kRoll0Fine) & 1u)) w.rollw[((f << kFineLog) + msg_loc(m)) >> 5] = 0u;
       }
     }
 #pragma unroll
@@ -2110,6 +1899,32 @@ __global__ void k_consume_sh(const WinState w, uint32_t t0, uint32_t L) {
   }
 }
 
+// Exclusive scan of one u64 per thread over a block of NW waves (s: NW words
+// of LDS); returns the thread's prefix, *total the block's sum.  Block-uniform.
+template <uint32_t NW>
+__device__ __forceinline__ unsigned long long block_exscan_u64(unsigned long long v, unsigned long long* s,
+                                                               unsigned long long* total) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned long long x = v;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s[wv] = x;
+  __syncthreads();
+  unsigned long long before = 0, all = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < NW; ++q) {
+    const unsigned long long t = s[q];
+    if (q < wv) before += t;
+    all += t;
+  }
+  __syncthreads();
+  *total = all;
+  return before + x - v;
+}
+
 // ---- device-driven shard windows ------------------
 // The host-driven shard window (gs_api.cpp shard_windows) reads every shard's
 // fire counts and region fills on the host to cut the window and lay out the
@@ -2168,7 +1983,7 @@ __device__ __forceinline__ void rtab_body(const WinState& w, unsigned long long*
     const unsigned long long nd = min((unsigned long long)w.seg_per, (unsigned long long)w.nglob - lo);
     const unsigned long long ncd = (((nd + kFineNodes - 1) >> kFineLog) + 255) / 256;
     const unsigned long long R = s_R[d];
-    if (fine_units_bound(R, ncd, w.kc) > w.glay[(size_t)d * kDDRow + kRegions + 1]) atomicOr(&s_abort, 2u);
+    if (R + R / 8 + ncd * 256 * 513 + 16 > w.glay[(size_t)d * kDDRow + kRegions + 1]) atomicOr(&s_abort, 2u);
   }
   __syncthreads();
   if (s_abort) {
@@ -2258,10 +2073,10 @@ __global__ __launch_bounds__(256) void k_rtab_m(const WinState* __restrict__ ws,
 __device__ __forceinline__ void fine_zero_body(const WinState& w) {
   uint32_t t0;
   if (!win_live(w, t0, 0)) return;
-  const uint32_t nh = w.ncoarse * kDigits + 1;
+  const uint32_t nh = w.ncoarse * 256 + 1;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nh; i += gridDim.x * blockDim.x) {
     w.fhist[i] = 0;
-    if (i < w.ncoarse * kDigits) w.ffill[i] = 0;
+    if (i < w.nfine) w.ffill[i] = 0;
   }
 }
 __global__ void k_fine_zero(const WinState w) { fine_zero_body(w); }
@@ -2271,13 +2086,11 @@ __device__ __forceinline__ void fine_scan_body(const WinState& w) {
   __shared__ unsigned long long s_x[16];
   uint32_t t0;
   if (!win_live(w, t0, 0)) return;
-  // region sizes rounded up to even units: every region starts even (the
-  // roll regions' u32 messages)
-  const uint32_t n = w.ncoarse * kDigits + 1, per = (n + 1023) / 1024, tid = threadIdx.x;
+  const uint32_t n = w.nfine + 1, per = (n + 1023) / 1024, tid = threadIdx.x;
   unsigned long long sum = 0;
   for (uint32_t j = 0; j < per; ++j) {
     const uint32_t i = tid * per + j;
-    if (i < n) sum += (w.fhist[i] + 1) & ~1ull;
+    if (i < n) sum += w.fhist[i];
   }
   unsigned long long tot;
   unsigned long long a = block_exscan_u64<16>(sum, s_x, &tot);
@@ -2285,8 +2098,8 @@ __device__ __forceinline__ void fine_scan_body(const WinState& w) {
     const uint32_t i = tid * per + j;
     if (i >= n) break;
     w.fstart[i] = a;
-    a += (w.fhist[i] + 1) & ~1ull;
-    if (i + 1 < n) w.ffill[i] = 0;
+    a += w.fhist[i];
+    if (i < w.nfine) w.ffill[i] = 0;
   }
 }
 __global__ __launch_bounds__(1024) void k_fine_scan(const WinState w) { fine_scan_body(w); }
@@ -2619,13 +2432,9 @@ hipError_t win_part2(const WinState& w, uint64_t T, bool scatter, hipStream_t s)
   return hipGetLastError();
 }
 
-// region sizes rounded up to even units (see fine_scan_body)
-struct EvenUnits {
-  __host__ __device__ unsigned long long operator()(unsigned long long x) const { return (x + 1) & ~1ull; }
-};
 hipError_t win_scan_fine(const WinState& w, void* tmp, size_t& tmp_bytes, hipStream_t s) {
-  hipcub::TransformInputIterator<unsigned long long, EvenUnits, const unsigned long long*> in(w.fhist, EvenUnits{});
-  return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, in, w.fstart, (int)(w.ncoarse * kDigits + 1), s);
+  return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, (const unsigned long long*)w.fhist,
+                                          w.fstart, (int)(w.nfine + 1), s);
 }
 
 hipError_t win_resolve(const WinState& w, uint32_t t0, uint32_t L, hipStream_t s) {

@@ -211,6 +211,8 @@ def test_gpu_pushpull_new_mask_and_table_on_one_context(oracle, rounds):
     with gs.Simulator(cfg) as sim:
         for case, (ti, mi) in enumerate(((0, 0), (0, 1), (1, 1))):
             deg, ids = tables[ti]
+            if case:
+                sim.reset()
             if case == 0 or ti != 0:
                 sim.load_peers(deg, ids)
             sim.set_failed(masks[mi])
