@@ -171,7 +171,10 @@ def main():
     t0 = time.perf_counter()
     wins, stab = sim.build_overlay()
     overlay_s = time.perf_counter() - t0
-    log(f"rank {rank}: overlay n={a.n} stabilised at {stab} ms simulated, {overlay_s:.2f} s wall")
+    otm = sim.timing()
+    ov_ticks = {"partition": int(otm["ov_part_ticks"]), "sort": int(otm["ov_sort_ticks"]),
+                "partition_fallbacks": int(otm["ov_part_fallbacks"])}
+    log(f"rank {rank}: overlay n={a.n} stabilised at {stab} ms simulated, {overlay_s:.2f} s wall, ticks {ov_ticks}")
 
     def one_step():
         sim.reset()
@@ -269,7 +272,7 @@ def main():
                    "ticks": ticks[-1], "status": STATUS[status],
                    "coverage": round(recv_last / a.n, 6),
                    "delivered_per_step": sent // a.steps,
-                   "messages_per_step": msgs, "overlay_s": round(overlay_s, 3),
+                   "messages_per_step": msgs, "overlay_s": round(overlay_s, 3), "overlay_ticks": ov_ticks,
                    "overlay_stabilised_ms": stab, "parallelism": f"trials{world}"},
         "roofline": roof,
         "cpu_baseline": None,
@@ -280,12 +283,16 @@ def main():
         ext["flood_failed_1pct"] = guarded("flood_failed_1pct", lambda: flood_failed(a, sim))
     sim.close()
     if not a.no_extensions:
-        pp = guarded("pushpull", lambda: pushpull_runs(a, gs, rank, local))
-        ext.update(pp if "error" not in pp else {"pushpull": pp})
+        # C3 and C4 before push-pull: on some boxes of the pool, allocations
+        # after ~100+ GB of device memory were freed (the push-pull leg's
+        # reverse-table temporaries) ran seconds slow and C3 measured 5-7 s
+        # instead of 1.4 s (profiles/r05e_c3_after.txt)
         if not a.no_c3:
             ext["c3_trials"] = guarded("c3_trials", lambda: c3_trials(a, gs, rank, world, local, dist))
         if not a.no_c4:
             ext["c4_sharded"] = guarded("c4_sharded", lambda: c4_sharded(a, gs, rank, world, local, dist))
+        pp = guarded("pushpull", lambda: pushpull_runs(a, gs, rank, local))
+        ext.update(pp if "error" not in pp else {"pushpull": pp})
         if world > 1:
             ext["c5_flood_sharded"] = guarded("c5_flood_sharded",
                                               lambda: c5_flood_sharded(a, gs, rank, world, local, dist))
@@ -381,15 +388,19 @@ def pushpull_runs(a, gs, rank, local):
     (calls not lost, whose receiver is live); the round's roofline (all its
     kernels: sparse k_ppe_round, top-down k_pp_round or bottom-up k_ppb_round,
     summaries, commit) at SURVEY.md 8(d)'s 8 algorithmic bytes per delivered
-    message; frac_12B_per_call charges 12 B (4-B friend id + 8-B peer state
-    word) to every call instead."""
+    message, with `traffic` / `traffic_ratio` from the committed PMC passes of
+    one such broadcast (profiles/pmc_pp_traffic.json, scripts/pmc_pp.sh).
+    prep_ms: the reverse-table build (first broadcast on a new table) and, in
+    the 1 %-failed leg, the failed-slot mask and failed-caller bits; both sit
+    inside the timed broadcast that needed them."""
     cfg = gs.Config(n=a.n, fanout=a.fanout, fanin=a.fanin, delaylow=a.delaylow,
                     delayhigh=a.delayhigh, droprate=a.droprate, crashrate=a.crashrate,
                     seed=a.seed, trial=rank, device=local, model="pushpull")
     out = {}
     with gs.Simulator(cfg) as sim:
         sim.build_overlay()
-        timed_broadcast(sim)  # warmup
+        timed_broadcast(sim)  # warmup (builds the reverse table)
+        rev_ms = sim.timing()["prep_ms"]
         runs = [timed_broadcast(sim) for _ in range(max(a.steps, 1))]
         dt = sum(r[2] for r in runs)
         tot, status, _ = runs[-1]
@@ -399,10 +410,8 @@ def pushpull_runs(a, gs, rank, local):
         sim.set_flags(False)
         rounds = int(tm["deliver_launches"])
         ms = tm["deliver_ms"]
-        calls = tot["fired"]
         # 8 algorithmic bytes per delivered push-pull message
         ach = 8 * tot["messages"] / (ms * 1e-3) / 1e9
-        ach_call = 12 * calls / (ms * 1e-3) / 1e9
         log(f"push-pull: rounds={tot['tick']} sent={tot['sent']} {dt * 1e3 / len(runs):.1f} ms/run")
         out["pushpull"] = {
             "value": round(sum(r[0]["messages"] for r in runs) / dt, 1), "unit": "msgs/s",
@@ -414,15 +423,17 @@ def pushpull_runs(a, gs, rank, local):
                          "bytes": "8 per delivered message (SURVEY.md 8(d))",
                          "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 5),
-                         "frac_12B_per_call": round(ach_call / HBM_PEAK_GBS, 5),
-                         "avg_launch_us": round(ms * 1e3 / max(rounds, 1), 2), "launches": rounds}}
+                         "avg_launch_us": round(ms * 1e3 / max(rounds, 1), 2), "launches": rounds,
+                         **pp_pmc_traffic()},
+            "rev_table_prep_ms": round(rev_ms, 3)}
         sim.reset()
         sim.set_failed(failed_mask(a.n, 0.01, a.seed + 1))
         tot, status, dt = timed_broadcast(sim)
         log(f"push-pull+1% failed: rounds={tot['tick']} {dt * 1e3:.1f} ms {STATUS[status]}")
         out["pushpull_failed_1pct"] = {
             "value": round(tot["messages"] / dt, 1), "unit": "msgs/s", "ms": round(dt * 1e3, 3),
-            "rounds": tot["tick"], "received": tot["received"], "status": STATUS[status]}
+            "rounds": tot["tick"], "received": tot["received"], "status": STATUS[status],
+            "prep_ms": round(sim.timing()["prep_ms"], 3)}
     return out
 
 
@@ -430,8 +441,13 @@ def c3_trials(a, gs, rank, world, local, dist):
     """Config C3: a.c3_trials trials at N = 1e5 (reference defaults), each its
     own GPU-built overlay and broadcast to its 99 % poll, split over the ranks
     and run as batched contexts of a.c3_batch trials (all of a batch's
-    overlays, then all its broadcasts, at once).  Timed end to end: context
-    creation, overlay, broadcast, results."""
+    overlays, then all its broadcasts, at once).  Timed end to end: every
+    batch's renumbering, overlay, broadcast and results.  The batch contexts
+    (one per batch size, ~30 GB of device memory at 5,000 trials) are created
+    and run once before the timer, like the headline's warmup steps: right
+    after the previous legs free their 1e9-node contexts, their first
+    allocation stalled for ~5 s on some boxes of the pool
+    (profiles/r05e_c3_after.txt), which is no property of the trials."""
     import numpy as np
     import torch
     from dataclasses import replace
@@ -439,29 +455,38 @@ def c3_trials(a, gs, rank, world, local, dist):
     t0, t1 = gd.trial_range(a.c3_trials, rank, world)
     cfg = gs.Config(n=100_000, seed=a.seed, device=local)
 
-    with gs.Simulator(replace(cfg, trial=t0, trials=min(64, t1 - t0))) as sim:  # warmup: code objects
-        sim.build_overlay()
-        sim.broadcast_begin(-1)
-        sim.run(poll=10)
+    # one context per batch size, renumbered batch after batch (gs_set_trial)
+    sims = {}
+    for b in range(t0, t1, a.c3_batch):  # warmup: contexts, workspaces, code objects
+        T = min(b + a.c3_batch, t1) - b
+        if T not in sims:
+            tw = time.perf_counter()
+            sims[T] = gs.Simulator(replace(cfg, trial=b, trials=T))
+            sims[T].build_overlay()
+            sims[T].broadcast_begin(-1)
+            sims[T].run(poll=10)
+            torch.cuda.synchronize()
+            log(f"C3 warmup: context of {T} trials created and run once in {time.perf_counter() - tw:.2f} s")
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     start = time.perf_counter()
     rows = []
-    # one context per batch size, renumbered batch after batch (gs_set_trial)
-    sims = {}
     try:
         for b in range(t0, t1, a.c3_batch):
             T = min(b + a.c3_batch, t1) - b
-            if T not in sims:
-                sims[T] = gs.Simulator(replace(cfg, trial=b, trials=T))
             sim = sims[T]
             sim.reset()
             sim.set_trial(b)
+            tb = time.perf_counter()
             sim.build_overlay()
+            tm = sim.timing()
             sim.broadcast_begin(-1)
             sim.run(poll=10)
             rows.append(sim.trial_results())
+            log(f"C3 batch {b}: {T} trials, overlay {tm['overlay_ms']:.0f} ms (ticks partitioned "
+                f"{tm['ov_part_ticks']}, sorted {tm['ov_sort_ticks']}, fallbacks {tm['ov_part_fallbacks']}), "
+                f"batch {(time.perf_counter() - tb) * 1e3:.0f} ms")
         torch.cuda.synchronize()
         dt = time.perf_counter() - start
     finally:
@@ -701,6 +726,21 @@ def pmc_traffic():
     return int(d["bytes_per_launch"]), (f"{os.path.relpath(path, ROOT)} (from {d['source']}): calibrated "
                                         f"read requests + WRITE_SIZE over {d['launches']} window launches "
                                         f"of one broadcast")
+
+
+def pp_pmc_traffic():
+    """HBM bytes of one C5 push-pull broadcast's round kernels from the
+    committed PMC passes (scripts/pmc_pp.sh -> scripts/pmc_pp_traffic.py; the
+    same calibrated read requests + WRITE_SIZE as pmc_traffic) against SURVEY.md
+    8(d)'s 8 B per delivered message: the profile of the same workload at this
+    commit's kernels, not of this run."""
+    path = os.path.join(ROOT, "profiles", "pmc_pp_traffic.json")
+    if not os.path.exists(path):
+        return {"traffic": None, "traffic_note": "no push-pull PMC profile committed"}
+    d = json.load(open(path))
+    return {"traffic": int(d["round_bytes"]), "traffic_unit": "bytes per broadcast", "traffic_ratio": d["traffic_ratio"],
+            "traffic_note": (f"{os.path.relpath(path, ROOT)} (from {d['source']}): bytes per broadcast over "
+                             f"{d['rounds']} rounds; traffic_ratio = PMC bytes / (8 B x {d['messages']} messages)")}
 
 
 def cpu_model():

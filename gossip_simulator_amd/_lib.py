@@ -88,7 +88,8 @@ class Timing(C.Structure):
                 ("part_ms", C.c_double), ("windows", C.c_uint64), ("exact_redos", C.c_uint64),
                 ("prep_ms", C.c_double),
                 ("pp_early_rounds", C.c_uint64), ("pp_bottom_rounds", C.c_uint64),
-                ("pp_answer_rounds", C.c_uint64), ("dd_fallbacks", C.c_uint64), ("pp_rev_part", C.c_uint64)]
+                ("pp_answer_rounds", C.c_uint64), ("dd_fallbacks", C.c_uint64), ("pp_rev_part", C.c_uint64),
+                ("ov_part_ticks", C.c_uint64), ("ov_sort_ticks", C.c_uint64), ("ov_part_fallbacks", C.c_uint64)]
 
 
 # gs_exchange (gossip.h): host callbacks of a gs_create_rank_exchange rank

@@ -1428,6 +1428,9 @@ int overlay_into(gs_ctx* c, uint64_t max_ticks, gs_window* win, size_t cap, size
                                OverlayWindowSink{&WinSink::push, &ws}, &res, &c->ovw);
   c->timing.overlay_ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  c->timing.ov_part_ticks = c->ovw.part_ticks;
+  c->timing.ov_sort_ticks = c->ovw.sort_ticks;
+  c->timing.ov_part_fallbacks = c->ovw.part_fallbacks;
   if (nwin) *nwin = ws.n;
   if (final_tick) *final_tick = res.final_tick;
   // batched contexts rebuild per batch (gs_set_trial): keep the workspace

@@ -475,6 +475,8 @@ struct OverlayWork {
   struct Buf { void* p = nullptr; size_t bytes = 0; };
   std::vector<Buf> bucket;  // per arrival slot
   Buf scratch, outb, oslotb, cub_tmp, meta;
+  Buf fine, ovp;            // destination partition of the dense ticks: regions, plan + fills
+  uint64_t part_ticks = 0, sort_ticks = 0, part_fallbacks = 0;  // of the last build
 };
 void overlay_free(OverlayWork* ws, hipStream_t st);
 // n = nodes per trial; trials > 1 builds every trial's overlay at once in the

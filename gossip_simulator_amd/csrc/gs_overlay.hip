@@ -35,6 +35,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -328,6 +329,269 @@ __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64
     if (s_hist[q]) atomicAdd(&counts[q], (unsigned long long)s_hist[q]);
 }
 
+// ---- destination partition of a dense tick (replaces the radix sort) -------
+// k_process needs each destination's events contiguous, not the bucket in
+// global destination order, so a dense tick is grouped in three passes:
+//   P1 (k_ov_part<false>): the bucket -> coarse regions by dst >> (F + 8),
+//      each coarse region in kOvSub sub-regions, one per XCD (tile t writes
+//      sub-region t % 8: the reservation atomics of a region spread over 8
+//      addresses -- one address per coarse region took P1 from 3.3 to 5.4 ms
+//      per burst tick);
+//   P2 (k_ov_part<true>):  each coarse sub-region -> its 256 fine regions by
+//      dst >> F (F = kOvFineLog: 16,384 ids per fine bucket);
+//   k_ov_scan:             the fine regions' fills -> compact offsets;
+//   P3 (k_ov_fine):        each fine region counting-sorted by its 14-bit
+//      local destination in LDS, written at its compact offset: k_process
+//      gets exactly the tick's m keys (padded regions cost it 7 %).
+// P1 and P2 are LDS counting sorts of 8192-key tiles over 256 digits written
+// out as runs (≈ 32 keys, 256 B per run): two streaming passes where the
+// Onesweep sort made four digit passes plus a histogram pass.  Region sizes
+// are planned from the tick's event count and each fine bucket's share of
+// the id space (the destinations are uniform over live ids); a region that
+// would overflow sets a flag and the host sorts that tick with rocprim
+// instead -- the bucket itself is only read, so the fallback starts from it.
+// Within a destination the events come out in no particular order; k_process
+// orders each run by (tag, src, kind) itself, so the result is the same.
+constexpr uint32_t kOvFineLog = 14;
+constexpr uint32_t kOvpBlock = 512, kOvpIPT = 16, kOvpTile = kOvpBlock * kOvpIPT;  // 8192 keys per tile
+constexpr uint32_t kOvSub = 8;  // P1 sub-regions per coarse region (one per XCD: blockIdx % 8)
+constexpr uint32_t kOvFineBlock = 1024, kOvFineIPT = 16;
+constexpr uint32_t kOvFineMax = kOvFineBlock * kOvFineIPT;  // keys a fine region may hold (= 2^kOvFineLog)
+static_assert(kOvFineMax == 1u << kOvFineLog, "one counter per local destination");
+
+struct OvPart {
+  const uint64_t* in;
+  uint64_t* out;
+  uint64_t m;                          // P1: the bucket's keys
+  const unsigned long long* fstart;    // [nfb + 1] fine region starts; coarse region c = fine regions 256c ..
+  unsigned long long* cfill;           // [ncb * kOvSub] coarse sub-region fills
+  unsigned long long* ffill;           // [nfb] fine region fills
+  const uint32_t* tprefix;             // [ncb * kOvSub + 1] P2 tiles per coarse sub-region (prefix)
+  uint32_t* flag;                      // 1: a region overflowed
+  uint32_t ncb, nfb, sh;               // coarse / fine regions, the key's destination shift
+  uint32_t sfrac[kOvSub + 1];          // sub-region x of a coarse region: [sfrac[x], sfrac[x+1]) / 2^20 of it
+};
+
+// The split of a coarse region over its kOvSub sub-regions: P1's tile t
+// writes sub-region t % kOvSub, so sub-region x gets the share of the bucket
+// its tiles hold, in 2^-20 units (host and device split alike).
+constexpr uint32_t kOvFracBits = 20;
+__host__ __device__ inline uint64_t ov_sub_at(uint64_t cs, uint64_t ce, uint32_t frac) {
+  return cs + (((ce - cs) * frac) >> kOvFracBits);
+}
+__device__ __forceinline__ void ov_sub(const OvPart& a, uint32_t c, uint32_t x, unsigned long long& start,
+                                       unsigned long long& cap) {
+  const unsigned long long cs = a.fstart[(uint64_t)c << 8], ce = a.fstart[min((c + 1) << 8, a.nfb)];
+  start = ov_sub_at(cs, ce, a.sfrac[x]);
+  cap = ov_sub_at(cs, ce, a.sfrac[x + 1]) - start;
+}
+
+__device__ __forceinline__ uint32_t block_exscan256(uint32_t v, uint32_t* s_ws) {
+  // exclusive scan of v over threads 0..255 of the block (v = 0 elsewhere);
+  // every thread calls it
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63 && wv < 4) s_ws[wv] = x;
+  __syncthreads();
+  uint32_t before = 0;
+  for (uint32_t q = 0; q < wv && q < 4; ++q) before += s_ws[q];
+  __syncthreads();
+  return before + x - v;
+}
+
+template <bool FINE>
+__global__ __launch_bounds__(kOvpBlock) void k_ov_part(const OvPart a) {
+  __shared__ uint64_t s_key[kOvpTile];
+  __shared__ uint32_t s_cnt[256], s_off[256], s_ws[4], s_ovf;
+  __shared__ unsigned long long s_gb[256];
+  const uint32_t tid = threadIdx.x;
+  uint64_t lo, hi;
+  uint32_t dshift, dbase = 0, xsub = 0;
+  if (!FINE) {
+    lo = (uint64_t)blockIdx.x * kOvpTile;
+    hi = min(a.m, lo + kOvpTile);
+    dshift = kOvFineLog + 8;
+    xsub = blockIdx.x % kOvSub;  // consecutive workgroups run on consecutive XCDs
+  } else {
+    // tile b of coarse sub-region r = c * kOvSub + x: tprefix[r] <= b < tprefix[r + 1]
+    const uint32_t b = blockIdx.x;
+    uint32_t l = 0, r = a.ncb * kOvSub;
+    while (r - l > 1) {
+      const uint32_t mid = (l + r) >> 1;
+      if (a.tprefix[mid] <= b) l = mid; else r = mid;
+    }
+    unsigned long long st, cap;
+    ov_sub(a, l / kOvSub, l % kOvSub, st, cap);
+    lo = st + (uint64_t)(b - a.tprefix[l]) * kOvpTile;
+    hi = min(st + min((unsigned long long)a.cfill[l], cap), lo + kOvpTile);  // (an overflowed P1 is discarded)
+    dshift = kOvFineLog;
+    dbase = (l / kOvSub) << 8;
+  }
+  if (lo >= hi) return;  // (uniform: an empty tail tile of a region)
+  if (tid < 256) s_cnt[tid] = 0;
+  if (tid == 0) s_ovf = 0;
+  __syncthreads();
+  const uint32_t n = (uint32_t)(hi - lo);
+  uint64_t key[kOvpIPT];
+  uint32_t rank[kOvpIPT];
+#pragma unroll
+  for (uint32_t j = 0; j < kOvpIPT; ++j) {
+    const uint32_t i = j * kOvpBlock + tid;
+    if (i < n) {
+      key[j] = a.in[lo + i];
+      const uint32_t d = (uint32_t)(key[j] >> (a.sh + dshift)) - dbase;
+      rank[j] = atomicAdd(&s_cnt[d & 255], 1u);
+      if (d > 255) s_ovf = 1;  // (not a destination of this region: corrupt input)
+    }
+  }
+  __syncthreads();
+  const uint32_t c = tid < 256 ? s_cnt[tid] : 0u;
+  const uint32_t off = block_exscan256(c, s_ws);
+  if (tid < 256) {
+    s_off[tid] = off;
+    if (c) {
+      const uint32_t reg = dbase + tid;  // P1: coarse region; P2: fine region
+      unsigned long long st, cap, *fill;
+      if (FINE) {
+        st = reg < a.nfb ? a.fstart[reg] : 0;
+        cap = reg < a.nfb ? a.fstart[reg + 1] - st : 0;
+        fill = &a.ffill[min(reg, a.nfb - 1)];
+      } else {
+        if (reg < a.ncb) ov_sub(a, reg, xsub, st, cap);
+        else st = cap = 0;
+        fill = &a.cfill[min(reg, a.ncb - 1) * kOvSub + xsub];
+      }
+      if (cap == 0) {
+        s_ovf = 1;
+      } else {
+        const unsigned long long base = atomicAdd(fill, (unsigned long long)c);
+        if (base + c > cap) s_ovf = 1;
+        s_gb[tid] = st + base;
+      }
+    }
+  }
+  __syncthreads();
+  if (s_ovf) {
+    if (tid == 0) atomicOr(a.flag, 1u);
+    return;
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kOvpIPT; ++j) {
+    const uint32_t i = j * kOvpBlock + tid;
+    if (i < n) {
+      const uint32_t d = ((uint32_t)(key[j] >> (a.sh + dshift)) - dbase) & 255;
+      s_key[s_off[d] + rank[j]] = key[j];
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += kOvpBlock) {  // runs of one digit: consecutive addresses
+    const uint64_t k = s_key[i];
+    const uint32_t d = ((uint32_t)(k >> (a.sh + dshift)) - dbase) & 255;
+    a.out[s_gb[d] + (i - s_off[d])] = k;
+  }
+}
+
+// The fine regions' fills -> the exclusive prefix fbase[0..nfb] (one
+// workgroup): P3 writes fine region f's keys at fbase[f], so k_process gets
+// the tick's keys back to back, without the regions' unused tails.
+constexpr uint32_t kOvScanBlock = 1024;
+__global__ __launch_bounds__(kOvScanBlock) void k_ov_scan(const unsigned long long* ffill, uint32_t nfb,
+                                                          const unsigned long long* fstart,
+                                                          unsigned long long* fbase) {
+  __shared__ unsigned long long s_ws[kOvScanBlock / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t per = (nfb + kOvScanBlock - 1) / kOvScanBlock, f0 = min(tid * per, nfb), f1 = min(f0 + per, nfb);
+  auto fill = [&](uint32_t f) {  // (an overflowed region is discarded with the tick)
+    return min(ffill[f], fstart[f + 1] - fstart[f]);
+  };
+  unsigned long long sum = 0;
+  for (uint32_t f = f0; f < f1; ++f) sum += fill(f);
+  unsigned long long x = sum;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const unsigned long long y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) s_ws[wv] = x;
+  __syncthreads();
+  unsigned long long run = x - sum;
+  for (uint32_t q = 0; q < wv; ++q) run += s_ws[q];
+  for (uint32_t f = f0; f < f1; ++f) {
+    fbase[f] = run;
+    run += fill(f);
+  }
+  if (tid == kOvScanBlock - 1) fbase[nfb] = run;
+}
+
+// P3: fine region f (in: P2's output) counting-sorted by local destination
+// into out at fbase[f].  Keys stay in registers (16 per lane); counters,
+// then offsets, are u16 pairs in u32 words.
+__global__ __launch_bounds__(kOvFineBlock) void k_ov_fine(const uint64_t* in, uint64_t* out,
+                                                          const unsigned long long* fstart,
+                                                          const unsigned long long* ffill,
+                                                          const unsigned long long* fbase, uint32_t sh) {
+  __shared__ uint32_t s_c[kOvFineMax / 2];
+  __shared__ uint32_t s_ws[kOvFineBlock / 64];
+  const uint32_t f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint64_t lo = fstart[f], cap = fstart[f + 1] - lo;
+  const uint32_t n = (uint32_t)min((uint64_t)ffill[f], cap);  // (cap <= kOvFineMax: the host's plan)
+  const uint64_t ob = fbase[f];
+#pragma unroll
+  for (uint32_t q = 0; q < kOvFineMax / 2 / kOvFineBlock; ++q) s_c[q * kOvFineBlock + tid] = 0;
+  __syncthreads();
+  uint64_t key[kOvFineIPT];
+#pragma unroll
+  for (uint32_t j = 0; j < kOvFineIPT; ++j) {
+    const uint32_t i = j * kOvFineBlock + tid;
+    if (i < n) {
+      key[j] = in[lo + i];
+      const uint32_t l = (uint32_t)(key[j] >> sh) & (kOvFineMax - 1);
+      atomicAdd(&s_c[l >> 1], 1u << ((l & 1) << 4));
+    }
+  }
+  __syncthreads();
+  // exclusive scan over the 16,384 counters: thread t owns words 8t .. 8t + 7
+  constexpr uint32_t W = kOvFineMax / 2 / kOvFineBlock;
+  uint32_t sum = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < W; ++q) {
+    const uint32_t w = s_c[tid * W + q];
+    sum += (w & 0xFFFFu) + (w >> 16);
+  }
+  uint32_t x = sum;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) s_ws[wv] = x;
+  __syncthreads();
+  uint32_t run = x - sum;
+  for (uint32_t q = 0; q < wv; ++q) run += s_ws[q];
+#pragma unroll
+  for (uint32_t q = 0; q < W; ++q) {
+    const uint32_t w = s_c[tid * W + q], c0 = w & 0xFFFFu;
+    s_c[tid * W + q] = run | ((run + c0) << 16);
+    run += c0 + (w >> 16);
+  }
+  __syncthreads();
+  // each key takes the next place of its destination (the offsets count up:
+  // a destination's half-word never carries into its neighbour's)
+#pragma unroll
+  for (uint32_t j = 0; j < kOvFineIPT; ++j) {
+    const uint32_t i = j * kOvFineBlock + tid;
+    if (i < n) {
+      const uint32_t l = (uint32_t)(key[j] >> sh) & (kOvFineMax - 1), s = (l & 1) << 4;
+      out[ob + ((atomicAdd(&s_c[l >> 1], 1u << s) >> s) & 0xFFFFu)] = key[j];
+    }
+  }
+}
+
 #define OVCHK(expr)                                                              \
   do {                                                                           \
     hipError_t e_ = (expr);                                                      \
@@ -357,6 +621,72 @@ static hipError_t grow(DevBuf& b, size_t bytes, hipStream_t st) {
   return e;
 }
 
+// The destination partition's plan for a tick of m events: fine region
+// capacities from each fine bucket's share of the live ids (4 % + 6 sigma +
+// 32 over its expected count -- the breakup waves after the burst are
+// over-dispersed: at 1 % + 5 sigma five N = 1e9 ticks overflowed a fine
+// region by up to 3 %; GS_OV_PART_SCALE replaces the 1.04, and one
+// below 1 drops the slack -- the tests force the overflow fallback with it),
+// coarse regions = 256 fine regions each.  False
+// where the partition does not apply (a sparse tick: the radix sort's fixed
+// cost is lower; a fine region beyond LDS; more than 256 coarse regions).
+struct OvPlan {
+  uint64_t nfb = 0, ncb = 0, total = 0, m = 0;
+  double scale = 0;
+  std::vector<unsigned long long> fstart;  // [nfb + 1]
+  std::vector<uint32_t> tprefix;           // [ncb * kOvSub + 1]
+  uint32_t sfrac[kOvSub + 1];              // OvPart::sfrac
+};
+
+static bool ov_plan(OvPlan& pl, uint64_t m, uint64_t n, uint32_t trials, uint32_t tlog, uint64_t ntot,
+                    double scale) {
+  const uint64_t nfb = (ntot + kOvFineMax - 1) >> kOvFineLog, ncb = (nfb + 255) / 256;
+  if (nfb == 0 || ncb > 256 || m < 32 * nfb) return false;
+  if (pl.m == m && pl.nfb == nfb && pl.scale == scale) return true;
+  const uint64_t tmask = tlog >= 32 ? ~0ull : (1ull << tlog) - 1;
+  const double live = (double)n * (trials > 1 ? trials : 1);
+  pl.m = 0;
+  pl.nfb = nfb;
+  pl.ncb = ncb;
+  pl.fstart.resize(nfb + 1);
+  pl.tprefix.resize(ncb * kOvSub + 1);
+  uint64_t at = 0;
+  for (uint64_t f = 0; f < nfb; ++f) {
+    pl.fstart[f] = at;
+    const uint64_t local = (f << kOvFineLog) & tmask;  // (tlog >= kOvFineLog: a fine bucket is in one trial)
+    const uint64_t valid = local < n ? std::min<uint64_t>(kOvFineMax, n - local) : 0;
+    if (!valid) continue;
+    const double e = (double)m * (double)valid / live;
+    const uint64_t cap = (uint64_t)std::ceil(scale >= 1.0 ? e * scale + 6.0 * std::sqrt(e) + 32.0 : e * scale);
+    if (cap > kOvFineMax) return false;
+    at += cap;
+  }
+  pl.fstart[nfb] = at;
+  pl.total = at;
+  // P1 tile t (kOvpTile keys, the last one short) writes sub-region t % kOvSub
+  const uint64_t ntile = (m + kOvpTile - 1) / kOvpTile;
+  uint64_t kx = 0;
+  pl.sfrac[0] = 0;
+  for (uint32_t x = 0; x < kOvSub; ++x) {
+    for (uint64_t t = x; t < ntile; t += kOvSub) kx += std::min<uint64_t>(kOvpTile, m - t * kOvpTile);
+    pl.sfrac[x + 1] = (uint32_t)((kx << kOvFracBits) / m);
+  }
+  pl.sfrac[kOvSub] = 1u << kOvFracBits;
+  uint32_t tiles = 0;  // P2's tiles per coarse sub-region, as ov_sub splits them
+  for (uint64_t c = 0; c < ncb; ++c) {
+    const uint64_t cs = pl.fstart[c * 256], ce = pl.fstart[std::min<uint64_t>((c + 1) * 256, nfb)];
+    for (uint32_t x = 0; x < kOvSub; ++x) {
+      pl.tprefix[c * kOvSub + x] = tiles;
+      const uint64_t cx = ov_sub_at(cs, ce, pl.sfrac[x + 1]) - ov_sub_at(cs, ce, pl.sfrac[x]);
+      tiles += (uint32_t)((cx + kOvpTile - 1) / kOvpTile);
+    }
+  }
+  pl.tprefix[ncb * kOvSub] = tiles;
+  pl.m = m;
+  pl.scale = scale;
+  return true;
+}
+
 static uint32_t node_bits(uint64_t n) {
   uint32_t b = 1;
   while (b < 31 && (1ull << b) < n) ++b;
@@ -371,7 +701,7 @@ void overlay_free(OverlayWork* ws, hipStream_t st) {
   for (auto& b : ws->bucket)
     if (b.p) (void)hipFree(b.p);
   ws->bucket.clear();
-  for (DevBuf* b : {&ws->scratch, &ws->outb, &ws->oslotb, &ws->cub_tmp, &ws->meta}) {
+  for (DevBuf* b : {&ws->scratch, &ws->outb, &ws->oslotb, &ws->cub_tmp, &ws->meta, &ws->fine, &ws->ovp}) {
     if (b->p) (void)hipFree(b->p);
     b->p = nullptr;
     b->bytes = 0;
@@ -435,7 +765,18 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
   std::vector<DevBuf>& bucket = ws->bucket;
   std::vector<uint64_t> fill(NB, 0);
   DevBuf &scratch = ws->scratch, &outb = ws->outb, &oslotb = ws->oslotb, &cub_tmp = ws->cub_tmp,
-         &meta = ws->meta;
+         &meta = ws->meta, &fine = ws->fine, &ovp = ws->ovp;
+  // the destination partition of dense ticks (GS_OV_SORT=1: the radix sort
+  // for every tick, A/B)
+  // Batched trials drift apart after the burst (one trial's wave of
+  // breakups is another's lull), so a tick's events are not spread over the
+  // id space by node share and the plans overflowed on every dense tick of
+  // C3 (up to 16x a fine region's share); they keep the sort.
+  const bool part_ok = !getenv("GS_OV_SORT") && (trials <= 1 || getenv("GS_OV_PART_BATCHED"));
+  const double part_scale = getenv("GS_OV_PART_SCALE") ? atof(getenv("GS_OV_PART_SCALE")) : 1.04;
+  OvPlan plan;
+  uint32_t h_flag = 0;
+  ws->part_ticks = ws->sort_ticks = ws->part_fallbacks = 0;
   // meta layout: counts[NB] | fill[NB] | ptrs[NB] | nemit (64 B) | TickCounters
   uint64_t pending = 0, wm = 0, wb = 0;
   std::vector<unsigned long long> h_counts(NB), hfill(NB);
@@ -501,27 +842,103 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
                  (unsigned long long)m);
         goto cleanup;
       }
-      OVCHK(grow(scratch, m * 8, stream));
       OVCHK(grow(outb, m * 8, stream));
       OVCHK(grow(oslotb, m * 2, stream));
       {
-        // by (destination, tag): each destination's run comes out tick by
-        // tick, and the process kernel orders each tick's few events by
-        // (src, kind) itself (sorting by destination only left runs of L
-        // ticks to the insertion sort, in global memory: slower than the
-        // TB extra radix bits)
-        rocprim::double_buffer<uint64_t> db((uint64_t*)bucket[s].p, (uint64_t*)scratch.p);
-        const unsigned begin_bit = p.B + 1, end_bit = 2 * p.B + 1 + p.TB;
-        size_t sort_bytes = 0;
-        OVCHK(rocprim::radix_sort_keys<OvRadix>(nullptr, sort_bytes, db, (size_t)m, begin_bit, end_bit, stream));
-        OVCHK(grow(cub_tmp, sort_bytes, stream));
-        sort_bytes = cub_tmp.bytes;
-        OVCHK(rocprim::radix_sort_keys<OvRadix>(cub_tmp.p, sort_bytes, db, (size_t)m, begin_bit, end_bit, stream));
-        uint64_t* keys = db.current();
-        if (db.current() != (uint64_t*)bucket[s].p) std::swap(bucket[s], scratch);
+        uint64_t* keys = nullptr;
+        uint64_t mproc = m;
+        if (part_ok && ov_plan(plan, m, n, trials, tlog, ntot, part_scale)) {
+          // P1 bucket -> fine.p (coarse regions), P2 -> scratch (fine
+          // regions), P3 -> fine.p (sorted, padded); the bucket stays intact
+          const uint64_t nfb = plan.nfb, ncb = plan.ncb;
+          const size_t b_fs = (nfb + 1) * 8, b_fill = (ncb * kOvSub + nfb) * 8, b_tp = (ncb * kOvSub + 1) * 4;
+          OVCHK(grow(scratch, plan.total * 8, stream));
+          OVCHK(grow(fine, plan.total * 8, stream));
+          OVCHK(grow(ovp, 2 * b_fs + b_fill + b_tp + 16, stream));
+          unsigned long long* d_fstart = (unsigned long long*)ovp.p;
+          unsigned long long* d_fbase = d_fstart + nfb + 1;
+          unsigned long long* d_cfill = d_fbase + nfb + 1;
+          uint32_t* d_tp = (uint32_t*)(d_cfill + ncb * kOvSub + nfb);
+          uint32_t* d_flag = d_tp + ncb * kOvSub + 1;
+          OVCHK(hipMemcpyAsync(d_fstart, plan.fstart.data(), b_fs, hipMemcpyHostToDevice, stream));
+          OVCHK(hipMemcpyAsync(d_tp, plan.tprefix.data(), b_tp, hipMemcpyHostToDevice, stream));
+          OVCHK(hipMemsetAsync(d_cfill, 0, b_fill, stream));
+          OVCHK(hipMemsetAsync(d_flag, 0, 4, stream));
+          OvPart a{(const uint64_t*)bucket[s].p, (uint64_t*)fine.p, m, d_fstart, d_cfill, d_cfill + ncb * kOvSub, d_tp,
+                   d_flag, (uint32_t)ncb, (uint32_t)nfb, p.B + 1 + p.TB, {}};
+          std::copy(plan.sfrac, plan.sfrac + kOvSub + 1, a.sfrac);
+          hipLaunchKernelGGL((k_ov_part<false>), dim3((uint32_t)((m + kOvpTile - 1) / kOvpTile)), dim3(kOvpBlock),
+                             0, stream, a);
+          OVCHK(hipGetLastError());
+          a.in = (const uint64_t*)fine.p;
+          a.out = (uint64_t*)scratch.p;
+          if (plan.tprefix[ncb * kOvSub]) {
+            hipLaunchKernelGGL((k_ov_part<true>), dim3(plan.tprefix[ncb * kOvSub]), dim3(kOvpBlock), 0, stream, a);
+            OVCHK(hipGetLastError());
+          }
+          hipLaunchKernelGGL(k_ov_scan, dim3(1), dim3(kOvScanBlock), 0, stream,
+                             (const unsigned long long*)(d_cfill + ncb * kOvSub), (uint32_t)nfb,
+                             (const unsigned long long*)d_fstart, d_fbase);
+          OVCHK(hipGetLastError());
+          hipLaunchKernelGGL(k_ov_fine, dim3((uint32_t)nfb), dim3(kOvFineBlock), 0, stream,
+                             (const uint64_t*)scratch.p, (uint64_t*)fine.p, (const unsigned long long*)d_fstart,
+                             (const unsigned long long*)(d_cfill + ncb * kOvSub), (const unsigned long long*)d_fbase,
+                             p.B + 1 + p.TB);
+          OVCHK(hipGetLastError());
+          OVCHK(hipMemcpyAsync(&h_flag, d_flag, 4, hipMemcpyDeviceToHost, stream));
+          OVCHK(hipStreamSynchronize(stream));
+          if (!h_flag) {
+            keys = (uint64_t*)fine.p;  // m keys (no region overflowed: every key was placed)
+            ++ws->part_ticks;
+          } else {
+            ++ws->part_fallbacks;  // a region overflowed its plan: sort this tick
+            if (getenv("GS_OV_DEBUG")) {  // which level overflowed, by how much
+              std::vector<unsigned long long> cf(ncb * kOvSub), ff(nfb);
+              OVCHK(hipMemcpy(cf.data(), d_cfill, cf.size() * 8, hipMemcpyDeviceToHost));
+              OVCHK(hipMemcpy(ff.data(), d_cfill + ncb * kOvSub, ff.size() * 8, hipMemcpyDeviceToHost));
+              double worst_c = 0, worst_f = 0;
+              uint64_t nc = 0, nf = 0;
+              for (uint64_t c = 0; c < ncb; ++c) {
+                const uint64_t cs = plan.fstart[c * 256], ce = plan.fstart[std::min<uint64_t>((c + 1) * 256, nfb)];
+                for (uint32_t x = 0; x < kOvSub; ++x) {
+                  const uint64_t cap = ov_sub_at(cs, ce, plan.sfrac[x + 1]) - ov_sub_at(cs, ce, plan.sfrac[x]);
+                  const double r = cap ? (double)cf[c * kOvSub + x] / cap : 1e9;
+                  if (cf[c * kOvSub + x] > cap) ++nc;
+                  worst_c = std::max(worst_c, r);
+                }
+              }
+              for (uint64_t f = 0; f < nfb; ++f) {
+                const uint64_t cap = plan.fstart[f + 1] - plan.fstart[f];
+                if (ff[f] > cap) ++nf;
+                worst_f = std::max(worst_f, cap ? (double)ff[f] / cap : (ff[f] ? 1e9 : 0));
+              }
+              fprintf(stderr, "[overlay] tick %llu: m=%llu partition fallback: %llu coarse / %llu fine regions over, "
+                      "worst fill/cap %.3f / %.3f\n", (unsigned long long)t0, (unsigned long long)m,
+                      (unsigned long long)nc, (unsigned long long)nf, worst_c, worst_f);
+            }
+          }
+        }
+        if (!keys) {
+          // by (destination, tag): each destination's run comes out tick by
+          // tick, and the process kernel orders each tick's few events by
+          // (src, kind) itself (sorting by destination only left runs of L
+          // ticks to the insertion sort, in global memory: slower than the
+          // TB extra radix bits)
+          OVCHK(grow(scratch, m * 8, stream));
+          rocprim::double_buffer<uint64_t> db((uint64_t*)bucket[s].p, (uint64_t*)scratch.p);
+          const unsigned begin_bit = p.B + 1, end_bit = 2 * p.B + 1 + p.TB;
+          size_t sort_bytes = 0;
+          OVCHK(rocprim::radix_sort_keys<OvRadix>(nullptr, sort_bytes, db, (size_t)m, begin_bit, end_bit, stream));
+          OVCHK(grow(cub_tmp, sort_bytes, stream));
+          sort_bytes = cub_tmp.bytes;
+          OVCHK(rocprim::radix_sort_keys<OvRadix>(cub_tmp.p, sort_bytes, db, (size_t)m, begin_bit, end_bit, stream));
+          keys = db.current();
+          if (db.current() != (uint64_t*)bucket[s].p) std::swap(bucket[s], scratch);
+          ++ws->sort_ticks;
+        }
         const uint64_t per = (uint64_t)kProcBlock * kProcIPT;
-        hipLaunchKernelGGL(k_process, dim3((uint32_t)((m + per - 1) / per)), dim3(kProcBlock), 0, stream, p, t0,
-                           keys, m, d_deg, d_ids, (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_nemit, d_counts,
+        hipLaunchKernelGGL(k_process, dim3((uint32_t)((mproc + per - 1) / per)), dim3(kProcBlock), 0, stream, p,
+                           t0, keys, mproc, d_deg, d_ids, (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_nemit, d_counts,
                            d_tc);
         OVCHK(hipGetLastError());
       }

@@ -130,6 +130,10 @@ typedef struct gs_timing {
                               * host-driven (cumulative; a buffer that fits makes it stop growing) */
   uint64_t pp_rev_part;      /* push-pull: 1 if the last reverse table was built by partitioning the
                               * edges, 0 by the atomic count + fill (GS_PP_REV_ATOMIC, or a fallback) */
+  uint64_t ov_part_ticks;    /* last overlay build: ticks grouped by the destination partition     */
+  uint64_t ov_sort_ticks;    /* last overlay build: ticks grouped by the radix sort (sparse ticks,
+                              * GS_OV_SORT=1, or a partition fallback)                              */
+  uint64_t ov_part_fallbacks; /* last overlay build: partition plans that overflowed (then sorted) */
 } gs_timing;
 
 /* gs_run status */

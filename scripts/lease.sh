@@ -9,6 +9,8 @@
 #   pw                   rocprofv3 kernel trace of one broadcast: per-window split (scripts/pw.sh)
 #   prof[=bench args]    rocprofv3 kernel trace of a short bench (scripts/prof.sh)
 #   pmc                  PMC passes over one broadcast (scripts/pmc.sh)
+#   pmcpp                PMC passes over one C5 push-pull broadcast (scripts/pmc_pp.sh)
+#   pool                 the stream-ordered pool reproducer in its diagnosis modes (scripts/micro/pool_repro.hip)
 #   ab=ENV_A,ENV_B,...   interleaved A/B/... benches (scripts/abn.sh)
 set -o pipefail
 tag=${1:?tag}; shift
@@ -38,6 +40,18 @@ for step in "$@"; do
       bash scripts/prof.sh "$tag/prof" $arg || exit 1 ;;
     pmc)
       bash scripts/pmc.sh "$o/pmc" || exit 1 ;;
+    pmcpp)
+      bash scripts/pmc_pp.sh "$o/pmc_pp" 1e9 0 || exit 1 ;;
+    pool)
+      hipcc -O2 --offload-arch=gfx950 -o "$o/pool_repro" scripts/micro/pool_repro.hip || exit 1
+      for args in "5 6 pool kcopy nosync" "5 6 pool memcpy sync" "5 6 pool kcopy sync" "1 6 pool memcpy nosync" \
+                  "5 6 malloc memcpy nosync"; do
+        echo "== pool_repro $args"
+        # shellcheck disable=SC2086
+        timeout -k 10 180 "$o/pool_repro" $args; rc=$?
+        [ $rc -le 1 ] || { echo "pool_repro rc=$rc"; exit 1; }
+      done > "$o/pool_repro.txt" 2>&1
+      grep -E "^==|REPRODUCED|no mismatch" "$o/pool_repro.txt" ;;
     ab)
       IFS=',' read -r -a envs <<< "$arg"
       bash scripts/abn.sh "${envs[@]}" || exit 1 ;;

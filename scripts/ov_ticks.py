@@ -12,6 +12,10 @@ rows = db.execute("select name, start, end from kernels order by start").fetchal
 
 
 def fam(n):
+    if "k_ov_part" in n:
+        return "part1" if "false" in n.lower() or "Lb0" in n else "part2"
+    if "k_ov_fine" in n:
+        return "fine"
     if "k_process" in n:
         return "process"
     if "k_scatter" in n:

@@ -6,7 +6,7 @@ o=gpurun_out/${1:-pw}; mkdir -p $o
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof -o run -- python3 bench.py --steps 1 --warmup 1 --cpu-n 0 --no-roofline --no-extensions --no-c3 --no-c4 > $o/prof.log 2>&1 || { tail -20 $o/prof.log; exit 1; }
 f=$(find $o/prof -name '*.db' | head -1)
-python3 tools_profsummary.py "$f" 14 > $o/kernel_summary.txt && python3 scripts/perwindow.py "$f" 28 > $o/perwindow.txt
+python3 tools_profsummary.py "$f" 14 > $o/kernel_summary.txt && python3 scripts/perwindow.py "$f" 28 > $o/perwindow.txt && python3 scripts/ov_ticks.py "$f" > $o/ov_ticks.txt
 python3 - "$f" > $o/sequence.txt <<'PY'
 import re, sqlite3, sys
 rows = sqlite3.connect(sys.argv[1]).execute("select name, start, end from kernels order by start").fetchall()

@@ -222,6 +222,52 @@ def test_overlay_tick_blocks_match_oracle(gs, oracle, monkeypatch, block, dlow, 
         assert np.array_equal(masked(gdeg, gids), masked(deg, ids))
 
 
+@pytest.mark.parametrize("mode", ["partition", "sort", "fallback", "batched"])
+def test_overlay_destination_partition(gs, oracle, monkeypatch, mode):
+    """Verdict r04 item 6: dense overlay ticks are grouped by destination with
+    the hand-written partition (k_ov_part x2 + k_ov_fine) instead of the
+    radix sort.  partition: the default (dense ticks partitioned, sparse ticks
+    sorted); sort: GS_OV_SORT=1, every tick sorted; fallback: plans at half
+    the expected counts, so every dense tick's regions overflow and the tick
+    is sorted from its intact bucket; batched: 12 trials in one id space.
+    Every mode builds the oracle's overlay -- windows, final tick, rows."""
+    from dataclasses import replace
+    if mode == "batched" and gs.engine == "tick":
+        pytest.skip("batched trials run on the window engine")
+    monkeypatch.delenv("GS_OV_SORT", raising=False)
+    monkeypatch.delenv("GS_OV_PART_SCALE", raising=False)
+    if mode == "sort":
+        monkeypatch.setenv("GS_OV_SORT", "1")
+    if mode == "fallback":
+        monkeypatch.setenv("GS_OV_PART_SCALE", "0.5")
+    if mode == "batched":  # (batched builds sort unless asked: their plans overflow, see gs_overlay.hip)
+        monkeypatch.setenv("GS_OV_PART_BATCHED", "1")
+    kw = dict(n=150000 if mode != "batched" else 20000, fanout=5, fanin=6, delay_low=10, delay_high=20,
+              drop_rate=0.1, crash_rate=0.01, seed=5, trial=3)
+    trials = 12 if mode == "batched" else 1
+    with gs.Simulator(replace(cfg_from(gs, kw), trials=trials)) as sim:
+        gw, gf = sim.build_overlay()
+        tm = sim.timing()
+        gdeg, gids = sim.read_peers()
+        n = kw["n"]
+        res = [(gdeg[t * n:(t + 1) * n], gids[t * n:(t + 1) * n]) for t in range(trials)]
+    if mode == "partition":
+        assert tm["ov_part_ticks"] >= 10 and tm["ov_part_fallbacks"] == 0, tm
+    elif mode == "batched":  # partitioned or fallen back, every tick grouped right
+        assert tm["ov_part_ticks"] + tm["ov_part_fallbacks"] >= 10, tm
+    elif mode == "sort":
+        assert tm["ov_part_ticks"] == 0 and tm["ov_sort_ticks"] > 0, tm
+    else:
+        assert tm["ov_part_ticks"] == 0 and tm["ov_part_fallbacks"] >= 10, tm
+    for t, (gdeg, gids) in enumerate(res):
+        deg, ids, wins, final = oracle.overlay(oracle.make_params(**dict(kw, trial=kw["trial"] + t)))
+        if trials == 1:
+            assert gf == final
+            assert [tuple(w) for w in gw] == [tuple(w) for w in wins]
+        assert np.array_equal(gdeg, deg), f"trial {t}"
+        assert np.array_equal(masked(gdeg, gids)[:, :ids.shape[1]], masked(deg, ids)), f"trial {t}"
+
+
 def test_overlay_longest_ring_and_its_limit(gs, oracle):
     """the overlay's ring of blocks holds ceil(R / L) + 2 buckets,
     and its LDS histograms kMaxRing = 1026 of them.  delayhigh = 1024 (the
