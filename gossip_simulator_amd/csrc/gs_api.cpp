@@ -240,6 +240,10 @@ int alloc_window(gs_ctx* c) {
   w.seg_per = (uint32_t)c->seg_per;
   w.csub = kCoarseSub;
   w.noxcd = getenv("GS_PART2_NOXCD") ? 1u : 0u;  // A/B knob: k_part2 tiles in region order
+  {
+    const char* xp = getenv("GS_XPAIR");  // A/B knob: 0 = k_expand's packed rows fetched per lane
+    w.nopair = xp && atoi(xp) == 0 ? 1u : 0u;
+  }
   w.ccap_end = nullptr;
   w.csrc = nullptr;
   if (c->shard) {  // owner expand (k_expand's coarse_bin)

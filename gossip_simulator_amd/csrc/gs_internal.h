@@ -147,6 +147,7 @@ struct WinState {
   uint32_t* gmap;                // [ceil(fires/64)] unit of every 64th firing index
   const uint32_t* pk;            // rows <= 6 slots: the sealed rows packed 5 per 128-B line, or null
   uint32_t noxcd;                // 1: k_part2 tiles in region order (GS_PART2_NOXCD=1, A/B); else dealt by XCD
+  uint32_t nopair;               // 1: k_expand's packed rows fetched per lane (GS_XPAIR=0, A/B); else by lane pairs
   uint32_t* cmsg;                // coarse regions: u_in_coarse | k << 22
   uint32_t* fmsg;                // fine regions:   u_in_fine   | k << 14
   unsigned long long* chist;     // [kRegions] exact coarse region counts (fallback)

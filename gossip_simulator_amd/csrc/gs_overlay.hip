@@ -199,6 +199,49 @@ __device__ __forceinline__ uint32_t active_append(uint32_t* n) {
   return base + __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
 }
 
+// A friends row of 8 slots in registers: named members and selects only (an
+// indexed array was left in scratch by the compiler).
+struct Row8 {
+  uint32_t v0, v1, v2, v3, v4, v5, v6, v7;
+  // (the empty asm keeps the members in VGPRs: without it the select chains
+  // were folded back into an indexed array in scratch)
+  __device__ __forceinline__ void pin() {
+    asm volatile("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6), "+v"(v7));
+  }
+  __device__ __forceinline__ uint32_t get(uint32_t j) const {
+    const bool b0 = j & 1, b1 = j & 2, b2 = j & 4;
+    const uint32_t l0 = b0 ? v1 : v0, l1 = b0 ? v3 : v2, l2 = b0 ? v5 : v4, l3 = b0 ? v7 : v6;
+    const uint32_t m0 = b1 ? l1 : l0, m1 = b1 ? l3 : l2;
+    return b2 ? m1 : m0;
+  }
+  __device__ __forceinline__ void set(uint32_t j, uint32_t x) {
+    v0 = j == 0 ? x : v0; v1 = j == 1 ? x : v1; v2 = j == 2 ? x : v2; v3 = j == 3 ? x : v3;
+    v4 = j == 4 ? x : v4; v5 = j == 5 ? x : v5; v6 = j == 6 ? x : v6; v7 = j == 7 ? x : v7;
+    pin();
+  }
+  // the first slot < d holding x, or d
+  __device__ __forceinline__ uint32_t find(uint32_t x, uint32_t d) const {
+    uint32_t i = d;
+    i = (7 < d && v7 == x) ? 7 : i; i = (6 < d && v6 == x) ? 6 : i; i = (5 < d && v5 == x) ? 5 : i;
+    i = (4 < d && v4 == x) ? 4 : i; i = (3 < d && v3 == x) ? 3 : i; i = (2 < d && v2 == x) ? 2 : i;
+    i = (1 < d && v1 == x) ? 1 : i; i = (0 < d && v0 == x) ? 0 : i;
+    return i;
+  }
+  // slots idx .. d-2 take their successors (removeFriend's shift)
+  __device__ __forceinline__ void remove(uint32_t idx, uint32_t d) {
+    v0 = (0 >= idx && 1 < d) ? v1 : v0; v1 = (1 >= idx && 2 < d) ? v2 : v1;
+    v2 = (2 >= idx && 3 < d) ? v3 : v2; v3 = (3 >= idx && 4 < d) ? v4 : v3;
+    v4 = (4 >= idx && 5 < d) ? v5 : v4; v5 = (5 >= idx && 6 < d) ? v6 : v5;
+    v6 = (6 >= idx && 7 < d) ? v7 : v6;
+    pin();
+  }
+};
+
+// ROW8 (stride 8, the window engine's padded rows): the run's friends row is
+// read once into registers (two 16-B loads), replayed there with unrolled
+// selects, and written back once -- instead of a dependent global load per
+// slot of every linear search, shift and victim read.
+template <bool ROW8>
 __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64_t t0, uint64_t* keys, uint64_t m,
                                                         uint8_t* deg, uint32_t* ids, uint64_t* eout,
                                                         uint16_t* eslot, unsigned long long* ecount,
@@ -252,6 +295,15 @@ __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64
     uint32_t* row = ids + (size_t)u * p.stride;
     uint32_t d = deg[u];
     uint32_t ptag = ~0u, k = 0;
+    Row8 r8{};  // ROW8: the row in registers
+    bool dirty = false;
+    if (ROW8) {
+      const uint4 a = reinterpret_cast<const uint4*>(row)[0], b = reinterpret_cast<const uint4*>(row)[1];
+      r8 = Row8{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      r8.pin();
+    }
+#define RGET8(j) (r8.get(j))
+#define RSET8(j, x) (r8.set((j), (x)), dirty = true)
     for (uint64_t i = start; i < end; ++i) {
       const uint64_t key = keys[i];
       const uint32_t src = (uint32_t)((key >> 1) & smask);
@@ -264,20 +316,30 @@ __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64
       if ((key & 1) == 0) {                                   // makeUpCh (:66-75)
         ++mk;
         if (d < p.fanin) {
-          row[d++] = src;
+          if (ROW8) RSET8(d, src); else row[d] = src;
+          ++d;
         } else {
           const uint32_t pos = uniform(ov_draw(p, K_VICTIM, u, t, k), d);
-          emitted_dst = row[pos];                             // Breakup (:73)
+          emitted_dst = ROW8 ? RGET8(pos) : row[pos];          // Breakup (:73)
           emitted_kind = 1;
-          row[pos] = src;
+          if (ROW8) RSET8(pos, src); else row[pos] = src;
         }
       } else {                                                // breakUpCh (:76-94)
         ++bk;
         uint32_t idx = 0;
-        while (idx < d && row[idx] != src) ++idx;
+        if (ROW8) {
+          idx = r8.find(src, d);
+        } else {
+          while (idx < d && row[idx] != src) ++idx;
+        }
         if (idx < d) {
           if (d > p.fanout) {                                 // removeFriend (:83)
-            for (uint32_t q = idx; q + 1 < d; ++q) row[q] = row[q + 1];
+            if (ROW8) {
+              r8.remove(idx, d);
+              dirty = true;
+            } else {
+              for (uint32_t q = idx; q + 1 < d; ++q) row[q] = row[q + 1];
+            }
             --d;
           } else {                                            // replace (:86-91)
             uint32_t nf = 0, a = 0, kn, c3;
@@ -291,7 +353,7 @@ __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64
             if (a == 256) {
               err |= 1;
             } else {
-              row[idx] = nf;
+              if (ROW8) RSET8(idx, nf); else row[idx] = nf;
               emitted_dst = nf;                               // Makeup (:91)
               emitted_kind = 0;
             }
@@ -303,8 +365,14 @@ __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64
         emit(ev_key(p, emitted_dst, a, u, emitted_kind), ev_bucket(p, a));
       }
     }
+    if (ROW8 && dirty) {
+      reinterpret_cast<uint4*>(row)[0] = make_uint4(r8.v0, r8.v1, r8.v2, r8.v3);
+      reinterpret_cast<uint4*>(row)[1] = make_uint4(r8.v4, r8.v5, r8.v6, r8.v7);
+    }
     deg[u] = (uint8_t)d;
   }
+#undef RGET8
+#undef RSET8
   if (mk) atomicAdd(&s_mk, mk);
   if (bk) atomicAdd(&s_bk, bk);
   if (err) atomicOr(&s_err, err);
@@ -499,33 +567,59 @@ __global__ __launch_bounds__(kOvpBlock) void k_ov_part(const OvPart a) {
 // The fine regions' fills -> the exclusive prefix fbase[0..nfb] (one
 // workgroup): P3 writes fine region f's keys at fbase[f], so k_process gets
 // the tick's keys back to back, without the regions' unused tails.
-constexpr uint32_t kOvScanBlock = 1024;
+constexpr uint32_t kOvScanBlock = 1024, kOvScanIPT = 8, kOvScanChunk = kOvScanBlock * kOvScanIPT;
 __global__ __launch_bounds__(kOvScanBlock) void k_ov_scan(const unsigned long long* ffill, uint32_t nfb,
                                                           const unsigned long long* fstart,
                                                           unsigned long long* fbase) {
+  // chunks of 8192 fills: coalesced loads into LDS, 8 consecutive per thread
+  // scanned in registers, a block scan of the thread sums, coalesced stores;
+  // the chunk total carries into the next chunk
+  __shared__ unsigned long long s_v[kOvScanChunk];
   __shared__ unsigned long long s_ws[kOvScanBlock / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const uint32_t per = (nfb + kOvScanBlock - 1) / kOvScanBlock, f0 = min(tid * per, nfb), f1 = min(f0 + per, nfb);
-  auto fill = [&](uint32_t f) {  // (an overflowed region is discarded with the tick)
-    return min(ffill[f], fstart[f + 1] - fstart[f]);
-  };
-  unsigned long long sum = 0;
-  for (uint32_t f = f0; f < f1; ++f) sum += fill(f);
-  unsigned long long x = sum;
+  unsigned long long carry = 0;
+  for (uint32_t c0 = 0; c0 < nfb; c0 += kOvScanChunk) {
 #pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const unsigned long long y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
+    for (uint32_t j = 0; j < kOvScanIPT; ++j) {
+      const uint32_t f = c0 + j * kOvScanBlock + tid;
+      // (an overflowed region is discarded with the tick)
+      s_v[j * kOvScanBlock + tid] = f < nfb ? min(ffill[f], fstart[f + 1] - fstart[f]) : 0ull;
+    }
+    __syncthreads();
+    unsigned long long v[kOvScanIPT], sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kOvScanIPT; ++j) {
+      v[j] = s_v[tid * kOvScanIPT + j];
+      sum += v[j];
+    }
+    unsigned long long x = sum;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const unsigned long long y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) s_ws[wv] = x;
+    __syncthreads();
+    unsigned long long run = carry + x - sum, total = 0;
+    for (uint32_t q = 0; q < kOvScanBlock / 64; ++q) {
+      if (q < wv) run += s_ws[q];
+      total += s_ws[q];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kOvScanIPT; ++j) {
+      s_v[tid * kOvScanIPT + j] = run;
+      run += v[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kOvScanIPT; ++j) {
+      const uint32_t f = c0 + j * kOvScanBlock + tid;
+      if (f < nfb) fbase[f] = s_v[j * kOvScanBlock + tid];
+    }
+    carry += total;
+    __syncthreads();
   }
-  if (lane == 63) s_ws[wv] = x;
-  __syncthreads();
-  unsigned long long run = x - sum;
-  for (uint32_t q = 0; q < wv; ++q) run += s_ws[q];
-  for (uint32_t f = f0; f < f1; ++f) {
-    fbase[f] = run;
-    run += fill(f);
-  }
-  if (tid == kOvScanBlock - 1) fbase[nfb] = run;
+  if (tid == 0) fbase[nfb] = carry;
 }
 
 // P3: fine region f (in: P2's output) counting-sorted by local destination
@@ -774,6 +868,8 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
   // C3 (up to 16x a fine region's share); they keep the sort.
   const bool part_ok = !getenv("GS_OV_SORT") && (trials <= 1 || getenv("GS_OV_PART_BATCHED"));
   const double part_scale = getenv("GS_OV_PART_SCALE") ? atof(getenv("GS_OV_PART_SCALE")) : 1.04;
+  // rows of 8 slots replayed in registers (GS_OV_ROW8=0: slot by slot in memory, A/B)
+  const bool row8 = stride == 8 && p.fanin <= 8 && !(getenv("GS_OV_ROW8") && atoi(getenv("GS_OV_ROW8")) == 0);
   OvPlan plan;
   uint32_t h_flag = 0;
   ws->part_ticks = ws->sort_ticks = ws->part_fallbacks = 0;
@@ -937,9 +1033,14 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
           ++ws->sort_ticks;
         }
         const uint64_t per = (uint64_t)kProcBlock * kProcIPT;
-        hipLaunchKernelGGL(k_process, dim3((uint32_t)((mproc + per - 1) / per)), dim3(kProcBlock), 0, stream, p,
-                           t0, keys, mproc, d_deg, d_ids, (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_nemit, d_counts,
-                           d_tc);
+        if (row8)
+          hipLaunchKernelGGL(k_process<true>, dim3((uint32_t)((mproc + per - 1) / per)), dim3(kProcBlock), 0, stream,
+                             p, t0, keys, mproc, d_deg, d_ids, (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_nemit,
+                             d_counts, d_tc);
+        else
+          hipLaunchKernelGGL(k_process<false>, dim3((uint32_t)((mproc + per - 1) / per)), dim3(kProcBlock), 0, stream,
+                             p, t0, keys, mproc, d_deg, d_ids, (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_nemit,
+                             d_counts, d_tc);
         OVCHK(hipGetLastError());
       }
       OVCHK(hipMemcpyAsync(&h_ne, d_nemit, 8, hipMemcpyDeviceToHost, stream));
