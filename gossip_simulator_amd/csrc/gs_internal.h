@@ -478,6 +478,7 @@ struct OverlayWork {
   Buf scratch, outb, oslotb, cub_tmp, meta;
   Buf fine, ovp;            // destination partition of the dense ticks: regions, plan + fills
   uint64_t part_ticks = 0, sort_ticks = 0, part_fallbacks = 0;  // of the last build
+  uint64_t pick_fallbacks = 0;  // the last build's tick-0 plan overflowed (then counted)
 };
 void overlay_free(OverlayWork* ws, hipStream_t st);
 // n = nodes per trial; trials > 1 builds every trial's overlay at once in the

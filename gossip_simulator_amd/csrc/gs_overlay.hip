@@ -131,11 +131,16 @@ struct OutSource {  // events emitted by a processing block (a compact list)
 };
 
 // COUNT: counts[s] += items bound for bucket s.  WRITE: append them to bucket s.
+// caps (WRITE, optional): bucket capacities; a workgroup whose reservation
+// would pass one sets *ovf and writes none of that bucket's items (tick 0's
+// planned buckets: the host then counts and writes again).
 template <bool WRITE, class Src>
 __global__ __launch_bounds__(kScatterBlock) void k_scatter(Src src, uint64_t nitems, uint32_t R,
                                                            unsigned long long* counts,
                                                            unsigned long long* fill,
-                                                           uint64_t* const* buckets) {
+                                                           uint64_t* const* buckets,
+                                                           const unsigned long long* caps = nullptr,
+                                                           uint32_t* ovf = nullptr) {
   __shared__ uint32_t s_hist[kMaxRing];
   __shared__ unsigned long long s_base[kMaxRing];
   for (uint32_t s = threadIdx.x; s < R; s += blockDim.x) s_hist[s] = 0;
@@ -160,11 +165,16 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(Src src, uint64_t nit
     return;
   }
   for (uint32_t s = threadIdx.x; s < R; s += blockDim.x)
-    if (s_hist[s]) s_base[s] = atomicAdd(&fill[s], (unsigned long long)s_hist[s]);
+    if (s_hist[s]) {
+      const unsigned long long b = atomicAdd(&fill[s], (unsigned long long)s_hist[s]);
+      const bool over = caps && b + s_hist[s] > caps[s];
+      if (over) atomicOr(ovf, 1u);
+      s_base[s] = over ? ~0ull : b;
+    }
   __syncthreads();
 #pragma unroll
   for (uint32_t k = 0; k < kScatterIPT; ++k)
-    if (slot[k] != 0xFFFFu) buckets[slot[k]][s_base[slot[k]] + rank[k]] = key[k];
+    if (slot[k] != 0xFFFFu && s_base[slot[k]] != ~0ull) buckets[slot[k]][s_base[slot[k]] + rank[k]] = key[k];
 }
 
 struct TickCounters {
@@ -872,7 +882,8 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
   const bool row8 = stride == 8 && p.fanin <= 8 && !(getenv("GS_OV_ROW8") && atoi(getenv("GS_OV_ROW8")) == 0);
   OvPlan plan;
   uint32_t h_flag = 0;
-  ws->part_ticks = ws->sort_ticks = ws->part_fallbacks = 0;
+  const int ov_debug = getenv("GS_OV_DEBUG") ? atoi(getenv("GS_OV_DEBUG")) : 0;
+  ws->part_ticks = ws->sort_ticks = ws->part_fallbacks = ws->pick_fallbacks = 0;
   // meta layout: counts[NB] | fill[NB] | ptrs[NB] | nemit (64 B) | TickCounters
   uint64_t pending = 0, wm = 0, wb = 0;
   std::vector<unsigned long long> h_counts(NB), hfill(NB);
@@ -881,8 +892,11 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
   unsigned long long h_ne = 0;
   uint64_t** d_ptrs = nullptr;
   TickCounters* d_tc = nullptr;
+  unsigned long long* d_caps = nullptr;  // tick 0's planned bucket capacities
+  uint32_t* d_ovf = nullptr, h_ovf = 0;
+  std::vector<unsigned long long> h_caps(NB, 0);
   TickCounters h_tc;
-  const size_t meta_bytes = NB * 8 * 3 + 64 + sizeof(TickCounters);
+  const size_t meta_bytes = NB * 8 * 3 + 64 + sizeof(TickCounters) + NB * 8 + 64;
 
   OVCHK(grow(meta, meta_bytes, stream));
   d_counts = (unsigned long long*)meta.p;
@@ -890,6 +904,8 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
   d_ptrs = (uint64_t**)(d_fill + NB);
   d_nemit = (unsigned long long*)(d_ptrs + NB);
   d_tc = (TickCounters*)((char*)d_nemit + 64);
+  d_caps = (unsigned long long*)(d_tc + 1);
+  d_ovf = (uint32_t*)(d_caps + NB);
   OVCHK(hipMemsetAsync(meta.p, 0, meta_bytes, stream));
 
   {
@@ -899,20 +915,68 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
       PickSource src{p, d_deg, d_ids, false};
       const uint64_t per = (uint64_t)kScatterBlock * kScatterIPT;
       const uint64_t blocks = (items + per - 1) / per;
-      hipLaunchKernelGGL((k_scatter<false, PickSource>), dim3((uint32_t)blocks), dim3(kScatterBlock),
-                         0, stream, src, items, NB, d_counts, d_fill, (uint64_t* const*)d_ptrs);
-      OVCHK(hipGetLastError());
-      OVCHK(hipMemcpyAsync(h_counts.data(), d_counts, NB * 8, hipMemcpyDeviceToHost, stream));
-      OVCHK(hipStreamSynchronize(stream));
-      for (uint32_t s = 0; s < NB; ++s) {
-        OVCHK(grow(bucket[s], (fill[s] + h_counts[s]) * 8, stream));
-        h_ptrs[s] = (uint64_t*)bucket[s].p;
+      // The picks' arrival buckets follow the delay draw alone: offset
+      // low + o, o uniform over the span (fire_offset), so bucket b expects
+      // items x P(b).  Buckets sized to that + 6 sigma + 1024 are written in
+      // ONE pass; a bucket past its plan (or GS_OV_PICK_COUNT=1) falls back to
+      // the exact count pass and the write again (the rows it writes are the
+      // same both times).  The count pass was 38 ms of the N = 1e9 build.
+      bool planned = !getenv("GS_OV_PICK_COUNT");
+      if (planned) {
+        std::vector<double> expct(NB, 0.0);
+        const uint32_t span = std::max<uint32_t>(p.delay_span, 1u);
+        for (uint32_t o = 0; o < span; ++o) {
+          // words r with floor(r * span / 2^32) == o
+          const double lo = std::ceil((double)o * 4294967296.0 / span), hi = std::ceil((double)(o + 1) * 4294967296.0 / span);
+          const uint32_t a = fire_offset(p.delay_low, span, (uint32_t)std::min(lo, 4294967295.0));
+          expct[((a - 1) / p.L) % NB] += (double)items * (hi - lo) / 4294967296.0;
+        }
+        // (GS_OV_PICK_SCALE < 1 shrinks the plan: the tests force the fallback with it)
+        const double psc = getenv("GS_OV_PICK_SCALE") ? atof(getenv("GS_OV_PICK_SCALE")) : 1.0;
+        for (uint32_t s = 0; s < NB; ++s) {
+          h_caps[s] = expct[s] <= 0 ? 0ull
+                      : psc < 1.0 ? (unsigned long long)(expct[s] * psc)
+                                  : (unsigned long long)std::ceil(expct[s] + 6.0 * std::sqrt(expct[s]) + 1024.0);
+        }
+        for (uint32_t s = 0; s < NB; ++s) {
+          OVCHK(grow(bucket[s], std::max<unsigned long long>(h_caps[s], 1) * 8, stream));
+          h_ptrs[s] = (uint64_t*)bucket[s].p;
+        }
+        OVCHK(hipMemcpyAsync(d_ptrs, h_ptrs.data(), NB * 8, hipMemcpyHostToDevice, stream));
+        OVCHK(hipMemcpyAsync(d_caps, h_caps.data(), NB * 8, hipMemcpyHostToDevice, stream));
+        OVCHK(hipMemsetAsync(d_ovf, 0, 4, stream));
+        src.write_rows = true;
+        hipLaunchKernelGGL((k_scatter<true, PickSource>), dim3((uint32_t)blocks), dim3(kScatterBlock), 0, stream,
+                           src, items, NB, d_counts, d_fill, (uint64_t* const*)d_ptrs,
+                           (const unsigned long long*)d_caps, d_ovf);
+        OVCHK(hipGetLastError());
+        OVCHK(hipMemcpyAsync(h_counts.data(), d_fill, NB * 8, hipMemcpyDeviceToHost, stream));
+        OVCHK(hipMemcpyAsync(&h_ovf, d_ovf, 4, hipMemcpyDeviceToHost, stream));
+        OVCHK(hipStreamSynchronize(stream));
+        if (h_ovf) {  // the exact path below, from empty buckets
+          planned = false;
+          ++ws->pick_fallbacks;
+          if (ov_debug) fprintf(stderr, "[overlay] tick 0: a planned pick bucket overflowed; counting\n");
+          OVCHK(hipMemsetAsync(d_fill, 0, NB * 8, stream));
+        }
       }
-      OVCHK(hipMemcpyAsync(d_ptrs, h_ptrs.data(), NB * 8, hipMemcpyHostToDevice, stream));
-      src.write_rows = true;
-      hipLaunchKernelGGL((k_scatter<true, PickSource>), dim3((uint32_t)blocks), dim3(kScatterBlock),
-                         0, stream, src, items, NB, d_counts, d_fill, (uint64_t* const*)d_ptrs);
-      OVCHK(hipGetLastError());
+      if (!planned) {
+        src.write_rows = false;
+        hipLaunchKernelGGL((k_scatter<false, PickSource>), dim3((uint32_t)blocks), dim3(kScatterBlock),
+                           0, stream, src, items, NB, d_counts, d_fill, (uint64_t* const*)d_ptrs);
+        OVCHK(hipGetLastError());
+        OVCHK(hipMemcpyAsync(h_counts.data(), d_counts, NB * 8, hipMemcpyDeviceToHost, stream));
+        OVCHK(hipStreamSynchronize(stream));
+        for (uint32_t s = 0; s < NB; ++s) {
+          OVCHK(grow(bucket[s], (fill[s] + h_counts[s]) * 8, stream));
+          h_ptrs[s] = (uint64_t*)bucket[s].p;
+        }
+        OVCHK(hipMemcpyAsync(d_ptrs, h_ptrs.data(), NB * 8, hipMemcpyHostToDevice, stream));
+        src.write_rows = true;
+        hipLaunchKernelGGL((k_scatter<true, PickSource>), dim3((uint32_t)blocks), dim3(kScatterBlock),
+                           0, stream, src, items, NB, d_counts, d_fill, (uint64_t* const*)d_ptrs);
+        OVCHK(hipGetLastError());
+      }
       for (uint32_t s = 0; s < NB; ++s) { fill[s] += h_counts[s]; pending += h_counts[s]; }
       OVCHK(hipMemsetAsync(d_counts, 0, NB * 8, stream));
     } else if (ntot) {
@@ -988,7 +1052,7 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
             ++ws->part_ticks;
           } else {
             ++ws->part_fallbacks;  // a region overflowed its plan: sort this tick
-            if (getenv("GS_OV_DEBUG")) {  // which level overflowed, by how much
+            if (ov_debug) {  // which level overflowed, by how much
               std::vector<unsigned long long> cf(ncb * kOvSub), ff(nfb);
               OVCHK(hipMemcpy(cf.data(), d_cfill, cf.size() * 8, hipMemcpyDeviceToHost));
               OVCHK(hipMemcpy(ff.data(), d_cfill + ncb * kOvSub, ff.size() * 8, hipMemcpyDeviceToHost));
@@ -1051,6 +1115,10 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
       {
         // the emitted events (k_process counted them per bucket): grow, write
         const uint64_t nitems = h_ne;
+        if (ov_debug > 1)
+          fprintf(stderr, "[overlay] tick %llu: %llu events, %llu emitted, %llu makeups %llu breakups\n",
+                  (unsigned long long)t0, (unsigned long long)m, (unsigned long long)nitems,
+                  (unsigned long long)h_tc.makeups, (unsigned long long)h_tc.breakups);
         OutSource osrc{(const uint64_t*)outb.p, (const uint16_t*)oslotb.p};
         const uint64_t per = (uint64_t)kScatterBlock * kScatterIPT;
         const uint32_t blocks = (uint32_t)((nitems + per - 1) / per);

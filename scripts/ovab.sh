@@ -1,0 +1,14 @@
+#!/bin/bash
+# overlay build A/B: kernel sums of one N=1e9 build per variant, interleaved
+set -o pipefail
+o=gpurun_out/$1; shift; mkdir -p $o
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+for rep in 1 2; do
+  for v in "$@"; do
+    tag=$(echo "$v" | tr '=, ' '___')
+    timeout -k 10 240 env $v rocprofv3 --kernel-trace -d $o/p_$tag -o run -- python3 scripts/ov_once.py > $o/l_$tag.log 2>&1 || { tail -5 $o/l_$tag.log; exit 1; }
+    f=$(find $o/p_$tag -name '*.db' | head -1)
+    echo "$rep [$v] $(python3 scripts/ov_ticks.py $f | tail -1)"
+    rm -rf $o/p_$tag
+  done
+done

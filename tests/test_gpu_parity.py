@@ -222,20 +222,27 @@ def test_overlay_tick_blocks_match_oracle(gs, oracle, monkeypatch, block, dlow, 
         assert np.array_equal(masked(gdeg, gids), masked(deg, ids))
 
 
-@pytest.mark.parametrize("mode", ["partition", "sort", "fallback", "batched"])
+@pytest.mark.parametrize("mode", ["partition", "sort", "fallback", "batched", "pick-count", "pick-overflow"])
 def test_overlay_destination_partition(gs, oracle, monkeypatch, mode):
     """Verdict r04 item 6: dense overlay ticks are grouped by destination with
     the hand-written partition (k_ov_part x2 + k_ov_fine) instead of the
     radix sort.  partition: the default (dense ticks partitioned, sparse ticks
     sorted); sort: GS_OV_SORT=1, every tick sorted; fallback: plans at half
     the expected counts, so every dense tick's regions overflow and the tick
-    is sorted from its intact bucket; batched: 12 trials in one id space.
+    is sorted from its intact bucket; batched: 12 trials in one id space;
+    pick-count / pick-overflow: tick 0's picks counted before they are written
+    (instead of one pass into planned buckets), or the plan too small so the
+    planned pass overflows and falls back to that.
     Every mode builds the oracle's overlay -- windows, final tick, rows."""
     from dataclasses import replace
     if mode == "batched" and gs.engine == "tick":
         pytest.skip("batched trials run on the window engine")
-    monkeypatch.delenv("GS_OV_SORT", raising=False)
-    monkeypatch.delenv("GS_OV_PART_SCALE", raising=False)
+    for var in ("GS_OV_SORT", "GS_OV_PART_SCALE", "GS_OV_PICK_COUNT", "GS_OV_PICK_SCALE"):
+        monkeypatch.delenv(var, raising=False)
+    if mode == "pick-count":  # tick 0 counted, then written (the planned single pass off)
+        monkeypatch.setenv("GS_OV_PICK_COUNT", "1")
+    if mode == "pick-overflow":  # tick 0's planned buckets too small: the count-and-write fallback
+        monkeypatch.setenv("GS_OV_PICK_SCALE", "0.5")
     if mode == "sort":
         monkeypatch.setenv("GS_OV_SORT", "1")
     if mode == "fallback":
@@ -251,7 +258,7 @@ def test_overlay_destination_partition(gs, oracle, monkeypatch, mode):
         gdeg, gids = sim.read_peers()
         n = kw["n"]
         res = [(gdeg[t * n:(t + 1) * n], gids[t * n:(t + 1) * n]) for t in range(trials)]
-    if mode == "partition":
+    if mode in ("partition", "pick-count", "pick-overflow"):
         assert tm["ov_part_ticks"] >= 10 and tm["ov_part_fallbacks"] == 0, tm
     elif mode == "batched":  # partitioned or fallen back, every tick grouped right
         assert tm["ov_part_ticks"] + tm["ov_part_fallbacks"] >= 10, tm
