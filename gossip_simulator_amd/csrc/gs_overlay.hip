@@ -447,21 +447,16 @@ struct OvPart {
   const uint32_t* tprefix;             // [ncb * kOvSub + 1] P2 tiles per coarse sub-region (prefix)
   uint32_t* flag;                      // 1: a region overflowed
   uint32_t ncb, nfb, sh;               // coarse / fine regions, the key's destination shift
-  uint32_t sfrac[kOvSub + 1];          // sub-region x of a coarse region: [sfrac[x], sfrac[x+1]) / 2^20 of it
+  const unsigned long long* cstart;    // [ncb * kOvSub + 1] coarse sub-region (c, x) starts in P1's output
 };
 
-// The split of a coarse region over its kOvSub sub-regions: P1's tile t
-// writes sub-region t % kOvSub, so sub-region x gets the share of the bucket
-// its tiles hold, in 2^-20 units (host and device split alike).
-constexpr uint32_t kOvFracBits = 20;
-__host__ __device__ inline uint64_t ov_sub_at(uint64_t cs, uint64_t ce, uint32_t frac) {
-  return cs + (((ce - cs) * frac) >> kOvFracBits);
-}
+// P1's tile t writes sub-region t % kOvSub of each coarse region: (c, x) is
+// [cstart[c * kOvSub + x], cstart[c * kOvSub + x + 1]).
 __device__ __forceinline__ void ov_sub(const OvPart& a, uint32_t c, uint32_t x, unsigned long long& start,
                                        unsigned long long& cap) {
-  const unsigned long long cs = a.fstart[(uint64_t)c << 8], ce = a.fstart[min((c + 1) << 8, a.nfb)];
-  start = ov_sub_at(cs, ce, a.sfrac[x]);
-  cap = ov_sub_at(cs, ce, a.sfrac[x + 1]) - start;
+  const uint32_t r = c * kOvSub + x;
+  start = a.cstart[r];
+  cap = a.cstart[r + 1] - start;
 }
 
 __device__ __forceinline__ uint32_t block_exscan256(uint32_t v, uint32_t* s_ws) {
@@ -572,6 +567,37 @@ __global__ __launch_bounds__(kOvpBlock) void k_ov_part(const OvPart a) {
     const uint32_t d = ((uint32_t)(k >> (a.sh + dshift)) - dbase) & 255;
     a.out[s_gb[d] + (i - s_off[d])] = k;
   }
+}
+
+// Batched trials: the tick's events per trial (trial = destination >> tlog),
+// so the partition plan can follow each trial's own count -- trials drift
+// apart after the burst, and a plan by node share alone overflowed on every
+// dense C3 tick.  LDS histogram per workgroup (<= kOvMaxTrials), one global
+// add per non-empty trial.
+// It also counts the keys of every coarse sub-region (c = dst >> 22, x = the
+// key's P1 tile % kOvSub) exactly: a batched bucket lies in trial order (tick
+// 0's picks are written trial by trial), so a tile's keys go to one or two
+// coarse regions and the tiles' shares of a region are far from even.
+constexpr uint32_t kOvMaxTrials = 8192, kOvTrialBlock = 1024, kOvTrialGrid = 512;
+__global__ __launch_bounds__(kOvTrialBlock) void k_ov_count(const uint64_t* keys, uint64_t m, uint32_t sh,
+                                                            uint32_t tlog, uint32_t ntr, uint32_t ncb,
+                                                            unsigned long long* tcnt, unsigned long long* cxcnt) {
+  __shared__ uint32_t h[kOvMaxTrials];
+  __shared__ uint32_t hc[256 * kOvSub];
+  for (uint32_t i = threadIdx.x; i < ntr; i += kOvTrialBlock) h[i] = 0;
+  for (uint32_t i = threadIdx.x; i < ncb * kOvSub; i += kOvTrialBlock) hc[i] = 0;
+  __syncthreads();
+  for (uint64_t i = (uint64_t)blockIdx.x * kOvTrialBlock + threadIdx.x; i < m; i += (uint64_t)gridDim.x * kOvTrialBlock) {
+    const uint64_t dst = keys[i] >> sh;
+    atomicAdd(&h[min((uint32_t)(dst >> tlog), ntr - 1)], 1u);
+    const uint32_t c = min((uint32_t)(dst >> (kOvFineLog + 8)), ncb - 1), x = (uint32_t)(i / kOvpTile) % kOvSub;
+    atomicAdd(&hc[c * kOvSub + x], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < ntr; i += kOvTrialBlock)
+    if (h[i]) atomicAdd(&tcnt[i], (unsigned long long)h[i]);
+  for (uint32_t i = threadIdx.x; i < ncb * kOvSub; i += kOvTrialBlock)
+    if (hc[i]) atomicAdd(&cxcnt[i], (unsigned long long)hc[i]);
 }
 
 // The fine regions' fills -> the exclusive prefix fbase[0..nfb] (one
@@ -735,18 +761,22 @@ static hipError_t grow(DevBuf& b, size_t bytes, hipStream_t st) {
 // where the partition does not apply (a sparse tick: the radix sort's fixed
 // cost is lower; a fine region beyond LDS; more than 256 coarse regions).
 struct OvPlan {
-  uint64_t nfb = 0, ncb = 0, total = 0, m = 0;
+  uint64_t nfb = 0, ncb = 0, total = 0, ctotal = 0, m = 0;
   double scale = 0;
   std::vector<unsigned long long> fstart;  // [nfb + 1]
   std::vector<uint32_t> tprefix;           // [ncb * kOvSub + 1]
-  uint32_t sfrac[kOvSub + 1];              // OvPart::sfrac
+  std::vector<unsigned long long> cstart;  // [ncb * kOvSub + 1] OvPart::cstart
 };
 
+// tcnt / cxcnt (batched trials, k_ov_count): the tick's events per trial and
+// per coarse sub-region -- fine regions then follow their trial's count and
+// the coarse sub-regions are exact.
 static bool ov_plan(OvPlan& pl, uint64_t m, uint64_t n, uint32_t trials, uint32_t tlog, uint64_t ntot,
-                    double scale) {
+                    double scale, const unsigned long long* tcnt = nullptr,
+                    const unsigned long long* cxcnt = nullptr) {
   const uint64_t nfb = (ntot + kOvFineMax - 1) >> kOvFineLog, ncb = (nfb + 255) / 256;
   if (nfb == 0 || ncb > 256 || m < 32 * nfb) return false;
-  if (pl.m == m && pl.nfb == nfb && pl.scale == scale) return true;
+  if (!tcnt && pl.m == m && pl.nfb == nfb && pl.scale == scale) return true;
   const uint64_t tmask = tlog >= 32 ? ~0ull : (1ull << tlog) - 1;
   const double live = (double)n * (trials > 1 ? trials : 1);
   pl.m = 0;
@@ -754,39 +784,47 @@ static bool ov_plan(OvPlan& pl, uint64_t m, uint64_t n, uint32_t trials, uint32_
   pl.ncb = ncb;
   pl.fstart.resize(nfb + 1);
   pl.tprefix.resize(ncb * kOvSub + 1);
+  pl.cstart.resize(ncb * kOvSub + 1);
   uint64_t at = 0;
   for (uint64_t f = 0; f < nfb; ++f) {
     pl.fstart[f] = at;
     const uint64_t local = (f << kOvFineLog) & tmask;  // (tlog >= kOvFineLog: a fine bucket is in one trial)
     const uint64_t valid = local < n ? std::min<uint64_t>(kOvFineMax, n - local) : 0;
     if (!valid) continue;
-    const double e = (double)m * (double)valid / live;
+    // batched: the fine bucket's trial's own count (tlog >= kOvFineLog)
+    const double e = tcnt ? (double)tcnt[(f << kOvFineLog) >> tlog] * (double)valid / (double)n
+                          : (double)m * (double)valid / live;
     const uint64_t cap = (uint64_t)std::ceil(scale >= 1.0 ? e * scale + 6.0 * std::sqrt(e) + 32.0 : e * scale);
     if (cap > kOvFineMax) return false;
     at += cap;
   }
   pl.fstart[nfb] = at;
   pl.total = at;
-  // P1 tile t (kOvpTile keys, the last one short) writes sub-region t % kOvSub
+  // coarse sub-regions (c, x): P1's tile t (kOvpTile keys, the last one
+  // short) writes sub-region t % kOvSub.  Exact counts when given; else the
+  // coarse region's fine capacity split by the share of the bucket the tiles
+  // of x hold (a single trial's bucket is well mixed)
+  uint64_t share[kOvSub] = {};
   const uint64_t ntile = (m + kOvpTile - 1) / kOvpTile;
-  uint64_t kx = 0;
-  pl.sfrac[0] = 0;
-  for (uint32_t x = 0; x < kOvSub; ++x) {
-    for (uint64_t t = x; t < ntile; t += kOvSub) kx += std::min<uint64_t>(kOvpTile, m - t * kOvpTile);
-    pl.sfrac[x + 1] = (uint32_t)((kx << kOvFracBits) / m);
-  }
-  pl.sfrac[kOvSub] = 1u << kOvFracBits;
-  uint32_t tiles = 0;  // P2's tiles per coarse sub-region, as ov_sub splits them
+  for (uint32_t x = 0; x < kOvSub; ++x)
+    for (uint64_t t = x; t < ntile; t += kOvSub) share[x] += std::min<uint64_t>(kOvpTile, m - t * kOvpTile);
+  uint64_t cat = 0;
+  uint32_t tiles = 0;  // P2's tiles per coarse sub-region
   for (uint64_t c = 0; c < ncb; ++c) {
-    const uint64_t cs = pl.fstart[c * 256], ce = pl.fstart[std::min<uint64_t>((c + 1) * 256, nfb)];
+    const uint64_t ccap = pl.fstart[std::min<uint64_t>((c + 1) * 256, nfb)] - pl.fstart[c * 256];
     for (uint32_t x = 0; x < kOvSub; ++x) {
-      pl.tprefix[c * kOvSub + x] = tiles;
-      const uint64_t cx = ov_sub_at(cs, ce, pl.sfrac[x + 1]) - ov_sub_at(cs, ce, pl.sfrac[x]);
+      const uint64_t r = c * kOvSub + x;
+      pl.cstart[r] = cat;
+      pl.tprefix[r] = tiles;
+      const uint64_t cx = cxcnt ? cxcnt[r] : (uint64_t)std::ceil((double)ccap * (double)share[x] / (double)m);
+      cat += cx;
       tiles += (uint32_t)((cx + kOvpTile - 1) / kOvpTile);
     }
   }
+  pl.cstart[ncb * kOvSub] = cat;
   pl.tprefix[ncb * kOvSub] = tiles;
-  pl.m = m;
+  pl.ctotal = cat;
+  pl.m = tcnt || cxcnt ? 0 : m;  // (a counted plan is not reused)
   pl.scale = scale;
   return true;
 }
@@ -873,10 +911,16 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
   // the destination partition of dense ticks (GS_OV_SORT=1: the radix sort
   // for every tick, A/B)
   // Batched trials drift apart after the burst (one trial's wave of
-  // breakups is another's lull), so a tick's events are not spread over the
-  // id space by node share and the plans overflowed on every dense tick of
-  // C3 (up to 16x a fine region's share); they keep the sort.
-  const bool part_ok = !getenv("GS_OV_SORT") && (trials <= 1 || getenv("GS_OV_PART_BATCHED"));
+  // breakups is another's lull), so a plan by node share overflowed on every
+  // dense C3 tick (up to 16x a fine region's share): batched plans follow
+  // each trial's own count of the tick's events and exact coarse sub-region
+  // counts (k_ov_count).  That is exact but not faster for C3's batches
+  // (overlay 559-566 vs 548-551 ms per 5,000-trial batch: the count pass, two
+  // syncs and a 40,000-region plan per tick cost what the sort saves), so
+  // batched builds sort unless GS_OV_PART_BATCHED=1 (the tests).
+  const bool part_ok = !getenv("GS_OV_SORT") && (trials <= 1 || (getenv("GS_OV_PART_BATCHED") &&
+                                                                  trials <= kOvMaxTrials));
+  std::vector<unsigned long long> h_tcnt(trials > 1 ? trials : 0), h_cxcnt;
   const double part_scale = getenv("GS_OV_PART_SCALE") ? atof(getenv("GS_OV_PART_SCALE")) : 1.04;
   // rows of 8 slots replayed in registers (GS_OV_ROW8=0: slot by slot in memory, A/B)
   const bool row8 = stride == 8 && p.fanin <= 8 && !(getenv("GS_OV_ROW8") && atoi(getenv("GS_OV_ROW8")) == 0);
@@ -1007,26 +1051,46 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
       {
         uint64_t* keys = nullptr;
         uint64_t mproc = m;
-        if (part_ok && ov_plan(plan, m, n, trials, tlog, ntot, part_scale)) {
+        bool plan_ok = part_ok && m >= 32 * ((ntot + kOvFineMax - 1) >> kOvFineLog);
+        const uint64_t ncb0 = (((ntot + kOvFineMax - 1) >> kOvFineLog) + 255) / 256;
+        plan_ok = plan_ok && ncb0 <= 256;
+        if (plan_ok && trials > 1) {  // the tick's events per trial and per coarse sub-region, for the plan
+          const size_t nc = ncb0 * kOvSub;
+          OVCHK(grow(ovp, (trials + nc) * 8 + 64, stream));
+          unsigned long long* d_tcnt = (unsigned long long*)ovp.p;
+          OVCHK(hipMemsetAsync(d_tcnt, 0, (trials + nc) * 8, stream));
+          hipLaunchKernelGGL(k_ov_count, dim3(kOvTrialGrid), dim3(kOvTrialBlock), 0, stream,
+                             (const uint64_t*)bucket[s].p, m, p.B + 1 + p.TB, tlog, trials, (uint32_t)ncb0, d_tcnt,
+                             d_tcnt + trials);
+          OVCHK(hipGetLastError());
+          h_cxcnt.resize(nc);
+          OVCHK(hipMemcpyAsync(h_tcnt.data(), d_tcnt, trials * 8, hipMemcpyDeviceToHost, stream));
+          OVCHK(hipMemcpyAsync(h_cxcnt.data(), d_tcnt + trials, nc * 8, hipMemcpyDeviceToHost, stream));
+          OVCHK(hipStreamSynchronize(stream));
+        }
+        if (plan_ok && ov_plan(plan, m, n, trials, tlog, ntot, part_scale, trials > 1 ? h_tcnt.data() : nullptr,
+                               trials > 1 ? h_cxcnt.data() : nullptr)) {
           // P1 bucket -> fine.p (coarse regions), P2 -> scratch (fine
           // regions), P3 -> fine.p (sorted, padded); the bucket stays intact
           const uint64_t nfb = plan.nfb, ncb = plan.ncb;
-          const size_t b_fs = (nfb + 1) * 8, b_fill = (ncb * kOvSub + nfb) * 8, b_tp = (ncb * kOvSub + 1) * 4;
+          const size_t b_fs = (nfb + 1) * 8, b_fill = (ncb * kOvSub + nfb) * 8, b_tp = (ncb * kOvSub + 1) * 4,
+                       b_cs = (ncb * kOvSub + 1) * 8;
           OVCHK(grow(scratch, plan.total * 8, stream));
-          OVCHK(grow(fine, plan.total * 8, stream));
-          OVCHK(grow(ovp, 2 * b_fs + b_fill + b_tp + 16, stream));
+          OVCHK(grow(fine, std::max(plan.total, plan.ctotal) * 8, stream));
+          OVCHK(grow(ovp, 2 * b_fs + b_cs + b_fill + b_tp + 16, stream));
           unsigned long long* d_fstart = (unsigned long long*)ovp.p;
           unsigned long long* d_fbase = d_fstart + nfb + 1;
-          unsigned long long* d_cfill = d_fbase + nfb + 1;
+          unsigned long long* d_cstart = d_fbase + nfb + 1;
+          unsigned long long* d_cfill = d_cstart + ncb * kOvSub + 1;
           uint32_t* d_tp = (uint32_t*)(d_cfill + ncb * kOvSub + nfb);
           uint32_t* d_flag = d_tp + ncb * kOvSub + 1;
           OVCHK(hipMemcpyAsync(d_fstart, plan.fstart.data(), b_fs, hipMemcpyHostToDevice, stream));
+          OVCHK(hipMemcpyAsync(d_cstart, plan.cstart.data(), b_cs, hipMemcpyHostToDevice, stream));
           OVCHK(hipMemcpyAsync(d_tp, plan.tprefix.data(), b_tp, hipMemcpyHostToDevice, stream));
           OVCHK(hipMemsetAsync(d_cfill, 0, b_fill, stream));
           OVCHK(hipMemsetAsync(d_flag, 0, 4, stream));
           OvPart a{(const uint64_t*)bucket[s].p, (uint64_t*)fine.p, m, d_fstart, d_cfill, d_cfill + ncb * kOvSub, d_tp,
-                   d_flag, (uint32_t)ncb, (uint32_t)nfb, p.B + 1 + p.TB, {}};
-          std::copy(plan.sfrac, plan.sfrac + kOvSub + 1, a.sfrac);
+                   d_flag, (uint32_t)ncb, (uint32_t)nfb, p.B + 1 + p.TB, (const unsigned long long*)d_cstart};
           hipLaunchKernelGGL((k_ov_part<false>), dim3((uint32_t)((m + kOvpTile - 1) / kOvpTile)), dim3(kOvpBlock),
                              0, stream, a);
           OVCHK(hipGetLastError());
@@ -1059,9 +1123,8 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
               double worst_c = 0, worst_f = 0;
               uint64_t nc = 0, nf = 0;
               for (uint64_t c = 0; c < ncb; ++c) {
-                const uint64_t cs = plan.fstart[c * 256], ce = plan.fstart[std::min<uint64_t>((c + 1) * 256, nfb)];
                 for (uint32_t x = 0; x < kOvSub; ++x) {
-                  const uint64_t cap = ov_sub_at(cs, ce, plan.sfrac[x + 1]) - ov_sub_at(cs, ce, plan.sfrac[x]);
+                  const uint64_t cap = plan.cstart[c * kOvSub + x + 1] - plan.cstart[c * kOvSub + x];
                   const double r = cap ? (double)cf[c * kOvSub + x] / cap : 1e9;
                   if (cf[c * kOvSub + x] > cap) ++nc;
                   worst_c = std::max(worst_c, r);
