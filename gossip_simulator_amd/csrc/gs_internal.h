@@ -473,7 +473,9 @@ struct OverlayWindowSink {
 };
 // Device buffers the overlay builder keeps between builds (one per context).
 struct OverlayWork {
-  struct Buf { void* p = nullptr; size_t bytes = 0; };
+  // p = raw + off: a bucket's data starts `off` bytes into its allocation
+  // (staggered per ring slot, see gs_overlay.hip)
+  struct Buf { void* p = nullptr; size_t bytes = 0; void* raw = nullptr; size_t off = 0; };
   std::vector<Buf> bucket;  // per arrival slot
   Buf scratch, outb, oslotb, cub_tmp, meta;
   Buf fine, ovp;            // destination partition of the dense ticks: regions, plan + fills

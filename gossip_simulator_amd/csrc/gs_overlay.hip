@@ -739,16 +739,36 @@ using DevBuf = OverlayWork::Buf;
 // 1.7 s where the next batch's events outnumbered the first's by a little.
 // (The stream-ordered pool allocator instead corrupted the N = 1e9 build:
 // profiles/r04s_overlay_pool.txt.)
+static void free_buf(DevBuf& b) {
+  if (b.raw) (void)hipFree(b.raw);
+  b.p = b.raw = nullptr;
+  b.bytes = 0;
+}
 static hipError_t grow(DevBuf& b, size_t bytes, hipStream_t st) {
   (void)st;
   if (b.bytes >= bytes) return hipSuccess;
   const size_t nb = std::max(bytes + bytes / 4, b.bytes * 3 / 2);
-  if (b.p) (void)hipFree(b.p);
-  b.p = nullptr;
-  b.bytes = 0;
-  hipError_t e = hipMalloc(&b.p, nb);
-  if (e == hipSuccess) b.bytes = nb;
+  free_buf(b);
+  hipError_t e = hipMalloc(&b.raw, nb + b.off);
+  if (e == hipSuccess) {
+    b.p = (char*)b.raw + b.off;
+    b.bytes = nb;
+  } else {
+    b.raw = nullptr;
+  }
   return e;
+}
+
+// The ring's buckets start at staggered offsets (slot s: s x 4352 B mod 64 KB;
+// GS_OV_STAGGER=0: all at their allocation's base, A/B).  A tick's emitted
+// events are appended to ~10 buckets at once, and with every bucket at the
+// same alignment and fills growing in step, the scatter of some burst ticks
+// ran 5x slower than that of others with the same requests, hits and misses
+// (profiles/r05ad_scatter_pmc.txt): the write fronts met in the same memory
+// channels.
+static size_t ov_stagger(uint32_t s) {
+  static const bool off = getenv("GS_OV_STAGGER") && atoi(getenv("GS_OV_STAGGER")) == 0;
+  return off ? 0 : ((size_t)s * 4352u) % 65536u;
 }
 
 // The destination partition's plan for a tick of m events: fine region
@@ -840,14 +860,9 @@ static uint32_t node_bits(uint64_t n) {
 void overlay_free(OverlayWork* ws, hipStream_t st) {
   (void)st;
   if (!ws) return;
-  for (auto& b : ws->bucket)
-    if (b.p) (void)hipFree(b.p);
+  for (auto& b : ws->bucket) free_buf(b);
   ws->bucket.clear();
-  for (DevBuf* b : {&ws->scratch, &ws->outb, &ws->oslotb, &ws->cub_tmp, &ws->meta, &ws->fine, &ws->ovp}) {
-    if (b->p) (void)hipFree(b->p);
-    b->p = nullptr;
-    b->bytes = 0;
-  }
+  for (DevBuf* b : {&ws->scratch, &ws->outb, &ws->oslotb, &ws->cub_tmp, &ws->meta, &ws->fine, &ws->ovp}) free_buf(*b);
 }
 
 int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, int32_t fanin,
@@ -904,6 +919,8 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
   // buffers live in the caller's workspace across builds (batched C3 builds
   // one overlay per batch; reallocating tens of GB per block was the cost)
   if (ws->bucket.size() < NB) ws->bucket.resize(NB);
+  for (uint32_t s = 0; s < NB; ++s)
+    if (!ws->bucket[s].raw) ws->bucket[s].off = ov_stagger(s);
   std::vector<DevBuf>& bucket = ws->bucket;
   std::vector<uint64_t> fill(NB, 0);
   DevBuf &scratch = ws->scratch, &outb = ws->outb, &oslotb = ws->oslotb, &cub_tmp = ws->cub_tmp,
@@ -1200,11 +1217,12 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
           if (!h_counts[q]) continue;
           if (bucket[q].bytes < (fill[q] + h_counts[q]) * 8) {
             DevBuf nb;
+            nb.off = bucket[q].off;
             OVCHK(grow(nb, (fill[q] + h_counts[q]) * 8 * 3 / 2, stream));
             if (fill[q])
               OVCHK(hipMemcpyAsync(nb.p, bucket[q].p, fill[q] * 8, hipMemcpyDeviceToDevice, stream));
             OVCHK(hipStreamSynchronize(stream));
-            (void)hipFree(bucket[q].p);
+            free_buf(bucket[q]);
             bucket[q] = nb;
           }
         }
