@@ -760,12 +760,10 @@ static hipError_t grow(DevBuf& b, size_t bytes, hipStream_t st) {
 }
 
 // The ring's buckets start at staggered offsets (slot s: s x 4352 B mod 64 KB;
-// GS_OV_STAGGER=0: all at their allocation's base, A/B).  A tick's emitted
-// events are appended to ~10 buckets at once, and with every bucket at the
-// same alignment and fills growing in step, the scatter of some burst ticks
-// ran 5x slower than that of others with the same requests, hits and misses
-// (profiles/r05ad_scatter_pmc.txt): the write fronts met in the same memory
-// channels.
+// GS_OV_STAGGER=0: all at their allocation's base, A/B): P1's reads of a
+// bucket took 84 -> 65 ms per N = 1e9 build (profiles/r05ad_scatter_pmc.txt).
+// (It was tried for the emitted events' scatter, whose burst ticks run 3 or
+// 16 ms with the same requests, hits and misses: no change there.)
 static size_t ov_stagger(uint32_t s) {
   static const bool off = getenv("GS_OV_STAGGER") && atoi(getenv("GS_OV_STAGGER")) == 0;
   return off ? 0 : ((size_t)s * 4352u) % 65536u;
