@@ -760,10 +760,12 @@ static hipError_t grow(DevBuf& b, size_t bytes, hipStream_t st) {
 }
 
 // The ring's buckets start at staggered offsets (slot s: s x 4352 B mod 64 KB;
-// GS_OV_STAGGER=0: all at their allocation's base, A/B): P1's reads of a
-// bucket took 84 -> 65 ms per N = 1e9 build (profiles/r05ad_scatter_pmc.txt).
-// (It was tried for the emitted events' scatter, whose burst ticks run 3 or
-// 16 ms with the same requests, hits and misses: no change there.)
+// GS_OV_STAGGER=0: all at their allocation's base, A/B).  In one interleaved
+// A/B P1 took 65 vs 84 ms per N = 1e9 build, but later runs spread 64-80 ms
+// either way (profiles/r05ad_scatter_pmc.txt): kept as harmless, not as a
+// measured win.  It was tried for the emitted events' scatter, whose burst
+// ticks run 3 or 16 ms with the same requests, hits and misses (also with a
+// 1-MB stagger): no change there.
 static size_t ov_stagger(uint32_t s) {
   static const bool off = getenv("GS_OV_STAGGER") && atoi(getenv("GS_OV_STAGGER")) == 0;
   return off ? 0 : ((size_t)s * 4352u) % 65536u;
