@@ -222,6 +222,37 @@ def test_overlay_tick_blocks_match_oracle(gs, oracle, monkeypatch, block, dlow, 
         assert np.array_equal(masked(gdeg, gids), masked(deg, ids))
 
 
+@pytest.mark.parametrize("n,trials", [(6_000_000, 1), (60_000, 120)])
+def test_overlay_partition_equals_sort_at_scale(gs, monkeypatch, n, trials):
+    """Past the oracle's reach: at n = 6e6 (367 fine regions, 2 coarse
+    regions, C5's fanout 5 / fanin 6) and at 120 batched trials (the opt-in
+    batched plans), the overlay built with the destination partition is the
+    one built with the radix sort -- table, degrees, windows, final tick --
+    and every tick is grouped (no fallback)."""
+    from dataclasses import replace
+    if gs.engine == "tick":
+        pytest.skip("one engine is enough: the overlay is the same code")
+    kw = dict(n=n, fanout=5, fanin=6, delay_low=10, delay_high=20, drop_rate=0.1, crash_rate=0.01,
+              seed=17, trial=2)
+    out = {}
+    for mode in ("sort", "partition"):
+        for var in ("GS_OV_SORT", "GS_OV_PART_BATCHED"):
+            monkeypatch.delenv(var, raising=False)
+        if mode == "sort":
+            monkeypatch.setenv("GS_OV_SORT", "1")
+        elif trials > 1:
+            monkeypatch.setenv("GS_OV_PART_BATCHED", "1")
+        with gs.Simulator(replace(cfg_from(gs, kw), trials=trials)) as sim:
+            wins, final = sim.build_overlay()
+            tm = sim.timing()
+            deg, ids = sim.read_peers()
+        out[mode] = (hashlib.sha256(deg.tobytes()).hexdigest(), hashlib.sha256(masked(deg, ids).tobytes()).hexdigest(),
+                     [tuple(w) for w in wins], final)
+        if mode == "partition":
+            assert tm["ov_part_ticks"] >= 10 and tm["ov_part_fallbacks"] == 0, tm
+    assert out["sort"] == out["partition"]
+
+
 @pytest.mark.parametrize("mode", ["partition", "sort", "fallback", "batched", "pick-count", "pick-overflow"])
 def test_overlay_destination_partition(gs, oracle, monkeypatch, mode):
     """Verdict r04 item 6: dense overlay ticks are grouped by destination with
