@@ -64,6 +64,8 @@ struct OvParams {
   uint32_t tlog, tmask;
   // tick blocks: L ticks per block, TB tag bits, NB buckets in the ring
   uint32_t L, TB, NB;
+  // per-bucket counters (counts, fill) lie fs words apart (GS_OV_FILL_STRIDE)
+  uint32_t fs;
 };
 
 // Key node and counter word 3 of global id g (per-trial keys, gs_internal.h).
@@ -135,7 +137,7 @@ struct OutSource {  // events emitted by a processing block (a compact list)
 // would pass one sets *ovf and writes none of that bucket's items (tick 0's
 // planned buckets: the host then counts and writes again).
 template <bool WRITE, class Src>
-__global__ __launch_bounds__(kScatterBlock) void k_scatter(Src src, uint64_t nitems, uint32_t R,
+__global__ __launch_bounds__(kScatterBlock) void k_scatter(Src src, uint64_t nitems, uint32_t R, uint32_t fs,
                                                            unsigned long long* counts,
                                                            unsigned long long* fill,
                                                            uint64_t* const* buckets,
@@ -161,12 +163,12 @@ __global__ __launch_bounds__(kScatterBlock) void k_scatter(Src src, uint64_t nit
   __syncthreads();
   if (!WRITE) {
     for (uint32_t s = threadIdx.x; s < R; s += blockDim.x)
-      if (s_hist[s]) atomicAdd(&counts[s], (unsigned long long)s_hist[s]);
+      if (s_hist[s]) atomicAdd(&counts[(size_t)s * fs], (unsigned long long)s_hist[s]);
     return;
   }
   for (uint32_t s = threadIdx.x; s < R; s += blockDim.x)
     if (s_hist[s]) {
-      const unsigned long long b = atomicAdd(&fill[s], (unsigned long long)s_hist[s]);
+      const unsigned long long b = atomicAdd(&fill[(size_t)s * fs], (unsigned long long)s_hist[s]);
       const bool over = caps && b + s_hist[s] > caps[s];
       if (over) atomicOr(ovf, 1u);
       s_base[s] = over ? ~0ull : b;
@@ -275,7 +277,7 @@ __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64
       const unsigned long long q = atomicAdd(ecount, 1ull);
       eout[q] = key;
       eslot[q] = (uint16_t)slot;
-      atomicAdd(&counts[slot], 1ull);
+      atomicAdd(&counts[(size_t)slot * p.fs], 1ull);
     }
   };
   const uint32_t sh = p.B + 1 + p.TB;  // destination field
@@ -404,7 +406,7 @@ __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64
   }
   __syncthreads();
   for (uint32_t q = tid; q < p.NB; q += kProcBlock)
-    if (s_hist[q]) atomicAdd(&counts[q], (unsigned long long)s_hist[q]);
+    if (s_hist[q]) atomicAdd(&counts[(size_t)q * p.fs], (unsigned long long)s_hist[q]);
 }
 
 // ---- destination partition of a dense tick (replaces the radix sort) -------
@@ -916,6 +918,10 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
     p.NB = (p.R + p.L - 1) / p.L + 2;  // <= R + 2 <= kMaxRing (checked above)
   }
   const uint32_t NB = p.NB;
+  // The per-bucket counters every workgroup of k_process and k_scatter adds
+  // to (counts, fill) lie fs words apart (GS_OV_FILL_STRIDE, A/B).
+  p.fs = getenv("GS_OV_FILL_STRIDE") ? std::max(1, atoi(getenv("GS_OV_FILL_STRIDE"))) : 1;
+  const uint32_t fs = p.fs;
   // buffers live in the caller's workspace across builds (batched C3 builds
   // one overlay per batch; reallocating tens of GB per block was the cost)
   if (ws->bucket.size() < NB) ws->bucket.resize(NB);
@@ -945,7 +951,7 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
   uint32_t h_flag = 0;
   const int ov_debug = getenv("GS_OV_DEBUG") ? atoi(getenv("GS_OV_DEBUG")) : 0;
   ws->part_ticks = ws->sort_ticks = ws->part_fallbacks = ws->pick_fallbacks = 0;
-  // meta layout: counts[NB] | fill[NB] | ptrs[NB] | nemit (64 B) | TickCounters
+  // meta layout: ptrs[NB] | nemit (64 B) | TickCounters | caps[NB] | ovf (64 B) | counts[NB * fs] | fill[NB * fs]
   uint64_t pending = 0, wm = 0, wb = 0;
   std::vector<unsigned long long> h_counts(NB), hfill(NB);
   std::vector<uint64_t*> h_ptrs(NB, nullptr);
@@ -957,16 +963,27 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
   uint32_t* d_ovf = nullptr, h_ovf = 0;
   std::vector<unsigned long long> h_caps(NB, 0);
   TickCounters h_tc;
-  const size_t meta_bytes = NB * 8 * 3 + 64 + sizeof(TickCounters) + NB * 8 + 64;
+  const size_t head_bytes = (NB * 8 + 64 + sizeof(TickCounters) + NB * 8 + 64 + 255) / 256 * 256;
+  const size_t meta_bytes = head_bytes + 2 * (size_t)NB * fs * 8;
 
+  // host <-> device copies of the strided counters
+  auto ctr_d2h = [&](unsigned long long* h, const unsigned long long* d) {
+    return fs == 1 ? hipMemcpyAsync(h, d, NB * 8, hipMemcpyDeviceToHost, stream)
+                   : hipMemcpy2DAsync(h, 8, d, (size_t)fs * 8, 8, NB, hipMemcpyDeviceToHost, stream);
+  };
+  auto ctr_h2d = [&](unsigned long long* d, const unsigned long long* h) {
+    return fs == 1 ? hipMemcpyAsync(d, h, NB * 8, hipMemcpyHostToDevice, stream)
+                   : hipMemcpy2DAsync(d, (size_t)fs * 8, h, 8, 8, NB, hipMemcpyHostToDevice, stream);
+  };
+  const size_t ctr_bytes = (size_t)NB * fs * 8;
   OVCHK(grow(meta, meta_bytes, stream));
-  d_counts = (unsigned long long*)meta.p;
-  d_fill = d_counts + NB;
-  d_ptrs = (uint64_t**)(d_fill + NB);
+  d_ptrs = (uint64_t**)meta.p;
   d_nemit = (unsigned long long*)(d_ptrs + NB);
   d_tc = (TickCounters*)((char*)d_nemit + 64);
   d_caps = (unsigned long long*)(d_tc + 1);
   d_ovf = (uint32_t*)(d_caps + NB);
+  d_counts = (unsigned long long*)((char*)meta.p + head_bytes);
+  d_fill = d_counts + (size_t)NB * fs;
   OVCHK(hipMemsetAsync(meta.p, 0, meta_bytes, stream));
 
   {
@@ -1008,25 +1025,25 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
         OVCHK(hipMemsetAsync(d_ovf, 0, 4, stream));
         src.write_rows = true;
         hipLaunchKernelGGL((k_scatter<true, PickSource>), dim3((uint32_t)blocks), dim3(kScatterBlock), 0, stream,
-                           src, items, NB, d_counts, d_fill, (uint64_t* const*)d_ptrs,
+                           src, items, NB, fs, d_counts, d_fill, (uint64_t* const*)d_ptrs,
                            (const unsigned long long*)d_caps, d_ovf);
         OVCHK(hipGetLastError());
-        OVCHK(hipMemcpyAsync(h_counts.data(), d_fill, NB * 8, hipMemcpyDeviceToHost, stream));
+        OVCHK(ctr_d2h(h_counts.data(), d_fill));
         OVCHK(hipMemcpyAsync(&h_ovf, d_ovf, 4, hipMemcpyDeviceToHost, stream));
         OVCHK(hipStreamSynchronize(stream));
         if (h_ovf) {  // the exact path below, from empty buckets
           planned = false;
           ++ws->pick_fallbacks;
           if (ov_debug) fprintf(stderr, "[overlay] tick 0: a planned pick bucket overflowed; counting\n");
-          OVCHK(hipMemsetAsync(d_fill, 0, NB * 8, stream));
+          OVCHK(hipMemsetAsync(d_fill, 0, ctr_bytes, stream));
         }
       }
       if (!planned) {
         src.write_rows = false;
         hipLaunchKernelGGL((k_scatter<false, PickSource>), dim3((uint32_t)blocks), dim3(kScatterBlock),
-                           0, stream, src, items, NB, d_counts, d_fill, (uint64_t* const*)d_ptrs);
+                           0, stream, src, items, NB, fs, d_counts, d_fill, (uint64_t* const*)d_ptrs);
         OVCHK(hipGetLastError());
-        OVCHK(hipMemcpyAsync(h_counts.data(), d_counts, NB * 8, hipMemcpyDeviceToHost, stream));
+        OVCHK(ctr_d2h(h_counts.data(), d_counts));
         OVCHK(hipStreamSynchronize(stream));
         for (uint32_t s = 0; s < NB; ++s) {
           OVCHK(grow(bucket[s], (fill[s] + h_counts[s]) * 8, stream));
@@ -1035,11 +1052,11 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
         OVCHK(hipMemcpyAsync(d_ptrs, h_ptrs.data(), NB * 8, hipMemcpyHostToDevice, stream));
         src.write_rows = true;
         hipLaunchKernelGGL((k_scatter<true, PickSource>), dim3((uint32_t)blocks), dim3(kScatterBlock),
-                           0, stream, src, items, NB, d_counts, d_fill, (uint64_t* const*)d_ptrs);
+                           0, stream, src, items, NB, fs, d_counts, d_fill, (uint64_t* const*)d_ptrs);
         OVCHK(hipGetLastError());
       }
       for (uint32_t s = 0; s < NB; ++s) { fill[s] += h_counts[s]; pending += h_counts[s]; }
-      OVCHK(hipMemsetAsync(d_counts, 0, NB * 8, stream));
+      OVCHK(hipMemsetAsync(d_counts, 0, ctr_bytes, stream));
     } else if (ntot) {
       OVCHK(hipMemsetAsync(d_deg, 0, ntot, stream));
     }
@@ -1188,7 +1205,7 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
         OVCHK(hipGetLastError());
       }
       OVCHK(hipMemcpyAsync(&h_ne, d_nemit, 8, hipMemcpyDeviceToHost, stream));
-      OVCHK(hipMemcpyAsync(h_counts.data(), d_counts, NB * 8, hipMemcpyDeviceToHost, stream));
+      OVCHK(ctr_d2h(h_counts.data(), d_counts));
       OVCHK(hipMemcpyAsync(&h_tc, d_tc, sizeof(h_tc), hipMemcpyDeviceToHost, stream));
       OVCHK(hipMemsetAsync(d_nemit, 0, 8, stream));
       OVCHK(hipStreamSynchronize(stream));
@@ -1235,16 +1252,16 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
         // hfill is rewritten only after the next block's count sync, which
         // orders it after this copy: no host sync after the scatter
         hfill.assign(fill.begin(), fill.end());
-        OVCHK(hipMemcpyAsync(d_fill, hfill.data(), NB * 8, hipMemcpyHostToDevice, stream));
+        OVCHK(ctr_h2d(d_fill, hfill.data()));
         if (blocks) {
           hipLaunchKernelGGL((k_scatter<true, OutSource>), dim3(blocks), dim3(kScatterBlock), 0, stream, osrc,
-                             nitems, NB, d_counts, d_fill, (uint64_t* const*)d_ptrs);
+                             nitems, NB, fs, d_counts, d_fill, (uint64_t* const*)d_ptrs);
           OVCHK(hipGetLastError());
         }
         for (uint32_t q = 0; q < NB; ++q) { fill[q] += h_counts[q]; pending += h_counts[q]; }
         wm += h_tc.makeups;
         wb += h_tc.breakups;
-        OVCHK(hipMemsetAsync(d_counts, 0, NB * 8, stream));
+        OVCHK(hipMemsetAsync(d_counts, 0, ctr_bytes, stream));
         OVCHK(hipMemsetAsync(d_tc, 0, sizeof(TickCounters), stream));
       }
     }

@@ -8,7 +8,8 @@ for rep in 1 2; do
     tag=$(echo "$v" | tr '=, ' '___')
     timeout -k 10 240 env $v rocprofv3 --kernel-trace -d $o/p_$tag -o run -- python3 scripts/ov_once.py > $o/l_$tag.log 2>&1 || { tail -5 $o/l_$tag.log; exit 1; }
     f=$(find $o/p_$tag -name '*.db' | head -1)
-    echo "$rep [$v] $(python3 scripts/ov_ticks.py $f | tail -1)"
+    python3 scripts/ov_ticks.py $f > $o/t_${rep}_$tag.txt
+    echo "$rep [$v] $(tail -1 $o/t_${rep}_$tag.txt)"
     rm -rf $o/p_$tag
   done
 done
