@@ -1107,20 +1107,25 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
           // P1 bucket -> fine.p (coarse regions), P2 -> scratch (fine
           // regions), P3 -> fine.p (sorted, padded); the bucket stays intact
           const uint64_t nfb = plan.nfb, ncb = plan.ncb;
-          const size_t b_fs = (nfb + 1) * 8, b_fill = (ncb * kOvSub + nfb) * 8, b_tp = (ncb * kOvSub + 1) * 4,
-                       b_cs = (ncb * kOvSub + 1) * 8;
+          // each array on lines of its own: a line that holds both a region
+          // fill (atomics, executed at the memory side) and plan words every
+          // tile reads sends those reads to memory too (the bucket scatter's
+          // pointer table beside its fills cost it 2.2x)
+          auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+          const size_t b_fs = al((nfb + 1) * 8), b_fill = al((ncb * kOvSub + nfb) * 8),
+                       b_tp = al((ncb * kOvSub + 1) * 4), b_cs = al((ncb * kOvSub + 1) * 8);
           OVCHK(grow(scratch, plan.total * 8, stream));
           OVCHK(grow(fine, std::max(plan.total, plan.ctotal) * 8, stream));
-          OVCHK(grow(ovp, 2 * b_fs + b_cs + b_fill + b_tp + 16, stream));
+          OVCHK(grow(ovp, 2 * b_fs + b_cs + b_fill + b_tp + 256, stream));
           unsigned long long* d_fstart = (unsigned long long*)ovp.p;
-          unsigned long long* d_fbase = d_fstart + nfb + 1;
-          unsigned long long* d_cstart = d_fbase + nfb + 1;
-          unsigned long long* d_cfill = d_cstart + ncb * kOvSub + 1;
-          uint32_t* d_tp = (uint32_t*)(d_cfill + ncb * kOvSub + nfb);
-          uint32_t* d_flag = d_tp + ncb * kOvSub + 1;
-          OVCHK(hipMemcpyAsync(d_fstart, plan.fstart.data(), b_fs, hipMemcpyHostToDevice, stream));
-          OVCHK(hipMemcpyAsync(d_cstart, plan.cstart.data(), b_cs, hipMemcpyHostToDevice, stream));
-          OVCHK(hipMemcpyAsync(d_tp, plan.tprefix.data(), b_tp, hipMemcpyHostToDevice, stream));
+          unsigned long long* d_fbase = (unsigned long long*)((char*)d_fstart + b_fs);
+          unsigned long long* d_cstart = (unsigned long long*)((char*)d_fbase + b_fs);
+          unsigned long long* d_cfill = (unsigned long long*)((char*)d_cstart + b_cs);
+          uint32_t* d_tp = (uint32_t*)((char*)d_cfill + b_fill);
+          uint32_t* d_flag = (uint32_t*)((char*)d_tp + b_tp);
+          OVCHK(hipMemcpyAsync(d_fstart, plan.fstart.data(), (nfb + 1) * 8, hipMemcpyHostToDevice, stream));
+          OVCHK(hipMemcpyAsync(d_cstart, plan.cstart.data(), (ncb * kOvSub + 1) * 8, hipMemcpyHostToDevice, stream));
+          OVCHK(hipMemcpyAsync(d_tp, plan.tprefix.data(), (ncb * kOvSub + 1) * 4, hipMemcpyHostToDevice, stream));
           OVCHK(hipMemsetAsync(d_cfill, 0, b_fill, stream));
           OVCHK(hipMemsetAsync(d_flag, 0, 4, stream));
           OvPart a{(const uint64_t*)bucket[s].p, (uint64_t*)fine.p, m, d_fstart, d_cfill, d_cfill + ncb * kOvSub, d_tp,
