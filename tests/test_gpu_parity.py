@@ -265,7 +265,8 @@ def test_overlay_destination_partition(gs, oracle, monkeypatch, mode):
     pick-count / pick-overflow: tick 0's picks counted before they are written
     (instead of one pass into planned buckets), or the plan too small so the
     planned pass overflows and falls back to that.
-    Every mode builds the oracle's overlay -- windows, final tick, rows."""
+    Every mode builds the oracle's overlay -- windows, final tick, rows -- and
+    a window context's rows come out sealed (slots past the degree empty)."""
     from dataclasses import replace
     if mode == "batched" and gs.engine == "tick":
         pytest.skip("batched trials run on the window engine")
@@ -290,6 +291,9 @@ def test_overlay_destination_partition(gs, oracle, monkeypatch, mode):
         gdeg, gids = sim.read_peers()
         n = kw["n"]
         res = [(gdeg[t * n:(t + 1) * n], gids[t * n:(t + 1) * n]) for t in range(trials)]
+    if gs.engine != "tick":  # sealed: every slot past a node's degree holds the empty id
+        pad = np.arange(gids.shape[1])[None, :] >= gdeg.astype(np.int64)[:, None]
+        assert np.all(gids[pad] == 0xFFFFFFFF)
     if mode in ("partition", "pick-count", "pick-overflow", "batched"):
         assert tm["ov_part_ticks"] >= 10 and tm["ov_part_fallbacks"] == 0, tm
     elif mode == "sort":
