@@ -253,19 +253,149 @@ struct Row8 {
 // read once into registers (two 16-B loads), replayed there with unrolled
 // selects, and written back once -- instead of a dependent global load per
 // slot of every linear search, shift and victim read.
-template <bool ROW8>
+// A run's keys, in LDS (the staged tile) or in global memory (a run that
+// leaves the staged keys); local index 0 .. len-1.
+struct LdsRun {
+  uint64_t* s;
+  __device__ __forceinline__ uint64_t get(uint32_t i) const { return s[i]; }
+  __device__ __forceinline__ void set(uint32_t i, uint64_t v) const { s[i] = v; }
+};
+struct GlobalRun {
+  uint64_t* g;
+  __device__ __forceinline__ uint64_t get(uint32_t i) const { return g[i]; }
+  __device__ __forceinline__ void set(uint32_t i, uint64_t v) const { g[i] = v; }
+};
+
+// One destination's run: ordered by (tag, src, kind) -- tick by tick, each
+// tick's events in the order the handlers replay them (runs are short:
+// insertion) -- and replayed against its friends row (in registers for ROW8,
+// loaded by the caller with its degree d; else in memory).
+template <bool ROW8, class Run, class Emit>
+__device__ __forceinline__ void ov_replay(const OvParams& p, uint64_t t0, Run run, uint32_t len, uint32_t u,
+                                          uint8_t* deg, uint32_t* ids, Row8 r8, uint32_t d, Emit& emit,
+                                          uint32_t& mk, uint32_t& bk, uint32_t& err) {
+  const uint32_t sh = p.B + 1 + p.TB;  // destination field
+  const uint64_t smask = (1ull << p.B) - 1, lmask = (1ull << sh) - 1;
+  const uint32_t tagmask = (1u << p.TB) - 1;
+  const uint32_t ul = u & p.tmask, tb = u & ~p.tmask;  // node within its trial, trial base
+  for (uint32_t i = 1; i < len; ++i) {
+    const uint64_t key = run.get(i);
+    uint32_t j = i;
+    for (; j > 0; --j) {
+      const uint64_t prev = run.get(j - 1);
+      if ((prev & lmask) <= (key & lmask)) break;
+      run.set(j, prev);
+    }
+    run.set(j, key);
+  }
+  uint32_t* row = ids + (size_t)u * p.stride;
+  uint32_t ptag = ~0u, k = 0;
+  bool dirty = false;
+#define RGET8(j) (r8.get(j))
+#define RSET8(j, x) (r8.set((j), (x)), dirty = true)
+  for (uint32_t i = 0; i < len; ++i) {
+    const uint64_t key = run.get(i);
+    const uint32_t src = (uint32_t)((key >> 1) & smask);
+    const uint32_t tag = (uint32_t)(key >> (p.B + 1)) & tagmask;
+    k = tag == ptag ? k + 1 : 0u;  // the ordinal restarts with each tick
+    ptag = tag;
+    const uint32_t t = (uint32_t)(t0 + tag);
+    uint32_t emitted_dst = ~0u, emitted_kind = 0;
+    if (k >= (1u << 26)) { err |= 2; continue; }
+    if ((key & 1) == 0) {                                   // makeUpCh (:66-75)
+      ++mk;
+      if (d < p.fanin) {
+        if (ROW8) RSET8(d, src); else row[d] = src;
+        ++d;
+      } else {
+        const uint32_t pos = uniform(ov_draw(p, K_VICTIM, u, t, k), d);
+        emitted_dst = ROW8 ? RGET8(pos) : row[pos];          // Breakup (:73)
+        emitted_kind = 1;
+        if (ROW8) RSET8(pos, src); else row[pos] = src;
+      }
+    } else {                                                // breakUpCh (:76-94)
+      ++bk;
+      uint32_t idx = 0;
+      if (ROW8) {
+        idx = r8.find(src, d);
+      } else {
+        while (idx < d && row[idx] != src) ++idx;
+      }
+      if (idx < d) {
+        if (d > p.fanout) {                                 // removeFriend (:83)
+          if (ROW8) {
+            r8.remove(idx, d);
+            dirty = true;
+          } else {
+            for (uint32_t q = idx; q + 1 < d; ++q) row[q] = row[q + 1];
+          }
+          --d;
+        } else {                                            // replace (:86-91)
+          uint32_t nf = 0, a = 0, kn, c3;
+          node_key(p.tlog, p.tmask, p.key, u, K_REPLACE, kn, c3);
+          for (; a < 256; ++a) {
+            const u32x4 rr = philox(kn, t, (k << 6) | (a >> 2), c3, p.key.k0, p.key.k1);
+            nf = uniform(lane_of(rr, a & 3), (uint32_t)p.n);
+            if (nf != (src & p.tmask) && nf != ul) break;
+          }
+          nf |= tb;
+          if (a == 256) {
+            err |= 1;
+          } else {
+            if (ROW8) RSET8(idx, nf); else row[idx] = nf;
+            emitted_dst = nf;                               // Makeup (:91)
+            emitted_kind = 0;
+          }
+        }
+      }
+    }
+    if (emitted_dst != ~0u) {
+      const uint32_t a = t + fire_offset(p.delay_low, p.delay_span, ov_draw(p, K_OVDELAY, u, t, k));
+      emit(ev_key(p, emitted_dst, a, u, emitted_kind), ev_bucket(p, a));
+    }
+  }
+#undef RGET8
+#undef RSET8
+  if (ROW8 && dirty) {
+    reinterpret_cast<uint4*>(row)[0] = make_uint4(r8.v0, r8.v1, r8.v2, r8.v3);
+    reinterpret_cast<uint4*>(row)[1] = make_uint4(r8.v4, r8.v5, r8.v6, r8.v7);
+  }
+  deg[u] = (uint8_t)d;
+}
+
+// STAGED: the workgroup's 1024 key positions plus kProcLook more are read
+// into LDS in one coalesced pass first; run heads, run ends and the runs'
+// insertion sorts then work there, and (ROW8) the rows and degrees of a
+// thread's up to kProcIPT runs are loaded together before any is replayed.
+// Without it every run walks a chain of dependent global loads (its key, the
+// key before it, each key to its end, the sort's re-reads, then the row): the
+// burst ticks' waves spent 77 % of their cycles waiting
+// (profiles/r05as_process_pmc.txt).  A run that leaves the staged keys is
+// replayed from global memory.
+constexpr uint32_t kProcLook = 64;
+template <bool ROW8, uint32_t STAGED>  // STAGED 1: keys in LDS, rows batched; 2: keys in LDS only
 __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64_t t0, uint64_t* keys, uint64_t m,
                                                         uint8_t* deg, uint32_t* ids, uint64_t* eout,
                                                         uint16_t* eslot, unsigned long long* ecount,
                                                         unsigned long long* counts, TickCounters* tc) {
+  constexpr uint32_t kTile = kProcBlock * kProcIPT, kStage = STAGED ? kTile + kProcLook : 1;
   __shared__ uint64_t s_ev[kEmitCap];
   __shared__ uint16_t s_sl[kEmitCap];
   __shared__ uint32_t s_hist[kMaxRing];  // the workgroup's emitted events per bucket
+  __shared__ uint64_t s_key[kStage + 1];  // STAGED: [0] = the key before the tile, [1 + i] = position base + i
   __shared__ uint32_t s_n, s_mk, s_bk, s_err;
   __shared__ unsigned long long s_base;
   const uint32_t tid = threadIdx.x;
   if (tid == 0) { s_n = 0; s_mk = 0; s_bk = 0; s_err = 0; }
   for (uint32_t q = tid; q < p.NB; q += kProcBlock) s_hist[q] = 0;
+  const uint64_t base = (uint64_t)blockIdx.x * kTile;
+  if (STAGED) {
+    for (uint32_t i = tid; i < kStage; i += kProcBlock) {
+      const uint64_t g = base + i;
+      s_key[1 + i] = g < m ? keys[g] : 0ull;
+    }
+    if (tid == 0) s_key[0] = base > 0 ? keys[base - 1] : 0ull;
+  }
   __syncthreads();
   uint32_t mk = 0, bk = 0, err = 0;
   auto emit = [&](uint64_t key, uint32_t slot) {
@@ -281,110 +411,83 @@ __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64
     }
   };
   const uint32_t sh = p.B + 1 + p.TB;  // destination field
-  const uint64_t smask = (1ull << p.B) - 1, lmask = (1ull << sh) - 1;
-  const uint32_t tagmask = (1u << p.TB) - 1;
-  const uint64_t base = (uint64_t)blockIdx.x * kProcBlock * kProcIPT;
-  for (uint32_t r = 0; r < kProcIPT; ++r) {
-    const uint64_t start = base + (uint64_t)r * kProcBlock + tid;
-    if (start >= m) break;
-    const uint32_t u = (uint32_t)(keys[start] >> sh);
-    if (start > 0 && (uint32_t)(keys[start - 1] >> sh) == u) continue;  // not a run head
-    uint64_t end = start + 1;
-    while (end < m && (uint32_t)(keys[end] >> sh) == u) ++end;
-    const uint32_t ul = u & p.tmask, tb = u & ~p.tmask;  // node within its trial, trial base
-    // the run in (tag, src, kind) order: tick by tick, each tick's events in
-    // the order the handlers replay them (runs are short: insertion)
-    for (uint64_t i = start + 1; i < end; ++i) {
-      const uint64_t key = keys[i];
-      uint64_t j = i;
-      for (; j > start; --j) {
-        const uint64_t prev = keys[j - 1];
-        if ((prev & lmask) <= (key & lmask)) break;
-        keys[j] = prev;
-      }
-      keys[j] = key;
-    }
-    uint32_t* row = ids + (size_t)u * p.stride;
-    uint32_t d = deg[u];
-    uint32_t ptag = ~0u, k = 0;
-    Row8 r8{};  // ROW8: the row in registers
-    bool dirty = false;
-    if (ROW8) {
-      const uint4 a = reinterpret_cast<const uint4*>(row)[0], b = reinterpret_cast<const uint4*>(row)[1];
-      r8 = Row8{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-      r8.pin();
-    }
-#define RGET8(j) (r8.get(j))
-#define RSET8(j, x) (r8.set((j), (x)), dirty = true)
-    for (uint64_t i = start; i < end; ++i) {
-      const uint64_t key = keys[i];
-      const uint32_t src = (uint32_t)((key >> 1) & smask);
-      const uint32_t tag = (uint32_t)(key >> (p.B + 1)) & tagmask;
-      k = tag == ptag ? k + 1 : 0u;  // the ordinal restarts with each tick
-      ptag = tag;
-      const uint32_t t = (uint32_t)(t0 + tag);
-      uint32_t emitted_dst = ~0u, emitted_kind = 0;
-      if (k >= (1u << 26)) { err |= 2; continue; }
-      if ((key & 1) == 0) {                                   // makeUpCh (:66-75)
-        ++mk;
-        if (d < p.fanin) {
-          if (ROW8) RSET8(d, src); else row[d] = src;
-          ++d;
-        } else {
-          const uint32_t pos = uniform(ov_draw(p, K_VICTIM, u, t, k), d);
-          emitted_dst = ROW8 ? RGET8(pos) : row[pos];          // Breakup (:73)
-          emitted_kind = 1;
-          if (ROW8) RSET8(pos, src); else row[pos] = src;
-        }
-      } else {                                                // breakUpCh (:76-94)
-        ++bk;
-        uint32_t idx = 0;
-        if (ROW8) {
-          idx = r8.find(src, d);
-        } else {
-          while (idx < d && row[idx] != src) ++idx;
-        }
-        if (idx < d) {
-          if (d > p.fanout) {                                 // removeFriend (:83)
-            if (ROW8) {
-              r8.remove(idx, d);
-              dirty = true;
-            } else {
-              for (uint32_t q = idx; q + 1 < d; ++q) row[q] = row[q + 1];
-            }
-            --d;
-          } else {                                            // replace (:86-91)
-            uint32_t nf = 0, a = 0, kn, c3;
-            node_key(p.tlog, p.tmask, p.key, u, K_REPLACE, kn, c3);
-            for (; a < 256; ++a) {
-              const u32x4 rr = philox(kn, t, (k << 6) | (a >> 2), c3, p.key.k0, p.key.k1);
-              nf = uniform(lane_of(rr, a & 3), (uint32_t)p.n);
-              if (nf != (src & p.tmask) && nf != ul) break;
-            }
-            nf |= tb;
-            if (a == 256) {
-              err |= 1;
-            } else {
-              if (ROW8) RSET8(idx, nf); else row[idx] = nf;
-              emitted_dst = nf;                               // Makeup (:91)
-              emitted_kind = 0;
-            }
-          }
+  auto load_row = [&](uint32_t u, Row8& r8) {
+    const uint32_t* row = ids + (size_t)u * p.stride;
+    const uint4 a = reinterpret_cast<const uint4*>(row)[0], b = reinterpret_cast<const uint4*>(row)[1];
+    r8 = Row8{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    r8.pin();
+  };
+  if (STAGED) {
+    // heads and run lengths from the staged keys (len 0: no run starts here;
+    // glob: the run leaves the staged keys)
+    uint32_t hu[kProcIPT], hlen[kProcIPT];
+    bool glob[kProcIPT];
+#pragma unroll
+    for (uint32_t r = 0; r < kProcIPT; ++r) {
+      const uint32_t pos = r * kProcBlock + tid;
+      const uint64_t start = base + pos;
+      hlen[r] = 0;
+      glob[r] = false;
+      hu[r] = 0;
+      if (start < m) {
+        const uint32_t u = (uint32_t)(s_key[1 + pos] >> sh);
+        if (start == 0 || (uint32_t)(s_key[pos] >> sh) != u) {
+          uint32_t len = 1;
+          while (pos + len < kStage && start + len < m && (uint32_t)(s_key[1 + pos + len] >> sh) == u) ++len;
+          glob[r] = pos + len == kStage && start + len < m;
+          hu[r] = u;
+          hlen[r] = len;
         }
       }
-      if (emitted_dst != ~0u) {
-        const uint32_t a = t + fire_offset(p.delay_low, p.delay_span, ov_draw(p, K_OVDELAY, u, t, k));
-        emit(ev_key(p, emitted_dst, a, u, emitted_kind), ev_bucket(p, a));
+    }
+    constexpr uint32_t NR = STAGED == 1 ? kProcIPT : 1;  // rows held at once
+    Row8 r8[NR];
+    uint32_t hd[NR];
+    if (STAGED == 1) {
+#pragma unroll
+      for (uint32_t r = 0; r < NR; ++r) {
+        r8[r] = Row8{};
+        hd[r] = 0;
+        if (hlen[r]) {
+          if (ROW8) load_row(hu[r], r8[r]);
+          hd[r] = deg[hu[r]];
+        }
       }
     }
-    if (ROW8 && dirty) {
-      reinterpret_cast<uint4*>(row)[0] = make_uint4(r8.v0, r8.v1, r8.v2, r8.v3);
-      reinterpret_cast<uint4*>(row)[1] = make_uint4(r8.v4, r8.v5, r8.v6, r8.v7);
+#pragma unroll
+    for (uint32_t r = 0; r < kProcIPT; ++r) {
+      if (!hlen[r]) continue;
+      const uint32_t q = STAGED == 1 ? r : 0;
+      if (STAGED != 1) {
+        r8[q] = Row8{};
+        if (ROW8) load_row(hu[r], r8[q]);
+        hd[q] = deg[hu[r]];
+      }
+      const uint32_t pos = r * kProcBlock + tid;
+      if (!glob[r]) {
+        ov_replay<ROW8>(p, t0, LdsRun{&s_key[1 + pos]}, hlen[r], hu[r], deg, ids, r8[q], hd[q], emit, mk, bk, err);
+      } else {
+        const uint64_t start = base + pos;
+        uint64_t end = start + hlen[r];
+        while (end < m && (uint32_t)(keys[end] >> sh) == hu[r]) ++end;
+        ov_replay<ROW8>(p, t0, GlobalRun{keys + start}, (uint32_t)(end - start), hu[r], deg, ids, r8[q], hd[q], emit,
+                        mk, bk, err);
+      }
     }
-    deg[u] = (uint8_t)d;
+  } else {
+    for (uint32_t r = 0; r < kProcIPT; ++r) {
+      const uint64_t start = base + (uint64_t)r * kProcBlock + tid;
+      if (start >= m) break;
+      const uint32_t u = (uint32_t)(keys[start] >> sh);
+      if (start > 0 && (uint32_t)(keys[start - 1] >> sh) == u) continue;  // not a run head
+      uint64_t end = start + 1;
+      while (end < m && (uint32_t)(keys[end] >> sh) == u) ++end;
+      Row8 r8{};
+      if (ROW8) load_row(u, r8);
+      ov_replay<ROW8>(p, t0, GlobalRun{keys + start}, (uint32_t)(end - start), u, deg, ids, r8, (uint32_t)deg[u], emit,
+                      mk, bk, err);
+    }
   }
-#undef RGET8
-#undef RSET8
   if (mk) atomicAdd(&s_mk, mk);
   if (bk) atomicAdd(&s_bk, bk);
   if (err) atomicOr(&s_err, err);
@@ -947,6 +1050,10 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
   const double part_scale = getenv("GS_OV_PART_SCALE") ? atof(getenv("GS_OV_PART_SCALE")) : 1.04;
   // rows of 8 slots replayed in registers (GS_OV_ROW8=0: slot by slot in memory, A/B)
   const bool row8 = stride == 8 && p.fanin <= 8 && !(getenv("GS_OV_ROW8") && atoi(getenv("GS_OV_ROW8")) == 0);
+  // k_process with its keys staged in LDS and (1) the rows of a thread's runs
+  // loaded together, or (2) each run's row loaded before it is replayed;
+  // GS_OV_STAGED=0: every key read from global memory (A/B)
+  const int staged = getenv("GS_OV_STAGED") ? atoi(getenv("GS_OV_STAGED")) : 1;
   OvPlan plan;
   uint32_t h_flag = 0;
   const int ov_debug = getenv("GS_OV_DEBUG") ? atoi(getenv("GS_OV_DEBUG")) : 0;
@@ -1199,14 +1306,11 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
           ++ws->sort_ticks;
         }
         const uint64_t per = (uint64_t)kProcBlock * kProcIPT;
-        if (row8)
-          hipLaunchKernelGGL(k_process<true>, dim3((uint32_t)((mproc + per - 1) / per)), dim3(kProcBlock), 0, stream,
-                             p, t0, keys, mproc, d_deg, d_ids, (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_nemit,
-                             d_counts, d_tc);
-        else
-          hipLaunchKernelGGL(k_process<false>, dim3((uint32_t)((mproc + per - 1) / per)), dim3(kProcBlock), 0, stream,
-                             p, t0, keys, mproc, d_deg, d_ids, (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_nemit,
-                             d_counts, d_tc);
+        const dim3 pgrid((uint32_t)((mproc + per - 1) / per));
+        auto* pk = row8 ? (staged == 2 ? k_process<true, 2> : staged ? k_process<true, 1> : k_process<true, 0>)
+                        : (staged == 2 ? k_process<false, 2> : staged ? k_process<false, 1> : k_process<false, 0>);
+        hipLaunchKernelGGL(pk, pgrid, dim3(kProcBlock), 0, stream, p, t0, keys, mproc, d_deg, d_ids,
+                           (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_nemit, d_counts, d_tc);
         OVCHK(hipGetLastError());
       }
       OVCHK(hipMemcpyAsync(&h_ne, d_nemit, 8, hipMemcpyDeviceToHost, stream));
