@@ -249,10 +249,6 @@ struct Row8 {
   }
 };
 
-// ROW8 (stride 8, the window engine's padded rows): the run's friends row is
-// read once into registers (two 16-B loads), replayed there with unrolled
-// selects, and written back once -- instead of a dependent global load per
-// slot of every linear search, shift and victim read.
 // A run's keys, in LDS (the staged tile) or in global memory (a run that
 // leaves the staged keys); local index 0 .. len-1.
 struct LdsRun {
@@ -268,8 +264,11 @@ struct GlobalRun {
 
 // One destination's run: ordered by (tag, src, kind) -- tick by tick, each
 // tick's events in the order the handlers replay them (runs are short:
-// insertion) -- and replayed against its friends row (in registers for ROW8,
-// loaded by the caller with its degree d; else in memory).
+// insertion) -- and replayed against its friends row.  ROW8 (stride 8, the
+// window engine's padded rows): the row was read into registers by the caller
+// (two 16-B loads, with its degree d), is replayed there with unrolled
+// selects and written back once -- instead of a dependent global load per
+// slot of every linear search, shift and victim read.  Else in memory.
 template <bool ROW8, class Run, class Emit>
 __device__ __forceinline__ void ov_replay(const OvParams& p, uint64_t t0, Run run, uint32_t len, uint32_t u,
                                           uint8_t* deg, uint32_t* ids, Row8 r8, uint32_t d, Emit& emit,
