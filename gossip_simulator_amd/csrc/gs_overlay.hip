@@ -364,8 +364,9 @@ __device__ __forceinline__ void ov_replay(const OvParams& p, uint64_t t0, Run ru
 
 // STAGED: the workgroup's 1024 key positions plus kProcLook more are read
 // into LDS in one coalesced pass first; run heads, run ends and the runs'
-// insertion sorts then work there, and (ROW8) the rows and degrees of a
-// thread's up to kProcIPT runs are loaded together before any is replayed.
+// insertion sorts then work there.  STAGED 2 loads each run's row and degree
+// just before its replay; STAGED 1 loads those of a thread's up to kProcIPT
+// runs together first (more loads in flight, but 97 VGPRs: measured slower).
 // Without it every run walks a chain of dependent global loads (its key, the
 // key before it, each key to its end, the sort's re-reads, then the row): the
 // burst ticks' waves spent 77 % of their cycles waiting
@@ -1049,10 +1050,11 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
   const double part_scale = getenv("GS_OV_PART_SCALE") ? atof(getenv("GS_OV_PART_SCALE")) : 1.04;
   // rows of 8 slots replayed in registers (GS_OV_ROW8=0: slot by slot in memory, A/B)
   const bool row8 = stride == 8 && p.fanin <= 8 && !(getenv("GS_OV_ROW8") && atoi(getenv("GS_OV_ROW8")) == 0);
-  // k_process with its keys staged in LDS and (1) the rows of a thread's runs
-  // loaded together, or (2) each run's row loaded before it is replayed;
-  // GS_OV_STAGED=0: every key read from global memory (A/B)
-  const int staged = getenv("GS_OV_STAGED") ? atoi(getenv("GS_OV_STAGED")) : 1;
+  // k_process with its keys staged in LDS and (2, the default) each run's row
+  // loaded just before it is replayed or (1) the rows of a thread's runs loaded
+  // together (97 VGPRs, 4 waves per SIMD: slower); 0: every key read from
+  // global memory (A/B; profiles/r05au_process_staged_rows_ab.txt)
+  const int staged = getenv("GS_OV_STAGED") ? atoi(getenv("GS_OV_STAGED")) : 2;
   OvPlan plan;
   uint32_t h_flag = 0;
   const int ov_debug = getenv("GS_OV_DEBUG") ? atoi(getenv("GS_OV_DEBUG")) : 0;

@@ -253,7 +253,8 @@ def test_overlay_partition_equals_sort_at_scale(gs, monkeypatch, n, trials):
     assert out["sort"] == out["partition"]
 
 
-@pytest.mark.parametrize("mode", ["partition", "sort", "fallback", "batched", "pick-count", "pick-overflow"])
+@pytest.mark.parametrize("mode", ["partition", "sort", "fallback", "batched", "pick-count", "pick-overflow",
+                                  "staged-rows", "unstaged"])
 def test_overlay_destination_partition(gs, oracle, monkeypatch, mode):
     """Verdict r04 item 6: dense overlay ticks are grouped by destination with
     the hand-written partition (k_ov_part x2 + k_ov_fine) instead of the
@@ -264,14 +265,19 @@ def test_overlay_destination_partition(gs, oracle, monkeypatch, mode):
     (plans from each trial's own count of the tick's events);
     pick-count / pick-overflow: tick 0's picks counted before they are written
     (instead of one pass into planned buckets), or the plan too small so the
-    planned pass overflows and falls back to that.
+    planned pass overflows and falls back to that; staged-rows / unstaged:
+    k_process with a thread's rows loaded together (GS_OV_STAGED=1) / with
+    every key read from global memory (GS_OV_STAGED=0).
     Every mode builds the oracle's overlay -- windows, final tick, rows -- and
     a window context's rows come out sealed (slots past the degree empty)."""
     from dataclasses import replace
     if mode == "batched" and gs.engine == "tick":
         pytest.skip("batched trials run on the window engine")
-    for var in ("GS_OV_SORT", "GS_OV_PART_SCALE", "GS_OV_PICK_COUNT", "GS_OV_PICK_SCALE", "GS_OV_PART_BATCHED"):
+    for var in ("GS_OV_SORT", "GS_OV_PART_SCALE", "GS_OV_PICK_COUNT", "GS_OV_PICK_SCALE", "GS_OV_PART_BATCHED",
+                "GS_OV_STAGED"):
         monkeypatch.delenv(var, raising=False)
+    if mode in ("staged-rows", "unstaged"):
+        monkeypatch.setenv("GS_OV_STAGED", "1" if mode == "staged-rows" else "0")
     if mode == "pick-count":  # tick 0 counted, then written (the planned single pass off)
         monkeypatch.setenv("GS_OV_PICK_COUNT", "1")
     if mode == "pick-overflow":  # tick 0's planned buckets too small: the count-and-write fallback
@@ -294,7 +300,7 @@ def test_overlay_destination_partition(gs, oracle, monkeypatch, mode):
     if gs.engine != "tick":  # sealed: every slot past a node's degree holds the empty id
         pad = np.arange(gids.shape[1])[None, :] >= gdeg.astype(np.int64)[:, None]
         assert np.all(gids[pad] == 0xFFFFFFFF)
-    if mode in ("partition", "pick-count", "pick-overflow", "batched"):
+    if mode in ("partition", "pick-count", "pick-overflow", "batched", "staged-rows", "unstaged"):
         assert tm["ov_part_ticks"] >= 10 and tm["ov_part_fallbacks"] == 0, tm
     elif mode == "sort":
         assert tm["ov_part_ticks"] == 0 and tm["ov_sort_ticks"] > 0, tm
