@@ -373,7 +373,7 @@ __device__ __forceinline__ void ov_replay(const OvParams& p, uint64_t t0, Run ru
 // (profiles/r05as_process_pmc.txt).  A run that leaves the staged keys is
 // replayed from global memory.
 constexpr uint32_t kProcLook = 64;
-template <bool ROW8, uint32_t STAGED>  // keys in LDS; rows: 1 batched, 2 per run, 3 next run's prefetched
+template <bool ROW8, uint32_t STAGED>  // STAGED 1: keys in LDS, rows batched; 2: keys in LDS only
 __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64_t t0, uint64_t* keys, uint64_t m,
                                                         uint8_t* deg, uint32_t* ids, uint64_t* eout,
                                                         uint16_t* eslot, unsigned long long* ecount,
@@ -440,12 +440,12 @@ __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64
         }
       }
     }
-    constexpr uint32_t NR = STAGED == 1 ? kProcIPT : STAGED == 3 ? 2 : 1;  // rows held at once
+    constexpr uint32_t NR = STAGED == 1 ? kProcIPT : 1;  // rows held at once
     Row8 r8[NR];
     uint32_t hd[NR];
-    if (STAGED == 1 || STAGED == 3) {
+    if (STAGED == 1) {
 #pragma unroll
-      for (uint32_t r = 0; r < (STAGED == 1 ? NR : 1u); ++r) {
+      for (uint32_t r = 0; r < NR; ++r) {
         r8[r] = Row8{};
         hd[r] = 0;
         if (hlen[r]) {
@@ -456,15 +456,9 @@ __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64
     }
 #pragma unroll
     for (uint32_t r = 0; r < kProcIPT; ++r) {
-      const uint32_t q = STAGED == 1 ? r : STAGED == 3 ? (r & 1) : 0;
-      if (STAGED == 3 && r + 1 < kProcIPT && hlen[r + 1]) {  // the next run's row, in flight during this replay
-        const uint32_t qn = (r + 1) & 1;
-        r8[qn] = Row8{};
-        if (ROW8) load_row(hu[r + 1], r8[qn]);
-        hd[qn] = deg[hu[r + 1]];
-      }
       if (!hlen[r]) continue;
-      if (STAGED == 2) {
+      const uint32_t q = STAGED == 1 ? r : 0;
+      if (STAGED != 1) {
         r8[q] = Row8{};
         if (ROW8) load_row(hu[r], r8[q]);
         hd[q] = deg[hu[r]];
@@ -1314,10 +1308,8 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
         }
         const uint64_t per = (uint64_t)kProcBlock * kProcIPT;
         const dim3 pgrid((uint32_t)((mproc + per - 1) / per));
-        auto* pk = row8 ? (staged == 3 ? k_process<true, 3> : staged == 2 ? k_process<true, 2>
-                           : staged ? k_process<true, 1> : k_process<true, 0>)
-                        : (staged == 3 ? k_process<false, 3> : staged == 2 ? k_process<false, 2>
-                           : staged ? k_process<false, 1> : k_process<false, 0>);
+        auto* pk = row8 ? (staged == 2 ? k_process<true, 2> : staged ? k_process<true, 1> : k_process<true, 0>)
+                        : (staged == 2 ? k_process<false, 2> : staged ? k_process<false, 1> : k_process<false, 0>);
         hipLaunchKernelGGL(pk, pgrid, dim3(kProcBlock), 0, stream, p, t0, keys, mproc, d_deg, d_ids,
                            (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_nemit, d_counts, d_tc);
         OVCHK(hipGetLastError());
