@@ -24,9 +24,12 @@ out receipts at crashed nodes and is reported as config.messages_per_step.
 
 Extensions in the same line: config C3 (10,000 trials of N = 1e5, batched
 contexts, split over the ranks), config C4 (N = 1e8, fanout 18, fanin 19,
-one broadcast node-range sharded over the ranks: RCCL all-gather of each
-window's firing lists inside libgossip_hip.so; one shard at --gpus 1), and
-config C5's push-pull and failure-mask runs.
+one broadcast node-range sharded over the ranks: each rank expands its own
+fires and an all-to-all per window inside libgossip_hip.so moves every message
+to its target's owner; one shard at --gpus 1), and config C5's push-pull and
+failure-mask runs.  `--transport gloo` runs the world > 1 legs with the
+exchange over a gloo group instead of RCCL, so two ranks can rehearse them on
+one GPU (tests/test_bench_ranks.py).
 
 Roofline: HBM-bound; 12 algorithmic bytes per delivered send (4-B friend id +
 4-B read and 4-B write of the target's state word), divided by
@@ -77,6 +80,10 @@ def parse():
     ap.add_argument("--pp-shards", type=int, default=8, help="in-process push-pull shards at --gpus 1")
     ap.add_argument("--ext-deadline", type=float, default=300.0,
                     help="seconds the extension legs may take before the line is printed without the rest")
+    ap.add_argument("--transport", choices=("rccl", "gloo"), default="rccl",
+                    help="world > 1: the ranks' exchange -- RCCL inside the library (one GPU per rank), or "
+                         "host callbacks over a gloo group (gs_create_rank_exchange; ranks may share a GPU)")
+    ap.add_argument("--c4-n", type=int, default=100_000_000, help="nodes of the C4 leg")
     return ap.parse_args()
 
 
@@ -84,20 +91,60 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+_DIST = ["cuda"]  # device of the bench's own host-side reductions: "cuda" (RCCL) or "cpu" (gloo)
+
+
+def allreduce(dist, vals, op):
+    """Element-wise sum or max of a few floats over the ranks (on the GPU for
+    RCCL, on the host for gloo)."""
+    import torch
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=_DIST[0])
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+    return [float(x) for x in t.cpu()]
+
+
+def open_rank_shard(a, gd, cfg, rank, world):
+    """This rank's shard of one node-range-sharded broadcast: RCCL inside the
+    library (gs_create_rank), or the gloo host exchange (--transport gloo)."""
+    if a.transport == "gloo":
+        return gd.open_shard_exchange(cfg, rank, world)
+    return gd.open_shard(cfg, rank, world)
+
+
 DEADLINE_EXIT = 3  # exit status after the extension deadline fired
 _LEG = ["headline"]  # the leg running now (for the deadline watchdog)
+
+
+def devmem_delta(before):
+    """The library's device-memory figures since `before` (gs_memory_stats):
+    time inside hipMalloc / hipFree, the longest single hipMalloc so far, and
+    the buffers served from its cache of large blocks."""
+    import gossip_simulator_amd as gs
+    now = gs.memory_stats()
+    return {"alloc_ms": round(now["alloc_ms"] - before["alloc_ms"], 3),
+            "free_ms": round(now["free_ms"] - before["free_ms"], 3),
+            "largest_alloc_ms_so_far": round(now["largest_alloc_ms"], 3),
+            "hip_mallocs": int(now["alloc_calls"] - before["alloc_calls"]),
+            "cache_hits": int(now["alloc_cache_hits"] - before["alloc_cache_hits"]),
+            "cached_gb_after": round(now["cached_bytes"] / 1e9, 3)}
 
 
 def guarded(name, fn):
     """An extension leg that raises is recorded as {"error": ...} so the
     headline line still prints (every rank runs the same legs, so a
-    parameter error raises on all of them alike)."""
+    parameter error raises on all of them alike).  A leg's result carries
+    its device-memory figures (devmem_delta)."""
+    import gossip_simulator_amd as gs
     _LEG[0] = name
+    before = gs.memory_stats()
     try:
-        return fn()
+        out = fn()
     except Exception as e:  # noqa: BLE001 -- reported in the line, not hidden
         log(f"{name} failed: {type(e).__name__}: {e}")
         return {"error": f"{type(e).__name__}: {e}"}
+    if isinstance(out, dict):
+        out["devmem"] = devmem_delta(before)
+    return out
 
 
 class Emitter:
@@ -159,14 +206,23 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.transport == "gloo":
+            # ranks may share a GPU (a one-GPU rehearsal of the multi-rank legs)
+            local = local % max(torch.cuda.device_count(), 1)
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+            _DIST[0] = "cpu"
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            _DIST[0] = "cuda"
 
     import gossip_simulator_amd as gs
 
     cfg = gs.Config(n=a.n, fanout=a.fanout, fanin=a.fanin, delaylow=a.delaylow,
                     delayhigh=a.delayhigh, droprate=a.droprate, crashrate=a.crashrate,
                     seed=a.seed, trial=rank, device=local)
+    mem0 = gs.memory_stats()
     sim = gs.Simulator(cfg)
     t0 = time.perf_counter()
     wins, stab = sim.build_overlay()
@@ -205,12 +261,8 @@ def main():
     elapsed = time.perf_counter() - t1
     msgs = tot["messages"]
     if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        st = torch.tensor([sent], dtype=torch.float64, device="cuda")
-        dist.all_reduce(st, op=dist.ReduceOp.SUM)
-        sent_all = int(st.item())
+        elapsed = allreduce(dist, [elapsed], "max")[0]
+        sent_all = int(allreduce(dist, [sent], "sum")[0])
     else:
         sent_all = sent
     value = sent_all / elapsed
@@ -273,8 +325,10 @@ def main():
                    "coverage": round(recv_last / a.n, 6),
                    "delivered_per_step": sent // a.steps,
                    "messages_per_step": msgs, "overlay_s": round(overlay_s, 3), "overlay_ticks": ov_ticks,
-                   "overlay_stabilised_ms": stab, "parallelism": f"trials{world}"},
+                   "overlay_stabilised_ms": stab, "parallelism": f"trials{world}",
+                   "transport": a.transport if world > 1 else None},
         "roofline": roof,
+        "devmem": {"headline": devmem_delta(mem0)},
         "cpu_baseline": None,
         "extensions": ext,
     }
@@ -283,10 +337,11 @@ def main():
         ext["flood_failed_1pct"] = guarded("flood_failed_1pct", lambda: flood_failed(a, sim))
     sim.close()
     if not a.no_extensions:
-        # C3 and C4 before push-pull: on some boxes of the pool, allocations
-        # after ~100+ GB of device memory were freed (the push-pull leg's
-        # reverse-table temporaries) ran seconds slow and C3 measured 5-7 s
-        # instead of 1.4 s (profiles/r05e_c3_after.txt)
+        # round 5 put C3 and C4 before push-pull when allocations after ~100 GB
+        # of frees ran seconds slow; the library's cache
+        # of large device blocks (gs_devmem.cpp) now keeps freed blocks mapped
+        # for the next context, and every leg reports its hipMalloc time
+        # (`devmem`)
         if not a.no_c3:
             ext["c3_trials"] = guarded("c3_trials", lambda: c3_trials(a, gs, rank, world, local, dist))
         if not a.no_c4:
@@ -302,6 +357,7 @@ def main():
             ext["c4_shards_inproc"] = guarded("c4_shards_inproc", lambda: shards_inproc(a, gs))
         out.line["strong_scaling"] = strong_scaling_block(world, out.line, ext)
     out.disarm()
+    out.line["devmem"]["process"] = devmem_delta({k: 0 for k in gs.memory_stats()})
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_n > 0:
@@ -457,15 +513,18 @@ def c3_trials(a, gs, rank, world, local, dist):
 
     # one context per batch size, renumbered batch after batch (gs_set_trial)
     sims = {}
+    create_s = warm_s = 0.0
     for b in range(t0, t1, a.c3_batch):  # warmup: contexts, workspaces, code objects
         T = min(b + a.c3_batch, t1) - b
         if T not in sims:
             tw = time.perf_counter()
             sims[T] = gs.Simulator(replace(cfg, trial=b, trials=T))
+            create_s += time.perf_counter() - tw
             sims[T].build_overlay()
             sims[T].broadcast_begin(-1)
             sims[T].run(poll=10)
             torch.cuda.synchronize()
+            warm_s += time.perf_counter() - tw
             log(f"C3 warmup: context of {T} trials created and run once in {time.perf_counter() - tw:.2f} s")
     if dist is not None:
         dist.barrier()
@@ -493,14 +552,13 @@ def c3_trials(a, gs, rank, world, local, dist):
         for s_ in sims.values():
             s_.close()
     res = np.concatenate(rows) if rows else np.zeros((0, 9), np.int64)
-    tot = torch.tensor([float(dt), float(res[:, 4].sum()), float(res[:, 5].sum()), float(len(res)),
-                        float((res[:, 8] == 0).sum())], dtype=torch.float64, device="cuda")
+    tot = [float(dt), float(res[:, 4].sum()), float(res[:, 5].sum()), float(len(res)),
+           float((res[:, 8] == 0).sum())]
     if dist is not None:
-        mx = tot[:1].clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        tot[0] = mx[0]
-    dt, sent, msgs, ntr, ncov = [float(x) for x in tot.cpu()]
+        mx = allreduce(dist, [dt, create_s, warm_s], "max")
+        tot = allreduce(dist, tot, "sum")
+        tot[0], create_s, warm_s = mx
+    dt, sent, msgs, ntr, ncov = tot
     cov = res[res[:, 8] == 0]
     log(f"C3: {int(ntr)} trials in {dt:.2f} s ({int(ncov)} covered)")
     return {"trials": int(ntr), "n": 100_000, "batch": a.c3_batch, "s_total": round(dt, 3),
@@ -508,7 +566,14 @@ def c3_trials(a, gs, rank, world, local, dist):
             "messages_per_s": round(msgs / dt, 1), "covered": int(ncov),
             "median_tick_99_rank0": int(np.median(cov[:, 1])) if len(cov) else None,
             "mean_messages_per_trial": round(msgs / max(ntr, 1), 1),
-            "note": "measured: every trial's overlay + broadcast to its stopping poll, whole job"}
+            # setup outside s_total: gs_create of the batch contexts (create_s) and their
+            # first overlay + broadcast (warmup_s includes create_s); s_end_to_end = the
+            # contexts' creation + every batch, round 4's end-to-end timer
+            "create_s": round(create_s, 3), "warmup_s": round(warm_s, 3),
+            "s_end_to_end": round(dt + create_s, 3),
+            "note": "s_total: every batch's renumbering (gs_set_trial), overlay, broadcast to its stopping poll "
+                    "and results on contexts created and run once before the timer; s_end_to_end adds "
+                    "the contexts' creation (create_s)"}
 
 
 def flood_sharded(a, gs, rank, world, local, dist, n, fanout, fanin, crashrate, name):
@@ -521,7 +586,7 @@ def flood_sharded(a, gs, rank, world, local, dist, n, fanout, fanin, crashrate, 
     from gossip_simulator_amd import dist as gd
     cfg = gs.Config(n=n, fanout=fanout, fanin=fanin, delaylow=a.delaylow, delayhigh=a.delayhigh,
                     droprate=a.droprate, crashrate=crashrate, seed=a.seed, device=local)
-    sim = gd.open_shard(cfg, rank, world) if world > 1 else gs.Simulator(cfg, devices=[local])
+    sim = open_rank_shard(a, gd, cfg, rank, world) if world > 1 else gs.Simulator(cfg, devices=[local])
     try:
         t0 = time.perf_counter()
         sim.build_overlay()
@@ -543,9 +608,7 @@ def flood_sharded(a, gs, rank, world, local, dist, n, fanout, fanin, crashrate, 
         dt = time.perf_counter() - t1
         tot = sim.totals()  # global counters on every rank
         if dist is not None:
-            t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
+            dt = allreduce(dist, [dt], "max")[0]
         sim.set_flags(True)
         sim.reset()
         sim.broadcast_begin(-1)
@@ -556,10 +619,9 @@ def flood_sharded(a, gs, rank, world, local, dist, n, fanout, fanin, crashrate, 
         launches = max(int(tm["resolve_launches"]), 1)
         per_rank = [round(kern, 3)]
         if dist is not None:
-            kt = torch.zeros(world, dtype=torch.float64, device="cuda")
+            kt = [0.0] * world
             kt[rank] = kern
-            dist.all_reduce(kt, op=dist.ReduceOp.SUM)
-            per_rank = [round(float(x), 3) for x in kt.cpu()]
+            per_rank = [round(x, 3) for x in allreduce(dist, kt, "sum")]
         shard_sent = tot["sent"] / world  # a shard's share of the deliveries (balanced ranges)
         ach = BYTES_PER_SEND * shard_sent / (kern * 1e-3) / 1e9 if kern > 0 else 0.0
         log(f"{name} sharded x{world}: {dt * 1e3 / steps:.1f} ms per broadcast, {tot['sent'] / (dt / steps):.3e} msgs/s")
@@ -589,7 +651,7 @@ def c4_sharded(a, gs, rank, world, local, dist):
     """Config C4: N = 1e8, fanout 18 (floor(ln 1e8)), fanin 19, reference
     defaults otherwise (crashrate 0.001 -> threshold 0), sharded over the
     ranks (flood_sharded)."""
-    return flood_sharded(a, gs, rank, world, local, dist, 100_000_000, 18, 19, 0.001, "C4")
+    return flood_sharded(a, gs, rank, world, local, dist, a.c4_n, 18, 19, 0.001, "C4")
 
 
 def c5_flood_sharded(a, gs, rank, world, local, dist):
@@ -610,7 +672,7 @@ def pushpull_sharded(a, gs, rank, world, local, dist):
     cfg = gs.Config(n=a.n, fanout=a.fanout, fanin=a.fanin, delaylow=a.delaylow, delayhigh=a.delayhigh,
                     droprate=a.droprate, crashrate=0.0, seed=a.seed, device=local, model="pushpull")
     G = world if world > 1 else a.pp_shards
-    sim = gd.open_shard(cfg, rank, world) if world > 1 else gs.Simulator(cfg, devices=[local] * G)
+    sim = open_rank_shard(a, gd, cfg, rank, world) if world > 1 else gs.Simulator(cfg, devices=[local] * G)
     out = {}
     try:
         t0 = time.perf_counter()
@@ -635,9 +697,7 @@ def pushpull_sharded(a, gs, rank, world, local, dist):
                     runs.append(dt)
             dt = sum(runs) / len(runs)
             if dist is not None:
-                t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                dt = float(t.item())
+                dt = allreduce(dist, [dt], "max")[0]
             tot = sim.totals()  # global counters on every rank
             log(f"push-pull sharded x{G}{tag}: {dt * 1e3:.1f} ms, rounds={tot['tick']} {STATUS[status]}")
             out["value" if not tag else "failed_1pct"] = (

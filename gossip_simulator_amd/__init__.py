@@ -8,6 +8,7 @@ Layers:
   csrc/gs_pushpull.hip      push-pull rounds (extension, config C5)
   csrc/gs_overlay.hip       overlay construction (makeup/breakup) on the GPU
   csrc/gs_api.cpp           C ABI implementation (device state, stream, polling)
+  csrc/gs_devmem.cpp        process-wide cache of large device blocks (gs_trim)
   csrc/gossip_sim.cpp       CLI with the reference's flags and stdout
   engine.py                 Python host API (ctypes)
   peers.py                  injected peer-table file format
@@ -15,7 +16,7 @@ Layers:
 """
 from ._lib import (GS_RUN_COVERED, GS_RUN_MAX_TICKS, GS_RUN_QUIESCENT,  # noqa: F401
                    GossipError, load)
-from .engine import Config, Simulator, covered  # noqa: F401
+from .engine import Config, Simulator, covered, memory_stats, trim  # noqa: F401
 
-__all__ = ["Config", "Simulator", "GossipError", "covered", "load", "GS_RUN_COVERED",
+__all__ = ["Config", "Simulator", "GossipError", "covered", "load", "trim", "memory_stats", "GS_RUN_COVERED",
            "GS_RUN_QUIESCENT", "GS_RUN_MAX_TICKS"]

@@ -36,7 +36,7 @@ EXPORTS = (
     "gs_format_float64", "gs_format_duration", "gs_threshold", "gs_philox",
     "gs_set_flags", "gs_reset", "gs_set_stream", "gs_create_multi", "gs_comm_unique_id",
     "gs_create_rank", "gs_shard_info", "gs_trial_results", "gs_set_trial",
-    "gs_create_rank_exchange", "gs_shard_timing",
+    "gs_create_rank_exchange", "gs_shard_timing", "gs_trim", "gs_memory_stats",
 )
 
 
@@ -89,7 +89,9 @@ class Timing(C.Structure):
                 ("prep_ms", C.c_double),
                 ("pp_early_rounds", C.c_uint64), ("pp_bottom_rounds", C.c_uint64),
                 ("pp_answer_rounds", C.c_uint64), ("dd_fallbacks", C.c_uint64), ("pp_rev_part", C.c_uint64),
-                ("ov_part_ticks", C.c_uint64), ("ov_sort_ticks", C.c_uint64), ("ov_part_fallbacks", C.c_uint64)]
+                ("ov_part_ticks", C.c_uint64), ("ov_sort_ticks", C.c_uint64), ("ov_part_fallbacks", C.c_uint64),
+                ("alloc_ms", C.c_double), ("largest_alloc_ms", C.c_double), ("free_ms", C.c_double),
+                ("alloc_calls", C.c_uint64), ("alloc_cache_hits", C.c_uint64), ("cached_bytes", C.c_uint64)]
 
 
 # gs_exchange (gossip.h): host callbacks of a gs_create_rank_exchange rank
@@ -153,6 +155,8 @@ def load():
         "gs_shard_info": ([ctx, C.c_uint32, P(C.c_uint32), P(C.c_uint64), P(C.c_uint64)], C.c_int),
         "gs_trial_results": ([ctx, P(TrialStats), sz, P(sz)], C.c_int),
         "gs_set_trial": ([ctx, C.c_uint32], C.c_int),
+        "gs_trim": ([C.c_int, P(sz)], C.c_int),
+        "gs_memory_stats": ([P(Timing)], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -185,13 +185,25 @@ int fail(gs_ctx* c, int code, const std::string& msg) {
   return code;
 }
 
+// gs_timing's device-memory fields: the library's process-wide figures
+void fill_devmem(gs_timing* out) {
+  DevMemStats d;
+  gs_devmem_stats(&d);
+  out->alloc_ms = d.alloc_ms;
+  out->largest_alloc_ms = d.largest_alloc_ms;
+  out->free_ms = d.free_ms;
+  out->alloc_calls = d.hip_allocs;
+  out->alloc_cache_hits = d.cache_hits;
+  out->cached_bytes = d.cached_bytes;
+}
+
 bool grow(Buf& b, size_t bytes) {
   if (b.bytes >= bytes) return true;
   const size_t nb = std::max(bytes, b.bytes + b.bytes / 4);
-  if (b.p) (void)hipFree(b.p);
+  if (b.p) (void)dev_free(b.p);
   b.p = nullptr;
   b.bytes = 0;
-  if (hipMalloc(&b.p, nb) != hipSuccess) return false;
+  if (dev_malloc(&b.p, nb) != hipSuccess) return false;
   b.bytes = nb;
   return true;
 }
@@ -251,7 +263,7 @@ int alloc_window(gs_ctx* c) {
     w.obins = 256 / c->G;
     w.oseg_q = (uint32_t)(c->seg_per >> kFineLog);
     w.oseg_magic = 0xFFFFFFFFu / w.oseg_q;
-    if (hipMalloc(&c->d_rtab, kRtabWords * 8) != hipSuccess ||
+    if (dev_malloc(&c->d_rtab, kRtabWords * 8) != hipSuccess ||
         hipHostMalloc((void**)&c->h_rtab, kRtabWords * 8) != hipSuccess)
       return fail(c, GS_ENOMEM, "cannot allocate the shard's receive layout");
   }
@@ -265,10 +277,10 @@ int alloc_window(gs_ctx* c) {
                b_rlcnt = al((size_t)w.nfine * 4),
                b_tsum = al((size_t)w.ncoarse * kMaxWindow * 8) + al(((size_t)w.ncoarse + 1) * 8);
   const size_t total = b_fc + 2 * b_units + b_small + b_fhist + b_fbase + b_ffill + b_sst + b_rlcnt + b_tsum;
-  if (hipMalloc(&c->d_win, total) != hipSuccess)
+  if (dev_malloc(&c->d_win, total) != hipSuccess)
     return fail(c, GS_ENOMEM, "cannot allocate window-engine buffers");
   const size_t flist = (size_t)w.R * w.nfine * kFineNodes * 2;
-  if (hipMalloc(&c->d_flist, flist) != hipSuccess)
+  if (dev_malloc(&c->d_flist, flist) != hipSuccess)
     return fail(c, GS_ENOMEM, "cannot allocate " + std::to_string(flist >> 20) + " MiB of fire lists");
   char* q = (char*)c->d_win;
   w.fcount = (uint32_t*)q; q += b_fc;
@@ -287,11 +299,11 @@ int alloc_window(gs_ctx* c) {
   w.rlcnt = (uint32_t*)q; q += b_rlcnt;
   w.tsum = (unsigned long long*)q; q += al((size_t)w.ncoarse * kMaxWindow * 8);
   w.toff = (unsigned long long*)q; q += al(((size_t)w.ncoarse + 1) * 8);
-  if (hipMalloc(&c->d_rlmsg, (size_t)w.nfine * kRolledCap * 4) != hipSuccess)
+  if (dev_malloc(&c->d_rlmsg, (size_t)w.nfine * kRolledCap * 4) != hipSuccess)
     return fail(c, GS_ENOMEM, "cannot allocate the rolled-receipt lists");
   w.rlmsg = (uint32_t*)c->d_rlmsg;
   w.dbg = nullptr;
-  if (getenv("GS_STAMPS") && hipMalloc(&w.dbg, kDbgWords * 8) == hipSuccess)
+  if (getenv("GS_STAMPS") && dev_malloc(&w.dbg, kDbgWords * 8) == hipSuccess)
     (void)hipMemset(w.dbg, 0, kDbgWords * 8);
   w.flist = (uint16_t*)c->d_flist;
   c->fcount_bytes = (size_t)w.R * w.nfine * 4;
@@ -304,7 +316,7 @@ int alloc_window(gs_ctx* c) {
     return fail(c, GS_ENOMEM, "cannot allocate pinned window buffers");
   if (c->trials > 1) {
     const size_t tb = (size_t)c->trials * kMaxWindow * kTStatFields * 4;
-    if (hipMalloc((void**)&c->d_tstat, tb) != hipSuccess ||
+    if (dev_malloc((void**)&c->d_tstat, tb) != hipSuccess ||
         hipHostMalloc((void**)&c->h_tstat, tb) != hipSuccess)
       return fail(c, GS_ENOMEM, "cannot allocate per-trial counters");
     w.tstat = c->d_tstat;
@@ -403,12 +415,12 @@ uint64_t table_n(const gs_ctx* c) { return c->shard ? c->p.n : c->ntot; }
 int alloc_table(gs_ctx* c, uint32_t stride) {
   const uint64_t n = table_n(c);
   if (!(c->d_deg && c->d_ids && c->tab_stride == stride)) {  // same shape: reuse (batch after batch)
-    if (c->d_deg) (void)hipFree(c->d_deg);
-    if (c->d_ids) (void)hipFree(c->d_ids);
+    if (c->d_deg) (void)dev_free(c->d_deg);
+    if (c->d_ids) (void)dev_free(c->d_ids);
     c->d_deg = nullptr;
     c->d_ids = nullptr;
     c->tab_stride = 0;
-    if (hipMalloc(&c->d_deg, n) != hipSuccess || hipMalloc(&c->d_ids, n * stride * 4ull) != hipSuccess)
+    if (dev_malloc(&c->d_deg, n) != hipSuccess || dev_malloc(&c->d_ids, n * stride * 4ull) != hipSuccess)
       return fail(c, GS_ENOMEM, "cannot allocate the peer table on the device");
     c->tab_stride = stride;
   }
@@ -466,10 +478,10 @@ int expand_view(gs_ctx* c) {
   if (c->pk_ver != c->table_ver || !c->d_pk) {
     const uint64_t rows = c->ntot, bytes = (rows + 4) / 5 * 128;
     if (c->pk_bytes < bytes) {
-      if (c->d_pk) (void)hipFree(c->d_pk);
+      if (c->d_pk) (void)dev_free(c->d_pk);
       c->d_pk = nullptr;
       c->pk_bytes = 0;
-      if (hipMalloc(&c->d_pk, bytes) != hipSuccess) {  // no room: expand reads the table itself
+      if (dev_malloc(&c->d_pk, bytes) != hipSuccess) {  // no room: expand reads the table itself
         (void)hipGetLastError();
         c->d_pk = nullptr;
         c->ws.pk = nullptr;
@@ -489,12 +501,12 @@ int expand_view(gs_ctx* c) {
 // only the rows of its own firing nodes.
 int own_rows(gs_ctx* c, const uint8_t* deg, const uint32_t* ids, uint32_t S, uint32_t row_slots, hipStream_t st) {
   const uint64_t n = c->ntot;
-  if (c->d_deg) (void)hipFree(c->d_deg);
-  if (c->d_ids) (void)hipFree(c->d_ids);
+  if (c->d_deg) (void)dev_free(c->d_deg);
+  if (c->d_ids) (void)dev_free(c->d_ids);
   c->d_deg = nullptr;
   c->d_ids = nullptr;
   c->tab_stride = 0;  // not the full-table shape: the next load reallocates
-  if (hipMalloc(&c->d_deg, n) != hipSuccess || hipMalloc(&c->d_ids, n * S * 4ull) != hipSuccess)
+  if (dev_malloc(&c->d_deg, n) != hipSuccess || dev_malloc(&c->d_ids, n * S * 4ull) != hipSuccess)
     return fail(c, GS_ENOMEM, "cannot allocate the shard's rows");
   RC(set_stride(c, S));
   c->row_slots = row_slots;
@@ -619,7 +631,7 @@ int ctx_setup(gs_ctx* c, const gs_params* params, int device, bool shard, uint32
   const size_t b_roll = c->win ? b_bits : 0;
   const size_t total = 2 * b_bits + b_roll + b_next + b_ring + b_cflag + b_clist + b_ccount + b_stats + 256;
   c->state_bytes = total;
-  if (hipMalloc(&c->d_state, total) != hipSuccess) {
+  if (dev_malloc(&c->d_state, total) != hipSuccess) {
     why = "cannot allocate " + std::to_string(total) + " bytes of device state";
     return GS_ENOMEM;
   }
@@ -641,7 +653,7 @@ int ctx_setup(gs_ctx* c, const gs_params* params, int device, bool shard, uint32
   s.grecv = s.recv;  // a push-pull shard points these at the replicated sets (attach_pp_sets)
   s.gcrash = s.crash;
   s.gbase = 0;
-  if (tick && s.kc > 0 && hipMalloc(&c->d_cnt, s.n * 4) != hipSuccess) {
+  if (tick && s.kc > 0 && dev_malloc(&c->d_cnt, s.n * 4) != hipSuccess) {
     why = "cannot allocate arrival counters";
     return GS_ENOMEM;
   }
@@ -670,19 +682,19 @@ void destroy_one(gs_ctx* c) {
     for (size_t i = 0; i < c->gdevs.size() && i < c->gbuf.size(); ++i)
       if (c->gbuf[i].p) {
         (void)hipSetDevice(c->gdevs[i]);
-        (void)hipFree(c->gbuf[i].p);
+        (void)dev_free(c->gbuf[i].p);
       }
     for (size_t i = 0; i < c->gdevs.size(); ++i) {
       (void)hipSetDevice(c->gdevs[i]);
-      if (i < c->gig.size() && c->gig[i]) (void)hipFree(c->gig[i]);
-      if (i < c->gfg.size() && c->gfg[i]) (void)hipFree(c->gfg[i]);
-      if (i < c->ggn.size() && c->ggn[i]) (void)hipFree(c->ggn[i]);
+      if (i < c->gig.size() && c->gig[i]) (void)dev_free(c->gig[i]);
+      if (i < c->gfg.size() && c->gfg[i]) (void)dev_free(c->gfg[i]);
+      if (i < c->ggn.size() && c->ggn[i]) (void)dev_free(c->ggn[i]);
     }
     for (hipEvent_t e : c->gev_c) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->gev_x) (void)hipEventDestroy(e);
     for (gs_ctx* r : c->greps) destroy_one(r);
     if (!c->gdevs.empty()) (void)hipSetDevice(c->gdevs[0]);
-    if (c->dd_mem) (void)hipFree(c->dd_mem);
+    if (c->dd_mem) (void)dev_free(c->dd_mem);
     for (void* ptr : {(void*)c->h_stage, (void*)c->h_ddlay, (void*)c->h_ddptrs})
       if (ptr) (void)hipHostFree(ptr);
     for (hipEvent_t e : c->wev) (void)hipEventDestroy(e);
@@ -710,30 +722,30 @@ void destroy_one(gs_ctx* c) {
         for (uint32_t i = 1; i < kStampPhases; ++i) fprintf(stderr, " %.2f", d[i] * 1e-3 / d[0]);
         fprintf(stderr, "\n");
       }
-    (void)hipFree(c->ws.dbg);
+    (void)dev_free(c->ws.dbg);
   }
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   overlay_free(&c->ovw, c->stream);
   if (c->own_ig) {
-    if (c->d_ig) (void)hipFree(c->d_ig);
-    if (c->d_fg) (void)hipFree(c->d_fg);
-    if (c->d_gn) (void)hipFree(c->d_gn);
-    if (c->d_gst) (void)hipFree(c->d_gst);
+    if (c->d_ig) (void)dev_free(c->d_ig);
+    if (c->d_fg) (void)dev_free(c->d_fg);
+    if (c->d_gn) (void)dev_free(c->d_gn);
+    if (c->d_gst) (void)dev_free(c->d_gst);
   }
   if (c->h_xbuf) (void)hipHostFree(c->h_xbuf);
-  if (c->d_pk) (void)hipFree(c->d_pk);
+  if (c->d_pk) (void)dev_free(c->d_pk);
   for (void* ptr : {(void*)c->d_deg, (void*)c->d_ids, c->d_state, (void*)c->d_cnt, (void*)c->d_failed, c->d_win,
                     c->d_flist, c->d_rlmsg, (void*)c->d_tstat, (void*)c->d_rtab, (void*)c->d_gcounts,
                     (void*)c->d_glay})
-    if (ptr) (void)hipFree(ptr);
+    if (ptr) (void)dev_free(ptr);
   for (Buf* b : {&c->gmap, &c->cmsg, &c->fmsg, &c->tmp, &c->xsend, &c->xrecv, &c->pp_rend, &c->pp_rsrc,
                  &c->pp_rslot, &c->pp_ilist, &c->pp_fmask, &c->pp_scan, &c->pp_ctlb, &c->pp_dset, &c->pp_dcnt, &c->pp_rfail})
-    if (b->p) (void)hipFree(b->p);
+    if (b->p) (void)dev_free(b->p);
   for (void* ptr : {(void*)c->h_cap, (void*)c->h_misc, (void*)c->h_err, (void*)c->h_stats, (void*)c->h_tstat,
                     (void*)c->h_stage, (void*)c->h_rtab, (void*)c->h_glay})
     if (ptr) (void)hipHostFree(ptr);
-  if (c->d_ctl) (void)hipFree(c->d_ctl);  // (d_stage maps h_stage)
-  if (c->dd_mem) (void)hipFree(c->dd_mem);
+  if (c->d_ctl) (void)dev_free(c->d_ctl);  // (d_stage maps h_stage)
+  if (c->dd_mem) (void)dev_free(c->dd_mem);
   for (void* ptr : {(void*)c->h_ddlay, (void*)c->h_ddptrs})
     if (ptr) (void)hipHostFree(ptr);
   for (hipEvent_t e : c->wev) (void)hipEventDestroy(e);
@@ -864,8 +876,8 @@ int make_replica(const gs_params* params, int dev, unsigned long long* ig, unsig
 // (flood) or its own replicated sets (push-pull).
 int finish_rank(gs_ctx* c, gs_ctx** out) {
   (void)hipSetDevice(c->dev);
-  if (hipMalloc(&c->d_gcounts, (size_t)c->G * kMaxWindow * 8 + (size_t)kMaxWindow * 8) != hipSuccess ||
-      (!c->pp_shard && (hipMalloc(&c->d_glay, (size_t)c->G * (kRegions + 1) * 8) != hipSuccess ||
+  if (dev_malloc(&c->d_gcounts, (size_t)c->G * kMaxWindow * 8 + (size_t)kMaxWindow * 8) != hipSuccess ||
+      (!c->pp_shard && (dev_malloc(&c->d_glay, (size_t)c->G * (kRegions + 1) * 8) != hipSuccess ||
                         hipHostMalloc((void**)&c->h_glay, (size_t)c->G * (kRegions + 1) * 8) != hipSuccess))) {
     destroy_one(c);
     return GS_ENOMEM;
@@ -876,7 +888,7 @@ int finish_rank(gs_ctx* c, gs_ctx** out) {
         alloc_pp_sets(c, (uint64_t)c->G * c->segw, &gst, nullptr, nullptr)) {
       fprintf(stderr, "gs_create_rank: %s\n", c->err.c_str());
       for (unsigned long long* q : {ig, fg, gn, gst})
-        if (q) (void)hipFree(q);
+        if (q) (void)dev_free(q);
       destroy_one(c);
       return GS_ENOMEM;
     }
@@ -900,7 +912,7 @@ int alloc_pp_sets(gs_ctx* c, uint64_t words, unsigned long long** ig, unsigned l
   for (unsigned long long** q : {ig, fg, gn}) {
     if (!q) continue;
     *q = nullptr;
-    if (hipMalloc(q, words * 8) != hipSuccess)
+    if (dev_malloc(q, words * 8) != hipSuccess)
       return fail(c, GS_ENOMEM, "cannot allocate the replicated informed / failed sets");
     CK(c, hipMemsetAsync(*q, 0, words * 8, c->stream));
   }
@@ -1189,11 +1201,11 @@ int partition_pp(gs_ctx* leader, const std::vector<gs_ctx*>& ms) {
   int rc = GS_OK;
   for (gs_ctx* m : ms) {
     const uint64_t n = m->ntot;
-    if (m->d_deg) (void)hipFree(m->d_deg);
-    if (m->d_ids) (void)hipFree(m->d_ids);
+    if (m->d_deg) (void)dev_free(m->d_deg);
+    if (m->d_ids) (void)dev_free(m->d_ids);
     m->d_deg = nullptr;
     m->d_ids = nullptr;
-    if (hipMalloc(&m->d_deg, n) != hipSuccess || hipMalloc(&m->d_ids, n * S * 4ull) != hipSuccess) {
+    if (dev_malloc(&m->d_deg, n) != hipSuccess || dev_malloc(&m->d_ids, n * S * 4ull) != hipSuccess) {
       rc = fail(m, GS_ENOMEM, "cannot allocate the shard's rows");
       break;
     }
@@ -1241,8 +1253,8 @@ int partition_pp(gs_ctx* leader, const std::vector<gs_ctx*>& ms) {
   }
   gs_ctx* r = ms[0]->rep;
   if (r && rc == GS_OK) {  // the full table stays on the device as the replica's
-    if (r->d_deg) (void)hipFree(r->d_deg);
-    if (r->d_ids) (void)hipFree(r->d_ids);
+    if (r->d_deg) (void)dev_free(r->d_deg);
+    if (r->d_ids) (void)dev_free(r->d_ids);
     r->d_deg = fdeg;
     r->d_ids = fids;
     r->tab_stride = S;
@@ -1253,8 +1265,8 @@ int partition_pp(gs_ctx* leader, const std::vector<gs_ctx*>& ms) {
     r->peers = true;
     return GS_OK;
   }
-  (void)hipFree(fdeg);
-  (void)hipFree(fids);
+  (void)dev_free(fdeg);
+  (void)dev_free(fids);
   return rc;
 }
 
@@ -1272,8 +1284,8 @@ int partition_from(gs_ctx* leader, const std::vector<gs_ctx*>& ms) {
     if ((rc = own_rows(m, fdeg, fids, S, slots, leader->stream))) break;
     m->peers = true;
   }
-  (void)hipFree(fdeg);
-  (void)hipFree(fids);
+  (void)dev_free(fdeg);
+  (void)dev_free(fids);
   return rc;
 }
 
@@ -1513,7 +1525,7 @@ int gs_set_failed(gs_ctx* c, const uint64_t* words, size_t nwords) {
   const uint64_t W = c->st.W, w0 = c->lo / 64;  // this context's words (a shard's own range)
   std::vector<uint64_t> w(words + w0, words + w0 + W);
   if (c->ntot & 63) w[W - 1] &= (1ull << (c->ntot & 63)) - 1;
-  if (!c->d_failed && hipMalloc(&c->d_failed, W * 8) != hipSuccess)
+  if (!c->d_failed && dev_malloc(&c->d_failed, W * 8) != hipSuccess)
     return fail(c, GS_ENOMEM, "cannot allocate the failure mask");
   CK(c, hipMemcpyAsync(c->d_failed, w.data(), W * 8, hipMemcpyHostToDevice, c->stream));
   CK(c, hipMemcpyAsync(c->st.crash, c->d_failed, W * 8, hipMemcpyDeviceToDevice, c->stream));
@@ -2119,6 +2131,19 @@ int gs_set_stream(gs_ctx* c, void* hip_stream) {
   return GS_OK;
 }
 
+int gs_memory_stats(gs_timing* out) {
+  if (!out) return GS_EINVAL;
+  *out = gs_timing{};
+  fill_devmem(out);
+  return GS_OK;
+}
+
+int gs_trim(int device, size_t* released) {
+  const size_t b = gs_devmem_trim(device);
+  if (released) *released = b;
+  return GS_OK;
+}
+
 }  // extern "C"
 
 namespace {
@@ -2283,7 +2308,7 @@ uint64_t cover_threshold(uint64_t n) {  // smallest r with covered(r, n)
 
 int async_setup(gs_ctx* c) {
   if (!c->d_ctl) {
-    CK(c, hipMalloc(&c->d_ctl, sizeof(WinCtl)));
+    CK(c, dev_malloc(&c->d_ctl, sizeof(WinCtl)));
     // k_close writes each window's results straight into pinned host memory
     // (no copy launch per window); d_stage is its device address
     CK(c, hipHostMalloc((void**)&c->h_stage, (size_t)kSlots * kStageWords * 8,
@@ -3039,7 +3064,7 @@ int dd_setup(gs_ctx* acc, const std::vector<gs_ctx*>& ms) {
     const size_t b1 = al((size_t)G * kMaxWindow * 8), b2 = al((size_t)G * kDDRow * 8),
                  b3 = al((size_t)M * kDDWStat * 8), b4 = al((size_t)M * sizeof(WinCtl)),
                  b5 = al((size_t)(4 * M + 2) * sizeof(void*)), b6 = al((size_t)3 * M * sizeof(WinState));
-    CK(acc, hipMalloc(&acc->dd_mem, b1 + b2 + b3 + b4 + b5 + b6));
+    CK(acc, dev_malloc(&acc->dd_mem, b1 + b2 + b3 + b4 + b5 + b6));
     char* q = (char*)acc->dd_mem;
     acc->dd_gcnt = (unsigned long long*)q; q += b1;
     acc->dd_glay = (unsigned long long*)q; q += b2;
@@ -3892,6 +3917,7 @@ int gs_timing_get(gs_ctx* c, gs_timing* out) {
     out->pp_answer_rounds = h.nanswer;
   }
   if (c->pp && c->begun) out->pp_early_rounds += c->rep_rounds;  // shards: the replicas' sparse rounds
+  fill_devmem(out);
   return GS_OK;
 }
 
@@ -3900,6 +3926,7 @@ int gs_shard_timing(gs_ctx* c, uint32_t index, gs_timing* out) {
   if (!c->group) return index == 0 ? gs_timing_get(c, out) : fail(c, GS_EINVAL, "no such shard");
   if (index >= c->mem.size()) return fail(c, GS_EINVAL, "no such shard");
   *out = c->mem[index]->timing;
+  fill_devmem(out);
   return GS_OK;
 }
 

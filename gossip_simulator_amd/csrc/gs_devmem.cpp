@@ -1,0 +1,246 @@
+// gs_devmem.cpp -- process-wide cache of large device blocks (gs_devmem.h).
+//
+// Layout: every block >= kCacheMin comes from a slab (one hipMalloc).  A slab
+// is cut into extents, each used or free; free extents are indexed by size per
+// device for best fit.  An allocation takes the smallest free extent that fits
+// and splits off the rest; a free coalesces with free neighbours of the same
+// slab, so a slab whose extents are all free is one extent again and can be
+// trimmed.  Only when no free extent fits is a new slab mapped; if the device
+// lacks the room beside the cache, the fully free slabs are trimmed first.
+#include "gs_devmem.h"
+
+#include <chrono>
+#include <cstdlib>
+#include <iterator>
+#include <map>
+#include <mutex>
+#include <vector>
+
+namespace {
+
+constexpr size_t kCacheMin = 64ull << 20;  // smaller blocks: plain hipMalloc / hipFree
+constexpr size_t kGran = 2ull << 20;
+
+struct Ext {
+  size_t size;
+  int slab;
+  bool used;
+};
+struct Slab {
+  char* base;
+  size_t size;
+  int device;
+  size_t used;
+};
+
+struct Cache {
+  std::mutex mu;
+  std::map<char*, Ext> ext;                            // every extent, by address
+  std::map<int, std::multimap<size_t, char*>> freeix;  // device -> free extents by size
+  std::vector<Slab> slab;                              // size 0 = returned to the driver
+  DevMemStats st{};
+};
+
+Cache& cache() {
+  static Cache* c = new Cache;  // never destroyed: frees may run at process exit
+  return *c;
+}
+
+bool enabled() {
+  static const bool on = [] {
+    const char* s = getenv("GS_DEVMEM_CACHE");
+    return !(s && atoi(s) == 0);
+  }();
+  return on;
+}
+
+double now_ms() {
+  using namespace std::chrono;
+  return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+hipError_t timed_malloc(Cache& c, void** p, size_t bytes) {
+  const double t0 = now_ms();
+  const hipError_t e = hipMalloc(p, bytes);
+  const double dt = now_ms() - t0;
+  std::lock_guard<std::mutex> g(c.mu);
+  c.st.alloc_ms += dt;
+  if (dt > c.st.largest_alloc_ms) c.st.largest_alloc_ms = dt;
+  ++c.st.hip_allocs;
+  return e;
+}
+
+void unindex(Cache& c, int dev, char* b, size_t size) {
+  auto& fi = c.freeix[dev];
+  auto r = fi.equal_range(size);
+  for (auto it = r.first; it != r.second; ++it)
+    if (it->second == b) {
+      fi.erase(it);
+      return;
+    }
+}
+
+// caller holds c.mu; returns the slabs to hipFree (done outside the lock)
+std::vector<char*> collect_trim(Cache& c, int device) {
+  std::vector<char*> out;
+  for (size_t i = 0; i < c.slab.size(); ++i) {
+    Slab& s = c.slab[i];
+    if (!s.size || s.used || (device >= 0 && s.device != device)) continue;
+    unindex(c, s.device, s.base, s.size);  // a free slab is one extent
+    c.ext.erase(s.base);
+    c.st.cached_bytes -= s.size;
+    c.st.mapped_bytes -= s.size;
+    out.push_back(s.base);
+    s.size = 0;
+  }
+  return out;
+}
+
+void release(Cache& c, const std::vector<char*>& blocks) {
+  for (char* b : blocks) {
+    const double t0 = now_ms();
+    (void)hipFree(b);
+    std::lock_guard<std::mutex> g(c.mu);
+    c.st.free_ms += now_ms() - t0;
+  }
+}
+
+}  // namespace
+
+hipError_t gs_dev_malloc(void** p, size_t bytes) {
+  if (!p) return hipErrorInvalidValue;
+  Cache& c = cache();
+  if (!enabled() || bytes < kCacheMin) return timed_malloc(c, p, bytes);
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const size_t need = (bytes + kGran - 1) & ~(kGran - 1);
+  {
+    std::lock_guard<std::mutex> g(c.mu);
+    auto& fi = c.freeix[dev];
+    auto it = fi.lower_bound(need);
+    if (it != fi.end()) {
+      char* b = it->second;
+      fi.erase(it);
+      Ext& x = c.ext[b];
+      if (x.size - need >= kGran) {  // split: the tail stays free
+        c.ext[b + need] = Ext{x.size - need, x.slab, false};
+        fi.emplace(x.size - need, b + need);
+        x.size = need;
+      }
+      x.used = true;
+      c.slab[x.slab].used += x.size;
+      c.st.cached_bytes -= x.size;
+      ++c.st.cache_hits;
+      *p = b;
+      return hipSuccess;
+    }
+  }
+  // a new slab; make room beside the cache first if the device lacks it
+  size_t freeb = 0, totalb = 0;
+  if (hipMemGetInfo(&freeb, &totalb) == hipSuccess && freeb < need + (kGran << 4)) {
+    std::vector<char*> t;
+    {
+      std::lock_guard<std::mutex> g(c.mu);
+      t = collect_trim(c, dev);
+    }
+    release(c, t);
+  }
+  void* q = nullptr;
+  e = timed_malloc(c, &q, need);
+  if (e != hipSuccess) {  // trim everything of this device and retry once
+    (void)hipGetLastError();
+    std::vector<char*> t;
+    {
+      std::lock_guard<std::mutex> g(c.mu);
+      t = collect_trim(c, dev);
+    }
+    if (t.empty()) return e;
+    release(c, t);
+    e = timed_malloc(c, &q, need);
+    if (e != hipSuccess) return e;
+  }
+  std::lock_guard<std::mutex> g(c.mu);
+  c.slab.push_back(Slab{(char*)q, need, dev, need});
+  c.ext[(char*)q] = Ext{need, (int)c.slab.size() - 1, true};
+  c.st.mapped_bytes += need;
+  *p = q;
+  return hipSuccess;
+}
+
+hipError_t gs_dev_free(void* p) {
+  if (!p) return hipSuccess;
+  Cache& c = cache();
+  int sdev = -1;
+  {
+    std::lock_guard<std::mutex> g(c.mu);
+    auto it = c.ext.find((char*)p);
+    if (it != c.ext.end() && it->second.used) sdev = c.slab[it->second.slab].device;
+  }
+  if (sdev < 0) {  // not a cached block
+    const double t0 = now_ms();
+    const hipError_t e = hipFree(p);
+    std::lock_guard<std::mutex> g(c.mu);
+    c.st.free_ms += now_ms() - t0;
+    return e;
+  }
+  // hipFree's contract: the block is idle before anyone can reuse it
+  const double t0 = now_ms();
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (cur != sdev) (void)hipSetDevice(sdev);
+  const hipError_t se = hipDeviceSynchronize();
+  if (cur != sdev) (void)hipSetDevice(cur);
+  std::lock_guard<std::mutex> g(c.mu);
+  c.st.free_ms += now_ms() - t0;
+  auto it = c.ext.find((char*)p);
+  if (it == c.ext.end() || !it->second.used) return hipErrorInvalidValue;  // freed twice
+  Ext x = it->second;
+  Slab& s = c.slab[x.slab];
+  s.used -= x.size;
+  c.st.cached_bytes += x.size;
+  char* b = (char*)p;
+  auto& fi = c.freeix[s.device];
+  // coalesce with the next extent of the same slab
+  auto nx = std::next(it);
+  if (nx != c.ext.end() && !nx->second.used && nx->second.slab == x.slab && b + x.size == nx->first) {
+    unindex(c, s.device, nx->first, nx->second.size);
+    x.size += nx->second.size;
+    c.ext.erase(nx);
+  }
+  // and with the previous one
+  if (it != c.ext.begin()) {
+    auto pv = std::prev(it);
+    if (!pv->second.used && pv->second.slab == x.slab && pv->first + pv->second.size == b) {
+      unindex(c, s.device, pv->first, pv->second.size);
+      pv->second.size += x.size;
+      c.ext.erase(it);
+      fi.emplace(pv->second.size, pv->first);
+      return se;
+    }
+  }
+  it->second = Ext{x.size, x.slab, false};
+  fi.emplace(x.size, b);
+  return se;
+}
+
+void gs_devmem_stats(DevMemStats* out) {
+  if (!out) return;
+  Cache& c = cache();
+  std::lock_guard<std::mutex> g(c.mu);
+  *out = c.st;
+}
+
+size_t gs_devmem_trim(int device) {
+  Cache& c = cache();
+  std::vector<char*> t;
+  size_t bytes = 0;
+  {
+    std::lock_guard<std::mutex> g(c.mu);
+    const uint64_t before = c.st.mapped_bytes;
+    t = collect_trim(c, device);
+    bytes = (size_t)(before - c.st.mapped_bytes);
+  }
+  release(c, t);
+  return bytes;
+}

@@ -21,6 +21,7 @@
 
 #include <vector>
 
+#include "gs_devmem.h"
 #include "gs_rng.h"
 
 namespace gs {

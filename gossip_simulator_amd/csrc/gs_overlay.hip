@@ -845,7 +845,7 @@ using DevBuf = OverlayWork::Buf;
 // (The stream-ordered pool allocator instead corrupted the N = 1e9 build:
 // profiles/r04s_overlay_pool.txt.)
 static void free_buf(DevBuf& b) {
-  if (b.raw) (void)hipFree(b.raw);
+  if (b.raw) (void)dev_free(b.raw);
   b.p = b.raw = nullptr;
   b.bytes = 0;
 }
@@ -854,7 +854,7 @@ static hipError_t grow(DevBuf& b, size_t bytes, hipStream_t st) {
   if (b.bytes >= bytes) return hipSuccess;
   const size_t nb = std::max(bytes + bytes / 4, b.bytes * 3 / 2);
   free_buf(b);
-  hipError_t e = hipMalloc(&b.raw, nb + b.off);
+  hipError_t e = dev_malloc(&b.raw, nb + b.off);
   if (e == hipSuccess) {
     b.p = (char*)b.raw + b.off;
     b.bytes = nb;

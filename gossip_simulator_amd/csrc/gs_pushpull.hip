@@ -1536,7 +1536,7 @@ hipError_t pp_rev_build_part(const DevState& s, unsigned long long* rend, uint32
   // small device arrays: chist[512] | cstart[513] | cend[512] | fstart[nbf+1] | ffill[nbf] | bbase[nbf] | tpre[513] | ovf
   const size_t small = 8 * (512 + 513 + 512 + (nbf + 1) + nbf + nbf) + 4 * 513 + 64;
   char* sm = nullptr;
-  hipError_t e = hipMalloc(&sm, small);
+  hipError_t e = dev_malloc(&sm, small);
   if (e != hipSuccess) return e;
   unsigned long long* d_chist = (unsigned long long*)sm;
   unsigned long long* d_cstart = d_chist + 512;
@@ -1554,9 +1554,9 @@ hipError_t pp_rev_build_part(const DevState& s, unsigned long long* rend, uint32
   const uint32_t grid = 512;
   auto done = [&](hipError_t r) {
     (void)hipStreamSynchronize(st);
-    if (rec) (void)hipFree(rec);
-    if (frec) (void)hipFree(frec);
-    (void)hipFree(sm);
+    if (rec) (void)dev_free(rec);
+    if (frec) (void)dev_free(frec);
+    (void)dev_free(sm);
     return r;
   };
 #define RV(x)                          \
@@ -1589,8 +1589,8 @@ hipError_t pp_rev_build_part(const DevState& s, unsigned long long* rend, uint32
   RV(hipMemcpyAsync(d_cend, ce.data(), 512 * 8, hipMemcpyHostToDevice, st));
   RV(hipMemcpyAsync(d_fstart, fs.data(), (nbf + 1) * 8, hipMemcpyHostToDevice, st));
   RV(hipMemcpyAsync(d_tpre, tp.data(), 513 * 4, hipMemcpyHostToDevice, st));
-  RV(hipMalloc(&rec, std::max<unsigned long long>(E, 1) * 8));
-  RV(hipMalloc(&frec, std::max<unsigned long long>(F, 1) * 8));
+  RV(dev_malloc(&rec, std::max<unsigned long long>(E, 1) * 8));
+  RV(dev_malloc(&frec, std::max<unsigned long long>(F, 1) * 8));
   {
     unsigned long long* d_cfill = d_chist;  // reused: the fills of the coarse pass
     RV(hipMemsetAsync(d_cfill, 0, 512 * 8, st));

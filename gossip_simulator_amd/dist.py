@@ -11,12 +11,23 @@ only concurrency is goroutines in one process (simulator.go:214-217):
   nothing is exchanged until the per-trial rows are summed at the end.
 
 * ``open_shard`` -- one huge-N broadcast with the node range split over ranks
-  (config C4).  Rank 0 makes an RCCL unique id, torch.distributed ships it to
-  every rank, and each rank opens its shard with gs_create_rank: from then on
-  every gs_step all-gathers the window's firing lists and sums the per-tick
-  counters with RCCL inside the library, so gs_run on every rank returns the
+  (configs C4 and C5).  Rank 0 makes an RCCL unique id, torch.distributed
+  ships it to every rank, and each rank opens its shard with gs_create_rank.
+  From then on the library runs the data path's exchange itself over RCCL:
+  the flood expands each rank's own fires and sends every message to its
+  target's owner (grouped ncclSend/ncclRecv, one all-to-all per window, with
+  the window cut agreed from an all-gather of the per-rank fire counts);
+  push-pull all-gathers the informed set's owned words per bottom-up round;
+  the per-tick counters are summed, so gs_run on every rank returns the
   global counters.  In one process, ``Simulator(cfg, devices=[...])`` does
   the same over several devices (gs_create_multi).
+
+* ``open_shard_exchange`` -- the same shard with the exchange done by the
+  caller (gs_create_rank_exchange) over a torch.distributed CPU group
+  (gloo).  It runs every multi-rank code path of the library except the
+  RCCL transport, so several processes can share one GPU (RCCL refuses two
+  ranks on one device): tests/test_rank_exchange.py and bench.py
+  ``--transport gloo``.
 """
 from __future__ import annotations
 
@@ -82,3 +93,35 @@ def comm_id(rank: int, world: int) -> bytes:
 def open_shard(cfg: Config, rank: int, world: int) -> Simulator:
     """This rank's shard of one node-range-sharded broadcast (gs_create_rank)."""
     return Simulator.rank(cfg, world, rank, comm_id(rank, world))
+
+
+def gloo_exchange(world: int, group=None):
+    """The three host exchange callbacks of gs_create_rank_exchange over a
+    torch.distributed CPU (gloo) group: all_gather of equal byte blocks,
+    element-wise u64 sum, all_to_allv of byte blocks (rank-major)."""
+
+    def all_gather(send: np.ndarray) -> np.ndarray:
+        t = torch.from_numpy(send)
+        out = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(out, t, group=group)
+        return torch.cat(out).numpy()
+
+    def all_reduce(x: np.ndarray) -> np.ndarray:
+        t = torch.from_numpy(x.view(np.int64).copy())
+        dist.all_reduce(t, group=group)
+        return t.numpy().view(np.uint64)
+
+    def all_to_allv(send: np.ndarray, send_sizes, recv_sizes) -> np.ndarray:
+        out = torch.empty(sum(recv_sizes), dtype=torch.uint8)
+        dist.all_to_all_single(out, torch.from_numpy(send), output_split_sizes=list(recv_sizes),
+                               input_split_sizes=list(send_sizes), group=group)
+        return out.numpy()
+
+    return all_gather, all_reduce, all_to_allv
+
+
+def open_shard_exchange(cfg: Config, rank: int, world: int, group=None) -> Simulator:
+    """This rank's shard with the exchange through the caller over gloo
+    (gs_create_rank_exchange): the library's per-rank logic is the RCCL
+    path's; only the transport differs."""
+    return Simulator.rank_exchange(cfg, world, rank, *gloo_exchange(world, group))

@@ -331,6 +331,30 @@ def comm_unique_id() -> bytes:
     return b.raw
 
 
+def trim(device: int = -1) -> int:
+    """Return the library's free cached device blocks to the driver (gs_trim);
+    returns the bytes released."""
+    L = _lib.load()
+    out = C.c_size_t(0)
+    rc = L.gs_trim(int(device), C.byref(out))
+    if rc != 0:
+        raise GossipError(rc, "gs_trim failed")
+    return int(out.value)
+
+
+MEMORY_FIELDS = ("alloc_ms", "largest_alloc_ms", "free_ms", "alloc_calls", "alloc_cache_hits", "cached_bytes")
+
+
+def memory_stats() -> dict:
+    """The library's process-wide device-memory figures (gs_memory_stats)."""
+    L = _lib.load()
+    t = Timing()
+    rc = L.gs_memory_stats(C.byref(t))
+    if rc != 0:
+        raise GossipError(rc, "gs_memory_stats failed")
+    return {f: getattr(t, f) for f in MEMORY_FIELDS}
+
+
 def covered(recv: int, n: int) -> bool:
     """simulator.go:246-248 in float32."""
     return bool(np.float32(recv) / np.float32(n) >= np.float32(0.99))

@@ -134,6 +134,15 @@ typedef struct gs_timing {
   uint64_t ov_sort_ticks;    /* last overlay build: ticks grouped by the radix sort (sparse ticks,
                               * GS_OV_SORT=1, or a partition fallback)                              */
   uint64_t ov_part_fallbacks; /* last overlay build: partition plans that overflowed (then sorted) */
+  /* Device memory, process-wide and cumulative since the library was loaded (every
+   * context shares the library's cache of large blocks; see gs_trim).  The reference
+   * allocates its nodes once per process (simulator.go:208-212). */
+  double alloc_ms;           /* wall time inside hipMalloc                                      */
+  double largest_alloc_ms;   /* the longest single hipMalloc                                    */
+  double free_ms;            /* wall time inside hipFree and the cache's idle waits             */
+  uint64_t alloc_calls;      /* hipMalloc calls                                                 */
+  uint64_t alloc_cache_hits; /* device buffers served from the cache (no hipMalloc)             */
+  uint64_t cached_bytes;     /* bytes the cache holds free now                                  */
 } gs_timing;
 
 /* gs_run status */
@@ -284,6 +293,20 @@ int gs_reset(gs_ctx* ctx);
 /* Run all later device work of a one-device context on `hip_stream` (a
  * hipStream_t owned by the caller); NULL restores the context's own stream. */
 int gs_set_stream(gs_ctx* ctx, void* hip_stream);
+/* Device-memory cache.  Device buffers of >= 64 MiB come from a process-wide
+ * cache: a destroyed context's blocks (or a rebuilt table's temporaries) stay
+ * mapped and serve the next context's requests, so a process that creates
+ * context after context does not hand tens of GB back to the driver and ask
+ * for them again (first allocations after large frees ran seconds slow on
+ * some MI355X boxes).  gs_trim returns every free cached
+ * block of `device` (-1: all devices) to the driver; *released (may be NULL)
+ * gets the bytes.  The cache also trims itself before a hipMalloc the device
+ * has no room for.  GS_DEVMEM_CACHE=0 in the environment disables it.  The
+ * reference allocates once per process (simulator.go:208-212). */
+int gs_trim(int device, size_t* released);
+/* The device-memory fields of a gs_timing, alloc_ms .. cached_bytes, without a
+ * context; every other field is zero. */
+int gs_memory_stats(gs_timing* out);
 
 /* ---- host-only helpers for the reference's stdout contract ------------- */
 /* Go fmt %v of a float32 (strconv 'g', -1, 32), e.g. 99.61 or 9.9999994e-08

@@ -263,6 +263,53 @@ def test_batched_trials_match_single(gs, n, T, crash):
     assert np.array_equal(got, want), f"\n{got}\n{want}"
 
 
+def batch_run(sim):
+    sim.build_overlay()
+    sim.broadcast_begin(-1)
+    sim.run(poll=10)
+    return sim.trial_results()
+
+
+def test_set_trial_renumbered_batches_match_fresh(gs):
+    """bench.py's C3 loop (verdict r05 item 3a): a batched context renumbered
+    with gs_set_trial after gs_reset, its overlay rebuilt in the kept
+    workspace, equals a fresh context of the same trials, for two successive
+    renumberings."""
+    n, T = 100_000, 24
+    with gs.Simulator(cfg(gs, n=n, crashrate=0.01, trial=0, trials=T)) as sim:
+        first = batch_run(sim)
+        for b in (T, 2 * T):
+            sim.reset()
+            sim.set_trial(b)
+            got = batch_run(sim)
+            with gs.Simulator(cfg(gs, n=n, crashrate=0.01, trial=b, trials=T)) as fresh:
+                want = batch_run(fresh)
+            assert list(got[:, 0]) == list(range(b, b + T))
+            assert np.array_equal(got, want), f"batch at trial {b}:\n{got}\n{want}"
+    with gs.Simulator(cfg(gs, n=n, crashrate=0.01, trial=0, trials=T)) as fresh:
+        assert np.array_equal(batch_run(fresh), first)
+
+
+def test_c3_batch_of_5000_matches_single_trials(gs):
+    """One 5,000-trial batch at N = 1e5 (bench.py's C3 batch, 5e8 ids in one
+    context) and its renumbering to trials 5000..9999 (the bench's second
+    batch) equal fresh one-trial contexts at both ends and in the middle;
+    single trials at 1e5 are oracle-pinned by the test below."""
+    n, T = 100_000, 5000
+    picks = (0, 1, 2499, 4999)
+    with gs.Simulator(gs.Config(n=n, seed=0x5EED, trial=0, trials=T)) as sim:
+        got = [batch_run(sim)]
+        sim.reset()
+        sim.set_trial(T)
+        got.append(batch_run(sim))
+    for b, res in zip((0, T), got):
+        assert res.shape[0] == T and list(res[[0, -1], 0]) == [b, b + T - 1]
+        for t in picks:
+            with gs.Simulator(gs.Config(n=n, seed=0x5EED, trial=b + t)) as one:
+                want = batch_run(one)[0]
+            assert np.array_equal(res[t], want), f"trial {b + t}: {res[t]} vs {want}"
+
+
 def test_batched_trials_injected_match_oracle_1e5(gs, oracle):
     """Config C3 size (N = 1e5), three trials: oracle overlay and oracle
     broadcast per trial vs one batched context fed the oracle's tables."""
