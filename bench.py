@@ -56,7 +56,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=1_000_000_000)
+    # --nodes: the same, unambiguous behind torch.distributed.run (whose own options --nnodes,
+    # --nproc-per-node, ... make a bare --n ambiguous there)
+    ap.add_argument("--n", "--nodes", dest="n", type=int, default=1_000_000_000)
     ap.add_argument("--fanout", type=int, default=5)
     ap.add_argument("--fanin", type=int, default=6)
     ap.add_argument("--delaylow", type=int, default=10)
@@ -347,7 +349,10 @@ def main():
         if not a.no_c4:
             ext["c4_sharded"] = guarded("c4_sharded", lambda: c4_sharded(a, gs, rank, world, local, dist))
         pp = guarded("pushpull", lambda: pushpull_runs(a, gs, rank, local))
+        dm = pp.pop("devmem", None)
         ext.update(pp if "error" not in pp else {"pushpull": pp})
+        if dm is not None and isinstance(ext.get("pushpull"), dict):
+            ext["pushpull"]["devmem"] = dm
         if world > 1:
             ext["c5_flood_sharded"] = guarded("c5_flood_sharded",
                                               lambda: c5_flood_sharded(a, gs, rank, world, local, dist))
@@ -457,6 +462,7 @@ def pushpull_runs(a, gs, rank, local):
         sim.build_overlay()
         timed_broadcast(sim)  # warmup (builds the reverse table)
         rev_ms = sim.timing()["prep_ms"]
+        rev_passes = int(sim.timing()["pp_rev_part"])
         runs = [timed_broadcast(sim) for _ in range(max(a.steps, 1))]
         dt = sum(r[2] for r in runs)
         tot, status, _ = runs[-1]
@@ -481,7 +487,10 @@ def pushpull_runs(a, gs, rank, local):
                          "frac": round(ach / HBM_PEAK_GBS, 5),
                          "avg_launch_us": round(ms * 1e3 / max(rounds, 1), 2), "launches": rounds,
                          **pp_pmc_traffic()},
-            "rev_table_prep_ms": round(rev_ms, 3)}
+            "rev_table_prep_ms": round(rev_ms, 3),
+            # passes of the partition build over the coarse bins (sized to the largest block the
+            # device allocator can give without a hipFree; 0 = the atomic build)
+            "rev_table_passes": rev_passes}
         sim.reset()
         sim.set_failed(failed_mask(a.n, 0.01, a.seed + 1))
         tot, status, dt = timed_broadcast(sim)

@@ -1656,17 +1656,19 @@ int pp_prepare(gs_ctx* c) {
     }
     // by partitioning (GS_PP_REV_ATOMIC=1: the atomic count + fill, A/B);
     // the atomic build also takes what the partition cannot (memory, skew)
-    static const bool rev_atomic = getenv("GS_PP_REV_ATOMIC") != nullptr;
+    // (both switches read per call, so tests can force either path)
+    const bool rev_atomic = getenv("GS_PP_REV_ATOMIC") != nullptr;
     bool part = false;
+    uint32_t passes = 0;
     if (!rev_atomic) {
       part = pp_rev_build_part(s, (unsigned long long*)c->pp_rend.p, (uint32_t*)c->pp_rsrc.p,
-                               (uint8_t*)c->pp_rslot.p, c->stream) == hipSuccess;
+                               (uint8_t*)c->pp_rslot.p, c->stream, &passes) == hipSuccess;
       if (!part) (void)hipGetLastError();
     }
     if (!part)
       CK(c, pp_rev_build(s, (unsigned long long*)c->pp_rend.p, (uint32_t*)c->pp_rsrc.p, (uint8_t*)c->pp_rslot.p,
                          c->pp_scan.p, c->pp_scan.bytes, c->stream));
-    c->timing.pp_rev_part = part ? 1 : 0;
+    c->timing.pp_rev_part = part ? passes : 0;
     c->rev_ver = c->table_ver;
     c->fm_tver = ~0ull;
     built = true;

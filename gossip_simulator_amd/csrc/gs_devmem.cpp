@@ -6,9 +6,11 @@
 // and splits off the rest; a free coalesces with free neighbours of the same
 // slab, so a slab whose extents are all free is one extent again and can be
 // trimmed.  Only when no free extent fits is a new slab mapped; if the device
-// lacks the room beside the cache, the fully free slabs are trimmed first.
+// lacks the room beside the cache, fully free slabs are trimmed first, largest
+// first, as many as the request needs.
 #include "gs_devmem.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <iterator>
@@ -20,6 +22,7 @@ namespace {
 
 constexpr size_t kCacheMin = 64ull << 20;  // smaller blocks: plain hipMalloc / hipFree
 constexpr size_t kGran = 2ull << 20;
+constexpr size_t kMargin = 2ull << 30;     // device memory left to others beside a new block
 
 struct Ext {
   size_t size;
@@ -80,17 +83,27 @@ void unindex(Cache& c, int dev, char* b, size_t size) {
     }
 }
 
-// caller holds c.mu; returns the slabs to hipFree (done outside the lock)
-std::vector<char*> collect_trim(Cache& c, int device) {
-  std::vector<char*> out;
+// caller holds c.mu; returns the slabs to hipFree (done outside the lock).
+// Fully free slabs of `device` (-1: all), largest first, until `want` bytes
+// are collected (~0: all of them).
+std::vector<char*> collect_trim(Cache& c, int device, size_t want = ~(size_t)0) {
+  std::vector<size_t> idx;
   for (size_t i = 0; i < c.slab.size(); ++i) {
+    const Slab& s = c.slab[i];
+    if (s.size && !s.used && (device < 0 || s.device == device)) idx.push_back(i);
+  }
+  std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return c.slab[a].size > c.slab[b].size; });
+  std::vector<char*> out;
+  size_t got = 0;
+  for (size_t i : idx) {
+    if (got >= want) break;
     Slab& s = c.slab[i];
-    if (!s.size || s.used || (device >= 0 && s.device != device)) continue;
     unindex(c, s.device, s.base, s.size);  // a free slab is one extent
     c.ext.erase(s.base);
     c.st.cached_bytes -= s.size;
     c.st.mapped_bytes -= s.size;
     out.push_back(s.base);
+    got += s.size;
     s.size = 0;
   }
   return out;
@@ -137,12 +150,14 @@ hipError_t gs_dev_malloc(void** p, size_t bytes) {
     }
   }
   // a new slab; make room beside the cache first if the device lacks it
+  // (only as much as the request needs: a hipMalloc right after large
+  // hipFrees is what stalls)
   size_t freeb = 0, totalb = 0;
-  if (hipMemGetInfo(&freeb, &totalb) == hipSuccess && freeb < need + (kGran << 4)) {
+  if (hipMemGetInfo(&freeb, &totalb) == hipSuccess && freeb < need + kMargin) {
     std::vector<char*> t;
     {
       std::lock_guard<std::mutex> g(c.mu);
-      t = collect_trim(c, dev);
+      t = collect_trim(c, dev, need + kMargin - freeb);
     }
     release(c, t);
   }
@@ -229,6 +244,19 @@ void gs_devmem_stats(DevMemStats* out) {
   Cache& c = cache();
   std::lock_guard<std::mutex> g(c.mu);
   *out = c.st;
+}
+
+size_t gs_devmem_largest() {
+  Cache& c = cache();
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  size_t freeb = 0, totalb = 0, best = 0;
+  if (hipMemGetInfo(&freeb, &totalb) == hipSuccess && freeb > kMargin) best = freeb - kMargin;
+  if (!enabled()) return best;
+  std::lock_guard<std::mutex> g(c.mu);
+  auto it = c.freeix.find(dev);
+  if (it != c.freeix.end() && !it->second.empty()) best = std::max(best, it->second.rbegin()->first);
+  return best;
 }
 
 size_t gs_devmem_trim(int device) {

@@ -46,5 +46,10 @@ void gs_devmem_stats(DevMemStats* out);
 // Return every fully free cached block of `device` (-1: all devices) to the
 // driver; returns the bytes released.
 size_t gs_devmem_trim(int device);
+// The largest block gs_dev_malloc can hand out on the current device without
+// returning cached blocks to the driver: the largest free cached extent, or a
+// new block in the device's free memory less a margin.  Builds with large
+// temporaries size their passes by it (pp_rev_build_part).
+size_t gs_devmem_largest();
 
 #endif

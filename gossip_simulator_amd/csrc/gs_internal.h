@@ -419,10 +419,11 @@ size_t pp_rev_scan_bytes(uint64_t n);
 hipError_t pp_rev_build(const DevState& s, unsigned long long* rend, uint32_t* rsrc, uint8_t* rslot, void* tmp,
                         size_t tmp_bytes, hipStream_t st);
 // The same table by partitioning the edges (no random atomic per edge;
-// temporaries ~17 B per edge, freed on return).  An error leaves the outputs
-// unspecified (pp_rev_build then builds them).
+// temporaries ~17 B per edge, in as many passes over the coarse bins as the
+// device allocator's largest block needs; *passes_out = the passes).  An
+// error leaves the outputs unspecified (pp_rev_build then builds them).
 hipError_t pp_rev_build_part(const DevState& s, unsigned long long* rend, uint32_t* rsrc, uint8_t* rslot,
-                             hipStream_t st);
+                             hipStream_t st, uint32_t* passes_out);
 // fmask from the reverse table and the failed mask (stride <= 8).
 hipError_t pp_fmask_build(const DevState& s, const unsigned long long* rend, const uint32_t* rsrc,
                           const uint8_t* rslot, uint8_t* fmask, hipStream_t st);

@@ -1278,9 +1278,13 @@ __global__ __launch_bounds__(kRvBlock) void k_rv_hist(const DevState s, unsigned
 
 // Rounds of kRvRows rows: count per coarse bin in LDS, one reservation per
 // (round, bin), then every record to its bin's run (the rows re-read from L2).
+// One pass covers the coarse bins [blo, bhi) (edges to other bins are
+// skipped; cstart / cfill are indexed by bin - blo): a build in several passes
+// bounds the temporaries (pp_rev_build_part).
 __global__ __launch_bounds__(kRvBlock) void k_rv_coarse(const DevState s, const unsigned long long* __restrict__ cstart,
                                                         unsigned long long* __restrict__ cfill,
-                                                        unsigned long long* __restrict__ rec) {
+                                                        unsigned long long* __restrict__ rec, uint32_t blo,
+                                                        uint32_t bhi) {
   __shared__ uint32_t cnt[kRvBins], off[kRvBins];
   __shared__ unsigned long long gb[kRvBins];
   const uint32_t tid = threadIdx.x;
@@ -1293,11 +1297,14 @@ __global__ __launch_bounds__(kRvBlock) void k_rv_coarse(const DevState s, const 
       const uint64_t v = r * kRvRows + k * kRvBlock + tid;
       if (v >= s.n) continue;
       const uint32_t d = s.deg[v];
-      for (uint32_t j = 0; j < d; ++j) atomicAdd(&cnt[s.ids[v * s.stride + j] >> kRvShift], 1u);
+      for (uint32_t j = 0; j < d; ++j) {
+        const uint32_t b = s.ids[v * s.stride + j] >> kRvShift;
+        if (b >= blo && b < bhi) atomicAdd(&cnt[b], 1u);
+      }
     }
     __syncthreads();
     for (uint32_t b = tid; b < kRvBins; b += kRvBlock)
-      if (cnt[b]) gb[b] = cstart[b] + atomicAdd(&cfill[b], (unsigned long long)cnt[b]);
+      if (cnt[b]) gb[b] = cstart[b - blo] + atomicAdd(&cfill[b - blo], (unsigned long long)cnt[b]);
     __syncthreads();
 #pragma unroll
     for (uint32_t k = 0; k < 2; ++k) {
@@ -1306,6 +1313,7 @@ __global__ __launch_bounds__(kRvBlock) void k_rv_coarse(const DevState s, const 
       const uint32_t d = s.deg[v];
       for (uint32_t j = 0; j < d; ++j) {
         const uint32_t u = s.ids[v * s.stride + j], b = u >> kRvShift;
+        if (b < blo || b >= bhi) continue;
         const unsigned long long pos = gb[b] + atomicAdd(&off[b], 1u);
         rec[pos] = (u & ((1u << kRvShift) - 1)) | (v << kRvShift) |
                    ((unsigned long long)rv_slot_byte(s.stride, j, d) << 53);
@@ -1375,11 +1383,12 @@ __global__ __launch_bounds__(kRvBlock) void k_rv_final(const unsigned long long*
                                                        const unsigned long long* __restrict__ ffill,
                                                        const unsigned long long* __restrict__ bbase, uint64_t n,
                                                        unsigned long long* __restrict__ rend, uint32_t* __restrict__ rsrc,
-                                                       uint8_t* __restrict__ rslot) {
+                                                       uint8_t* __restrict__ rslot, uint32_t fb0) {
   __shared__ uint32_t cnt[16384];
   __shared__ unsigned long long s_x[kRvBlock / 64];
-  const uint32_t tid = threadIdx.x, b = blockIdx.x;
-  const unsigned long long M = ffill[b], f0 = fstart[b], ob = bbase[b];
+  // bucket b of the table = bucket blockIdx.x of this pass's arrays
+  const uint32_t tid = threadIdx.x, b = fb0 + blockIdx.x;
+  const unsigned long long M = ffill[blockIdx.x], f0 = fstart[blockIdx.x], ob = bbase[blockIdx.x];
   for (uint32_t i = tid; i < 16384; i += kRvBlock) cnt[i] = 0;
   __syncthreads();
   for (unsigned long long i = tid; i < M; i += kRvBlock) atomicAdd(&cnt[frec[f0 + i] & 16383], 1u);
@@ -1525,12 +1534,19 @@ hipError_t pp_rev_build(const DevState& s, unsigned long long* rend, uint32_t* r
 }
 
 // The reverse table by partitioning (the k_rv_* kernels above): host-paced
-// (three small read-backs), temporaries allocated here and freed before
-// return.  An error (no memory for the ~17 B per edge of temporaries, or a
-// fine region past its planned size on a skewed table) leaves the outputs
-// unspecified: the caller then builds with pp_rev_build.
+// (a few small read-backs per pass).  The coarse bins are taken in passes of
+// consecutive bins whose temporaries (8-B records: the coarse copy, then the
+// fine regions, ~17 B per edge) fit the largest block the device allocator can
+// give without returning cached memory to the driver (gs_devmem_largest): one
+// pass when memory allows, more after other contexts left their blocks cached
+// (every pass streams the table again, ~8 ms per pass at N = 1e9, where a
+// hipMalloc right after large hipFrees stalled for seconds: DESIGN.md section
+// 9).  GS_PP_REV_PASSES=k (read per call) forces k passes.  An error (no
+// memory even for one bin, or a fine region past its planned size on a skewed
+// table) leaves the outputs unspecified: the caller then builds with
+// pp_rev_build.
 hipError_t pp_rev_build_part(const DevState& s, unsigned long long* rend, uint32_t* rsrc, uint8_t* rslot,
-                             hipStream_t st) {
+                             hipStream_t st, uint32_t* passes_out) {
   if (!s.n || s.n >= (1ull << 31)) return hipErrorInvalidValue;
   const uint64_t n = s.n, nbins = (n + (1ull << kRvShift) - 1) >> kRvShift, nbf = (n + 16383) >> 14;
   // small device arrays: chist[512] | cstart[513] | cend[512] | fstart[nbf+1] | ffill[nbf] | bbase[nbf] | tpre[513] | ovf
@@ -1546,16 +1562,13 @@ hipError_t pp_rev_build_part(const DevState& s, unsigned long long* rend, uint32
   unsigned long long* d_bbase = d_ffill + nbf;
   uint32_t* d_tpre = (uint32_t*)(d_bbase + nbf);
   uint32_t* d_ovf = d_tpre + 513;
-  unsigned long long *rec = nullptr, *frec = nullptr;
-  std::vector<unsigned long long> h(512, 0), cs(513, 0), ce(512, 0), fs(nbf + 1, 0), ff(nbf, 0), bb(nbf, 0);
-  std::vector<uint32_t> tp(513, 0);
+  unsigned long long* tmp = nullptr;
+  std::vector<unsigned long long> h(512, 0), cs(513, 0), fsz(nbf, 0), need(nbins, 0);
   uint32_t ovf = 0;
-  unsigned long long E = 0, F = 0;
   const uint32_t grid = 512;
   auto done = [&](hipError_t r) {
     (void)hipStreamSynchronize(st);
-    if (rec) (void)dev_free(rec);
-    if (frec) (void)dev_free(frec);
+    if (tmp) (void)dev_free(tmp);
     (void)dev_free(sm);
     return r;
   };
@@ -1570,49 +1583,98 @@ hipError_t pp_rev_build_part(const DevState& s, unsigned long long* rend, uint32
   RV(hipMemcpyAsync(h.data(), d_chist, 512 * 8, hipMemcpyDeviceToHost, st));
   RV(hipStreamSynchronize(st));
   // exact coarse regions; a fine region planned at 1.125 x its node share of
-  // its coarse region + 1024
+  // its coarse region + 1024; need[c] = bin c's records in both copies
   for (uint64_t c = 0; c < nbins; ++c) {
     cs[c + 1] = cs[c] + h[c];
-    ce[c] = cs[c] + h[c];
-    tp[c + 1] = tp[c] + (uint32_t)((h[c] + kRvTile - 1) / kRvTile);
     const uint64_t nf = std::min<uint64_t>(256, nbf - c * 256);
     const uint64_t nodes_c = std::min<uint64_t>(1ull << kRvShift, n - (c << kRvShift));
+    need[c] = h[c];
     for (uint64_t d = 0; d < nf; ++d) {
       const uint64_t fb = c * 256 + d, nodes_b = std::min<uint64_t>(16384, n - fb * 16384);
       const unsigned long long share = (unsigned long long)((double)h[c] * nodes_b / nodes_c);
-      fs[fb + 1] = fs[fb] + share + share / 8 + 1024;
+      fsz[fb] = share + share / 8 + 1024;
+      need[c] += fsz[fb];
     }
   }
-  E = cs[nbins];
-  F = fs[nbf];
-  RV(hipMemcpyAsync(d_cstart, cs.data(), 513 * 8, hipMemcpyHostToDevice, st));
-  RV(hipMemcpyAsync(d_cend, ce.data(), 512 * 8, hipMemcpyHostToDevice, st));
-  RV(hipMemcpyAsync(d_fstart, fs.data(), (nbf + 1) * 8, hipMemcpyHostToDevice, st));
-  RV(hipMemcpyAsync(d_tpre, tp.data(), 513 * 4, hipMemcpyHostToDevice, st));
-  RV(dev_malloc(&rec, std::max<unsigned long long>(E, 1) * 8));
-  RV(dev_malloc(&frec, std::max<unsigned long long>(F, 1) * 8));
+  const unsigned long long E = cs[nbins];
+  // passes of consecutive bins: forced count, or as many bins as fit the
+  // largest block the allocator can give
+  std::vector<uint32_t> cut{0};
   {
+    const char* fp = getenv("GS_PP_REV_PASSES");
+    const uint64_t forced = fp ? (uint64_t)std::max(atoi(fp), 1) : 0;
+    if (forced) {
+      const uint64_t per = (nbins + forced - 1) / forced;
+      for (uint64_t c = per; c < nbins; c += per) cut.push_back((uint32_t)c);
+    } else {
+      const uint64_t cap = gs_devmem_largest() / 8;
+      uint64_t acc = 0;
+      for (uint64_t c = 0; c < nbins; ++c) {
+        if (need[c] > cap) return done(hipErrorOutOfMemory);  // not even one bin: the atomic build
+        if (acc + need[c] > cap) {
+          cut.push_back((uint32_t)c);
+          acc = 0;
+        }
+        acc += need[c];
+      }
+    }
+    cut.push_back((uint32_t)nbins);
+  }
+  const size_t P = cut.size() - 1;
+  if (passes_out) *passes_out = (uint32_t)P;
+  unsigned long long rec_max = 1, frec_max = 1;
+  for (size_t p = 0; p < P; ++p) {
+    unsigned long long r = 0, f = 0;
+    for (uint32_t c = cut[p]; c < cut[p + 1]; ++c) {
+      r += h[c];
+      f += need[c] - h[c];
+    }
+    rec_max = std::max(rec_max, r);
+    frec_max = std::max(frec_max, f);
+  }
+  // one block for both copies: it fits the extent the plan was made for
+  RV(dev_malloc(&tmp, (rec_max + frec_max) * 8));
+  unsigned long long* rec = tmp;
+  unsigned long long* frec = tmp + rec_max;
+  for (size_t p = 0; p < P; ++p) {
+    const uint32_t blo = cut[p], bhi = cut[p + 1], nb = bhi - blo;
+    const uint64_t fb0 = (uint64_t)blo * 256, fb1 = std::min<uint64_t>((uint64_t)bhi * 256, nbf), nfl = fb1 - fb0;
+    std::vector<unsigned long long> csl(nb + 1, 0), cel(nb, 0), fsl(nfl + 1, 0), ffl(nfl, 0), bbl(nfl, 0);
+    std::vector<uint32_t> tpl(nb + 1, 0);
+    for (uint32_t c = 0; c < nb; ++c) {
+      csl[c + 1] = csl[c] + h[blo + c];
+      cel[c] = csl[c + 1];
+      tpl[c + 1] = tpl[c] + (uint32_t)((h[blo + c] + kRvTile - 1) / kRvTile);
+    }
+    for (uint64_t i = 0; i < nfl; ++i) fsl[i + 1] = fsl[i] + fsz[fb0 + i];
+    RV(hipMemcpyAsync(d_cstart, csl.data(), (nb + 1) * 8, hipMemcpyHostToDevice, st));
+    RV(hipMemcpyAsync(d_cend, cel.data(), nb * 8, hipMemcpyHostToDevice, st));
+    RV(hipMemcpyAsync(d_fstart, fsl.data(), (nfl + 1) * 8, hipMemcpyHostToDevice, st));
+    RV(hipMemcpyAsync(d_tpre, tpl.data(), (nb + 1) * 4, hipMemcpyHostToDevice, st));
+    RV(hipMemsetAsync(d_ffill, 0, nfl * 8, st));
     unsigned long long* d_cfill = d_chist;  // reused: the fills of the coarse pass
     RV(hipMemsetAsync(d_cfill, 0, 512 * 8, st));
     const uint64_t rounds = (n + kRvRows - 1) / kRvRows;
     hipLaunchKernelGGL(k_rv_coarse, dim3((uint32_t)std::min<uint64_t>(rounds, grid)), dim3(kRvBlock), 0, st, s,
-                       d_cstart, d_cfill, rec);
+                       d_cstart, d_cfill, rec, blo, bhi);
     RV(hipGetLastError());
-  }
-  if (tp[nbins]) {
-    hipLaunchKernelGGL(k_rv_fine, dim3(std::min<uint32_t>(tp[nbins], grid)), dim3(kRvBlock), 0, st, rec, d_cstart,
-                       d_cend, d_tpre, (uint32_t)nbins, d_fstart, d_ffill, frec, d_ovf);
+    if (tpl[nb]) {
+      hipLaunchKernelGGL(k_rv_fine, dim3(std::min<uint32_t>(tpl[nb], grid)), dim3(kRvBlock), 0, st, rec, d_cstart,
+                         d_cend, d_tpre, nb, d_fstart, d_ffill, frec, d_ovf);
+      RV(hipGetLastError());
+    }
+    RV(hipMemcpyAsync(ffl.data(), d_ffill, nfl * 8, hipMemcpyDeviceToHost, st));
+    RV(hipMemcpyAsync(&ovf, d_ovf, 4, hipMemcpyDeviceToHost, st));
+    RV(hipStreamSynchronize(st));
+    if (ovf) return done(hipErrorInvalidValue);  // a skewed table: the atomic build
+    bbl[0] = cs[blo];  // every in-edge of the earlier buckets lies in the earlier bins
+    for (uint64_t b = 1; b < nfl; ++b) bbl[b] = bbl[b - 1] + ffl[b - 1];
+    RV(hipMemcpyAsync(d_bbase, bbl.data(), nfl * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_rv_final, dim3((uint32_t)nfl), dim3(kRvBlock), 0, st, frec, d_fstart, d_ffill, d_bbase, n,
+                       rend, rsrc, rslot, (uint32_t)fb0);
     RV(hipGetLastError());
+    RV(hipStreamSynchronize(st));  // this pass's host arrays and the temporaries are reused
   }
-  RV(hipMemcpyAsync(ff.data(), d_ffill, nbf * 8, hipMemcpyDeviceToHost, st));
-  RV(hipMemcpyAsync(&ovf, d_ovf, 4, hipMemcpyDeviceToHost, st));
-  RV(hipStreamSynchronize(st));
-  if (ovf) return done(hipErrorInvalidValue);  // a skewed table: the atomic build
-  for (uint64_t b = 1; b < nbf; ++b) bb[b] = bb[b - 1] + ff[b - 1];
-  RV(hipMemcpyAsync(d_bbase, bb.data(), nbf * 8, hipMemcpyHostToDevice, st));
-  hipLaunchKernelGGL(k_rv_final, dim3((uint32_t)nbf), dim3(kRvBlock), 0, st, frec, d_fstart, d_ffill, d_bbase, n, rend,
-                     rsrc, rslot);
-  RV(hipGetLastError());
   RV(hipMemcpyAsync(rend + n, &E, 8, hipMemcpyHostToDevice, st));
 #undef RV
   return done(hipSuccess);

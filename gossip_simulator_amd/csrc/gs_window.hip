@@ -1258,6 +1258,15 @@ __device__ __forceinline__ void stamp(const WinState& w, ResolveLds& sm, uint32_
 
 // receipt (fine message): loc | k << 14 | roll0 << 18
 
+// GS_RESOLVE_PROBE=1 (timing probe builds only, results differ): k_resolve's
+// receipts phase skips the per-receipt (crashed, rolled) read, every node is
+// plain -- the floor of the b1 atomics alone
+#if defined(GS_RESOLVE_PROBE) && GS_RESOLVE_PROBE == 1
+#define GS_RESOLVE_CR0(loc) make_uint2(0u, 0u)
+#else
+#define GS_RESOLVE_CR0(loc) sm.cr0[(loc) >> 5]
+#endif
+
 __device__ __forceinline__ uint32_t msg_loc(uint32_t m) { return m & (kFineNodes - 1); }
 __device__ __forceinline__ uint32_t msg_tick(uint32_t m) { return (m >> kFineLog) & (kMaxWindow - 1); }
 
@@ -1515,7 +1524,7 @@ __device__ __forceinline__ void resolve_body(const WinState& w, uint32_t t0, uin
         if (VALID) {                                                                              \
           const uint32_t loc = msg_loc(m[u]);                                                     \
           atomicOr(&sm.b1[msg_tick(m[u])][loc >> 5], 1u << (loc & 31)); /* no return */         \
-          sp[u] = sm.cr0[loc >> 5];                                                               \
+          sp[u] = GS_RESOLVE_CR0(loc);                                                            \
         }                                                                                         \
       }                                                                                           \
       uint32_t dm = 0; /* bit u: receipt u is at a rolled node */                                 \

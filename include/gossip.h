@@ -128,8 +128,9 @@ typedef struct gs_timing {
   uint64_t pp_answer_rounds; /* push-pull: dense rounds of this broadcast run pull-answer        */
   uint64_t dd_fallbacks;     /* device-driven shard windows stopped by an overflow and redone
                               * host-driven (cumulative; a buffer that fits makes it stop growing) */
-  uint64_t pp_rev_part;      /* push-pull: 1 if the last reverse table was built by partitioning the
-                              * edges, 0 by the atomic count + fill (GS_PP_REV_ATOMIC, or a fallback) */
+  uint64_t pp_rev_part;      /* push-pull: the passes of the last reverse table's partition build
+                              * (>= 1), or 0 if the atomic count + fill built it (GS_PP_REV_ATOMIC, or a
+                              * fallback) */
   uint64_t ov_part_ticks;    /* last overlay build: ticks grouped by the destination partition     */
   uint64_t ov_sort_ticks;    /* last overlay build: ticks grouped by the radix sort (sparse ticks,
                               * GS_OV_SORT=1, or a partition fallback)                              */

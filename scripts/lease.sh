@@ -44,8 +44,9 @@ for step in "$@"; do
       bash scripts/pmc_pp.sh "$o/pmc_pp" 1e9 0 || exit 1 ;;
     pool)
       hipcc -O2 --offload-arch=gfx950 -o "$o/pool_repro" scripts/micro/pool_repro.hip || exit 1
-      for args in "5 6 pool kcopy nosync" "5 6 pool memcpy sync" "5 6 pool kcopy sync" "1 6 pool memcpy nosync" \
-                  "5 6 malloc memcpy nosync"; do
+      for args in "5 6 pool memcpy nosync" "5 6 pool memcpy sync" "5 6 pool kcopy nosync" "5 6 pool kcopy sync" \
+                  "5 6 malloc memcpy nosync" "5 6 malloc memcpy sync" "5 6 malloc kcopy nosync" \
+                  "5 6 malloc kcopy sync" "1 6 pool memcpy nosync"; do
         echo "== pool_repro $args"
         # shellcheck disable=SC2086
         timeout -k 10 180 "$o/pool_repro" $args; rc=$?

@@ -23,7 +23,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SMALL = ["--n", "2000000", "--c4-n", "2000000", "--c3-trials", "200", "--c3-batch", "100",
+SMALL = ["--nodes", "2000000", "--c4-n", "2000000", "--c3-trials", "200", "--c3-batch", "100",
          "--steps", "2", "--warmup", "1", "--cpu-n", "0", "--pp-shards", "2", "--ext-deadline", "240"]
 
 
