@@ -1704,7 +1704,7 @@ int pp_prepare(gs_ctx* c) {
       CK(c, pp_fmask_build(s, c->sp.rend, c->sp.rsrc, c->sp.rslot, (uint8_t*)c->pp_fmask.p, c->stream));
       CK(c, pp_fmask_any((const uint8_t*)c->pp_fmask.p, n, fmask_any(c), c->stream));
       // (optional: without it the answer test gathers the caller's failed word)
-      if (grow(c->pp_rfail, ((n * s.stride + 31) >> 5) * 4 + 4))
+      if (grow(c->pp_rfail, ((n * s.stride + 31) >> 5) * 4 + 8))  // + the hub flag word
         CK(c, pp_rfail_build(s, c->sp.rend, c->sp.rsrc, c->sp.rslot, (uint32_t*)c->pp_rfail.p, c->stream));
       else
         (void)hipGetLastError();

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <iterator>
 #include <map>
@@ -22,7 +23,15 @@ namespace {
 
 constexpr size_t kCacheMin = 64ull << 20;  // smaller blocks: plain hipMalloc / hipFree
 constexpr size_t kGran = 2ull << 20;
-constexpr size_t kMargin = 2ull << 30;     // device memory left to others beside a new block
+// device memory left to the rest of the process (RCCL's buffers, torch, a
+// small hipMalloc): a new slab is mapped only with this much beside it, and a
+// free that leaves the device with less returns cached slabs until it has it
+constexpr size_t kMargin = 8ull << 30;
+
+bool logging() {
+  static const bool on = getenv("GS_DEVMEM_LOG") != nullptr;
+  return on;
+}
 
 struct Ext {
   size_t size;
@@ -70,6 +79,10 @@ hipError_t timed_malloc(Cache& c, void** p, size_t bytes) {
   c.st.alloc_ms += dt;
   if (dt > c.st.largest_alloc_ms) c.st.largest_alloc_ms = dt;
   ++c.st.hip_allocs;
+  if (logging() && bytes >= (1ull << 30))  // GS_DEVMEM_LOG: every hipMalloc of >= 1 GiB
+    fprintf(stderr, "[devmem] hipMalloc %.2f GiB: %.1f ms%s (cached free %.2f GiB, mapped %.2f GiB)\n",
+            bytes / 1073741824.0, dt, e == hipSuccess ? "" : " FAILED", c.st.cached_bytes / 1073741824.0,
+            c.st.mapped_bytes / 1073741824.0);
   return e;
 }
 
@@ -84,8 +97,9 @@ void unindex(Cache& c, int dev, char* b, size_t size) {
 }
 
 // caller holds c.mu; returns the slabs to hipFree (done outside the lock).
-// Fully free slabs of `device` (-1: all), largest first, until `want` bytes
-// are collected (~0: all of them).
+// Fully free slabs of `device` (-1: all) worth at least `want` bytes (~0: all
+// of them): the smallest single slab that covers `want` if there is one, else
+// the largest first -- as few bytes back to the driver as the request needs.
 std::vector<char*> collect_trim(Cache& c, int device, size_t want = ~(size_t)0) {
   std::vector<size_t> idx;
   for (size_t i = 0; i < c.slab.size(); ++i) {
@@ -93,6 +107,13 @@ std::vector<char*> collect_trim(Cache& c, int device, size_t want = ~(size_t)0) 
     if (s.size && !s.used && (device < 0 || s.device == device)) idx.push_back(i);
   }
   std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return c.slab[a].size > c.slab[b].size; });
+  if (want != ~(size_t)0) {
+    for (size_t k = idx.size(); k-- > 0;)  // ascending sizes
+      if (c.slab[idx[k]].size >= want) {
+        idx = {idx[k]};
+        break;
+      }
+  }
   std::vector<char*> out;
   size_t got = 0;
   for (size_t i : idx) {
@@ -116,6 +137,7 @@ void release(Cache& c, const std::vector<char*>& blocks) {
     std::lock_guard<std::mutex> g(c.mu);
     c.st.free_ms += now_ms() - t0;
   }
+  if (logging() && !blocks.empty()) fprintf(stderr, "[devmem] returned %zu cached slab(s) to the driver\n", blocks.size());
 }
 
 }  // namespace
@@ -183,6 +205,27 @@ hipError_t gs_dev_malloc(void** p, size_t bytes) {
   return hipSuccess;
 }
 
+namespace {
+// After a free: keep kMargin of device memory for the rest of the process
+// (hipFree'd memory comes back slowly, so only what the margin needs).
+void keep_headroom(int dev) {
+  Cache& c = cache();
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (cur != dev) (void)hipSetDevice(dev);
+  size_t freeb = 0, totalb = 0;
+  if (hipMemGetInfo(&freeb, &totalb) == hipSuccess && freeb < kMargin) {
+    std::vector<char*> t;
+    {
+      std::lock_guard<std::mutex> g(c.mu);
+      t = collect_trim(c, dev, kMargin - freeb);
+    }
+    release(c, t);
+  }
+  if (cur != dev) (void)hipSetDevice(cur);
+}
+}  // namespace
+
 hipError_t gs_dev_free(void* p) {
   if (!p) return hipSuccess;
   Cache& c = cache();
@@ -206,38 +249,45 @@ hipError_t gs_dev_free(void* p) {
   if (cur != sdev) (void)hipSetDevice(sdev);
   const hipError_t se = hipDeviceSynchronize();
   if (cur != sdev) (void)hipSetDevice(cur);
-  std::lock_guard<std::mutex> g(c.mu);
-  c.st.free_ms += now_ms() - t0;
-  auto it = c.ext.find((char*)p);
-  if (it == c.ext.end() || !it->second.used) return hipErrorInvalidValue;  // freed twice
-  Ext x = it->second;
-  Slab& s = c.slab[x.slab];
-  s.used -= x.size;
-  c.st.cached_bytes += x.size;
-  char* b = (char*)p;
-  auto& fi = c.freeix[s.device];
-  // coalesce with the next extent of the same slab
-  auto nx = std::next(it);
-  if (nx != c.ext.end() && !nx->second.used && nx->second.slab == x.slab && b + x.size == nx->first) {
-    unindex(c, s.device, nx->first, nx->second.size);
-    x.size += nx->second.size;
-    c.ext.erase(nx);
-  }
-  // and with the previous one
-  if (it != c.ext.begin()) {
-    auto pv = std::prev(it);
-    if (!pv->second.used && pv->second.slab == x.slab && pv->first + pv->second.size == b) {
-      unindex(c, s.device, pv->first, pv->second.size);
-      pv->second.size += x.size;
-      c.ext.erase(it);
-      fi.emplace(pv->second.size, pv->first);
-      return se;
+  {
+    std::lock_guard<std::mutex> g(c.mu);
+    c.st.free_ms += now_ms() - t0;
+    auto it = c.ext.find((char*)p);
+    if (it == c.ext.end() || !it->second.used) return hipErrorInvalidValue;  // freed twice
+    Ext x = it->second;
+    Slab& s = c.slab[x.slab];
+    s.used -= x.size;
+    c.st.cached_bytes += x.size;
+    char* b = (char*)p;
+    auto& fi = c.freeix[s.device];
+    // coalesce with the next extent of the same slab
+    auto nx = std::next(it);
+    if (nx != c.ext.end() && !nx->second.used && nx->second.slab == x.slab && b + x.size == nx->first) {
+      unindex(c, s.device, nx->first, nx->second.size);
+      x.size += nx->second.size;
+      c.ext.erase(nx);
+    }
+    // and with the previous one
+    bool merged = false;
+    if (it != c.ext.begin()) {
+      auto pv = std::prev(it);
+      if (!pv->second.used && pv->second.slab == x.slab && pv->first + pv->second.size == b) {
+        unindex(c, s.device, pv->first, pv->second.size);
+        pv->second.size += x.size;
+        c.ext.erase(it);
+        fi.emplace(pv->second.size, pv->first);
+        merged = true;
+      }
+    }
+    if (!merged) {
+      it->second = Ext{x.size, x.slab, false};
+      fi.emplace(x.size, b);
     }
   }
-  it->second = Ext{x.size, x.slab, false};
-  fi.emplace(x.size, b);
+  keep_headroom(sdev);
   return se;
 }
+
 
 void gs_devmem_stats(DevMemStats* out) {
   if (!out) return;

@@ -1140,9 +1140,13 @@ __global__ __launch_bounds__(kPPBlock) void k_rev_fill_range(const uint8_t* deg,
 // cost quadratically): k_pp_rfail_hubs walks them once instead.
 constexpr uint32_t kRfailScan = 64;
 
+// *hub = 1 when some failed caller has a friend whose in-list is longer than
+// kRfailScan: only then does k_pp_rfail_hubs walk the in-lists (ADVICE r05:
+// it read every rend entry, ~8 GB at N = 1e9, whether or not a hub existed).
 __global__ __launch_bounds__(kPPBlock) void k_pp_rfail(const DevState s, const unsigned long long* __restrict__ rend,
                                                        const uint32_t* __restrict__ rsrc,
-                                                       const uint8_t* __restrict__ rslot, uint32_t* __restrict__ rfail) {
+                                                       const uint8_t* __restrict__ rslot, uint32_t* __restrict__ rfail,
+                                                       uint32_t* __restrict__ hub) {
   for (uint64_t wd = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; wd < s.W;
        wd += (uint64_t)gridDim.x * blockDim.x) {
     for (unsigned long long m = s.crash[wd]; m; m &= m - 1) {
@@ -1152,7 +1156,10 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_rfail(const DevState s, const u
       for (uint32_t j = 0; j < d; ++j) {
         const uint32_t w = s.ids[v * s.stride + j];
         const unsigned long long qb = w ? rend[w - 1] : 0ull, qe = rend[w];
-        if (qe - qb > kRfailScan) continue;  // a hub: k_pp_rfail_hubs
+        if (qe - qb > kRfailScan) {  // a hub: k_pp_rfail_hubs
+          if (!*hub) atomicOr(hub, 1u);
+          continue;
+        }
         for (unsigned long long q = qb; q < qe; ++q)
           if (rsrc[q] == (uint32_t)v && (rslot[q] & 15u) == j) {
             atomicOr(&rfail[q >> 5], 1u << (q & 31));
@@ -1168,7 +1175,9 @@ __global__ __launch_bounds__(kPPBlock) void k_pp_rfail(const DevState s, const u
 // (linear in the hubs' in-degrees).
 __global__ __launch_bounds__(kPPBlock) void k_pp_rfail_hubs(const DevState s, const unsigned long long* __restrict__ rend,
                                                             const uint32_t* __restrict__ rsrc,
-                                                            uint32_t* __restrict__ rfail) {
+                                                            uint32_t* __restrict__ rfail,
+                                                            const uint32_t* __restrict__ hub) {
+  if (!*hub) return;  // no failed caller lists a hub
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -1711,13 +1720,14 @@ hipError_t pp_rev_fill_range(const uint8_t* deg, const uint32_t* ids, uint64_t n
 
 hipError_t pp_rfail_build(const DevState& s, const unsigned long long* rend, const uint32_t* rsrc,
                           const uint8_t* rslot, uint32_t* rfail, hipStream_t st) {
-  const uint64_t NW = (s.n * s.stride + 31) >> 5;  // at most
-  hipError_t e = hipMemsetAsync(rfail, 0, NW * 4, st);
+  const uint64_t NW = (s.n * s.stride + 31) >> 5;  // at most; word NW + 1 is the hub flag
+  uint32_t* hub = rfail + NW + 1;
+  hipError_t e = hipMemsetAsync(rfail, 0, (NW + 2) * 4, st);
   if (e != hipSuccess) return e;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>((s.W + kPPBlock - 1) / kPPBlock, 8192);
-  hipLaunchKernelGGL(k_pp_rfail, dim3(blocks ? blocks : 1), dim3(kPPBlock), 0, st, s, rend, rsrc, rslot, rfail);
+  hipLaunchKernelGGL(k_pp_rfail, dim3(blocks ? blocks : 1), dim3(kPPBlock), 0, st, s, rend, rsrc, rslot, rfail, hub);
   const uint32_t hblocks = (uint32_t)std::min<uint64_t>((s.n + 64 * (kPPBlock / 64) - 1) / (64 * (kPPBlock / 64)), 4096);
-  hipLaunchKernelGGL(k_pp_rfail_hubs, dim3(hblocks ? hblocks : 1), dim3(kPPBlock), 0, st, s, rend, rsrc, rfail);
+  hipLaunchKernelGGL(k_pp_rfail_hubs, dim3(hblocks ? hblocks : 1), dim3(kPPBlock), 0, st, s, rend, rsrc, rfail, hub);
   return hipGetLastError();
 }
 

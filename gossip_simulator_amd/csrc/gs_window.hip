@@ -1260,7 +1260,7 @@ __device__ __forceinline__ void stamp(const WinState& w, ResolveLds& sm, uint32_
 
 // GS_RESOLVE_PROBE=1 (timing probe builds only, results differ): k_resolve's
 // receipts phase skips the per-receipt (crashed, rolled) read, every node is
-// plain -- the floor of the b1 atomics alone (DESIGN.md section 4.4.1)
+// plain -- the floor of the b1 atomics alone (DESIGN.md section 4.4.2)
 #if defined(GS_RESOLVE_PROBE) && GS_RESOLVE_PROBE == 1
 #define GS_RESOLVE_CR0(loc) make_uint2(0u, 0u)
 #else

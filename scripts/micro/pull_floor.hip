@@ -1,5 +1,5 @@
 // Micro-benchmark: the floor of a receiver-driven ("pull") flood window at
-// N = 1e9.  A pull window makes every live receiver scan
+// N = 1e9 (docs/DESIGN_NOTEBOOK.md 4.4.2).  A pull window makes every live receiver scan
 // its in-edges (v, j) from the reverse table (rsrc u32 + rslot u8, as the
 // push-pull engine's) and ask whether the in-neighbour v fires in the window
 // and at which tick; only then can the sender-keyed drop digit be recomputed
