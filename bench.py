@@ -74,6 +74,10 @@ def parse():
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 node-range-sharded run")
     ap.add_argument("--c3-trials", type=int, default=10_000)
     ap.add_argument("--c3-batch", type=int, default=5000, help="trials per batched context")
+    ap.add_argument("--c3-members", type=int, default=4,
+                    help="C3: contexts of one rank's trials run at once on its GPU (gs_create_multi with the "
+                         "device repeated: every member builds and runs its batch on its own stream); 1 = "
+                         "one batch context renumbered batch after batch")
     ap.add_argument("--no-extensions", action="store_true",
                     help="skip the C5 extension runs (1%% failed mask, push-pull)")
     ap.add_argument("--shard-scaling", action="store_true",
@@ -229,6 +233,10 @@ def main():
     t0 = time.perf_counter()
     wins, stab = sim.build_overlay()
     overlay_s = time.perf_counter() - t0
+    # the build's wait inside hipMalloc: on a box whose previous process freed
+    # most of the HBM, the first large allocations wait seconds for that memory
+    # (DESIGN.md section 9); reported beside the wall time, not hidden
+    overlay_alloc_ms = gs.memory_stats()["alloc_ms"] - mem0["alloc_ms"]
     otm = sim.timing()
     ov_ticks = {"partition": int(otm["ov_part_ticks"]), "sort": int(otm["ov_sort_ticks"]),
                 "partition_fallbacks": int(otm["ov_part_fallbacks"])}
@@ -326,7 +334,8 @@ def main():
                    "ticks": ticks[-1], "status": STATUS[status],
                    "coverage": round(recv_last / a.n, 6),
                    "delivered_per_step": sent // a.steps,
-                   "messages_per_step": msgs, "overlay_s": round(overlay_s, 3), "overlay_ticks": ov_ticks,
+                   "messages_per_step": msgs, "overlay_s": round(overlay_s, 3),
+                   "overlay_alloc_ms": round(overlay_alloc_ms, 3), "overlay_ticks": ov_ticks,
                    "overlay_stabilised_ms": stab, "parallelism": f"trials{world}",
                    "transport": a.transport if world > 1 else None},
         "roofline": roof,
@@ -504,15 +513,18 @@ def pushpull_runs(a, gs, rank, local):
 
 def c3_trials(a, gs, rank, world, local, dist):
     """Config C3: a.c3_trials trials at N = 1e5 (reference defaults), each its
-    own GPU-built overlay and broadcast to its 99 % poll, split over the ranks
-    and run as batched contexts of a.c3_batch trials (all of a batch's
-    overlays, then all its broadcasts, at once).  Timed end to end: every
-    batch's renumbering, overlay, broadcast and results.  The batch contexts
-    (one per batch size, ~30 GB of device memory at 5,000 trials) are created
-    and run once before the timer, like the headline's warmup steps: right
-    after the previous legs free their 1e9-node contexts, their first
-    allocation stalled for ~5 s on some boxes of the pool
-    (profiles/r05e_c3_after.txt), which is no property of the trials."""
+    own GPU-built overlay and broadcast to its 99 % poll, split over the ranks.
+    A rank runs its trials as batched contexts: one context of up to
+    a.c3_members * a.c3_batch trials whose a.c3_members members (gs_create_multi
+    with the rank's device repeated) each build all their trials' overlays and
+    then run all their broadcasts at once, on their own streams, concurrently
+    (the per-tick kernels of a batched overlay leave the GPU half idle: four
+    members measured 0.91-0.97 s against 1.09 s for one 5,000-trial context
+    renumbered batch after batch, profiles/r06d_c3_members.txt).  Timed: every
+    batch's renumbering (gs_set_trial), overlay, broadcast and results.  The
+    contexts are created and run once before the timer, like the headline's
+    warmup steps; create_s / warmup_s report that setup and s_end_to_end adds
+    the creation to the batches."""
     import numpy as np
     import torch
     from dataclasses import replace
@@ -520,14 +532,24 @@ def c3_trials(a, gs, rank, world, local, dist):
     t0, t1 = gd.trial_range(a.c3_trials, rank, world)
     cfg = gs.Config(n=100_000, seed=a.seed, device=local)
 
-    # one context per batch size, renumbered batch after batch (gs_set_trial)
+    # one context per batch size, renumbered batch after batch (gs_set_trial);
+    # with --c3-members M a batch is M * c3_batch trials in ONE context whose M
+    # members (the same device repeated) build and run concurrently
+    M = max(1, a.c3_members)
+    step = a.c3_batch * M
+
+    def open_batch(b, T):
+        m = min(M, T)
+        c = replace(cfg, trial=b, trials=T)
+        return gs.Simulator(c, devices=[local] * m) if m > 1 else gs.Simulator(c)
+
     sims = {}
     create_s = warm_s = 0.0
-    for b in range(t0, t1, a.c3_batch):  # warmup: contexts, workspaces, code objects
-        T = min(b + a.c3_batch, t1) - b
+    for b in range(t0, t1, step):  # warmup: contexts, workspaces, code objects
+        T = min(b + step, t1) - b
         if T not in sims:
             tw = time.perf_counter()
-            sims[T] = gs.Simulator(replace(cfg, trial=b, trials=T))
+            sims[T] = open_batch(b, T)
             create_s += time.perf_counter() - tw
             sims[T].build_overlay()
             sims[T].broadcast_begin(-1)
@@ -541,8 +563,8 @@ def c3_trials(a, gs, rank, world, local, dist):
     start = time.perf_counter()
     rows = []
     try:
-        for b in range(t0, t1, a.c3_batch):
-            T = min(b + a.c3_batch, t1) - b
+        for b in range(t0, t1, step):
+            T = min(b + step, t1) - b
             sim = sims[T]
             sim.reset()
             sim.set_trial(b)
@@ -570,7 +592,7 @@ def c3_trials(a, gs, rank, world, local, dist):
     dt, sent, msgs, ntr, ncov = tot
     cov = res[res[:, 8] == 0]
     log(f"C3: {int(ntr)} trials in {dt:.2f} s ({int(ncov)} covered)")
-    return {"trials": int(ntr), "n": 100_000, "batch": a.c3_batch, "s_total": round(dt, 3),
+    return {"trials": int(ntr), "n": 100_000, "batch": a.c3_batch, "members": M, "s_total": round(dt, 3),
             "trials_per_s": round(ntr / dt, 1), "delivered_per_s": round(sent / dt, 1),
             "messages_per_s": round(msgs / dt, 1), "covered": int(ncov),
             "median_tick_99_rank0": int(np.median(cov[:, 1])) if len(cov) else None,
