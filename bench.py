@@ -377,6 +377,7 @@ def main():
     if rank == 0 and world == 1 and a.cpu_n > 0:
         cpu = cpu_baseline(a, gs)
     out.line["cpu_baseline"] = cpu
+    gs.trim()  # (see cpu_baseline) every rank gives its cached device blocks back before it exits
     out.emit()
     if dist is not None:
         dist.destroy_process_group()
@@ -889,6 +890,10 @@ def cpu_baseline(a, gs):
     with gs.Simulator(cfg) as s:
         s.build_overlay()
         deg, ids = s.read_peers()
+    # the GPU legs are over: hand the library's cached blocks back now, so the
+    # driver clears them while the CPU runs, not while the next process waits
+    # for its first allocations
+    gs.trim()
     p = O.make_params(n=n, fanout=a.fanout, fanin=a.fanin, delay_low=a.delaylow,
                       delay_high=a.delayhigh, drop_rate=a.droprate, crash_rate=a.crashrate,
                       seed=a.seed, trial=0)
