@@ -27,28 +27,37 @@ for mode in modes:
     sim = gs.Simulator(cfg, devices=[0] * int(mode[1:])) if mode != "seq" else gs.Simulator(cfg)
     create = time.perf_counter() - t0
 
+    split = [0.0, 0.0]
+
     def one_pass():
         rows = []
+        split[0] = split[1] = 0.0
         for b in ((0,) if mode != "seq" else range(0, total, 5000)):
             sim.reset()
             sim.set_trial(b)
+            a0 = time.perf_counter()
             sim.build_overlay()
+            a1 = time.perf_counter()
             sim.broadcast_begin(-1)
             sim.run(poll=10)
             rows.append(sim.trial_results())
+            split[0] += a1 - a0
+            split[1] += time.perf_counter() - a1
         return np.concatenate(rows)
 
     w0 = time.perf_counter()
     one_pass()
     warm = time.perf_counter() - w0
-    best = []
+    best, splits = [], []
     for _ in range(2):
         s0 = time.perf_counter()
         res = one_pass()
         best.append(time.perf_counter() - s0)
+        splits.append(f"overlay {split[0]:.3f} + broadcast {split[1]:.3f}")
     sim.close()
     same = "n/a" if want is None else bool(np.array_equal(res, want))
     if want is None:
         want = res
     print(f"C3 {mode}: {len(res)} trials, create {create:.3f} s, first pass {warm:.3f} s, "
-          f"timed passes {', '.join(f'{x:.3f}' for x in best)} s, equal to first mode: {same}", flush=True)
+          f"timed passes {', '.join(f'{x:.3f}' for x in best)} s ({'; '.join(splits)}), equal to first mode: {same}",
+          flush=True)
