@@ -247,6 +247,9 @@ int alloc_window(gs_ctx* c) {
   w.base = (uint32_t)c->lo;
   w.tlog = c->tlog;
   w.tmask = c->tlog >= 32 ? ~0u : (1u << c->tlog) - 1;
+  // a batched context's fine buckets are whole-trial runs of 2^(tlog-14) with
+  // the last ones of each trial partly or wholly past its n nodes
+  w.tnodes = c->trials > 1 && c->tlog <= kCoarseShift && !c->shard ? (uint32_t)c->p.n : 0u;
   w.G = c->G;
   w.rank = c->rank;
   w.seg_per = (uint32_t)c->seg_per;
@@ -343,6 +346,40 @@ void plan_coarse(gs_ctx* c, uint64_t T, const unsigned long long* exact) {
       if (b >= w.ncoarse) continue;
       a += exact ? exact[r] : sub;
     }
+  }
+  c->h_cap[kRegions] = a;
+}
+
+// Batched trials (trials > 1, tlog <= kCoarseShift): a message never leaves
+// its sender's trial, so it lands in the sender's coarse bin, and the
+// sub-region it goes to is the XCD whose rounds expanded the sender
+// (xcd_rounds in gs_window.hip).  fb[b] = the first firing index of bin b
+// (bins are contiguous in the bucket-major unit order), fb[ncoarse] = Tn.
+// Region (b, x) gets an exact upper bound -- the window's firing nodes of bin
+// b in XCD x's rounds, times the row length -- so it never overflows: the
+// node-share estimate of plan_coarse assumed targets spread over every bin
+// and overflowed almost every window of a C3 batch (each then expanded three
+// times: estimate, count, redo).
+void plan_coarse_trials(gs_ctx* c, const unsigned long long* fb, unsigned long long Tn) {
+  const WinState& w = c->ws;
+  uint32_t per_round = 0;
+  const uint32_t blocks = win_expand_geometry(w, Tn, &per_round, nullptr, nullptr);
+  const unsigned long long rounds = (Tn + per_round - 1) / per_round;
+  const bool by_xcd = blocks && (blocks & 7) == 0;
+  const unsigned long long per = (rounds + 7) >> 3;
+  std::vector<unsigned long long> cap(kRegions, 0);
+  for (uint32_t b = 0; b < w.ncoarse; ++b) {
+    const unsigned long long lo = fb[b], hi = fb[b + 1];
+    for (unsigned long long r = lo / per_round; lo < hi && r * per_round < hi; ++r) {
+      const unsigned long long a = std::max(lo, r * per_round), e = std::min(hi, (r + 1) * per_round);
+      const uint32_t x = by_xcd ? (uint32_t)std::min<unsigned long long>(r / per, 7) : (uint32_t)((r % blocks) & 7);
+      cap[b * kCoarseSub + x] += (e - a) * w.slots;
+    }
+  }
+  unsigned long long a = 0;
+  for (uint32_t r = 0; r < kRegions; ++r) {
+    c->h_cap[r] = a;
+    a += cap[r] ? cap[r] + 16 : 0;
   }
   c->h_cap[kRegions] = a;
 }
@@ -2161,6 +2198,9 @@ int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing, uint64_t tchunk
   // Receipts per fine bucket are ~density * 16384 whatever N is; a window whose
   // slots would overflow k_resolve's LDS message buffer on average is cut short.
   const uint64_t slot_budget = (uint64_t)w.nfine * kWinSlotsPerBucket;
+  // batched trials: each coarse bin's first firing index comes back with the
+  // window's fire counts (plan_coarse_trials)
+  const bool trial_plan = c->trials > 1 && c->tlog <= kCoarseShift && !c->shard;
   while (done < n) {
     const uint32_t Lw = std::min(Lmax, n - done);
     const uint32_t t = (uint32_t)(t0 + done);
@@ -2174,6 +2214,9 @@ int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing, uint64_t tchunk
       need = c->tmp.bytes;
       CK(c, win_scan_units(w, Lu, c->tmp.p, need, c->stream));
       CK(c, hipMemcpyAsync(c->h_misc, w.tfires, kMaxWindow * 8, hipMemcpyDeviceToHost, c->stream));
+      if (trial_plan)
+        CK(c, hipMemcpy2DAsync(c->h_misc + kMaxWindow, 8, w.unit_off, (size_t)256 * Lu * 8, 8, w.ncoarse,
+                               hipMemcpyDeviceToHost, c->stream));
       CK(c, hipStreamSynchronize(c->stream));
       return GS_OK;
     };
@@ -2185,7 +2228,15 @@ int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing, uint64_t tchunk
     // units are bucket-major: a cut window is laid out again for its L ticks
     if (L < Lw) RC(units(L));
     const unsigned long long T = Tn * w.stride;  // friend slots of the firing nodes
-    plan_coarse(c, T, nullptr);
+    if (trial_plan && Tn) {
+      // batched trials: exact per-(bin, XCD) bounds from the bins' first firing
+      // indices (unit_off at every 256 * L-th unit, copied by units())
+      std::vector<unsigned long long> fb(c->h_misc + kMaxWindow, c->h_misc + kMaxWindow + w.ncoarse);
+      fb.push_back(Tn);
+      plan_coarse_trials(c, fb.data(), Tn);
+    } else {
+      plan_coarse(c, T, nullptr);
+    }
     const uint64_t fcap = T + T / 8 + (uint64_t)w.ncoarse * 256 * 513 + 16;
     if (!grow(c->gmap, ((Tn + 63) / 64 + 1) * 4) || !grow(c->cmsg, (c->h_cap[kRegions] + 16) * 4) ||
         !grow(c->fmsg, (fcap + 16) * 4))  // buf_cap(fmsg) >= fcap (the device-driven windows' bound)

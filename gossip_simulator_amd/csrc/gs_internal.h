@@ -215,6 +215,7 @@ struct WinState {
   // trial is key.trial + (g >> tlog) (tlog = 32: one trial)
   uint32_t base;
   uint32_t tlog, tmask;
+  uint32_t tnodes;  // batched trials: nodes per trial (k_plan's fine estimate); 0: one trial
   Key key;
 };
 constexpr uint32_t kStatShards = 32;  // per-window counter copies (k_close reads them all: 32 KB)
@@ -258,6 +259,9 @@ hipError_t win_scan_units(const WinState& w, uint32_t L, void* tmp, size_t& tmp_
 hipError_t win_groupmap(const WinState& w, uint32_t L, hipStream_t s);
 hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, int mode,
                       hipStream_t s);
+// win_expand's grid for Tn firing nodes (returned) and firing nodes per round
+uint32_t win_expand_geometry(const WinState& w, uint64_t Tn, uint32_t* per_round, uint32_t* bsz,
+                             uint32_t* npt);
 hipError_t win_plan(const WinState& w, bool exact, hipStream_t s);
 hipError_t win_scan_fine(const WinState& w, void* tmp, size_t& tmp_bytes, hipStream_t s);
 hipError_t win_part2(const WinState& w, uint64_t T, bool scatter, hipStream_t s);

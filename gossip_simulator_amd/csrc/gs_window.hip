@@ -1042,6 +1042,45 @@ __device__ __forceinline__ void plan_body(const WinState& w, bool exact) {
   // device-driven windows: regions past the buffer are empty, and the window
   // is flagged for the host to grow the buffer and redo it
   const unsigned long long cap = w.ctl ? w.ctl->fmsg_cap : ~0ull;
+  if (w.tnodes) {
+    // batched trials: a coarse bucket is whole trials of bpt fine buckets, the
+    // first `full` of them full, one partial (rem nodes), the rest empty (ids
+    // past the trial's n); a message stays in its trial, so a fine bucket's
+    // share of the coarse count is its share of the nodes, not 1/256 (the
+    // uniform share under-planned every full bucket by n / 2^tlog and sent most
+    // dense windows of a C3 batch to the exact redo)
+    const uint32_t bpt = 1u << (w.tlog - kFineLog);
+    const uint32_t full = w.tnodes >> kFineLog, rem = w.tnodes & (kFineNodes - 1);
+    __syncthreads();
+    if (tid < w.ncoarse) {  // s_cap[c] = one trial's capacity in bucket c
+      const uint32_t nf = min(256u, w.nfine - tid * 256);
+      const unsigned long long nodes = (unsigned long long)(nf / bpt) * w.tnodes;
+      const unsigned long long cf = (cnt * 9 * kFineNodes + 8 * nodes - 1) / (8 * nodes) + 512;
+      const unsigned long long cr = rem ? (cnt * 9 * rem + 8 * nodes - 1) / (8 * nodes) + 512 : 0;
+      s_cap[tid] = full * cf + cr;
+      s_tp[tid] = (uint32_t)(nf / bpt);
+      s_base[tid] = cf;  // (s_base is rebuilt below)
+      fl[0] = cr;
+    }
+    __syncthreads();
+    __shared__ unsigned long long s_cf[256], s_cr[256];
+    if (tid < w.ncoarse) { s_cf[tid] = s_base[tid]; s_cr[tid] = fl[0]; }
+    unsigned long long tb2;
+    const unsigned long long btot = tid < w.ncoarse ? s_tp[tid] * s_cap[tid] : 0ull;
+    __syncthreads();
+    s_base[tid] = block_exscan256_u64(btot, s_x, &tb2);
+    if (tid == 0) s_base[256] = tb2;
+    __syncthreads();
+    if (w.ctl && blockIdx.x == 0 && tid == 0 && s_base[w.ncoarse] > cap) atomicOr(w.err, kErrFine);
+    for (uint32_t f = blockIdx.x * blockDim.x + tid; f <= w.nfine; f += gridDim.x * blockDim.x) {
+      const uint32_t c = f >> 8, d = f & 255, q = d / bpt, j = d % bpt;
+      const unsigned long long x =
+          f == w.nfine ? s_base[w.ncoarse]
+                       : s_base[c] + q * s_cap[c] + min(j, full) * s_cf[c] + (j > full ? s_cr[c] : 0ull);
+      w.fstart[f] = x < cap ? x : cap;
+    }
+    return;
+  }
   if (w.ctl && blockIdx.x == 0 && tid == 0 && s_base[w.ncoarse] > cap) atomicOr(w.err, kErrFine);
   for (uint32_t f = blockIdx.x * blockDim.x + tid; f <= w.nfine; f += gridDim.x * blockDim.x) {
     const uint32_t c = f >> 8, d = f & 255;
@@ -2380,8 +2419,12 @@ hipError_t win_groupmap(const WinState& w, uint32_t L, hipStream_t s) {
 }
 
 // mode 0: count coarse buckets only; 1: write + per-tick stats; 2: write only
-hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, int mode,
-                      hipStream_t s) {
+// k_expand's launch geometry for a window of Tn firing nodes: firing nodes per
+// round, workgroup size, grid.  One source for win_expand and for the host's
+// per-XCD region plan of batched trials (plan_coarse_trials, gs_api.cpp),
+// which must know which sub-region each round writes (xcd_rounds).
+uint32_t win_expand_geometry(const WinState& w, uint64_t Tn, uint32_t* per_round_out, uint32_t* bsz_out,
+                             uint32_t* npt_out) {
   // rows of <= 6 (C5's fanin 6) and <= 8 slots: 4 nodes per thread; LDS holds
   // block * 4 * row slots, so 6-slot rows fit four workgroups per CU
   // GS_XNPT=2: two firing nodes per thread (experiment: LDS and VGPRs for 8 workgroups per CU)
@@ -2417,6 +2460,18 @@ hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, i
   // 1024 rounds per workgroup, <= 4096 nodes and 32768 sends per thread)
   const uint64_t grid_cap = std::max<uint64_t>(rs <= 8 ? cap * kExpandBlock / bsz : 8192, (rounds + 1023) / 1024);
   const uint32_t blocks = (uint32_t)std::min<uint64_t>(rounds, grid_cap);
+  if (per_round_out) *per_round_out = per_round;
+  if (bsz_out) *bsz_out = bsz;
+  if (npt_out) *npt_out = npt;
+  return blocks;
+}
+
+hipError_t win_expand(const WinState& w, uint32_t t0, uint32_t L, uint64_t Tn, int mode,
+                      hipStream_t s) {
+  uint32_t per_round = 0, bsz = 0, npt = 0;
+  const uint32_t blocks = win_expand_geometry(w, Tn, &per_round, &bsz, &npt);
+  const uint32_t rs = w.slots;
+  (void)per_round;
   const dim3 grid(blocks ? blocks : 1), blk(kExpandBlock);
   const unsigned long long tn = Tn;
   const int st = mode == 1 ? 1 : 0;
