@@ -91,7 +91,8 @@ class Timing(C.Structure):
                 ("pp_answer_rounds", C.c_uint64), ("dd_fallbacks", C.c_uint64), ("pp_rev_part", C.c_uint64),
                 ("ov_part_ticks", C.c_uint64), ("ov_sort_ticks", C.c_uint64), ("ov_part_fallbacks", C.c_uint64),
                 ("alloc_ms", C.c_double), ("largest_alloc_ms", C.c_double), ("free_ms", C.c_double),
-                ("alloc_calls", C.c_uint64), ("alloc_cache_hits", C.c_uint64), ("cached_bytes", C.c_uint64)]
+                ("alloc_calls", C.c_uint64), ("alloc_cache_hits", C.c_uint64), ("cached_bytes", C.c_uint64),
+                ("coarse_redos", C.c_uint64)]
 
 
 # gs_exchange (gossip.h): host callbacks of a gs_create_rank_exchange rank

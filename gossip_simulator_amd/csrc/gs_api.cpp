@@ -2265,6 +2265,7 @@ int run_windows(gs_ctx* c, uint64_t t0, uint32_t n, bool timing, uint64_t tchunk
       CK(c, hipStreamSynchronize(c->stream));
       uint32_t err = (uint32_t)c->h_misc[0];
       if (err & kErrCoarse) {
+        ++c->timing.coarse_redos;
         CK(c, hipMemsetAsync(w.chist, 0, kRegions * 8, c->stream));
         CK(c, win_expand(w, t, L, Tn, 0, c->stream));
         CK(c, hipMemcpyAsync(c->h_misc, w.chist, kRegions * 8, hipMemcpyDeviceToHost, c->stream));

@@ -144,6 +144,8 @@ typedef struct gs_timing {
   uint64_t alloc_calls;      /* hipMalloc calls                                                 */
   uint64_t alloc_cache_hits; /* device buffers served from the cache (no hipMalloc)             */
   uint64_t cached_bytes;     /* bytes the cache holds free now                                  */
+  uint64_t coarse_redos;     /* window engine, host-driven windows: windows whose k_expand overflowed
+                              * a coarse region estimate and ran again from exact counts (cumulative) */
 } gs_timing;
 
 /* gs_run status */

@@ -310,6 +310,23 @@ def test_c3_batch_of_5000_matches_single_trials(gs):
             assert np.array_equal(res[t], want), f"trial {b + t}: {res[t]} vs {want}"
 
 
+def test_batched_trial_windows_never_redo_their_coarse_plan(gs):
+    """Round 6: a batched context's messages stay in
+    their sender's trial, so each (coarse bin, XCD) region gets an exact
+    upper bound from the window's firing nodes and never overflows -- the
+    node-share estimate sent most windows of a C3 batch through an exact
+    recount and a second expand.  400 trials of N = 1e5 (50 coarse bins,
+    trials at different phases in every window)."""
+    with gs.Simulator(cfg(gs, n=100_000, trials=400)) as sim:
+        sim.build_overlay()
+        sim.broadcast_begin(-1)
+        sim.run(poll=10)
+        res = sim.trial_results()
+        tm = sim.timing()
+    assert tm["coarse_redos"] == 0, tm["coarse_redos"]
+    assert len(res) == 400 and int((res[:, 8] == 0).sum()) > 0
+
+
 def test_batched_trials_injected_match_oracle_1e5(gs, oracle):
     """Config C3 size (N = 1e5), three trials: oracle overlay and oracle
     broadcast per trial vs one batched context fed the oracle's tables."""
