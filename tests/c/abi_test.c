@@ -75,6 +75,13 @@ static int cpu_checks(void) {
   CHECK(gs_threshold(0.29) == 28 && gs_threshold(0.001) == 0, "Go int(rate*100)");
   CHECK(gs_last_error(NULL) != NULL, "gs_last_error(NULL)");
   gs_destroy(NULL);
+  /* the device-memory cache without a device: nothing cached, nothing to trim */
+  gs_timing mt;
+  CHECK(gs_memory_stats(NULL) == GS_EINVAL, "gs_memory_stats(NULL)");
+  CHECK(gs_memory_stats(&mt) == GS_OK && mt.cached_bytes == 0 && mt.deliver_ms == 0.0, "gs_memory_stats");
+  size_t released = 1;
+  CHECK(gs_trim(-1, &released) == GS_OK && released == 0, "gs_trim on an empty cache");
+  CHECK(gs_trim(0, NULL) == GS_OK, "gs_trim(0, NULL)");
   return failures;
 }
 
@@ -156,6 +163,13 @@ static int gpu_checks(void) {
     ring_run(c, n, g == 1 ? "multi(1)" : "multi(2)");
     gs_destroy(c);
   }
+  /* the destroyed contexts' large blocks are cached; gs_trim hands them back */
+  gs_timing mt;
+  CHECK(gs_memory_stats(&mt) == GS_OK && mt.alloc_calls > 0, "gs_memory_stats after runs");
+  size_t released = 0;
+  CHECK(gs_trim(-1, &released) == GS_OK, "gs_trim");
+  CHECK(gs_memory_stats(&mt) == GS_OK && mt.cached_bytes == 0, "cache empty after gs_trim (%llu bytes left)",
+        (unsigned long long)mt.cached_bytes);
   return failures;
 }
 
