@@ -142,6 +142,32 @@ void release(Cache& c, const std::vector<char*>& blocks) {
 
 }  // namespace
 
+namespace {
+// Best-fit from the free extents of `dev` (caller holds c.mu).  With `picky`,
+// an extent more than 4x the request (and more than 1 GiB over it) is left
+// alone: a small buffer carved out of a big free slab pins the slab, which can
+// then never be returned to the driver when a big request needs the room.
+char* take_cached(Cache& c, int dev, size_t need, bool picky) {
+  auto& fi = c.freeix[dev];
+  auto it = fi.lower_bound(need);
+  if (it == fi.end()) return nullptr;
+  if (picky && it->first > 4 * need && it->first - need > (1ull << 30)) return nullptr;
+  char* b = it->second;
+  fi.erase(it);
+  Ext& x = c.ext[b];
+  if (x.size - need >= kGran) {  // split: the tail stays free
+    c.ext[b + need] = Ext{x.size - need, x.slab, false};
+    fi.emplace(x.size - need, b + need);
+    x.size = need;
+  }
+  x.used = true;
+  c.slab[x.slab].used += x.size;
+  c.st.cached_bytes -= x.size;
+  ++c.st.cache_hits;
+  return b;
+}
+}  // namespace
+
 hipError_t gs_dev_malloc(void** p, size_t bytes) {
   if (!p) return hipErrorInvalidValue;
   Cache& c = cache();
@@ -152,21 +178,7 @@ hipError_t gs_dev_malloc(void** p, size_t bytes) {
   const size_t need = (bytes + kGran - 1) & ~(kGran - 1);
   {
     std::lock_guard<std::mutex> g(c.mu);
-    auto& fi = c.freeix[dev];
-    auto it = fi.lower_bound(need);
-    if (it != fi.end()) {
-      char* b = it->second;
-      fi.erase(it);
-      Ext& x = c.ext[b];
-      if (x.size - need >= kGran) {  // split: the tail stays free
-        c.ext[b + need] = Ext{x.size - need, x.slab, false};
-        fi.emplace(x.size - need, b + need);
-        x.size = need;
-      }
-      x.used = true;
-      c.slab[x.slab].used += x.size;
-      c.st.cached_bytes -= x.size;
-      ++c.st.cache_hits;
+    if (char* b = take_cached(c, dev, need, true)) {
       *p = b;
       return hipSuccess;
     }
@@ -185,17 +197,31 @@ hipError_t gs_dev_malloc(void** p, size_t bytes) {
   }
   void* q = nullptr;
   e = timed_malloc(c, &q, need);
-  if (e != hipSuccess) {  // trim everything of this device and retry once
+  if (e != hipSuccess) {
+    // no room: any cached extent that fits, however big; then every fully free
+    // slab back to the driver and one more try
     (void)hipGetLastError();
     std::vector<char*> t;
     {
       std::lock_guard<std::mutex> g(c.mu);
+      if (char* b = take_cached(c, dev, need, false)) {
+        *p = b;
+        return hipSuccess;
+      }
       t = collect_trim(c, dev);
     }
     if (t.empty()) return e;
     release(c, t);
     e = timed_malloc(c, &q, need);
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      std::lock_guard<std::mutex> g(c.mu);
+      if (char* b = take_cached(c, dev, need, false)) {  // (another thread freed one meanwhile)
+        *p = b;
+        return hipSuccess;
+      }
+      return e;
+    }
   }
   std::lock_guard<std::mutex> g(c.mu);
   c.slab.push_back(Slab{(char*)q, need, dev, need});

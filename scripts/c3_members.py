@@ -5,6 +5,7 @@
         broadcasts concurrently, each on its own stream (par_members)
 Each is created and run once untimed, then timed end to end for one pass over
 all trials (overlay + broadcast + results); the trial tables must be equal.
+  mMp   the same with the batched overlay ticks partitioned (GS_OV_PART_BATCHED=1)
 Usage: python scripts/c3_members.py [total] [modes...]"""
 import os
 import sys
@@ -22,9 +23,16 @@ gs.load()
 hip = _lib.load()
 want = None
 for mode in modes:
+    # a trailing "p": batched overlay ticks by the destination partition
+    # (GS_OV_PART_BATCHED=1, read per build) instead of the radix sort
+    if mode.endswith("p"):
+        os.environ["GS_OV_PART_BATCHED"] = "1"
+    else:
+        os.environ.pop("GS_OV_PART_BATCHED", None)
+    members = int(mode[1:].rstrip("p")) if mode[0] == "m" else 1
     cfg = gs.Config(n=100_000, seed=0x5EED, trial=0, trials=total if mode != "seq" else 5000)
     t0 = time.perf_counter()
-    sim = gs.Simulator(cfg, devices=[0] * int(mode[1:])) if mode != "seq" else gs.Simulator(cfg)
+    sim = gs.Simulator(cfg, devices=[0] * members) if mode != "seq" else gs.Simulator(cfg)
     create = time.perf_counter() - t0
 
     split = [0.0, 0.0]
