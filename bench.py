@@ -501,6 +501,13 @@ def pushpull_runs(a, gs, rank, local):
             # passes of the partition build over the coarse bins (sized to the largest block the
             # device allocator can give without a hipFree; 0 = the atomic build)
             "rev_table_passes": rev_passes}
+        # the same broadcast polled after every round instead of main's 10-tick
+        # poll (simulator.go:243): push-pull is round-synchronous, so this is its
+        # exact rounds-to-99 % and the rounds the 10-tick poll adds past it
+        # (late bottom-up rounds, ~1.8 ms each); ms_per_step above keeps poll 10
+        tot1, st1, dt1 = timed_broadcast(sim, poll=1)
+        out["pushpull"]["poll_every_round"] = {"ms": round(dt1 * 1e3, 3), "rounds_to_99": tot1["tick"],
+                                               "messages": tot1["messages"], "status": STATUS[st1]}
         sim.reset()
         sim.set_failed(failed_mask(a.n, 0.01, a.seed + 1))
         tot, status, dt = timed_broadcast(sim)
