@@ -377,7 +377,9 @@ template <bool ROW8, uint32_t STAGED>  // STAGED 1: keys in LDS, rows batched; 2
 __global__ __launch_bounds__(kProcBlock) void k_process(const OvParams p, uint64_t t0, uint64_t* keys, uint64_t m,
                                                         uint8_t* deg, uint32_t* ids, uint64_t* eout,
                                                         uint16_t* eslot, unsigned long long* ecount,
-                                                        unsigned long long* counts, TickCounters* tc) {
+                                                        unsigned long long* counts, TickCounters* tc,
+                                                        const uint32_t* skip) {
+  if (skip && *skip) return;  // (the destination partition overflowed: the host sorts the tick)
   constexpr uint32_t kTile = kProcBlock * kProcIPT, kStage = STAGED ? kTile + kProcLook : 1;
   __shared__ uint64_t s_ev[kEmitCap];
   __shared__ uint16_t s_sl[kEmitCap];
@@ -555,6 +557,42 @@ struct OvPart {
   const unsigned long long* cstart;    // [ncb * kOvSub + 1] coarse sub-region (c, x) starts in P1's output
 };
 
+// A wave's LDS counter increments, one atomic per DISTINCT digit: the lanes
+// of the lowest pending lane's digit are ranked together (ballot + mbcnt)
+// and leave, until none is pending.  A batched bucket is a sequence of
+// single-trial chunks (each k_process workgroup appends its emitted events at
+// once, ~100 per bucket, in no trial order), so a wave's 64 consecutive keys
+// fall in one or two trials: the per-trial count pass took 70.7 -> 27.4 ms
+// per two C3 builds with it (profiles/r06o_*).  Not for waves that hold
+// several digits: in P2 (~8 fine regions per wave) it cost 60 -> 145 ms, and
+// P1 was unchanged.
+// Every lane of the wave calls it; returns the lane's rank among its digit's
+// keys (0 for an invalid lane).
+template <bool RET>
+__device__ __forceinline__ uint32_t peel_rank(uint32_t* cnt, uint32_t d, bool valid) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t rank = 0;
+  unsigned long long todo = __ballot(valid);
+  while (todo) {
+    const uint32_t leader = (uint32_t)__ffsll((long long)todo) - 1;
+    const uint32_t ld = (uint32_t)__shfl((int)d, (int)leader, 64);
+    const bool mine = valid && d == ld;
+    const unsigned long long peers = __ballot(mine);
+    uint32_t base = 0;
+    if (lane == leader) {
+      if (RET) base = atomicAdd(&cnt[ld], (uint32_t)__popcll(peers));
+      else atomicAdd(&cnt[ld], (uint32_t)__popcll(peers));
+    }
+    if (RET) {
+      base = (uint32_t)__shfl((int)base, (int)leader, 64);
+      if (mine)
+        rank = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
+    }
+    todo &= ~peers;
+  }
+  return rank;
+}
+
 // P1's tile t writes sub-region t % kOvSub of each coarse region: (c, x) is
 // [cstart[c * kOvSub + x], cstart[c * kOvSub + x + 1]).
 __device__ __forceinline__ void ov_sub(const OvPart& a, uint32_t c, uint32_t x, unsigned long long& start,
@@ -692,11 +730,15 @@ __global__ __launch_bounds__(kOvTrialBlock) void k_ov_count(const uint64_t* keys
   for (uint32_t i = threadIdx.x; i < ntr; i += kOvTrialBlock) h[i] = 0;
   for (uint32_t i = threadIdx.x; i < ncb * kOvSub; i += kOvTrialBlock) hc[i] = 0;
   __syncthreads();
-  for (uint64_t i = (uint64_t)blockIdx.x * kOvTrialBlock + threadIdx.x; i < m; i += (uint64_t)gridDim.x * kOvTrialBlock) {
-    const uint64_t dst = keys[i] >> sh;
-    atomicAdd(&h[min((uint32_t)(dst >> tlog), ntr - 1)], 1u);
+  // block-uniform trip count (peel_rank: every lane of a wave takes part);
+  // a wave's keys lie in one or two trials: one atomic per distinct counter
+  for (uint64_t i0 = (uint64_t)blockIdx.x * kOvTrialBlock; i0 < m; i0 += (uint64_t)gridDim.x * kOvTrialBlock) {
+    const uint64_t i = i0 + threadIdx.x;
+    const bool in = i < m;
+    const uint64_t dst = in ? keys[i] >> sh : 0ull;
+    peel_rank<false>(h, min((uint32_t)(dst >> tlog), ntr - 1), in);
     const uint32_t c = min((uint32_t)(dst >> (kOvFineLog + 8)), ncb - 1), x = (uint32_t)(i / kOvpTile) % kOvSub;
-    atomicAdd(&hc[c * kOvSub + x], 1u);
+    peel_rank<false>(hc, c * kOvSub + x, in);
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < ntr; i += kOvTrialBlock)
@@ -1193,6 +1235,9 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
       {
         uint64_t* keys = nullptr;
         uint64_t mproc = m;
+        uint32_t* d_pflag = nullptr;  // the partition's overflow flag (k_process stands down on it)
+        uint64_t p_ncb = 0, p_nfb = 0;
+        unsigned long long* d_pcfill = nullptr;
         bool plan_ok = part_ok && m >= 32 * ((ntot + kOvFineMax - 1) >> kOvFineLog);
         const uint64_t ncb0 = (((ntot + kOvFineMax - 1) >> kOvFineLog) + 255) / 256;
         plan_ok = plan_ok && ncb0 <= 256;
@@ -1256,69 +1301,81 @@ int overlay_build(uint64_t n, uint32_t trials, uint32_t tlog, int32_t fanout, in
                              (const unsigned long long*)(d_cfill + ncb * kOvSub), (const unsigned long long*)d_fbase,
                              p.B + 1 + p.TB);
           OVCHK(hipGetLastError());
-          OVCHK(hipMemcpyAsync(&h_flag, d_flag, 4, hipMemcpyDeviceToHost, stream));
-          OVCHK(hipStreamSynchronize(stream));
-          if (!h_flag) {
-            keys = (uint64_t*)fine.p;  // m keys (no region overflowed: every key was placed)
-            ++ws->part_ticks;
-          } else {
-            ++ws->part_fallbacks;  // a region overflowed its plan: sort this tick
-            if (ov_debug) {  // which level overflowed, by how much
-              std::vector<unsigned long long> cf(ncb * kOvSub), ff(nfb);
-              OVCHK(hipMemcpy(cf.data(), d_cfill, cf.size() * 8, hipMemcpyDeviceToHost));
-              OVCHK(hipMemcpy(ff.data(), d_cfill + ncb * kOvSub, ff.size() * 8, hipMemcpyDeviceToHost));
-              double worst_c = 0, worst_f = 0;
-              uint64_t nc = 0, nf = 0;
-              for (uint64_t c = 0; c < ncb; ++c) {
-                for (uint32_t x = 0; x < kOvSub; ++x) {
-                  const uint64_t cap = plan.cstart[c * kOvSub + x + 1] - plan.cstart[c * kOvSub + x];
-                  const double r = cap ? (double)cf[c * kOvSub + x] / cap : 1e9;
-                  if (cf[c * kOvSub + x] > cap) ++nc;
-                  worst_c = std::max(worst_c, r);
-                }
-              }
-              for (uint64_t f = 0; f < nfb; ++f) {
-                const uint64_t cap = plan.fstart[f + 1] - plan.fstart[f];
-                if (ff[f] > cap) ++nf;
-                worst_f = std::max(worst_f, cap ? (double)ff[f] / cap : (ff[f] ? 1e9 : 0));
-              }
-              fprintf(stderr, "[overlay] tick %llu: m=%llu partition fallback: %llu coarse / %llu fine regions over, "
-                      "worst fill/cap %.3f / %.3f\n", (unsigned long long)t0, (unsigned long long)m,
-                      (unsigned long long)nc, (unsigned long long)nf, worst_c, worst_f);
-            }
+          // no host round trip here: k_process reads the flag (a region
+          // over its plan) and stands down; the tick's sync below sees it
+          keys = (uint64_t*)fine.p;  // m keys (when no region overflowed)
+          d_pflag = d_flag;
+          p_ncb = ncb;
+          p_nfb = nfb;
+          d_pcfill = d_cfill;
+        }
+        for (;;) {
+          if (!keys) {
+            // by (destination, tag): each destination's run comes out tick by
+            // tick, and the process kernel orders each tick's few events by
+            // (src, kind) itself (sorting by destination only left runs of L
+            // ticks to the insertion sort, in global memory: slower than the
+            // TB extra radix bits)
+            OVCHK(grow(scratch, m * 8, stream));
+            rocprim::double_buffer<uint64_t> db((uint64_t*)bucket[s].p, (uint64_t*)scratch.p);
+            const unsigned begin_bit = p.B + 1, end_bit = 2 * p.B + 1 + p.TB;
+            size_t sort_bytes = 0;
+            OVCHK(rocprim::radix_sort_keys<OvRadix>(nullptr, sort_bytes, db, (size_t)m, begin_bit, end_bit, stream));
+            OVCHK(grow(cub_tmp, sort_bytes, stream));
+            sort_bytes = cub_tmp.bytes;
+            OVCHK(rocprim::radix_sort_keys<OvRadix>(cub_tmp.p, sort_bytes, db, (size_t)m, begin_bit, end_bit, stream));
+            keys = db.current();
+            if (db.current() != (uint64_t*)bucket[s].p) std::swap(bucket[s], scratch);
+            ++ws->sort_ticks;
           }
+          const uint64_t per = (uint64_t)kProcBlock * kProcIPT;
+          const dim3 pgrid((uint32_t)((mproc + per - 1) / per));
+          auto* pk = row8 ? (staged == 2 ? k_process<true, 2> : staged ? k_process<true, 1> : k_process<true, 0>)
+                          : (staged == 2 ? k_process<false, 2> : staged ? k_process<false, 1> : k_process<false, 0>);
+          hipLaunchKernelGGL(pk, pgrid, dim3(kProcBlock), 0, stream, p, t0, keys, mproc, d_deg, d_ids,
+                             (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_nemit, d_counts, d_tc,
+                             (const uint32_t*)d_pflag);
+          OVCHK(hipGetLastError());
+          OVCHK(hipMemcpyAsync(&h_ne, d_nemit, 8, hipMemcpyDeviceToHost, stream));
+          OVCHK(ctr_d2h(h_counts.data(), d_counts));
+          OVCHK(hipMemcpyAsync(&h_tc, d_tc, sizeof(h_tc), hipMemcpyDeviceToHost, stream));
+          OVCHK(hipMemsetAsync(d_nemit, 0, 8, stream));
+          if (d_pflag) OVCHK(hipMemcpyAsync(&h_flag, d_pflag, 4, hipMemcpyDeviceToHost, stream));
+          OVCHK(hipStreamSynchronize(stream));
+          if (d_pflag && !h_flag) ++ws->part_ticks;
+          if (!d_pflag || !h_flag) break;
+          // a region overflowed its plan: k_process did nothing (its counters
+          // are still zero); sort this tick from its intact bucket
+          ++ws->part_fallbacks;
+          if (ov_debug) {  // which level overflowed, by how much
+            const uint64_t ncb = p_ncb, nfb = p_nfb;
+            unsigned long long* d_cfill = d_pcfill;
+            std::vector<unsigned long long> cf(ncb * kOvSub), ff(nfb);
+            OVCHK(hipMemcpy(cf.data(), d_cfill, cf.size() * 8, hipMemcpyDeviceToHost));
+            OVCHK(hipMemcpy(ff.data(), d_cfill + ncb * kOvSub, ff.size() * 8, hipMemcpyDeviceToHost));
+            double worst_c = 0, worst_f = 0;
+            uint64_t nc = 0, nf = 0;
+            for (uint64_t c = 0; c < ncb; ++c) {
+              for (uint32_t x = 0; x < kOvSub; ++x) {
+                const uint64_t cap = plan.cstart[c * kOvSub + x + 1] - plan.cstart[c * kOvSub + x];
+                const double r = cap ? (double)cf[c * kOvSub + x] / cap : 1e9;
+                if (cf[c * kOvSub + x] > cap) ++nc;
+                worst_c = std::max(worst_c, r);
+              }
+            }
+            for (uint64_t f = 0; f < nfb; ++f) {
+              const uint64_t cap = plan.fstart[f + 1] - plan.fstart[f];
+              if (ff[f] > cap) ++nf;
+              worst_f = std::max(worst_f, cap ? (double)ff[f] / cap : (ff[f] ? 1e9 : 0));
+            }
+            fprintf(stderr, "[overlay] tick %llu: m=%llu partition fallback: %llu coarse / %llu fine regions over, "
+                    "worst fill/cap %.3f / %.3f\n", (unsigned long long)t0, (unsigned long long)m,
+                    (unsigned long long)nc, (unsigned long long)nf, worst_c, worst_f);
+          }
+          keys = nullptr;
+          d_pflag = nullptr;
         }
-        if (!keys) {
-          // by (destination, tag): each destination's run comes out tick by
-          // tick, and the process kernel orders each tick's few events by
-          // (src, kind) itself (sorting by destination only left runs of L
-          // ticks to the insertion sort, in global memory: slower than the
-          // TB extra radix bits)
-          OVCHK(grow(scratch, m * 8, stream));
-          rocprim::double_buffer<uint64_t> db((uint64_t*)bucket[s].p, (uint64_t*)scratch.p);
-          const unsigned begin_bit = p.B + 1, end_bit = 2 * p.B + 1 + p.TB;
-          size_t sort_bytes = 0;
-          OVCHK(rocprim::radix_sort_keys<OvRadix>(nullptr, sort_bytes, db, (size_t)m, begin_bit, end_bit, stream));
-          OVCHK(grow(cub_tmp, sort_bytes, stream));
-          sort_bytes = cub_tmp.bytes;
-          OVCHK(rocprim::radix_sort_keys<OvRadix>(cub_tmp.p, sort_bytes, db, (size_t)m, begin_bit, end_bit, stream));
-          keys = db.current();
-          if (db.current() != (uint64_t*)bucket[s].p) std::swap(bucket[s], scratch);
-          ++ws->sort_ticks;
-        }
-        const uint64_t per = (uint64_t)kProcBlock * kProcIPT;
-        const dim3 pgrid((uint32_t)((mproc + per - 1) / per));
-        auto* pk = row8 ? (staged == 2 ? k_process<true, 2> : staged ? k_process<true, 1> : k_process<true, 0>)
-                        : (staged == 2 ? k_process<false, 2> : staged ? k_process<false, 1> : k_process<false, 0>);
-        hipLaunchKernelGGL(pk, pgrid, dim3(kProcBlock), 0, stream, p, t0, keys, mproc, d_deg, d_ids,
-                           (uint64_t*)outb.p, (uint16_t*)oslotb.p, d_nemit, d_counts, d_tc);
-        OVCHK(hipGetLastError());
       }
-      OVCHK(hipMemcpyAsync(&h_ne, d_nemit, 8, hipMemcpyDeviceToHost, stream));
-      OVCHK(ctr_d2h(h_counts.data(), d_counts));
-      OVCHK(hipMemcpyAsync(&h_tc, d_tc, sizeof(h_tc), hipMemcpyDeviceToHost, stream));
-      OVCHK(hipMemsetAsync(d_nemit, 0, 8, stream));
-      OVCHK(hipStreamSynchronize(stream));
       {
         // the emitted events (k_process counted them per bucket): grow, write
         const uint64_t nitems = h_ne;
