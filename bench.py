@@ -530,7 +530,7 @@ def c3_trials(a, gs, rank, world, local, dist):
     members measured 0.91-0.97 s against 1.09 s for one 5,000-trial context
     renumbered batch after batch, profiles/r06d_c3_members.txt).  Timed: every
     batch's renumbering (gs_set_trial), overlay, broadcast and results.  The
-    contexts are created and run once before the timer, like the headline's
+    contexts are created and run twice before the timer, like the headline's
     warmup steps; create_s / warmup_s report that setup and s_end_to_end adds
     the creation to the batches."""
     import numpy as np
@@ -553,6 +553,7 @@ def c3_trials(a, gs, rank, world, local, dist):
 
     sims = {}
     create_s = warm_s = 0.0
+    warm_passes = []  # each untimed pass (overlay + broadcast) of each context, s
     for b in range(t0, t1, step):  # warmup: contexts, workspaces, code objects
         T = min(b + step, t1) - b
         if T not in sims:
@@ -560,15 +561,18 @@ def c3_trials(a, gs, rank, world, local, dist):
             sims[T] = open_batch(b, T)
             create_s += time.perf_counter() - tw
             for rep in range(2):  # two passes: the members' buffers settle in the block cache
+                tp = time.perf_counter()
                 if rep:
                     sims[T].reset()
                     sims[T].set_trial(b)
                 sims[T].build_overlay()
                 sims[T].broadcast_begin(-1)
                 sims[T].run(poll=10)
-            torch.cuda.synchronize()
+                torch.cuda.synchronize()
+                warm_passes.append(round(time.perf_counter() - tp, 3))
             warm_s += time.perf_counter() - tw
-            log(f"C3 warmup: context of {T} trials created and run once in {time.perf_counter() - tw:.2f} s")
+            log(f"C3 warmup: context of {T} trials created and run twice in {time.perf_counter() - tw:.2f} s "
+                f"(passes {warm_passes[-2:]} s)")
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -610,12 +614,13 @@ def c3_trials(a, gs, rank, world, local, dist):
             "median_tick_99_rank0": int(np.median(cov[:, 1])) if len(cov) else None,
             "mean_messages_per_trial": round(msgs / max(ntr, 1), 1),
             # setup outside s_total: gs_create of the batch contexts (create_s) and their
-            # first overlay + broadcast (warmup_s includes create_s); s_end_to_end = the
-            # contexts' creation + every batch, round 4's end-to-end timer
-            "create_s": round(create_s, 3), "warmup_s": round(warm_s, 3),
+            # two untimed passes of overlay + broadcast (warmup_s includes create_s;
+            # warmup_passes_s each pass, rank 0); s_end_to_end = the contexts' creation +
+            # every batch, round 4's end-to-end timer
+            "create_s": round(create_s, 3), "warmup_s": round(warm_s, 3), "warmup_passes_s": warm_passes,
             "s_end_to_end": round(dt + create_s, 3),
             "note": "s_total: every batch's renumbering (gs_set_trial), overlay, broadcast to its stopping poll "
-                    "and results on contexts created and run once before the timer; s_end_to_end adds "
+                    "and results on contexts created and run twice before the timer; s_end_to_end adds "
                     "the contexts' creation (create_s)"}
 
 
