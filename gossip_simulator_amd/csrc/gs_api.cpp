@@ -77,6 +77,8 @@ struct gs_ctx {
   Buf pp_rend, pp_rsrc, pp_rslot, pp_ilist, pp_fmask, pp_scan, pp_ctlb;
   Buf pp_rfail;  // push-pull: failed-caller bit per in-edge (with pp_fmask)
   Buf pp_dset, pp_dcnt;  // deferred sets of the pull-answer rounds (PPSparse::dset)
+  Buf pp_rend16;         // the compact view of pp_rend: rend16 [n] u16, then rbase [n/64 + 1] u64, then a flag
+  bool rend16_ok = false;  // the view fits (no 64-node block with more than 65,535 in-edges)
   uint64_t table_ver = 0, fail_ver = 0, rev_ver = ~0ull, fm_tver = ~0ull, fm_fver = ~0ull;
   // push-pull: live callers and live empty rows of (cl_tver, cl_fver) (pp_seed_ctx)
   uint64_t cl_tver = ~0ull, cl_fver = ~0ull;
@@ -776,7 +778,8 @@ void destroy_one(gs_ctx* c) {
                     (void*)c->d_glay})
     if (ptr) (void)dev_free(ptr);
   for (Buf* b : {&c->gmap, &c->cmsg, &c->fmsg, &c->tmp, &c->xsend, &c->xrecv, &c->pp_rend, &c->pp_rsrc,
-                 &c->pp_rslot, &c->pp_ilist, &c->pp_fmask, &c->pp_scan, &c->pp_ctlb, &c->pp_dset, &c->pp_dcnt, &c->pp_rfail})
+                 &c->pp_rslot, &c->pp_ilist, &c->pp_fmask, &c->pp_scan, &c->pp_ctlb, &c->pp_dset, &c->pp_dcnt, &c->pp_rfail,
+                 &c->pp_rend16})
     if (b->p) (void)dev_free(b->p);
   for (void* ptr : {(void*)c->h_cap, (void*)c->h_misc, (void*)c->h_err, (void*)c->h_stats, (void*)c->h_tstat,
                     (void*)c->h_stage, (void*)c->h_rtab, (void*)c->h_glay})
@@ -1709,12 +1712,34 @@ int pp_prepare(gs_ctx* c) {
     c->rev_ver = c->table_ver;
     c->fm_tver = ~0ull;
     built = true;
+    // the dense rounds' compact view of rend (2.1 B per node instead of 8)
+    c->rend16_ok = false;
+    const size_t r16 = (n * 2 + 255) / 256 * 256, rb = ((n >> 6) + 1) * 8;
+    if (grow(c->pp_rend16, r16 + rb + 8)) {
+      char* base = (char*)c->pp_rend16.p;
+      uint32_t* ovf = (uint32_t*)(base + r16 + rb);
+      uint32_t h_ovf = 1;
+      CK(c, hipMemsetAsync(ovf, 0, 4, c->stream));
+      CK(c, pp_rev_compact((const unsigned long long*)c->pp_rend.p, n, (uint16_t*)base,
+                           (unsigned long long*)(base + r16), ovf, c->stream));
+      CK(c, hipMemcpyAsync(&h_ovf, ovf, 4, hipMemcpyDeviceToHost, c->stream));
+      CK(c, hipStreamSynchronize(c->stream));
+      c->rend16_ok = h_ovf == 0;
+    } else {
+      (void)hipGetLastError();  // rend only
+    }
   }
   c->sp.ctl = (PPCtl*)c->pp_ctlb.p;
   c->sp.ilist = (uint32_t*)c->pp_ilist.p;
   c->sp.rend = (const unsigned long long*)c->pp_rend.p;
   c->sp.rsrc = (const uint32_t*)c->pp_rsrc.p;
   c->sp.rslot = (const uint8_t*)c->pp_rslot.p;
+  // (GS_PP_REND16=0: the dense rounds read rend, A/B; read per call)
+  if (c->rend16_ok && !(getenv("GS_PP_REND16") && atoi(getenv("GS_PP_REND16")) == 0)) {
+    const size_t r16 = (n * 2 + 255) / 256 * 256;
+    c->sp.rend16 = (const uint16_t*)c->pp_rend16.p;
+    c->sp.rbase = (const unsigned long long*)((const char*)c->pp_rend16.p + r16);
+  }
   // the pull-answer rounds' deferred sets (n <= 2^30; GS_PP_NODEFER=1: atomics, A/B):
   // lists, coarse and fine regions for 0.6 n sets each (more fall back to atomicOr)
   if (!getenv("GS_PP_NODEFER") && n <= (1ull << 30) && pp_rslot_packed(s.stride)) {

@@ -379,6 +379,11 @@ struct PPSparse {
   PPCtl* ctl;                   // null: dense rounds only
   uint32_t* ilist;              // [nseg][seg_cap] informed nodes, per segment in order of informing
   const unsigned long long* rend;  // [n] end of node u's in-edges
+  // the dense rounds' compact view of rend (null: read rend): node u's in-edges
+  // end at rbase[u >> 6] + rend16[u] and start at rbase[u >> 6] (u % 64 == 0)
+  // or rbase[u >> 6] + rend16[u - 1] -- 2.1 B per node instead of 8
+  const uint16_t* rend16;       // [n]
+  const unsigned long long* rbase;  // [ceil(n / 64)] start of node 64w's in-edges
   const uint32_t* rsrc;         // [E] caller v of each in-edge
   const uint8_t* rslot;         // [E] its slot j
   const uint8_t* fmask;         // [n] bit j: friend j is failed (stride <= 8 and a mask set), else null
@@ -426,6 +431,10 @@ hipError_t pp_rev_build(const DevState& s, unsigned long long* rend, uint32_t* r
 // temporaries ~17 B per edge, in as many passes over the coarse bins as the
 // device allocator's largest block needs; *passes_out = the passes).  An
 // error leaves the outputs unspecified (pp_rev_build then builds them).
+// rend16 / rbase (PPSparse) from rend; *ovf = 1 where a 64-node block's
+// in-edges pass 65,535 (the view is then not used)
+hipError_t pp_rev_compact(const unsigned long long* rend, uint64_t n, uint16_t* rend16, unsigned long long* rbase,
+                          uint32_t* ovf, hipStream_t st);
 hipError_t pp_rev_build_part(const DevState& s, unsigned long long* rend, uint32_t* rsrc, uint8_t* rslot,
                              hipStream_t st, uint32_t* passes_out);
 // fmask from the reverse table and the failed mask (stride <= 8).

@@ -284,6 +284,21 @@ __device__ __forceinline__ void for_each_bit(unsigned long long m, uint32_t* pre
   wave_lds_sync();  // pre / msk are reused by the next range
 }
 
+// Node u's in-edges [qb, qe): from the compact view (PPSparse::rend16 /
+// rbase: the dense rounds read 2 B per node of it instead of 8 of rend, and
+// they read it for most nodes) or from rend.
+__device__ __forceinline__ void in_edges(const PPSparse& sp, uint64_t u, unsigned long long& qb,
+                                         unsigned long long& qe) {
+  if (sp.rend16) {
+    const unsigned long long b = sp.rbase[u >> 6];
+    qb = b + ((u & 63) ? (unsigned long long)sp.rend16[u - 1] : 0ull);
+    qe = b + sp.rend16[u];
+  } else {
+    qb = u ? sp.rend[u - 1] : 0ull;
+    qe = sp.rend[u];
+  }
+}
+
 // Resolves queue entries [0, cnt) (cnt <= 64), one per lane.  Entry = node
 // offset in the range (12 bits) | deg << 16.
 __device__ __forceinline__ void ppb_resolve(const DevState& s, const PPSparse& sp, uint32_t t, uint32_t c3,
@@ -293,7 +308,8 @@ __device__ __forceinline__ void ppb_resolve(const DevState& s, const PPSparse& s
   if (lane >= cnt) return;
   const uint32_t e = q[lane], loc = e & 0xFFFu, d = e >> 16;
   const uint64_t v = base + loc;  // local id (global s.gbase + v)
-  const unsigned long long qb = v ? sp.rend[v - 1] : 0ull, qe = sp.rend[v];
+  unsigned long long qb, qe;
+  in_edges(sp, v, qb, qe);
   bool pull = false;
   uint32_t u = 0;
   if (d > 0) {
@@ -541,7 +557,8 @@ __device__ __forceinline__ void ppa_resolve(const DevState& s, const PPSparse& s
     pp_set(sp, next, take, w, s_dn);
 #endif
   }
-  const unsigned long long qb = u ? sp.rend[u - 1] : 0ull, qe = sp.rend[u];
+  unsigned long long qb, qe;
+  in_edges(sp, u, qb, qe);
   for (unsigned long long q0 = qb; q0 < qe; q0 += kPPEdges) {
     uint32_t src[kPPEdges], x[kPPEdges];
 #pragma unroll
@@ -1272,6 +1289,20 @@ __device__ __forceinline__ uint8_t rv_slot_byte(uint32_t stride, uint32_t j, uin
   return (uint8_t)(pp_rslot_packed(stride) ? j | (d - 1) << 4 : j);
 }
 
+// The compact view of rend (PPSparse::rend16 / rbase): one thread per node.
+__global__ __launch_bounds__(kPPBlock) void k_rv_compact(const unsigned long long* __restrict__ rend, uint64_t n,
+                                                         uint16_t* __restrict__ rend16,
+                                                         unsigned long long* __restrict__ rbase, uint32_t* ovf) {
+  for (uint64_t u = (uint64_t)blockIdx.x * kPPBlock + threadIdx.x; u < n; u += (uint64_t)gridDim.x * kPPBlock) {
+    const uint64_t w = u >> 6;
+    const unsigned long long b = w ? rend[(w << 6) - 1] : 0ull;
+    if ((u & 63) == 0) rbase[w] = b;
+    const unsigned long long d = rend[u] - b;
+    if (d > 0xFFFFull) atomicOr(ovf, 1u);
+    rend16[u] = (uint16_t)d;
+  }
+}
+
 __global__ __launch_bounds__(kRvBlock) void k_rv_hist(const DevState s, unsigned long long* chist) {
   __shared__ uint32_t h[kRvBins];
   for (uint32_t b = threadIdx.x; b < kRvBins; b += kRvBlock) h[b] = 0;
@@ -1554,6 +1585,14 @@ hipError_t pp_rev_build(const DevState& s, unsigned long long* rend, uint32_t* r
 // memory even for one bin, or a fine region past its planned size on a skewed
 // table) leaves the outputs unspecified: the caller then builds with
 // pp_rev_build.
+hipError_t pp_rev_compact(const unsigned long long* rend, uint64_t n, uint16_t* rend16, unsigned long long* rbase,
+                          uint32_t* ovf, hipStream_t st) {
+  if (!n) return hipSuccess;
+  const uint64_t blocks = std::min<uint64_t>((n + kPPBlock - 1) / kPPBlock, 8192);
+  hipLaunchKernelGGL(k_rv_compact, dim3((uint32_t)blocks), dim3(kPPBlock), 0, st, rend, n, rend16, rbase, ovf);
+  return hipGetLastError();
+}
+
 hipError_t pp_rev_build_part(const DevState& s, unsigned long long* rend, uint32_t* rsrc, uint8_t* rslot,
                              hipStream_t st, uint32_t* passes_out) {
   if (!s.n || s.n >= (1ull << 31)) return hipErrorInvalidValue;

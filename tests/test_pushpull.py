@@ -236,16 +236,21 @@ def test_gpu_pushpull_reverse_table_builds_agree(monkeypatch):
     and by the atomic count + fill (GS_PP_REV_ATOMIC, the fallback) drive the
     same rounds: every pull-answer and bottom-up round scans it, so per-round
     counters and the informed set must be identical, with and without a
-    failure mask (whose failed-caller bits are built from it).  Both switches
-    are read per build.  N = 1e7 spans three 2^22-node coarse bins."""
+    failure mask (whose failed-caller bits are built from it).  The dense
+    rounds' compact view of the in-edge ends (rend16 / rbase, the default)
+    must also equal reading the 8-B ends (GS_PP_REND16=0).  The switches are
+    read per build (per broadcast for GS_PP_REND16).  N = 1e7 spans three
+    2^22-node coarse bins."""
     import gossip_simulator_amd as gs
     gs.load()
     n = 10_000_000
     failed = words_of(np.random.default_rng(2).random(n) < 0.01)
     runs = {}
-    for mode in ("one", "three", "atomic"):
-        monkeypatch.delenv("GS_PP_REV_PASSES", raising=False)
-        monkeypatch.delenv("GS_PP_REV_ATOMIC", raising=False)
+    for mode in ("one", "three", "atomic", "rend64"):
+        for var in ("GS_PP_REV_PASSES", "GS_PP_REV_ATOMIC", "GS_PP_REND16"):
+            monkeypatch.delenv(var, raising=False)
+        if mode == "rend64":
+            monkeypatch.setenv("GS_PP_REND16", "0")
         if mode == "three":
             monkeypatch.setenv("GS_PP_REV_PASSES", "3")
         if mode == "atomic":
@@ -264,10 +269,11 @@ def test_gpu_pushpull_reverse_table_builds_agree(monkeypatch):
                 out.append((rows, sha(sim.received())))
                 if mask is None:
                     tm = sim.timing()
-                    assert tm["pp_rev_part"] == {"one": 1, "three": 3, "atomic": 0}[mode], tm["pp_rev_part"]
+                    assert tm["pp_rev_part"] == {"one": 1, "three": 3, "atomic": 0, "rend64": 1}[mode], \
+                        tm["pp_rev_part"]
                     assert tm["pp_bottom_rounds"] > 0 and tm["pp_answer_rounds"] > 0
             runs[mode] = out
-    for mode in ("three", "atomic"):
+    for mode in ("three", "atomic", "rend64"):
         for (a, ha), (b, hb) in zip(runs["one"], runs[mode]):
             assert np.array_equal(a, b), f"{mode}: per-round counters differ"
             assert ha == hb, f"{mode}: informed sets differ"
