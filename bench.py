@@ -406,16 +406,16 @@ def strong_scaling_block(world, line, ext):
         out["flood"] = {k: fl.get(k) for k in ("value", "unit", "ms_per_step", "device_ms_per_step",
                                                "device_ms_per_rank", "wall_over_device", "status", "error")
                         if k in fl}
-        out["pushpull"] = {k: pp.get(k) for k in ("value", "unit", "ms_per_step", "rounds_to_99", "status",
-                                                  "placement", "error") if k in pp}
+        out["pushpull"] = {k: pp.get(k) for k in ("value", "unit", "ms_per_step", "rounds_to_99", "rounds_run",
+                                                  "status", "placement", "error") if k in pp}
     else:
         roof = line.get("roofline") or {}
         out["flood"] = {"value": line.get("value"), "unit": line.get("unit"), "ms_per_step": line.get("ms_per_step"),
                         "device_ms_per_step": roof.get("broadcast_device_ms"),
                         "device_ms_per_rank": [roof.get("broadcast_device_ms")], "status": line["config"].get("status")}
         pp = ext.get("pushpull") or {}
-        out["pushpull"] = {k: pp.get(k) for k in ("value", "unit", "ms_per_step", "rounds_to_99", "status", "error")
-                           if k in pp}
+        out["pushpull"] = {k: pp.get(k) for k in ("value", "unit", "ms_per_step", "rounds_to_99", "rounds_run",
+                                                  "status", "error") if k in pp}
     return out
 
 
@@ -495,7 +495,7 @@ def pushpull_runs(a, gs, rank, local):
         log(f"push-pull: rounds={tot['tick']} sent={tot['sent']} {dt * 1e3 / len(runs):.1f} ms/run")
         out["pushpull"] = {
             "value": round(sum(r[0]["messages"] for r in runs) / dt, 1), "unit": "msgs/s",
-            "ms_per_step": round(dt * 1e3 / len(runs), 3), "rounds_to_99": tot["tick"],
+            "ms_per_step": round(dt * 1e3 / len(runs), 3), "poll": 10, "rounds_run": tot["tick"],
             "calls_per_s": round(sum(r[0]["fired"] for r in runs) / dt, 1),
             "messages_per_step": tot["messages"], "received": tot["received"],
             "status": STATUS[status],
@@ -516,6 +516,8 @@ def pushpull_runs(a, gs, rank, local):
         tot1, st1, dt1 = timed_broadcast(sim, poll=1)
         out["pushpull"]["poll_every_round"] = {"ms": round(dt1 * 1e3, 3), "rounds_to_99": tot1["tick"],
                                                "messages": tot1["messages"], "status": STATUS[st1]}
+        # the exact rounds to 99 % (rounds_run: where the 10-round poll stopped)
+        out["pushpull"]["rounds_to_99"] = tot1["tick"]
         sim.reset()
         sim.set_failed(failed_mask(a.n, 0.01, a.seed + 1))
         tot, status, dt = timed_broadcast(sim)
@@ -764,8 +766,15 @@ def pushpull_sharded(a, gs, rank, world, local, dist):
                 {"value": round(tot["messages"] / dt, 1), "ms": round(dt * 1e3, 3), "rounds": tot["tick"],
                  "received": tot["received"], "status": STATUS[status]})
             if not tag:
+                # rounds_run: where the 10-round poll stopped; rounds_to_99: one more
+                # broadcast polled every round (push-pull is round-synchronous)
+                sim.reset()
+                sim.broadcast_begin(-1)
+                sim.run(poll=1)
+                exact = sim.totals()["tick"]
                 out.update({"unit": "msgs/s", "shards": G, "placement": "ranks" if world > 1 else "one GPU",
-                            "ms_per_step": round(dt * 1e3, 3), "steps": len(runs), "rounds_to_99": tot["tick"],
+                            "ms_per_step": round(dt * 1e3, 3), "steps": len(runs), "poll": 10,
+                            "rounds_run": tot["tick"], "rounds_to_99": exact,
                             "messages_per_step": tot["messages"], "received": tot["received"],
                             "status": STATUS[status], "overlay_s": round(ov, 3)})
     finally:
