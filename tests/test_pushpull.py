@@ -184,6 +184,41 @@ def test_gpu_pushpull_bit_exact(oracle, kw, stride, dlo, dhi, fail_frac, rounds,
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("rounds", ["answer", "bottom"])
+def test_gpu_pushpull_hub_past_the_compact_view(oracle, rounds):
+    """A hub: every node's slot 0 names node 1, so node 1 has ~70,000
+    in-edges and its 64-node block passes the 65,535 the dense rounds'
+    compact view of the in-edge ends holds (u16 per node, PPSparse::rend16):
+    that context reads the 8-B ends instead (and a fine region of the
+    partition build overflows, so the reverse table may come from the atomic
+    fill).  Per round bit-exact to the oracle through pull-answer or
+    bottom-up rounds."""
+    import gossip_simulator_amd as gs
+    gs.load()
+    n = 70_000
+    deg, ids = random_table(n, 6, 5, 6, seed=11)
+    ids[:, 0] = 1
+    ids[1, 0] = 2
+    kw = dict(PP, n=n)
+    e = oracle.Engine(oracle.make_params(**kw), deg, ids)
+    e.begin(-1)
+    cfg = gs.Config(n=n, fanout=kw["fanout"], fanin=kw["fanin"], delaylow=kw["delay_low"],
+                    delayhigh=kw["delay_high"], droprate=kw["drop_rate"], crashrate=kw["crash_rate"],
+                    seed=kw["seed"], trial=kw["trial"], model="pushpull", pp_rounds=rounds)
+    with gs.Simulator(cfg) as sim:
+        sim.load_peers(deg, ids)
+        sim.broadcast_begin(-1)
+        for r in range(60):
+            a, b = e.step(1), sim.step(1)
+            assert np.array_equal(a, b), f"round {r + 1}:\n{a}\n{b}"
+            assert sha(e.received()) == sha(sim.received()), f"informed set differs at round {r + 1}"
+            if oracle.covered(int(a[0, 4]), n) or int(a[0, 4]) == 0:
+                break
+        tm = sim.timing()
+        assert tm["pp_answer_rounds"] + tm["pp_bottom_rounds"] > 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("rounds", ["answer", "bottom", "auto"])
 def test_gpu_pushpull_new_mask_and_table_on_one_context(oracle, rounds):
     """the per-(table, failure mask) caches (live-caller counts,
