@@ -563,7 +563,7 @@ struct OvPart {
 // single-trial chunks (each k_process workgroup appends its emitted events at
 // once, ~100 per bucket, in no trial order), so a wave's 64 consecutive keys
 // fall in one or two trials: the per-trial count pass took 70.7 -> 27.4 ms
-// per two C3 builds with it (profiles/r06o_*).  Not for waves that hold
+// per two C3 builds with it (profiles/r06_c3_partition_experiments.txt).  Not for waves that hold
 // several digits: in P2 (~8 fine regions per wave) it cost 60 -> 145 ms, and
 // P1 was unchanged.
 // Every lane of the wave calls it; returns the lane's rank among its digit's
