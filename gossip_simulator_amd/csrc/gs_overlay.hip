@@ -718,9 +718,10 @@ __global__ __launch_bounds__(kOvpBlock) void k_ov_part(const OvPart a) {
 // dense C3 tick.  LDS histogram per workgroup (<= kOvMaxTrials), one global
 // add per non-empty trial.
 // It also counts the keys of every coarse sub-region (c = dst >> 22, x = the
-// key's P1 tile % kOvSub) exactly: a batched bucket lies in trial order (tick
-// 0's picks are written trial by trial), so a tile's keys go to one or two
-// coarse regions and the tiles' shares of a region are far from even.
+// key's P1 tile % kOvSub) exactly: a batched bucket is made of single-trial
+// runs (tick 0's picks written trial by trial, later ticks' emissions one
+// k_process workgroup at a time), so the tiles' shares of a coarse region are
+// far from even.
 constexpr uint32_t kOvMaxTrials = 8192, kOvTrialBlock = 1024, kOvTrialGrid = 512;
 __global__ __launch_bounds__(kOvTrialBlock) void k_ov_count(const uint64_t* keys, uint64_t m, uint32_t sh,
                                                             uint32_t tlog, uint32_t ntr, uint32_t ncb,
